@@ -1,0 +1,148 @@
+"""ctypes bindings for the CPU oracle (oracle/liboracle*.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, always as the checker / the timed CPU baseline,
+never as the product path.  The oracle restates the reference algorithm
+(see paged_oracle.h for the file:line map).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_F = ctypes.POINTER(ctypes.c_float)
+_I = ctypes.POINTER(ctypes.c_int)
+_PF = ctypes.POINTER(_F)
+
+
+class OracleConfig(ctypes.Structure):
+    _fields_ = [("max_seq_len", ctypes.c_int), ("vocab_size", ctypes.c_int),
+                ("num_layers", ctypes.c_int), ("num_heads", ctypes.c_int),
+                ("channels", ctypes.c_int)]
+
+
+def build(fast=False):
+    """(Re)build the oracle libraries with make; returns the library path."""
+    name = "liboracle_fast.so" if fast else "liboracle.so"
+    subprocess.run(["make", "-s", "-C", HERE, name], check=True)
+    return os.path.join(HERE, name)
+
+
+_libs = {}
+
+
+def lib(fast=False):
+    key = bool(fast)
+    if key in _libs:
+        return _libs[key]
+    path = os.path.join(HERE, "liboracle_fast.so" if fast else "liboracle.so")
+    src = os.path.join(HERE, "paged_oracle.c")
+    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+        build(fast)
+    L = ctypes.CDLL(path)
+    L.oracle_num_params.restype = ctypes.c_size_t
+    L.oracle_num_params.argtypes = [OracleConfig]
+    L.oracle_param_offsets.argtypes = [OracleConfig, ctypes.POINTER(ctypes.c_size_t)]
+    L.oracle_attention_paged.argtypes = [_F, _F, _F, _F, _PF, _PF] + [ctypes.c_int] * 6
+    L.oracle_attention_forward.argtypes = [_F, _F, _F, _F] + [ctypes.c_int] * 4
+    L.oracle_matmul_forward.argtypes = [_F, _F, _F, _F] + [ctypes.c_int] * 4
+    L.oracle_matmul_cached.argtypes = [_F, _F, _F, _F] + [ctypes.c_int] * 4
+    L.oracle_layernorm_forward.argtypes = [_F, _F, _F, _F, _F, _F] + [ctypes.c_int] * 3
+    L.oracle_gelu_forward.argtypes = [_F, _F, ctypes.c_int]
+    L.oracle_gpt2_forward.argtypes = [_F, OracleConfig, _I, ctypes.c_int, ctypes.c_int, _F]
+    L.oracle_paged_create.restype = ctypes.c_void_p
+    L.oracle_paged_create.argtypes = [_F, OracleConfig, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_ulonglong]
+    L.oracle_paged_step.restype = ctypes.c_int
+    L.oracle_paged_step.argtypes = [ctypes.c_void_p, _I, _F, _I]
+    L.oracle_paged_fill_random.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_ulonglong]
+    L.oracle_paged_pos.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.oracle_paged_pos.restype = ctypes.c_int
+    L.oracle_paged_free.argtypes = [ctypes.c_void_p]
+    L.oracle_argmax.argtypes = [_F, ctypes.c_int]
+    L.oracle_argmax.restype = ctypes.c_int
+    _libs[key] = L
+    return L
+
+
+def fp(a):
+    assert a.dtype == np.float32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_F)
+
+
+def ip(a):
+    assert a.dtype == np.int32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_I)
+
+
+def cfg(maxT, V, L, NH, C):
+    return OracleConfig(maxT, V, L, NH, C)
+
+
+def num_params(c, fast=False):
+    return lib(fast).oracle_num_params(c)
+
+
+def attention_paged(inp, kpool, vpool, page_order, B, T, C, NH, offset, block_size):
+    """oracle_attention_paged on a pool whose logical page i lives at
+    kpool[page_order[i]] (kpool: (npages, block_size, C))."""
+    L = lib()
+    out = np.zeros((B, T, C), np.float32)
+    preatt = np.zeros((B, NH, T, T), np.float32)
+    att = np.zeros((B, NH, T, T), np.float32)
+    n = len(page_order)
+    kb = (_F * n)(*[kpool[p].ctypes.data_as(_F) for p in page_order])
+    vb = (_F * n)(*[vpool[p].ctypes.data_as(_F) for p in page_order])
+    L.oracle_attention_paged(fp(out), fp(preatt), fp(att), fp(inp), kb, vb, B, T, C, NH, offset,
+                             block_size)
+    return out, preatt, att
+
+
+def gpt2_forward(params, c, tokens, fast=False):
+    B, T = tokens.shape
+    logits = np.zeros((B, T, c.vocab_size), np.float32)
+    lib(fast).oracle_gpt2_forward(fp(params), c, ip(np.ascontiguousarray(tokens, np.int32)), B, T,
+                                  fp(logits))
+    return logits
+
+
+class PagedDecoder:
+    """oracle_paged_* : incremental paged decode, absolute positions, all layers."""
+
+    def __init__(self, params, c, B, page_size, max_ctx, page_seed=7, fast=False):
+        self.L = lib(fast)
+        self.params = params  # keep alive
+        self.c = c
+        self.B = B
+        self.h = self.L.oracle_paged_create(fp(params), c, B, page_size, max_ctx, page_seed)
+        if not self.h:
+            raise MemoryError("oracle_paged_create failed")
+
+    def step(self, tokens, want_logits=True):
+        tokens = np.ascontiguousarray(tokens, np.int32)
+        nxt = np.zeros(self.B, np.int32)
+        logits = np.zeros((self.B, self.c.vocab_size), np.float32) if want_logits else None
+        rc = self.L.oracle_paged_step(self.h, ip(tokens), fp(logits) if want_logits else None,
+                                      ip(nxt))
+        if rc != 0:
+            raise RuntimeError("oracle_paged_step failed (context full)")
+        return nxt, logits
+
+    def fill_random(self, ctx, seed=1):
+        self.L.oracle_paged_fill_random(self.h, ctx, seed)
+
+    def pos(self, b):
+        return self.L.oracle_paged_pos(self.h, b)
+
+    def close(self):
+        if self.h:
+            self.L.oracle_paged_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
