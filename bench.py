@@ -1,0 +1,280 @@
+#!/usr/bin/env python3
+"""Decode throughput benchmark of the MI355X paged-attention decode path.
+
+Metric (BASELINE.json): decode tokens/sec, GPT-2 124M paged attention,
+B=64, ctx 1024, page 16, fp32, on 1/2/4/8 MI355X (configs[1]; the global
+batch of 64 sequences is sharded by sequence across ranks -> strong scaling).
+
+One "step" = one decode step of the whole batch: every sequence gets one new
+token at its absolute position, all 12 layers (LN, QKV + KV append into the
+HBM page pool, paged attention over 0..pos through the block table,
+projections, MLP, residuals), final LN, logits (B x 50257), greedy argmax.
+The KV cache is prefilled to ctx - (warmup + steps) positions with synthetic
+K/V (default; --prefill decode runs real decode steps instead); the timed
+steps then decode at positions up to ctx - 1.  Weights are seeded synthetic
+GPT-2 124M (no checkpoints offline).
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "llm.c-paged_amd"))
+
+import numpy as np  # noqa: E402
+
+METRIC = "decode tokens/sec GPT-2 124M paged-attn, B=64 T=1024, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def shard_range(B, world, rank):
+    """contiguous sequence range of `rank` (B_local = B / n)"""
+    base, rem = divmod(B, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64, help="global batch (sequences)")
+    ap.add_argument("--ctx", type=int, default=1024)
+    ap.add_argument("--page-size", type=int, default=16)
+    ap.add_argument("--model", default="124M", choices=["124M", "XL"])
+    ap.add_argument("--prefill", default="synthetic", choices=["synthetic", "decode"])
+    ap.add_argument("--gather", default="ids", choices=["ids", "logits", "none"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--prof-steps", type=int, default=4,
+                    help="extra eager steps with HIP events around each attention launch")
+    ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--attn-waves", type=int, default=4)
+    return ap.parse_args()
+
+
+def cpu_baseline(cfgd, B, P, ctx, budget_s):
+    """The oracle's OpenMP C restatement of the same paged decode, timed on the
+    host cores on a bounded sample (rank 0, N=1).  Test infrastructure only."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle_ctypes as oc
+    import pagedattn
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    params = pagedattn.synthetic_params(cfgd, seed=1337)
+    c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
+    dec = oc.PagedDecoder(params, c, B, P, cfgd["maxT"], page_seed=3, fast=True)
+    start_ctx = ctx - 16
+    dec.fill_random(start_ctx, seed=5)
+    rng = np.random.default_rng(0)
+    tok = rng.integers(0, cfgd["V"], B).astype(np.int32)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        tok, _ = dec.step(tok, want_logits=False)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or steps >= 16:
+            break
+    dec.close()
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": B * steps / el, "unit": "tokens/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/liboracle_fast.so (-O3 -Ofast OpenMP C restatement), GPT-2 124M fp32, "
+                      f"B={B}, page {P}, {steps} decode steps at ctx {start_ctx}..{start_ctx + steps} "
+                      f"after a synthetic K/V fill, {el:.1f} s; cpu: {cpu_model}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.gpus != world:
+        args.gpus = world
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    import pagedattn
+    L = pagedattn.lib()
+    pagedattn.init(local_rank)
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_rank)
+        # one non-default stream shared by the library and torch: the decode
+        # kernels, the id copy and the RCCL gather are ordered on it, and it
+        # can be captured into a hipGraph (the legacy null stream cannot)
+        stream = torch.cuda.Stream()
+        torch.cuda.set_stream(stream)
+        L.hpa_set_stream(stream.cuda_stream)
+    pagedattn.check(L.hpa_set_attention_waves(args.attn_waves), "attention waves")
+
+    cfgd = dict(pagedattn.GPT2_124M if args.model == "124M" else pagedattn.GPT2_XL)
+    B = args.batch
+    lo, hi = shard_range(B, world, rank)
+    B_local = hi - lo
+    P = args.page_size
+    ctx = min(args.ctx, cfgd["maxT"])
+    need = args.warmup + args.steps + args.prof_steps
+    window = min(need, ctx // 2)
+    start = ctx - window  # positions of the first decoded token
+
+    model = pagedattn.Model(cfgd, seed=1337)
+    model.decode_init(B_local, P, ctx)
+    model.reserve(ctx)
+    rng = np.random.default_rng(1000 + rank)
+    if args.prefill == "synthetic":
+        model.fill_random(start, seed=77 + rank)
+    else:
+        for p in range(start):
+            model.step(rng.integers(0, cfgd["V"], B_local).astype(np.int32), want_next=False)
+    model.set_graph(not args.no_graph)
+    first = rng.integers(0, cfgd["V"], B_local).astype(np.int32)
+    pos_now = [start]
+
+    ids = torch.zeros(B_local, dtype=torch.int32, device="cuda")
+    all_ids = torch.zeros(B_local * world, dtype=torch.int32, device="cuda") if world > 1 else None
+    logits_t = None
+    all_logits = None
+    if args.gather == "logits" and world > 1:
+        logits_t = torch.zeros(B_local, cfgd["V"], dtype=torch.float32, device="cuda")
+        all_logits = torch.zeros(B_local * world, cfgd["V"], dtype=torch.float32, device="cuda")
+
+    def one_step(tokens=None):
+        if pos_now[0] >= ctx:  # slide back: pages kept, positions rewritten
+            model.set_positions(np.full(B_local, start, np.int32))
+            pos_now[0] = start
+        model.step_async(tokens)
+        pos_now[0] += 1
+        if world > 1 and args.gather != "none":
+            if args.gather == "ids":
+                L.hpa_memcpy_async(ids.data_ptr(), model.next_ptr(), B_local * 4)
+                dist.all_gather_into_tensor(all_ids, ids)
+            else:
+                L.hpa_memcpy_async(logits_t.data_ptr(), model.logits_ptr(), logits_t.numel() * 4)
+                dist.all_gather_into_tensor(all_logits, logits_t)
+
+    def sync():
+        pagedattn.check(L.hpa_synchronize(), "sync")
+        torch.cuda.synchronize()
+
+    one_step(first)
+    for _ in range(args.warmup - 1 if args.warmup > 0 else 0):
+        one_step(None)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    bytes_before, _ = model.step_bytes()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step(None)
+    sync()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    bytes_after, attn_after = model.step_bytes()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
+    tokens_per_s = B * args.steps / elapsed  # whole job: every rank's sequences
+
+    # ---- live attention-kernel timing (HIP events on the launch stream)
+    attn = None
+    if args.prof_steps > 0:
+        L.gpt2_decode_profile.argtypes = [pagedattn._V, pagedattn.ctypes.c_int]
+        L.gpt2_decode_profile_collect.argtypes = [pagedattn._V]
+        L.gpt2_decode_profile_read.argtypes = [pagedattn._V, pagedattn.ctypes.POINTER(pagedattn.ctypes.c_long)]
+        L.gpt2_decode_profile_read.restype = pagedattn.ctypes.c_double
+        pagedattn.check(L.gpt2_decode_profile(model.h, 1), "profile on")
+        attn_bytes = 0.0
+        for _ in range(args.prof_steps):
+            if pos_now[0] >= ctx:
+                model.set_positions(np.full(B_local, start, np.int32))
+                pos_now[0] = start
+            _, ab = model.step_bytes()  # KV bytes this step will read (ctx = pos + 1)
+            attn_bytes += ab
+            model.step_async(None)
+            pos_now[0] += 1
+            pagedattn.check(L.gpt2_decode_profile_collect(model.h), "profile collect")
+        n = pagedattn.ctypes.c_long()
+        ms = L.gpt2_decode_profile_read(model.h, pagedattn.ctypes.byref(n))
+        pagedattn.check(L.gpt2_decode_profile(model.h, 0), "profile off")
+        # per launch: K+V of every sequence's context for one layer (+ q in, out)
+        per_launch_bytes = attn_bytes / (args.prof_steps * cfgd["L"]) + 2 * B_local * cfgd["C"] * 4
+        avg_ms = ms / max(n.value, 1)
+        achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
+        attn = dict(avg_ms=avg_ms, launches=n.value, per_launch_bytes=per_launch_bytes,
+                    achieved=achieved)
+
+    result = None
+    if rank == 0:
+        cpu = None
+        want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
+        if want_cpu and args.model == "124M":
+            try:
+                cpu = cpu_baseline(cfgd, B, P, ctx, args.cpu_seconds)
+            except Exception as e:  # reported, never fatal for the GPU number
+                cpu = {"value": None, "error": repr(e)}
+        name, cus, mem = pagedattn.device_info()
+        roof = None
+        if attn:
+            roof = {"bound": "hbm", "kernel": "paged_attn_decode_f32", "achieved": round(attn["achieved"], 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(attn["achieved"] / HBM_PEAK_GBS, 4),
+                    "traffic": None, "avg_launch_ms": round(attn["avg_ms"], 5),
+                    "bytes_per_launch": int(attn["per_launch_bytes"]), "launches_timed": attn["launches"]}
+        step_bytes = 0.5 * (bytes_before + bytes_after)
+        result = {
+            "metric": METRIC,
+            "value": round(tokens_per_s, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (seeded random GPT-2 124M weights and tokens; KV prefill: "
+                    + ("synthetic U(-1,1)" if args.prefill == "synthetic" else "decode steps") + ")",
+            "config": {"workload": f"GPT-2 {args.model} fp32 paged decode, batch={B}, ctx {ctx}, "
+                                   f"page_size={P} (BASELINE.json configs[1])",
+                       "global_batch": B, "seq_len": ctx, "page_size": P,
+                       "decode_positions": f"{start}..{start + args.warmup + args.steps - 1}",
+                       "parallelism": f"seq-shard x{world}" + (f" + RCCL all_gather({args.gather})"
+                                                               if world > 1 else ""),
+                       "hip_graph": not args.no_graph, "device": name},
+            "step_roofline": {"bytes_per_step_rank0": int(step_bytes),
+                              "achieved_GBps": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+                              "frac_of_8TBps": round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    model.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,176 @@
+/*
+ * hip_paged_attn.h -- C-ABI of the MI355X (gfx950) paged-attention decode
+ * library libpaged_hip.so.  Plain pointers and sizes only.
+ *
+ * Two families of entry points:
+ *
+ *  hpa_*            MI355X-native building blocks of the decode step
+ *                   (device memory, page pool, fused kernels).  Called by
+ *                   paged_infer.c's decode driver (gpt2_decode_*), which is
+ *                   the replacement for the reference's gpt2_forward
+ *                   (paged_infer.c:575-729 of mx60s/llm.c-paged).
+ *  reference-named  the drop-in functions of the reference's
+ *                   paged_infer.c / block_manager.c API, declared in
+ *                   paged_infer.h and block_manager.h.
+ *
+ * Error convention (reference: stderr + NULL from the allocator,
+ * block_manager.c:117,139,149; exit(1) with location for device errors like
+ * cudaCheck, train_gpt2.cu:27-34): hpa_* return 0 on success and a nonzero
+ * code after printing "[hpa] <file>:<line> <error>" to stderr; with
+ * HPA_FATAL=1 in the environment they exit(1) instead.
+ *
+ * Device pointers passed to hpa_* kernels must live in device-accessible
+ * memory (hpa_malloc / hpa_malloc_managed / hipHostMalloc).  All launches go
+ * to the library's current stream (hpa_set_stream) and are asynchronous.
+ */
+#ifndef HIP_PAGED_ATTN_H
+#define HIP_PAGED_ATTN_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------- device, stream, memory, events ---------------- */
+int   hpa_init(int device);            /* select device, create the default stream */
+int   hpa_device_count(void);
+int   hpa_get_device(void);
+int   hpa_set_stream(void* hip_stream); /* NULL = library default stream */
+void* hpa_get_stream(void);
+int   hpa_synchronize(void);            /* stream sync */
+int   hpa_device_synchronize(void);
+void* hpa_malloc(size_t bytes);          /* hipMalloc; NULL on failure */
+void* hpa_malloc_managed(size_t bytes);  /* hipMallocManaged (host-dereferenceable) */
+void* hpa_host_alloc(size_t bytes);      /* pinned host memory */
+int   hpa_free(void* p);
+int   hpa_host_free(void* p);
+int   hpa_memcpy(void* dst, const void* src, size_t bytes);       /* hipMemcpyDefault, sync */
+int   hpa_memcpy_async(void* dst, const void* src, size_t bytes); /* on the current stream */
+int   hpa_memset_async(void* dst, int value, size_t bytes);
+int   hpa_is_device_accessible(const void* p); /* 1 if a kernel may dereference p */
+void* hpa_event_create(void);
+int   hpa_event_record(void* ev);
+float hpa_event_elapsed_ms(void* start, void* stop); /* syncs on stop */
+int   hpa_event_destroy(void* ev);
+const char* hpa_last_error(void);
+/* hipGraph capture of everything enqueued on the current stream between
+ * begin and end (the decode step: ~9 launches per layer); replay with
+ * hpa_graph_launch.  Kernel arguments are frozen at capture, so per-step
+ * state (tokens, positions, block tables) must live in device memory. */
+int   hpa_graph_begin(void);
+void* hpa_graph_end(void);               /* instantiated executable graph, NULL on failure */
+int   hpa_graph_launch(void* graph_exec);
+int   hpa_graph_destroy(void* graph_exec);
+/* waves per (sequence, head) workgroup of the decode attention: 1, 2, 4, 8 */
+int   hpa_set_attention_waves(int nw);
+int   hpa_device_info(char* name, int name_len, int* num_cus, size_t* total_mem);
+
+/* ---------------- paged KV pool (fast layout) ----------------
+ * One allocation per device: pool[layer][page][kv][head][tile], tile =
+ * page_size x head_size elements.  K tiles are stored as
+ * [head_size/4][page_size][4] (so one wave64 instruction reads 4-byte x 4
+ * columns of 64 consecutive tokens = 128..512 contiguous bytes per page, the
+ * lane-per-token QK^T layout); V tiles are token-major [page_size][head_size]
+ * (one 256-byte row per token-head, the lane-per-dimension PV layout).
+ * A page id names the same slot in every layer's pool (vLLM-style shared
+ * block table), so the block table is [seq][logical page] int32. */
+typedef struct HpaKVPool {
+    void*  base;          /* device pointer */
+    int    num_layers, num_heads, head_size, page_size, num_pages;
+    int    dtype;         /* HPA_F32 (round 1) */
+    size_t elem_bytes;
+    size_t page_elems;    /* elements of one page of one layer (K and V, all heads) */
+    size_t layer_elems;   /* num_pages * page_elems */
+    size_t bytes;
+    int    managed;
+} HpaKVPool;
+enum { HPA_F32 = 0, HPA_BF16 = 1 };
+int  hpa_pool_create(HpaKVPool* pool, int num_layers, int num_heads, int head_size, int page_size,
+                     int num_pages, int dtype, int managed);
+void hpa_pool_destroy(HpaKVPool* pool);
+/* device address of the K (kv=0) or V (kv=1) tile of (layer, page, head) */
+void* hpa_pool_tile(const HpaKVPool* pool, int layer, int page, int kv, int head);
+/* host-side layout helpers (tests / compat copies) */
+size_t hpa_pool_k_index(const HpaKVPool* pool, int layer, int page, int head, int slot, int d);
+size_t hpa_pool_v_index(const HpaKVPool* pool, int layer, int page, int head, int slot, int d);
+
+/* ---------------- decode-step kernels (fp32) ----------------
+ * B = sequences in the batch, C = channels, NH heads of head_size 64.
+ * pos[b] = absolute position of the token decoded this step (== tokens
+ * already cached for b); the token's K/V go to slot pos[b] and attention
+ * covers positions 0..pos[b]. */
+
+/* residual[b] = wte[tok[b]] + wpe[pos[b]];  ln_out[b] = LN(residual[b])
+ * (encoder_forward paged_infer.c:24-47 at absolute positions, fused with
+ * layernorm_forward :49-89) */
+int hpa_embed_ln(const int* tokens, const int* pos, const float* wte, const float* wpe,
+                 const float* ln_w, const float* ln_b, float* residual, float* ln_out, int B, int C);
+
+/* out = x[M][K] . W[N][K]^T on fp32 MFMA (v_mfma_f32_32x32x2_f32).
+ * splitk == 1: out[m][n] = acc + bias[n] (+GELU when epilogue == HPA_EPI_BIAS_GELU)
+ * splitk  > 1: out is a partial-slab array [splitk][M][N] (bias not added);
+ *              a row epilogue (below) reduces it.
+ * Replaces matmul_forward / matmul_cached for decode rows (paged_infer.c:92-160). */
+enum { HPA_EPI_PARTIAL = 0, HPA_EPI_BIAS = 1, HPA_EPI_BIAS_GELU = 2 };
+int hpa_gemm_f32(const float* x, int ldx, const float* W, const float* bias, float* out, int ldo,
+                 int M, int N, int K, int splitk, int epilogue);
+/* the split-K the library would choose for this shape (deterministic) */
+int hpa_gemm_pick_splitk(int M, int N, int K);
+
+/* QKV epilogue + KV append (add_to_cache paged_infer.c:505-573 fused):
+ * qkv = sum_s part[s] + bias; q[b] <- qkv[0:C]; K,V -> pool page
+ * block_table[b*bt_stride + pos[b]/P], slot pos[b]%P of `layer`. */
+int hpa_qkv_append(const float* part, int splitk, const float* bias, float* q, const HpaKVPool* pool,
+                   int layer, const int* block_table, int bt_stride, const int* pos, int B, int C);
+
+/* paged decode attention (attention_paged paged_infer.c:163-240 for one
+ * query row per sequence at absolute position pos[b]): block-table gather of
+ * K/V pages -> q.k^T -> online softmax -> PV.  q, out: [B][C]. */
+int hpa_paged_attention_decode(const float* q, const HpaKVPool* pool, int layer,
+                               const int* block_table, int bt_stride, const int* pos, float* out,
+                               int B);
+
+/* residual_out = residual_in + bias + sum_s part[s];  ln_out = LN(residual_out)
+ * (residual_forward :253-257 + layernorm_forward :49-89 fused).  ln_w may be
+ * NULL to skip the LN. */
+int hpa_residual_ln(const float* part, int splitk, const float* bias, const float* residual_in,
+                    float* residual_out, const float* ln_w, const float* ln_b, float* ln_out,
+                    int B, int C);
+
+/* out = GELU(bias + sum_s part[s])  (gelu_forward :243-251) */
+int hpa_bias_gelu(const float* part, int splitk, const float* bias, float* out, int M, int N);
+
+/* greedy token choice (generate_tokens_from_logits :937-951 over logits,
+ * lowest index wins ties); writes next[b], tokens[b] = next[b] (feeds the
+ * next step's embedding) and advances pos[b] += 1.  tokens/pos may be NULL. */
+int hpa_argmax_advance(const float* logits, int B, int V, int* next, int* tokens, int* pos);
+
+/* synthetic K/V fill of positions [0, ctx) for every sequence with U(-1,1)
+ * from a counter-based hash (attention microbench / bench synthetic prefill) */
+int hpa_pool_fill_random(const HpaKVPool* pool, const int* block_table, int bt_stride, int B,
+                         int ctx, uint64_t seed);
+
+/* ---------------- reference-layout kernels (drop-in compat) ----------------
+ * Pages in the reference layout: token-major [block_size][C] per page
+ * (block_manager.c:145-146).  key_blocks/value_blocks: DEVICE arrays of
+ * DEVICE page pointers.  Reference arithmetic order (no FMA contraction), so
+ * results match the reference bit-for-bit up to expf/tanhf ulps. */
+int hpa_ref_attention_paged(float* out, float* preatt, float* att, const float* inp,
+                            float* const* key_blocks, float* const* value_blocks, int B, int T,
+                            int C, int NH, int offset, int block_size);
+/* cached == 0: matmul_forward (:92-114); cached == 1: matmul_cached
+ * (:117-160): rows t < T-1 compute only the first C outputs (Q) */
+int hpa_ref_matmul(float* out, const float* inp, const float* weight, const float* bias, int B,
+                   int T, int C, int OC, int cached);
+int hpa_ref_layernorm(float* out, float* mean, float* rstd, const float* inp, const float* weight,
+                      const float* bias, int N, int C);
+int hpa_ref_encoder(float* out, const int* inp, const float* wte, const float* wpe, int B, int T,
+                    int C, int pos_offset);
+int hpa_ref_gelu(float* out, const float* inp, int N);
+int hpa_ref_residual(float* out, const float* a, const float* b, int N);
+int hpa_ref_softmax(float* probs, const float* logits, int N, int V);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,169 @@
+/*
+ * paged_infer.h -- drop-in for the API of mx60s/llm.c-paged paged_infer.c
+ * (GPT-2 inference over a paged KV cache), backed by MI355X kernels.
+ *
+ * Reference-named functions keep the reference signatures
+ * (paged_infer.c:24-302, :436-745, :826-951).  Their data may live on the
+ * host or in device memory: host buffers are staged through HBM and the
+ * result copied back, so a caller written for the reference works unchanged.
+ * The layer functions compute on the GPU with the reference's arithmetic
+ * order (hpa_ref_* kernels).
+ *
+ * The decode hot path is additive: gpt2_decode_* run one batched decode
+ * step (one token for each of B sequences at absolute positions) entirely
+ * on device through hand-written gfx950 kernels, the page pool in HBM and
+ * per-sequence block tables from the BlockManager.  gpt2_forward() is
+ * implemented on top of it with corrected semantics (all L layers, absolute
+ * positions, one page list per sequence).
+ */
+#ifndef PAGED_INFER_H
+#define PAGED_INFER_H
+#include <stddef.h>
+
+#include "block_manager.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* paged_infer.c:397-403 */
+typedef struct {
+    int max_seq_len;
+    int vocab_size;
+    int num_layers;
+    int num_heads;
+    int channels;
+} GPT2Config;
+
+/* paged_infer.c:308-326; DEVICE pointers into params_memory */
+#define NUM_PARAMETER_TENSORS 16
+typedef struct {
+    float* wte;      /* (V, C) */
+    float* wpe;      /* (maxT, C) */
+    float* ln1w;     /* (L, C) */
+    float* ln1b;     /* (L, C) */
+    float* qkvw;     /* (L, 3C, C) */
+    float* qkvb;     /* (L, 3C) */
+    float* attprojw; /* (L, C, C) */
+    float* attprojb; /* (L, C) */
+    float* ln2w;     /* (L, C) */
+    float* ln2b;     /* (L, C) */
+    float* fcw;      /* (L, 4C, C) */
+    float* fcb;      /* (L, 4C) */
+    float* fcprojw;  /* (L, C, 4C) */
+    float* fcprojb;  /* (L, C) */
+    float* lnfw;     /* (C) */
+    float* lnfb;     /* (C) */
+} ParameterTensors;
+
+/* the caller-visible outputs of gpt2_forward (paged_infer.c:350-375 keeps 23
+ * activation tensors; decode needs only these, host-readable) */
+typedef struct {
+    float* logits; /* (B, T, V): row T-1 of every b written by gpt2_forward */
+    float* probs;  /* (B, T, V): softmax of those rows */
+} ActivationTensors;
+
+typedef struct GPT2Decode GPT2Decode;
+
+/* paged_infer.c:405-434 (training-only fields dropped) */
+typedef struct {
+    GPT2Config config;
+    ParameterTensors params;
+    size_t param_sizes[NUM_PARAMETER_TENSORS];
+    float* params_memory; /* device */
+    size_t num_parameters;
+    ActivationTensors acts;
+    float* acts_memory;   /* managed memory behind acts */
+    int batch_size;
+    int seq_len;
+    int* inputs;
+    int* targets;
+    float mean_loss;
+    BlockManager* manager; /* kv cache stuff (set by the caller, paged_infer.c:986-987) */
+    GPT2Decode* decode;    /* device decode engine (lazily created) */
+} GPT2;
+
+/* ---------------- reference API ---------------- */
+void encoder_forward(float* out, int* inp, float* wte, float* wpe, int B, int T, int C);
+void layernorm_forward(float* out, float* mean, float* rstd, float* inp, float* weight, float* bias,
+                       int B, int T, int C);
+void matmul_forward(float* out, float* inp, float* weight, float* bias, int B, int T, int C, int OC);
+void matmul_cached(float* out, float* inp, float* weight, float* bias, int B, int T, int C, int OC);
+void attention_paged(float* out, float* preatt, float* att, float* inp, float** key_blocks,
+                     float** value_blocks, int B, int T, int C, int NH, int offset);
+void gelu_forward(float* out, float* inp, int N);
+void residual_forward(float* out, float* inp1, float* inp2, int N);
+void softmax_forward(float* probs, float* logits, int B, int T, int V);
+void add_to_cache(BlockManager* manager, float* qkv, int B, int T, int C,
+                  int how_many_tokens_to_copy_from_the_end_of_sequence);
+void gpt2_build_from_checkpoint(GPT2* model, const char* checkpoint_path);
+void gpt2_forward(GPT2* model, int* inputs, int* targets, size_t B, size_t T, size_t max_total,
+                  int offset);
+void gpt2_free(GPT2* model);
+unsigned int random_u32(unsigned long long* state);
+float random_f32(unsigned long long* state);
+int sample_mult(float* probabilities, int n, float coin);
+int* generate_tokens_from_logits(float* probs, int B, int T, int V);
+
+/* attention_paged with the page size as an argument (the reference fixes
+ * BLOCK_SIZE = 32); attention_paged() uses BLOCK_SIZE */
+void attention_paged_bs(float* out, float* preatt, float* att, float* inp, float** key_blocks,
+                        float** value_blocks, int B, int T, int C, int NH, int offset,
+                        int block_size);
+
+/* ---------------- model construction (additive) ---------------- */
+/* upload host params (checkpoint order) to the device; 0 on success */
+int gpt2_build_from_params(GPT2* model, GPT2Config config, const float* host_params);
+/* seeded synthetic GPT-2 weights (the reference xorshift, paged_infer.c:826-835) */
+int gpt2_build_synthetic(GPT2* model, GPT2Config config, unsigned long long seed);
+size_t gpt2_num_parameters(GPT2Config config);
+int gpt2_synthetic_params(GPT2Config config, unsigned long long seed, float* host_params);
+int gpt2_write_checkpoint(const char* path, GPT2Config config, const float* host_params);
+
+/* heap handle for FFI callers (ctypes / cgo) that cannot size GPT2 */
+GPT2* gpt2_alloc(void);
+void gpt2_release(GPT2* model); /* gpt2_free + free */
+void gpt2_set_manager(GPT2* model, BlockManager* manager);
+float* gpt2_acts_logits(GPT2* model);
+float* gpt2_acts_probs(GPT2* model);
+
+/* ---------------- decode engine (the MI355X hot path) ---------------- */
+/* B sequences, page_size tokens per page, up to max_ctx tokens per sequence.
+ * Uses model->manager when it was set by the caller (its block_size becomes
+ * the page size), otherwise creates one sized B x ceil(max_ctx/page_size). */
+int  gpt2_decode_init(GPT2* model, int B, int page_size, int max_ctx);
+/* one decode step for every sequence: tokens[b] (host) at position pos[b];
+ * tokens == NULL feeds back the previous step's greedy ids (device-resident).
+ * next_tokens (host, may be NULL) receives argmax(logits[b]). */
+int  gpt2_decode_step(GPT2* model, const int* tokens, int* next_tokens);
+/* the same, but enqueue only (no host sync; next ids stay on device) */
+int  gpt2_decode_step_async(GPT2* model, const int* tokens);
+/* free every sequence's pages and rewind positions to 0 */
+int  gpt2_decode_reset(GPT2* model);
+/* synthetic K/V for positions [0, ctx) of every sequence (benchmark prefill) */
+int  gpt2_decode_fill_random(GPT2* model, int ctx, unsigned long long seed);
+/* allocate the pages of positions [0, ctx) up front (no host work per step) */
+int  gpt2_decode_reserve(GPT2* model, int ctx);
+/* rewind/advance positions (pages kept) */
+int  gpt2_decode_set_positions(GPT2* model, const int* pos);
+/* capture the step into a hipGraph and replay it (1) or launch eagerly (0) */
+int  gpt2_decode_set_graph(GPT2* model, int enable);
+/* attention-kernel timing with HIP events around every layer's attention
+ * launch (forces eager launches while enabled); collect after each step */
+int    gpt2_decode_profile(GPT2* model, int enable);
+int    gpt2_decode_profile_collect(GPT2* model);
+double gpt2_decode_profile_read(GPT2* model, long* launches);
+/* device buffers: logits [B][V], next ids [B], positions [B] */
+float* gpt2_decode_logits(GPT2* model);
+int*   gpt2_decode_next(GPT2* model);
+int    gpt2_decode_positions(GPT2* model, int* host_pos);
+/* the per-GEMM split-K chosen for this model/batch (qkv, attproj, fc, fcproj) */
+int    gpt2_decode_splits(GPT2* model, int* splits4);
+/* algorithmic HBM bytes one step reads+writes at the current positions
+ * (SURVEY.md 8d formula) and the attention kernel's share of them */
+double gpt2_decode_step_bytes(GPT2* model, double* attention_bytes);
+void   gpt2_decode_free(GPT2* model);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

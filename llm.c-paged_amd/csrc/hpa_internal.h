@@ -1,0 +1,50 @@
+// hpa_internal.h -- shared by the HIP translation units of libpaged_hip.so.
+// gfx950 (CDNA4) only: wave64, fp32 MFMA, no CUDA compatibility layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "hip_paged_attn.h"
+
+// Returns a nonzero status after reporting; exits when HPA_FATAL=1
+// (cudaCheck convention, reference train_gpt2.cu:27-34).
+int hpa_fail(const char* file, int line, const char* what);
+hipStream_t hpa_stream();
+
+#define HPA_CHECK(call)                                                          \
+    do {                                                                         \
+        hipError_t e_ = (call);                                                  \
+        if (e_ != hipSuccess) return hpa_fail(__FILE__, __LINE__, hipGetErrorString(e_)); \
+    } while (0)
+
+#define HPA_REQUIRE(cond, msg)                                                   \
+    do {                                                                         \
+        if (!(cond)) return hpa_fail(__FILE__, __LINE__, msg);                   \
+    } while (0)
+
+// checks the launch that was just enqueued
+#define HPA_LAUNCH_CHECK() HPA_CHECK(hipGetLastError())
+
+namespace hpa {
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// GELU of the reference (paged_infer.c:243-251): 0.5 x (1 + tanh(sqrt(2/pi)(x + 0.044715 x^3)))
+__device__ __forceinline__ float gelu_ref(float x) {
+    // sqrtf(2.0f / M_PI) as the reference computes it: float(2/pi) then sqrtf
+    const float s = __uint_as_float(0x3F4C4229u);  // 0.79788452
+    float cube = __fmul_rn(__fmul_rn(__fmul_rn(0.044715f, x), x), x);
+    return __fmul_rn(__fmul_rn(0.5f, x), __fadd_rn(1.0f, tanhf(__fmul_rn(s, __fadd_rn(x, cube)))));
+}
+}  // namespace hpa

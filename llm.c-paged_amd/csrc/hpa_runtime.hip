@@ -1,0 +1,266 @@
+// hpa_runtime.hip -- device selection, stream, memory, events, page pool.
+#include <stdlib.h>
+#include <string.h>
+
+#include "hpa_internal.h"
+
+static hipStream_t g_default_stream = nullptr;
+static hipStream_t g_stream = nullptr;  // current (default or external)
+static int g_device = -1;
+static char g_last_error[512] = "";
+
+int hpa_fail(const char* file, int line, const char* what) {
+    snprintf(g_last_error, sizeof(g_last_error), "%s:%d %s", file, line, what);
+    fprintf(stderr, "[hpa] %s\n", g_last_error);
+    const char* f = getenv("HPA_FATAL");
+    if (f && f[0] == '1') exit(1);
+    return 1;
+}
+
+hipStream_t hpa_stream() { return g_stream; }
+
+extern "C" {
+
+const char* hpa_last_error(void) { return g_last_error; }
+
+int hpa_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int hpa_init(int device) {
+    int n = 0;
+    HPA_CHECK(hipGetDeviceCount(&n));
+    HPA_REQUIRE(n > 0, "no HIP device visible");
+    HPA_REQUIRE(device >= 0 && device < n, "device index out of range");
+    HPA_CHECK(hipSetDevice(device));
+    if (g_device != device || !g_default_stream) {
+        HPA_CHECK(hipStreamCreateWithFlags(&g_default_stream, hipStreamNonBlocking));
+        g_device = device;
+    }
+    if (!g_stream) g_stream = g_default_stream;
+    return 0;
+}
+
+int hpa_get_device(void) { return g_device; }
+
+int hpa_set_stream(void* s) {
+    g_stream = s ? (hipStream_t)s : g_default_stream;
+    return 0;
+}
+
+void* hpa_get_stream(void) { return (void*)g_stream; }
+
+int hpa_synchronize(void) {
+    HPA_CHECK(hipStreamSynchronize(g_stream));
+    return 0;
+}
+
+int hpa_device_synchronize(void) {
+    HPA_CHECK(hipDeviceSynchronize());
+    return 0;
+}
+
+void* hpa_malloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) {
+        hpa_fail(__FILE__, __LINE__, "hipMalloc failed");
+        return nullptr;
+    }
+    return p;
+}
+
+void* hpa_malloc_managed(size_t bytes) {
+    void* p = nullptr;
+    if (hipMallocManaged(&p, bytes ? bytes : 1, hipMemAttachGlobal) != hipSuccess) {
+        hpa_fail(__FILE__, __LINE__, "hipMallocManaged failed");
+        return nullptr;
+    }
+    return p;
+}
+
+void* hpa_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+        hpa_fail(__FILE__, __LINE__, "hipHostMalloc failed");
+        return nullptr;
+    }
+    return p;
+}
+
+int hpa_free(void* p) {
+    if (p) HPA_CHECK(hipFree(p));
+    return 0;
+}
+
+int hpa_host_free(void* p) {
+    if (p) HPA_CHECK(hipHostFree(p));
+    return 0;
+}
+
+int hpa_memcpy(void* dst, const void* src, size_t bytes) {
+    if (!bytes) return 0;
+    HPA_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, g_stream));
+    HPA_CHECK(hipStreamSynchronize(g_stream));
+    return 0;
+}
+
+int hpa_memcpy_async(void* dst, const void* src, size_t bytes) {
+    if (!bytes) return 0;
+    HPA_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, g_stream));
+    return 0;
+}
+
+int hpa_memset_async(void* dst, int value, size_t bytes) {
+    if (!bytes) return 0;
+    HPA_CHECK(hipMemsetAsync(dst, value, bytes, g_stream));
+    return 0;
+}
+
+int hpa_is_device_accessible(const void* p) {
+    if (!p) return 0;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    switch (a.type) {
+        case hipMemoryTypeDevice:
+        case hipMemoryTypeManaged:
+        case hipMemoryTypeUnified:
+            return 1;
+        case hipMemoryTypeHost:
+            return a.devicePointer != nullptr;  // pinned / registered host memory
+        default:
+            return 0;
+    }
+}
+
+void* hpa_event_create(void) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) {
+        hpa_fail(__FILE__, __LINE__, "hipEventCreate failed");
+        return nullptr;
+    }
+    return (void*)e;
+}
+
+int hpa_event_record(void* ev) {
+    HPA_CHECK(hipEventRecord((hipEvent_t)ev, g_stream));
+    return 0;
+}
+
+float hpa_event_elapsed_ms(void* start, void* stop) {
+    float ms = -1.f;
+    if (hipEventSynchronize((hipEvent_t)stop) != hipSuccess) return -1.f;
+    if (hipEventElapsedTime(&ms, (hipEvent_t)start, (hipEvent_t)stop) != hipSuccess) return -1.f;
+    return ms;
+}
+
+int hpa_event_destroy(void* ev) {
+    if (ev) HPA_CHECK(hipEventDestroy((hipEvent_t)ev));
+    return 0;
+}
+
+int hpa_device_info(char* name, int name_len, int* num_cus, size_t* total_mem) {
+    hipDeviceProp_t p;
+    int dev = g_device >= 0 ? g_device : 0;
+    HPA_CHECK(hipGetDeviceProperties(&p, dev));
+    if (name && name_len > 0) {
+        snprintf(name, name_len, "%s (%s)", p.name, p.gcnArchName);
+    }
+    if (num_cus) *num_cus = p.multiProcessorCount;
+    if (total_mem) *total_mem = p.totalGlobalMem;
+    return 0;
+}
+
+// ---------------- hipGraph capture ----------------
+int hpa_graph_begin(void) {
+    HPA_REQUIRE(g_stream, "hpa_init first");
+    HPA_CHECK(hipStreamBeginCapture(g_stream, hipStreamCaptureModeThreadLocal));
+    return 0;
+}
+
+void* hpa_graph_end(void) {
+    hipGraph_t graph = nullptr;
+    if (hipStreamEndCapture(g_stream, &graph) != hipSuccess || !graph) {
+        hpa_fail(__FILE__, __LINE__, "hipStreamEndCapture failed");
+        return nullptr;
+    }
+    hipGraphExec_t exec = nullptr;
+    hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (e != hipSuccess) {
+        hpa_fail(__FILE__, __LINE__, hipGetErrorString(e));
+        return nullptr;
+    }
+    return (void*)exec;
+}
+
+int hpa_graph_launch(void* exec) {
+    HPA_REQUIRE(exec, "null graph");
+    HPA_CHECK(hipGraphLaunch((hipGraphExec_t)exec, g_stream));
+    return 0;
+}
+
+int hpa_graph_destroy(void* exec) {
+    if (exec) HPA_CHECK(hipGraphExecDestroy((hipGraphExec_t)exec));
+    return 0;
+}
+
+// ---------------- page pool ----------------
+int hpa_pool_create(HpaKVPool* pool, int num_layers, int num_heads, int head_size, int page_size,
+                    int num_pages, int dtype, int managed) {
+    HPA_REQUIRE(pool, "pool is NULL");
+    memset(pool, 0, sizeof(*pool));
+    HPA_REQUIRE(dtype == HPA_F32, "only fp32 pages are supported in this build");
+    HPA_REQUIRE(head_size % 4 == 0, "head_size must be a multiple of 4");
+    HPA_REQUIRE(page_size > 0 && num_pages > 0 && num_layers > 0 && num_heads > 0, "bad pool shape");
+    pool->num_layers = num_layers;
+    pool->num_heads = num_heads;
+    pool->head_size = head_size;
+    pool->page_size = page_size;
+    pool->num_pages = num_pages;
+    pool->dtype = dtype;
+    pool->elem_bytes = 4;
+    pool->page_elems = (size_t)2 * num_heads * page_size * head_size;
+    pool->layer_elems = (size_t)num_pages * pool->page_elems;
+    pool->bytes = (size_t)num_layers * pool->layer_elems * pool->elem_bytes;
+    pool->managed = managed;
+    pool->base = managed ? hpa_malloc_managed(pool->bytes) : hpa_malloc(pool->bytes);
+    HPA_REQUIRE(pool->base, "page pool allocation failed");
+    // defined contents: a masked-out lane never multiplies garbage (NaN) pages
+    HPA_CHECK(hipMemsetAsync(pool->base, 0, pool->bytes, g_stream));
+    HPA_CHECK(hipStreamSynchronize(g_stream));
+    return 0;
+}
+
+void hpa_pool_destroy(HpaKVPool* pool) {
+    if (pool && pool->base) {
+        hpa_free(pool->base);
+        pool->base = nullptr;
+    }
+}
+
+void* hpa_pool_tile(const HpaKVPool* p, int layer, int page, int kv, int head) {
+    size_t tile = (size_t)p->page_size * p->head_size;
+    size_t e = (size_t)layer * p->layer_elems + (size_t)page * p->page_elems +
+               ((size_t)kv * p->num_heads + head) * tile;
+    return (char*)p->base + e * p->elem_bytes;
+}
+
+size_t hpa_pool_k_index(const HpaKVPool* p, int layer, int page, int head, int slot, int d) {
+    size_t tile = (size_t)p->page_size * p->head_size;
+    size_t base = (size_t)layer * p->layer_elems + (size_t)page * p->page_elems + (size_t)head * tile;
+    return base + ((size_t)(d >> 2) * p->page_size + slot) * 4 + (d & 3);
+}
+
+size_t hpa_pool_v_index(const HpaKVPool* p, int layer, int page, int head, int slot, int d) {
+    size_t tile = (size_t)p->page_size * p->head_size;
+    size_t base = (size_t)layer * p->layer_elems + (size_t)page * p->page_elems +
+                  ((size_t)p->num_heads + head) * tile;
+    return base + (size_t)slot * p->head_size + d;
+}
+
+}  // extern "C"

@@ -1,0 +1,964 @@
+/*
+ * paged_infer.c -- host side (C) of the MI355X paged-attention decode path:
+ *   - drop-in versions of the reference paged_infer.c functions
+ *     (mx60s/llm.c-paged paged_infer.c), computing on the GPU;
+ *   - the llm.c checkpoint loader and a seeded synthetic-weights generator;
+ *   - the decode engine (gpt2_decode_*): per-step orchestration of the
+ *     gfx950 kernels of hip_paged_attn.h over the HBM page pool, block
+ *     tables from the BlockManager, hipGraph replay.
+ * No Python and no CPU compute on the product path: every tensor op is a
+ * HIP kernel; the host only allocates pages and enqueues work.
+ */
+#include "paged_infer.h"
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "block_manager.h"
+#include "hip_paged_attn.h"
+
+#define PI_FATAL(...)                                         \
+    do {                                                      \
+        fprintf(stderr, "[paged_infer] " __VA_ARGS__);        \
+        fprintf(stderr, " (%s:%d)\n", __FILE__, __LINE__);    \
+        exit(1);                                              \
+    } while (0)
+#define PI_CHECK(call)                                                        \
+    do {                                                                      \
+        if ((call) != 0) PI_FATAL("%s failed: %s", #call, hpa_last_error());  \
+    } while (0)
+
+/* ------------------------------------------------------------------------ */
+/* device init + host/device staging for the drop-in functions              */
+/* ------------------------------------------------------------------------ */
+static void ensure_device(void) {
+    if (hpa_get_device() >= 0) return;
+    const char* e = getenv("HPA_DEVICE");
+    int dev = e ? atoi(e) : 0;
+    if (hpa_init(dev) != 0) PI_FATAL("no usable HIP device (the MI355X path has no CPU fallback)");
+}
+
+typedef struct {
+    void* d;
+    void* h;
+    size_t n;
+    int owned;
+} Stage;
+
+/* device-accessible view of p (copied in when copy_in) */
+static void* stage_in(Stage* s, const void* p, size_t n, int copy_in) {
+    s->h = (void*)p;
+    s->n = n;
+    s->owned = 0;
+    s->d = (void*)p;
+    if (!p || n == 0 || hpa_is_device_accessible(p)) return s->d;
+    s->d = hpa_malloc(n);
+    if (!s->d) PI_FATAL("staging allocation of %zu bytes failed", n);
+    if (copy_in) PI_CHECK(hpa_memcpy(s->d, p, n));
+    s->owned = 1;
+    return s->d;
+}
+static void stage_out(Stage* s) {
+    if (s->owned) PI_CHECK(hpa_memcpy(s->h, s->d, s->n));
+}
+static void stage_free(Stage* s) {
+    if (s->owned) hpa_free(s->d);
+    s->owned = 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* reference layer functions (paged_infer.c:24-302), on the GPU             */
+/* ------------------------------------------------------------------------ */
+void encoder_forward(float* out, int* inp, float* wte, float* wpe, int B, int T, int C) {
+    ensure_device();
+    Stage so, si, st, sp;
+    float* d_out = stage_in(&so, out, (size_t)B * T * C * 4, 0);
+    int* d_inp = stage_in(&si, inp, (size_t)B * T * 4, 1);
+    /* wte/wpe sizes are not part of the signature: assume device-resident
+     * model weights, or stage the rows the tokens touch when on the host */
+    float* d_wte = wte;
+    float* d_wpe = wpe;
+    if (!hpa_is_device_accessible(wte) || !hpa_is_device_accessible(wpe)) {
+        int* h = (int*)malloc((size_t)B * T * sizeof(int));
+        if (hpa_is_device_accessible(inp)) PI_CHECK(hpa_memcpy(h, inp, (size_t)B * T * 4));
+        else memcpy(h, inp, (size_t)B * T * 4);
+        int mx = 0;
+        for (int i = 0; i < B * T; i++) mx = h[i] > mx ? h[i] : mx;
+        free(h);
+        d_wte = stage_in(&st, wte, (size_t)(mx + 1) * C * 4, 1);
+        d_wpe = stage_in(&sp, wpe, (size_t)T * C * 4, 1);
+    } else {
+        st.owned = sp.owned = 0;
+    }
+    PI_CHECK(hpa_ref_encoder(d_out, d_inp, d_wte, d_wpe, B, T, C, 0));
+    PI_CHECK(hpa_synchronize());
+    stage_out(&so);
+    stage_free(&so); stage_free(&si); stage_free(&st); stage_free(&sp);
+}
+
+void layernorm_forward(float* out, float* mean, float* rstd, float* inp, float* weight, float* bias,
+                       int B, int T, int C) {
+    ensure_device();
+    size_t N = (size_t)B * T;
+    Stage so, sm, sr, si, sw, sb;
+    float* d_out = stage_in(&so, out, N * C * 4, 0);
+    float* d_mean = stage_in(&sm, mean, N * 4, 0);
+    float* d_rstd = stage_in(&sr, rstd, N * 4, 0);
+    float* d_inp = stage_in(&si, inp, N * C * 4, 1);
+    float* d_w = stage_in(&sw, weight, (size_t)C * 4, 1);
+    float* d_b = stage_in(&sb, bias, (size_t)C * 4, 1);
+    PI_CHECK(hpa_ref_layernorm(d_out, d_mean, d_rstd, d_inp, d_w, d_b, (int)N, C));
+    PI_CHECK(hpa_synchronize());
+    stage_out(&so); stage_out(&sm); stage_out(&sr);
+    stage_free(&so); stage_free(&sm); stage_free(&sr); stage_free(&si); stage_free(&sw);
+    stage_free(&sb);
+}
+
+static void matmul_any(float* out, float* inp, float* weight, float* bias, int B, int T, int C, int OC,
+                       int cached) {
+    ensure_device();
+    size_t N = (size_t)B * T;
+    Stage so, si, sw, sb;
+    /* matmul_cached leaves K/V of the earlier rows untouched: copy out in */
+    float* d_out = stage_in(&so, out, N * OC * 4, cached);
+    float* d_inp = stage_in(&si, inp, N * C * 4, 1);
+    float* d_w = stage_in(&sw, weight, (size_t)OC * C * 4, 1);
+    float* d_b = stage_in(&sb, bias, (size_t)OC * 4, 1);
+    PI_CHECK(hpa_ref_matmul(d_out, d_inp, d_w, d_b, B, T, C, OC, cached));
+    PI_CHECK(hpa_synchronize());
+    stage_out(&so);
+    stage_free(&so); stage_free(&si); stage_free(&sw); stage_free(&sb);
+}
+
+void matmul_forward(float* out, float* inp, float* weight, float* bias, int B, int T, int C, int OC) {
+    matmul_any(out, inp, weight, bias, B, T, C, OC, 0);
+}
+
+void matmul_cached(float* out, float* inp, float* weight, float* bias, int B, int T, int C, int OC) {
+    matmul_any(out, inp, weight, bias, B, T, C, OC, 1);
+}
+
+void attention_paged_bs(float* out, float* preatt, float* att, float* inp, float** key_blocks,
+                        float** value_blocks, int B, int T, int C, int NH, int offset,
+                        int block_size) {
+    ensure_device();
+    if (B <= 0 || T <= 0 || NH <= 0 || C % NH || block_size <= 0 || offset < 0)
+        PI_FATAL("attention_paged: bad shape");
+    int npages = (offset + T + block_size - 1) / block_size;
+    size_t page_bytes = (size_t)block_size * C * 4;
+    Stage so, sp, sa, si;
+    float* d_out = stage_in(&so, out, (size_t)B * T * C * 4, 0);
+    /* preatt rows are written only up to t (:202): keep the caller's tail */
+    float* d_pre = stage_in(&sp, preatt, (size_t)B * NH * T * T * 4, 1);
+    float* d_att = stage_in(&sa, att, (size_t)B * NH * T * T * 4, 0);
+    float* d_inp = stage_in(&si, inp, (size_t)B * T * 3 * C * 4, 1);
+    Stage* pk = (Stage*)calloc((size_t)2 * npages, sizeof(Stage));
+    float** hptr = (float**)malloc(sizeof(float*) * 2 * npages);
+    for (int i = 0; i < npages; i++) {
+        hptr[i] = stage_in(&pk[i], key_blocks[i], page_bytes, 1);
+        hptr[npages + i] = stage_in(&pk[npages + i], value_blocks[i], page_bytes, 1);
+    }
+    float** d_ptr = (float**)hpa_malloc(sizeof(float*) * 2 * npages);
+    if (!d_ptr) PI_FATAL("attention_paged: allocation failed");
+    PI_CHECK(hpa_memcpy(d_ptr, hptr, sizeof(float*) * 2 * npages));
+    PI_CHECK(hpa_ref_attention_paged(d_out, d_pre, d_att, d_inp, d_ptr, d_ptr + npages, B, T, C, NH,
+                                     offset, block_size));
+    PI_CHECK(hpa_synchronize());
+    stage_out(&so); stage_out(&sp); stage_out(&sa);
+    stage_free(&so); stage_free(&sp); stage_free(&sa); stage_free(&si);
+    for (int i = 0; i < 2 * npages; i++) stage_free(&pk[i]);
+    free(pk);
+    free(hptr);
+    hpa_free(d_ptr);
+}
+
+/* paged_infer.c:163-240 (pages of BLOCK_SIZE tokens, as the reference) */
+void attention_paged(float* out, float* preatt, float* att, float* inp, float** key_blocks,
+                     float** value_blocks, int B, int T, int C, int NH, int offset) {
+    attention_paged_bs(out, preatt, att, inp, key_blocks, value_blocks, B, T, C, NH, offset,
+                       BLOCK_SIZE);
+}
+
+void gelu_forward(float* out, float* inp, int N) {
+    ensure_device();
+    Stage so, si;
+    float* d_out = stage_in(&so, out, (size_t)N * 4, 0);
+    float* d_inp = stage_in(&si, inp, (size_t)N * 4, 1);
+    PI_CHECK(hpa_ref_gelu(d_out, d_inp, N));
+    PI_CHECK(hpa_synchronize());
+    stage_out(&so);
+    stage_free(&so); stage_free(&si);
+}
+
+void residual_forward(float* out, float* inp1, float* inp2, int N) {
+    ensure_device();
+    Stage so, sa, sb;
+    float* d_out = stage_in(&so, out, (size_t)N * 4, 0);
+    float* d_a = stage_in(&sa, inp1, (size_t)N * 4, 1);
+    float* d_b = stage_in(&sb, inp2, (size_t)N * 4, 1);
+    PI_CHECK(hpa_ref_residual(d_out, d_a, d_b, N));
+    PI_CHECK(hpa_synchronize());
+    stage_out(&so);
+    stage_free(&so); stage_free(&sa); stage_free(&sb);
+}
+
+void softmax_forward(float* probs, float* logits, int B, int T, int V) {
+    ensure_device();
+    size_t n = (size_t)B * T * V * 4;
+    Stage sp, sl;
+    float* d_p = stage_in(&sp, probs, n, 0);
+    float* d_l = stage_in(&sl, logits, n, 1);
+    PI_CHECK(hpa_ref_softmax(d_p, d_l, B * T, V));
+    PI_CHECK(hpa_synchronize());
+    stage_out(&sp);
+    stage_free(&sp); stage_free(&sl);
+}
+
+/* add_to_cache, paged_infer.c:505-573.  Corrected semantics:
+ * sequence b appends to prompt b's pages (the reference hard-codes prompt 0
+ * and overwrites the same slots for every b), spilling into new pages when
+ * the current one fills (the reference assumes it never does, :542-545).
+ * Pages are token-major [block_size][C] as in the reference. */
+void add_to_cache(BlockManager* manager, float* qkv, int B, int T, int C,
+                  int how_many_tokens_to_copy_from_the_end_of_sequence) {
+    ensure_device();
+    int n = how_many_tokens_to_copy_from_the_end_of_sequence;
+    if (n < 0 || n > T) PI_FATAL("add_to_cache: bad token count");
+    int bs = manager->block_size;
+    for (int b = 0; b < B; b++) {
+        int t = T - n;
+        while (t < T) {
+            KVBlock* cur = get_current_block(manager, b);
+            if (!cur || cur->filled >= bs) {
+                cur = request_block(manager, b);
+                if (!cur) PI_FATAL("add_to_cache: no page available for prompt %d", b);
+            } else {
+                cur->lru_counter = ++manager->lru_epoch; /* :524 */
+            }
+            int take = bs - cur->filled;
+            if (take > T - t) take = T - t;
+            for (int j = 0; j < take; j++) {
+                const float* k = qkv + (size_t)b * T * 3 * C + (size_t)(t + j) * 3 * C + C;
+                const float* v = k + C;
+                PI_CHECK(hpa_memcpy(cur->keys + (size_t)(cur->filled + j) * C, k, (size_t)C * 4));
+                PI_CHECK(hpa_memcpy(cur->values + (size_t)(cur->filled + j) * C, v, (size_t)C * 4));
+            }
+            cur->filled += take;
+            t += take;
+        }
+    }
+}
+
+/* paged_infer.c:826-835 */
+unsigned int random_u32(unsigned long long* state) {
+    *state ^= *state >> 12;
+    *state ^= *state << 25;
+    *state ^= *state >> 27;
+    return (*state * 0x2545F4914F6CDD1Dull) >> 32;
+}
+float random_f32(unsigned long long* state) { return (random_u32(state) >> 8) / 16777216.0f; }
+
+/* paged_infer.c:837-848 */
+int sample_mult(float* probabilities, int n, float coin) {
+    float cdf = 0.0f;
+    for (int i = 0; i < n; i++) {
+        cdf += probabilities[i];
+        if (coin < cdf) return i;
+    }
+    return n - 1;
+}
+
+/* paged_infer.c:937-951 (host, strict > so the lowest index wins) */
+int* generate_tokens_from_logits(float* probs, int B, int T, int V) {
+    int* tokens = (int*)malloc((size_t)B * T * sizeof(int));
+    for (int i = 0; i < B * T; i++) {
+        int mi = 0;
+        float mv = probs[(size_t)i * V];
+        for (int v = 1; v < V; v++)
+            if (probs[(size_t)i * V + v] > mv) { mv = probs[(size_t)i * V + v]; mi = v; }
+        tokens[i] = mi;
+    }
+    return tokens;
+}
+
+/* ------------------------------------------------------------------------ */
+/* parameters: checkpoint loader, synthetic weights, writer                 */
+/* ------------------------------------------------------------------------ */
+static void param_sizes(GPT2Config c, size_t* s) {
+    size_t V = c.vocab_size, maxT = c.max_seq_len, L = c.num_layers, C = c.channels;
+    s[0] = V * C; s[1] = maxT * C; s[2] = L * C; s[3] = L * C;
+    s[4] = L * 3 * C * C; s[5] = L * 3 * C; s[6] = L * C * C; s[7] = L * C;
+    s[8] = L * C; s[9] = L * C; s[10] = L * 4 * C * C; s[11] = L * 4 * C;
+    s[12] = L * C * 4 * C; s[13] = L * C; s[14] = C; s[15] = C;
+}
+
+size_t gpt2_num_parameters(GPT2Config c) {
+    size_t s[NUM_PARAMETER_TENSORS], n = 0;
+    param_sizes(c, s);
+    for (int i = 0; i < NUM_PARAMETER_TENSORS; i++) n += s[i];
+    return n;
+}
+
+static void model_zero(GPT2* m) {
+    memset(m, 0, sizeof(*m));
+    m->mean_loss = -1.0f;
+}
+
+int gpt2_build_from_params(GPT2* model, GPT2Config c, const float* host_params) {
+    ensure_device();
+    model_zero(model);
+    if (c.channels <= 0 || c.num_heads <= 0 || c.channels % c.num_heads || c.num_layers <= 0 ||
+        c.vocab_size <= 0 || c.max_seq_len <= 0) {
+        fprintf(stderr, "[paged_infer] bad GPT-2 config\n");
+        return 1;
+    }
+    model->config = c;
+    param_sizes(c, model->param_sizes);
+    model->num_parameters = gpt2_num_parameters(c);
+    model->params_memory = (float*)hpa_malloc(model->num_parameters * sizeof(float));
+    if (!model->params_memory) return 1;
+    if (hpa_memcpy(model->params_memory, host_params, model->num_parameters * sizeof(float))) return 1;
+    float** ptrs[NUM_PARAMETER_TENSORS] = {
+        &model->params.wte, &model->params.wpe, &model->params.ln1w, &model->params.ln1b,
+        &model->params.qkvw, &model->params.qkvb, &model->params.attprojw, &model->params.attprojb,
+        &model->params.ln2w, &model->params.ln2b, &model->params.fcw, &model->params.fcb,
+        &model->params.fcprojw, &model->params.fcprojb, &model->params.lnfw, &model->params.lnfb};
+    float* it = model->params_memory;
+    for (int i = 0; i < NUM_PARAMETER_TENSORS; i++) {
+        *ptrs[i] = it;
+        it += model->param_sizes[i];
+    }
+    return 0;
+}
+
+/* paged_infer.c:436-502: 256 x int32 header, magic 20240326, version 1 (fp32) */
+void gpt2_build_from_checkpoint(GPT2* model, const char* checkpoint_path) {
+    FILE* f = fopen(checkpoint_path, "rb");
+    if (!f) { printf("Error opening model file\n"); exit(1); }
+    int hdr[256];
+    if (fread(hdr, sizeof(int), 256, f) != 256) { printf("Bad model file\n"); exit(1); }
+    if (hdr[0] != 20240326) { printf("Bad magic model file"); exit(1); }
+    if (hdr[1] != 1) { printf("Bad version in model file"); exit(1); }
+    GPT2Config c;
+    c.max_seq_len = hdr[2];
+    c.vocab_size = hdr[3];
+    c.num_layers = hdr[4];
+    c.num_heads = hdr[5];
+    c.channels = hdr[6];
+    size_t n = gpt2_num_parameters(c);
+    float* host = (float*)malloc(n * sizeof(float));
+    if (!host) { printf("Out of host memory for parameters\n"); exit(1); }
+    if (fread(host, sizeof(float), n, f) != n) { printf("Truncated model file\n"); exit(1); }
+    fclose(f);
+    if (gpt2_build_from_params(model, c, host) != 0) { printf("Parameter upload failed\n"); exit(1); }
+    free(host);
+}
+
+int gpt2_synthetic_params(GPT2Config c, unsigned long long seed, float* p) {
+    size_t s[NUM_PARAMETER_TENSORS];
+    param_sizes(c, s);
+    unsigned long long st = seed ? seed : 1337;
+    const float a = 0.02f * 1.7320508f; /* U(-a, a): std 0.02 */
+    size_t o = 0;
+    for (int t = 0; t < NUM_PARAMETER_TENSORS; t++) {
+        for (size_t i = 0; i < s[t]; i++) {
+            float u = 2.0f * random_f32(&st) - 1.0f; /* U(-1, 1) */
+            float v;
+            switch (t) {
+                case 2: case 8: case 14: v = 1.0f + 0.1f * u; break;  /* LN weights */
+                case 3: case 9: case 15: v = 0.05f * u; break;        /* LN biases */
+                case 5: case 7: case 11: case 13: v = 0.02f * u; break; /* linear biases */
+                case 1: v = 0.01f * 1.7320508f * u; break;             /* wpe */
+                default: v = a * u; break;
+            }
+            p[o + i] = v;
+        }
+        o += s[t];
+    }
+    return 0;
+}
+
+int gpt2_build_synthetic(GPT2* model, GPT2Config c, unsigned long long seed) {
+    size_t n = gpt2_num_parameters(c);
+    float* host = (float*)malloc(n * sizeof(float));
+    if (!host) return 1;
+    gpt2_synthetic_params(c, seed, host);
+    int rc = gpt2_build_from_params(model, c, host);
+    free(host);
+    return rc;
+}
+
+int gpt2_write_checkpoint(const char* path, GPT2Config c, const float* host_params) {
+    FILE* f = fopen(path, "wb");
+    if (!f) return 1;
+    int hdr[256];
+    memset(hdr, 0, sizeof(hdr));
+    hdr[0] = 20240326; hdr[1] = 1; hdr[2] = c.max_seq_len; hdr[3] = c.vocab_size;
+    hdr[4] = c.num_layers; hdr[5] = c.num_heads; hdr[6] = c.channels;
+    size_t n = gpt2_num_parameters(c);
+    int ok = fwrite(hdr, sizeof(int), 256, f) == 256 && fwrite(host_params, sizeof(float), n, f) == n;
+    fclose(f);
+    return ok ? 0 : 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* decode engine                                                            */
+/* ------------------------------------------------------------------------ */
+struct GPT2Decode {
+    int B, P, max_ctx, max_pages;
+    HpaKVPool pool;
+    BlockManager* bm;
+    int own_bm;
+    int bt_stride;
+    int* d_bt;        /* [max_prompts][bt_stride] device mirror of bm->block_table */
+    int* d_pos;       /* [B] */
+    int* d_tokens;    /* [B] */
+    int* d_next;      /* [B] */
+    int* h_pos;       /* host mirror of d_pos */
+    int* h_stage;     /* pinned staging: tokens / next */
+    int* h_bt_stage;  /* pinned staging for block-table rows */
+    float *d_res, *d_res2, *d_ln, *d_q, *d_att, *d_fch, *d_part, *d_logits;
+    int split[4];     /* qkv, attproj, fc, fcproj */
+    int use_graph;
+    void* graph;
+    int graph_valid;
+    /* per-layer HIP events around the attention launch (eager profiling) */
+    void** prof_ev;   /* [L][2] or NULL */
+    double prof_ms;   /* accumulated attention kernel time */
+    long prof_launches;
+};
+
+/* the pool view backend: page payload pointers are layer-0 tiles in HBM */
+static void* pool_view_alloc(void* ctx, int page, int kv, size_t bytes) {
+    (void)bytes;
+    HpaKVPool* pool = (HpaKVPool*)ctx;
+    if (page < 0 || page >= pool->num_pages) return NULL;
+    return hpa_pool_tile(pool, 0, page, kv, 0);
+}
+static void pool_view_release(void* ctx, int page, int kv, void* p) {
+    (void)ctx; (void)page; (void)kv; (void)p;
+}
+
+static void dec_prof_free(GPT2Decode* d, int L) {
+    if (!d->prof_ev) return;
+    for (int i = 0; i < 2 * L; i++) hpa_event_destroy(d->prof_ev[i]);
+    free(d->prof_ev);
+    d->prof_ev = NULL;
+}
+
+static void dec_free(GPT2Decode* d) {
+    if (!d) return;
+    dec_prof_free(d, d->pool.num_layers);
+    if (d->graph) hpa_graph_destroy(d->graph);
+    hpa_pool_destroy(&d->pool);
+    hpa_free(d->d_bt); hpa_free(d->d_pos); hpa_free(d->d_tokens); hpa_free(d->d_next);
+    hpa_free(d->d_res); hpa_free(d->d_res2); hpa_free(d->d_ln); hpa_free(d->d_q);
+    hpa_free(d->d_att); hpa_free(d->d_fch); hpa_free(d->d_part); hpa_free(d->d_logits);
+    hpa_host_free(d->h_stage);
+    hpa_host_free(d->h_bt_stage);
+    free(d->h_pos);
+    if (d->own_bm) destroy_block_manager(d->bm);
+    free(d);
+}
+
+void gpt2_decode_free(GPT2* model) {
+    if (model && model->decode) {
+        hpa_synchronize();
+        dec_free(model->decode);
+        model->decode = NULL;
+    }
+}
+
+int gpt2_decode_init(GPT2* model, int B, int page_size, int max_ctx) {
+    ensure_device();
+    if (!model->params_memory) { fprintf(stderr, "[paged_infer] model not built\n"); return 1; }
+    GPT2Config c = model->config;
+    if (c.channels != c.num_heads * 64) {
+        fprintf(stderr, "[paged_infer] decode engine needs head_size 64 (C = 64*NH)\n");
+        return 1;
+    }
+    if (B <= 0 || max_ctx <= 0 || max_ctx > c.max_seq_len) {
+        fprintf(stderr, "[paged_infer] bad batch / context (max_ctx <= max_seq_len)\n");
+        return 1;
+    }
+    gpt2_decode_free(model);
+    GPT2Decode* d = (GPT2Decode*)calloc(1, sizeof(GPT2Decode));
+    if (model->manager) {
+        d->bm = model->manager;
+        page_size = d->bm->block_size;
+        if (d->bm->max_prompts < B || d->bm->C != c.channels) {
+            fprintf(stderr, "[paged_infer] model->manager too small for this batch\n");
+            free(d);
+            return 1;
+        }
+    }
+    if (page_size != 8 && page_size != 16 && page_size != 32 && page_size != 64) {
+        fprintf(stderr, "[paged_infer] page size must be 8, 16, 32 or 64\n");
+        free(d);
+        return 1;
+    }
+    d->B = B;
+    d->P = page_size;
+    d->max_ctx = max_ctx;
+    d->max_pages = (max_ctx + page_size - 1) / page_size;
+    int num_pages;
+    if (model->manager) {
+        num_pages = d->bm->max_blocks;
+    } else {
+        num_pages = B * d->max_pages;
+        d->bm = create_block_manager_ex(c.channels, B, num_pages, page_size, d->max_pages);
+        if (!d->bm) { free(d); return 1; }
+        d->own_bm = 1;
+    }
+    if (d->bm->max_blocks_per_prompt < d->max_pages) {
+        fprintf(stderr, "[paged_infer] manager's per-prompt page list shorter than max_ctx\n");
+        if (d->own_bm) destroy_block_manager(d->bm);
+        free(d);
+        return 1;
+    }
+    if (hpa_pool_create(&d->pool, c.num_layers, c.num_heads, 64, page_size, num_pages, HPA_F32, 0)) {
+        if (d->own_bm) destroy_block_manager(d->bm);
+        free(d);
+        return 1;
+    }
+    /* pages of this manager are views into the pool from now on */
+    for (int p = 0; p < d->bm->max_prompts; p++)
+        if (d->bm->prompt_block_count[p]) free_blocks_for_prompt(d->bm, p);
+    BMPageBackend be = {pool_view_alloc, pool_view_release, &d->pool};
+    bm_set_backend(d->bm, &be);
+    d->bt_stride = d->bm->max_blocks_per_prompt;
+    int C = c.channels, V = c.vocab_size;
+    size_t btn = (size_t)d->bm->max_prompts * d->bt_stride;
+    d->d_bt = (int*)hpa_malloc(btn * sizeof(int));
+    d->d_pos = (int*)hpa_malloc(B * sizeof(int));
+    d->d_tokens = (int*)hpa_malloc(B * sizeof(int));
+    d->d_next = (int*)hpa_malloc(B * sizeof(int));
+    d->h_pos = (int*)calloc(B, sizeof(int));
+    d->h_stage = (int*)hpa_host_alloc(2 * (size_t)B * sizeof(int));
+    d->h_bt_stage = (int*)hpa_host_alloc(btn * sizeof(int));
+    d->split[0] = hpa_gemm_pick_splitk(B, 3 * C, C);
+    d->split[1] = hpa_gemm_pick_splitk(B, C, C);
+    d->split[2] = hpa_gemm_pick_splitk(B, 4 * C, C);
+    d->split[3] = hpa_gemm_pick_splitk(B, C, 4 * C);
+    size_t part = 0, t;
+    t = (size_t)d->split[0] * B * 3 * C; part = t > part ? t : part;
+    t = (size_t)d->split[1] * B * C; part = t > part ? t : part;
+    t = (size_t)d->split[2] * B * 4 * C; part = t > part ? t : part;
+    t = (size_t)d->split[3] * B * C; part = t > part ? t : part;
+    d->d_res = (float*)hpa_malloc((size_t)B * C * 4);
+    d->d_res2 = (float*)hpa_malloc((size_t)B * C * 4);
+    d->d_ln = (float*)hpa_malloc((size_t)B * C * 4);
+    d->d_q = (float*)hpa_malloc((size_t)B * C * 4);
+    d->d_att = (float*)hpa_malloc((size_t)B * C * 4);
+    d->d_fch = (float*)hpa_malloc((size_t)B * 4 * C * 4);
+    d->d_part = (float*)hpa_malloc(part * 4);
+    d->d_logits = (float*)hpa_malloc((size_t)B * V * 4);
+    if (!d->d_bt || !d->d_pos || !d->d_tokens || !d->d_next || !d->h_pos || !d->h_stage ||
+        !d->h_bt_stage || !d->d_res || !d->d_res2 || !d->d_ln || !d->d_q || !d->d_att ||
+        !d->d_fch || !d->d_part || !d->d_logits) {
+        dec_free(d);
+        return 1;
+    }
+    for (size_t i = 0; i < btn; i++) d->h_bt_stage[i] = -1;
+    if (hpa_memcpy(d->d_bt, d->h_bt_stage, btn * sizeof(int)) ||
+        hpa_memset_async(d->d_pos, 0, B * sizeof(int)) ||
+        hpa_memset_async(d->d_tokens, 0, B * sizeof(int)) || hpa_synchronize()) {
+        dec_free(d);
+        return 1;
+    }
+    bm_clear_dirty(d->bm);
+    model->decode = d;
+    return 0;
+}
+
+/* upload the block-table rows the manager changed since the last upload */
+static int dec_sync_block_table(GPT2Decode* d) {
+    BlockManager* m = d->bm;
+    if (m->dirty_hi < m->dirty_lo) return 0;
+    size_t lo = (size_t)m->dirty_lo * d->bt_stride;
+    size_t n = (size_t)(m->dirty_hi - m->dirty_lo + 1) * d->bt_stride;
+    /* the staging copy must not be overwritten while a previous async copy
+     * may still read it: wait for the stream's earlier work first */
+    if (hpa_synchronize()) return 1;
+    memcpy(d->h_bt_stage + lo, m->block_table + lo, n * sizeof(int));
+    if (hpa_memcpy_async(d->d_bt + lo, d->h_bt_stage + lo, n * sizeof(int))) return 1;
+    bm_clear_dirty(m);
+    return 0;
+}
+
+/* make sure every sequence owns the page its next token lands in */
+static int dec_ensure_pages(GPT2Decode* d) {
+    for (int b = 0; b < d->B; b++) {
+        int p = d->h_pos[b];
+        if (p >= d->max_ctx) {
+            fprintf(stderr, "[paged_infer] sequence %d is full (%d tokens)\n", b, p);
+            return 1;
+        }
+        int need = p / d->P + 1;
+        while (d->bm->prompt_block_count[b] < need) {
+            KVBlock* blk = request_block(d->bm, b);
+            if (!blk) return 1;
+            int ev = d->bm->last_evicted_prompt;
+            if (ev >= 0 && ev < d->B && ev != b) {
+                /* the reference policy evicted a whole live sequence: it restarts */
+                fprintf(stderr, "[paged_infer] page pool full: sequence %d evicted (LRU)\n", ev);
+                d->h_pos[ev] = 0;
+                if (hpa_memcpy_async(d->d_pos + ev, &d->h_pos[ev], sizeof(int))) return 1;
+                if (hpa_synchronize()) return 1;
+            }
+        }
+    }
+    return 0;
+}
+
+static int dec_launch(GPT2* model) {
+    GPT2Decode* d = model->decode;
+    const GPT2Config c = model->config;
+    const int B = d->B, C = c.channels, L = c.num_layers, V = c.vocab_size;
+    const ParameterTensors* w = &model->params;
+    int rc = 0;
+    rc |= hpa_embed_ln(d->d_tokens, d->d_pos, w->wte, w->wpe, w->ln1w, w->ln1b, d->d_res, d->d_ln, B, C);
+    for (int l = 0; l < L && !rc; l++) {
+        const size_t lc = (size_t)l * C;
+        /* QKV + KV append into the page of pos[b] (add_to_cache fused) */
+        int s = d->split[0];
+        rc |= hpa_gemm_f32(d->d_ln, C, w->qkvw + lc * 3 * C, w->qkvb + 3 * lc, d->d_part, 3 * C, B,
+                           3 * C, C, s, s > 1 ? HPA_EPI_PARTIAL : HPA_EPI_BIAS);
+        rc |= hpa_qkv_append(d->d_part, s, s > 1 ? w->qkvb + 3 * lc : NULL, d->d_q, &d->pool, l,
+                             d->d_bt, d->bt_stride, d->d_pos, B, C);
+        /* paged attention over 0..pos[b] */
+        if (d->prof_ev) rc |= hpa_event_record(d->prof_ev[2 * l]);
+        rc |= hpa_paged_attention_decode(d->d_q, &d->pool, l, d->d_bt, d->bt_stride, d->d_pos,
+                                         d->d_att, B);
+        if (d->prof_ev) rc |= hpa_event_record(d->prof_ev[2 * l + 1]);
+        /* attn proj + residual + LN2 */
+        s = d->split[1];
+        rc |= hpa_gemm_f32(d->d_att, C, w->attprojw + lc * C, w->attprojb + lc, d->d_part, C, B, C, C,
+                           s, s > 1 ? HPA_EPI_PARTIAL : HPA_EPI_BIAS);
+        rc |= hpa_residual_ln(d->d_part, s, s > 1 ? w->attprojb + lc : NULL, d->d_res, d->d_res2,
+                              w->ln2w + lc, w->ln2b + lc, d->d_ln, B, C);
+        /* fc + GELU */
+        s = d->split[2];
+        if (s > 1) {
+            rc |= hpa_gemm_f32(d->d_ln, C, w->fcw + lc * 4 * C, NULL, d->d_part, 4 * C, B, 4 * C, C,
+                               s, HPA_EPI_PARTIAL);
+            rc |= hpa_bias_gelu(d->d_part, s, w->fcb + 4 * lc, d->d_fch, B, 4 * C);
+        } else {
+            rc |= hpa_gemm_f32(d->d_ln, C, w->fcw + lc * 4 * C, w->fcb + 4 * lc, d->d_fch, 4 * C, B,
+                               4 * C, C, 1, HPA_EPI_BIAS_GELU);
+        }
+        /* fc proj + residual + next LN (LN1 of l+1, or the final LN) */
+        s = d->split[3];
+        rc |= hpa_gemm_f32(d->d_fch, 4 * C, w->fcprojw + lc * 4 * C, w->fcprojb + lc, d->d_part, C, B,
+                           C, 4 * C, s, s > 1 ? HPA_EPI_PARTIAL : HPA_EPI_BIAS);
+        const float* nw = l + 1 < L ? w->ln1w + lc + C : w->lnfw;
+        const float* nb = l + 1 < L ? w->ln1b + lc + C : w->lnfb;
+        rc |= hpa_residual_ln(d->d_part, s, s > 1 ? w->fcprojb + lc : NULL, d->d_res2, d->d_res, nw,
+                              nb, d->d_ln, B, C);
+    }
+    /* logits = lnf . wte^T (paged_infer.c:727), greedy id, advance positions */
+    rc |= hpa_gemm_f32(d->d_ln, C, w->wte, NULL, d->d_logits, V, B, V, C, 1, HPA_EPI_BIAS);
+    rc |= hpa_argmax_advance(d->d_logits, B, V, d->d_next, d->d_tokens, d->d_pos);
+    return rc;
+}
+
+int gpt2_decode_set_graph(GPT2* model, int enable) {
+    GPT2Decode* d = model->decode;
+    if (!d) return 1;
+    d->use_graph = enable;
+    if (!enable && d->graph) {
+        hpa_graph_destroy(d->graph);
+        d->graph = NULL;
+    }
+    return 0;
+}
+
+static int dec_enqueue(GPT2* model, const int* tokens) {
+    GPT2Decode* d = model->decode;
+    if (!d) { fprintf(stderr, "[paged_infer] gpt2_decode_init first\n"); return 1; }
+    if (tokens) {
+        for (int b = 0; b < d->B; b++)
+            if (tokens[b] < 0 || tokens[b] >= model->config.vocab_size) {
+                fprintf(stderr, "[paged_infer] token out of range\n"); /* :591-596 */
+                return 1;
+            }
+    }
+    if (dec_ensure_pages(d)) return 1;
+    if (dec_sync_block_table(d)) return 1;
+    if (tokens) {
+        if (hpa_synchronize()) return 1; /* staging buffer reuse */
+        memcpy(d->h_stage, tokens, d->B * sizeof(int));
+        if (hpa_memcpy_async(d->d_tokens, d->h_stage, d->B * sizeof(int))) return 1;
+    }
+    if (d->use_graph) {
+        if (!d->graph) {
+            if (hpa_graph_begin()) return 1;
+            int rc = dec_launch(model);
+            void* g = hpa_graph_end();
+            if (rc || !g) return 1;
+            d->graph = g;
+        }
+        if (hpa_graph_launch(d->graph)) return 1;
+    } else {
+        if (dec_launch(model)) return 1;
+    }
+    for (int b = 0; b < d->B; b++) d->h_pos[b]++;
+    return 0;
+}
+
+int gpt2_decode_step_async(GPT2* model, const int* tokens) { return dec_enqueue(model, tokens); }
+
+int gpt2_decode_step(GPT2* model, const int* tokens, int* next_tokens) {
+    if (dec_enqueue(model, tokens)) return 1;
+    GPT2Decode* d = model->decode;
+    if (next_tokens) {
+        if (hpa_memcpy(d->h_stage + d->B, d->d_next, d->B * sizeof(int))) return 1;
+        memcpy(next_tokens, d->h_stage + d->B, d->B * sizeof(int));
+    }
+    return 0;
+}
+
+int gpt2_decode_reset(GPT2* model) {
+    GPT2Decode* d = model->decode;
+    if (!d) return 1;
+    if (hpa_synchronize()) return 1;
+    for (int b = 0; b < d->B; b++) {
+        if (d->bm->prompt_block_count[b]) free_blocks_for_prompt(d->bm, b);
+        d->h_pos[b] = 0;
+    }
+    if (hpa_memset_async(d->d_pos, 0, d->B * sizeof(int))) return 1;
+    return dec_sync_block_table(d) || hpa_synchronize();
+}
+
+int gpt2_decode_fill_random(GPT2* model, int ctx, unsigned long long seed) {
+    GPT2Decode* d = model->decode;
+    if (!d) return 1;
+    if (ctx < 0 || ctx >= d->max_ctx) {
+        fprintf(stderr, "[paged_infer] fill_random: ctx must be < max_ctx\n");
+        return 1;
+    }
+    if (gpt2_decode_reset(model)) return 1;
+    for (int b = 0; b < d->B; b++) {
+        int need = (ctx + d->P - 1) / d->P;
+        while (d->bm->prompt_block_count[b] < need)
+            if (!request_block(d->bm, b)) return 1;
+        d->h_pos[b] = ctx;
+    }
+    if (dec_sync_block_table(d)) return 1;
+    if (hpa_pool_fill_random(&d->pool, d->d_bt, d->bt_stride, d->B, ctx, seed)) return 1;
+    if (hpa_memcpy(d->d_pos, d->h_pos, d->B * sizeof(int))) return 1;
+    return 0;
+}
+
+float* gpt2_decode_logits(GPT2* model) { return model->decode ? model->decode->d_logits : NULL; }
+int* gpt2_decode_next(GPT2* model) { return model->decode ? model->decode->d_next : NULL; }
+
+int gpt2_decode_positions(GPT2* model, int* host_pos) {
+    GPT2Decode* d = model->decode;
+    if (!d) return 1;
+    memcpy(host_pos, d->h_pos, d->B * sizeof(int));
+    return 0;
+}
+
+int gpt2_decode_splits(GPT2* model, int* s4) {
+    GPT2Decode* d = model->decode;
+    if (!d) return 1;
+    memcpy(s4, d->split, sizeof(d->split));
+    return 0;
+}
+
+/* weights + wpe rows + KV read (ctx = pos+1) + KV append + logits */
+double gpt2_decode_step_bytes(GPT2* model, double* attn_bytes) {
+    GPT2Decode* d = model->decode;
+    if (!d) return 0.0;
+    const GPT2Config c = model->config;
+    const double C = c.channels, L = c.num_layers, V = c.vocab_size, w = 4.0;
+    double weights = (L * (12 * C * C + 13 * C) + V * C + 2 * C) * w;
+    double kv = 0.0;
+    for (int b = 0; b < d->B; b++) kv += 2.0 * L * (d->h_pos[b] + 1) * C * w;
+    double append = 2.0 * L * d->B * C * w;
+    double logits = (double)d->B * V * 4.0;
+    if (attn_bytes) *attn_bytes = kv;
+    return weights + d->B * C * w + kv + append + logits;
+}
+
+/* ------------------------------------------------------------------------ */
+/* gpt2_forward (paged_infer.c:575-729) on the decode engine                */
+/* ------------------------------------------------------------------------ */
+/* inputs (B, T) hold the token window at absolute positions offset..offset+T-1
+ * (the reference driver's convention, :1028-1080).  Positions not yet cached
+ * are decoded in order through the engine (all L layers, absolute positions,
+ * sequence b on prompt b's pages); logits/probs of row T-1 are written for
+ * every b.  targets are accepted and ignored (mean_loss = -1). */
+void gpt2_forward(GPT2* model, int* inputs, int* targets, size_t B, size_t T, size_t max_total,
+                  int offset) {
+    (void)targets;
+    if (model->params_memory == NULL) {
+        printf("Error: model was not initialized properly.\n");
+        exit(1);
+    }
+    const size_t V = model->config.vocab_size;
+    for (size_t i = 0; i < B * T; i++) /* :591-596 */
+        if (inputs[i] < 0 || (size_t)inputs[i] >= V) PI_FATAL("token out of range");
+    if (!model->acts_memory) {
+        model->batch_size = (int)B;
+        model->seq_len = (int)T;
+        size_t n = B * T * V;
+        model->acts_memory = (float*)hpa_malloc_managed(2 * n * sizeof(float));
+        if (!model->acts_memory) PI_FATAL("activation allocation failed");
+        memset(model->acts_memory, 0, 2 * n * sizeof(float));
+        model->acts.logits = model->acts_memory;
+        model->acts.probs = model->acts_memory + n;
+        model->inputs = (int*)malloc(B * T * sizeof(int));
+        model->targets = (int*)malloc(B * T * sizeof(int));
+        size_t maxctx = max_total > (size_t)model->config.max_seq_len ? (size_t)model->config.max_seq_len
+                                                                       : max_total;
+        if (maxctx < (size_t)offset + T) maxctx = (size_t)offset + T;
+        if (gpt2_decode_init(model, (int)B, model->manager ? 0 : 16, (int)maxctx) != 0)
+            PI_FATAL("decode engine init failed");
+    } else if ((int)B != model->batch_size || (int)T != model->seq_len) {
+        printf("Model: B=%d T=%d, Desired: B=%d T=%d\n", model->batch_size, model->seq_len, (int)B,
+               (int)T);
+        exit(EXIT_FAILURE);
+    }
+    memcpy(model->inputs, inputs, B * T * sizeof(int));
+    GPT2Decode* d = model->decode;
+    int* tok = (int*)malloc(B * sizeof(int));
+    /* all sequences share the window, so they advance together */
+    int cached = d->h_pos[0];
+    for (int p = cached; p < offset + (int)T; p++) {
+        int t = p - offset;
+        if (t < 0) PI_FATAL("window starts after uncached positions");
+        for (size_t b = 0; b < B; b++) tok[b] = inputs[b * T + t];
+        if (gpt2_decode_step(model, tok, NULL)) PI_FATAL("decode step failed");
+    }
+    free(tok);
+    PI_CHECK(hpa_synchronize());
+    for (size_t b = 0; b < B; b++) {
+        float* row = model->acts.logits + (b * T + (T - 1)) * V;
+        PI_CHECK(hpa_memcpy(row, d->d_logits + b * V, V * sizeof(float)));
+    }
+    /* probs of the same rows (softmax_forward, :259-286) */
+    for (size_t b = 0; b < B; b++) {
+        float* lg = model->acts.logits + (b * T + (T - 1)) * V;
+        float* pr = model->acts.probs + (b * T + (T - 1)) * V;
+        PI_CHECK(hpa_ref_softmax(pr, lg, 1, (int)V));
+    }
+    PI_CHECK(hpa_synchronize());
+    model->mean_loss = -1.0f;
+}
+
+/* paged_infer.c:736-745 (does not free model->manager, like the reference) */
+void gpt2_free(GPT2* model) {
+    if (model->decode) {
+        GPT2Decode* d = model->decode;
+        /* a caller-owned manager must not keep pointers into the freed pool */
+        if (!d->own_bm) {
+            for (int p = 0; p < d->bm->max_prompts; p++)
+                if (d->bm->prompt_block_count[p]) free_blocks_for_prompt(d->bm, p);
+            bm_set_backend(d->bm, NULL);
+        }
+    }
+    gpt2_decode_free(model);
+    hpa_free(model->params_memory);
+    hpa_free(model->acts_memory);
+    free(model->inputs);
+    free(model->targets);
+    model->params_memory = NULL;
+    model->acts_memory = NULL;
+    model->inputs = NULL;
+    model->targets = NULL;
+}
+
+/* heap GPT2 handle for FFI callers that cannot size the struct (ctypes) */
+GPT2* gpt2_alloc(void) {
+    GPT2* m = (GPT2*)calloc(1, sizeof(GPT2));
+    if (m) m->mean_loss = -1.0f;
+    return m;
+}
+void gpt2_release(GPT2* model) {
+    if (!model) return;
+    gpt2_free(model);
+    free(model);
+}
+void gpt2_set_manager(GPT2* model, BlockManager* manager) { model->manager = manager; }
+float* gpt2_acts_logits(GPT2* model) { return model->acts.logits; }
+float* gpt2_acts_probs(GPT2* model) { return model->acts.probs; }
+
+/* allocate (but do not fill) the pages of positions [0, ctx) for every
+ * sequence, so decode steps up to ctx never touch the allocator */
+int gpt2_decode_reserve(GPT2* model, int ctx) {
+    GPT2Decode* d = model->decode;
+    if (!d || ctx < 0 || ctx > d->max_ctx) return 1;
+    for (int b = 0; b < d->B; b++) {
+        int need = (ctx + d->P - 1) / d->P;
+        while (d->bm->prompt_block_count[b] < need)
+            if (!request_block(d->bm, b)) return 1;
+    }
+    return dec_sync_block_table(d) || hpa_synchronize();
+}
+
+/* move every sequence to position pos[b] (pages are kept; positions >= pos
+ * will be overwritten).  Requires pages for pos[b] to exist already. */
+int gpt2_decode_set_positions(GPT2* model, const int* pos) {
+    GPT2Decode* d = model->decode;
+    if (!d) return 1;
+    for (int b = 0; b < d->B; b++) {
+        if (pos[b] < 0 || pos[b] >= d->max_ctx) return 1;
+        if (d->bm->prompt_block_count[b] * d->P < pos[b]) return 1;
+        d->h_pos[b] = pos[b];
+    }
+    if (hpa_synchronize()) return 1;
+    memcpy(d->h_stage, pos, d->B * sizeof(int));
+    if (hpa_memcpy_async(d->d_pos, d->h_stage, d->B * sizeof(int))) return 1;
+    return hpa_synchronize();
+}
+
+/* attention-kernel timing with HIP events on the launch stream: enable (1)
+ * switches the engine to eager launches bracketed by per-layer events;
+ * gpt2_decode_profile_collect() waits for the last step and adds its L
+ * attention durations; read returns (total ms, launches). */
+int gpt2_decode_profile(GPT2* model, int enable) {
+    GPT2Decode* d = model->decode;
+    if (!d) return 1;
+    int L = model->config.num_layers;
+    if (!enable) {
+        if (hpa_synchronize()) return 1;
+        dec_prof_free(d, L);
+        return 0;
+    }
+    if (!d->prof_ev) {
+        d->prof_ev = (void**)calloc(2 * (size_t)L, sizeof(void*));
+        for (int i = 0; i < 2 * L; i++) {
+            d->prof_ev[i] = hpa_event_create();
+            if (!d->prof_ev[i]) return 1;
+        }
+    }
+    d->use_graph = 0;
+    d->prof_ms = 0.0;
+    d->prof_launches = 0;
+    return 0;
+}
+
+int gpt2_decode_profile_collect(GPT2* model) {
+    GPT2Decode* d = model->decode;
+    if (!d || !d->prof_ev) return 1;
+    int L = model->config.num_layers;
+    for (int l = 0; l < L; l++) {
+        float ms = hpa_event_elapsed_ms(d->prof_ev[2 * l], d->prof_ev[2 * l + 1]);
+        if (ms < 0) return 1;
+        d->prof_ms += ms;
+        d->prof_launches++;
+    }
+    return 0;
+}
+
+double gpt2_decode_profile_read(GPT2* model, long* launches) {
+    GPT2Decode* d = model->decode;
+    if (!d) return -1.0;
+    if (launches) *launches = d->prof_launches;
+    return d->prof_ms;
+}

@@ -1,0 +1,467 @@
+"""Python host mirror of libpaged_hip.so (ctypes over the C-ABI).
+
+This is a thin binding, not a compute path: every call lands in the C
+library (include/hip_paged_attn.h, paged_infer.h, block_manager.h), which
+runs the MI355X kernels.  There is no fallback: if the library is missing or
+no HIP device is visible, the calls raise.
+
+Names mirror the reference API (paged_infer.c / block_manager.c of
+mx60s/llm.c-paged): Model wraps GPT2 + gpt2_decode_* (the decode hot path),
+BlockManager wraps create_block_manager / request_block / ... .
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpaged_hip.so")
+INCLUDE_DIR = os.path.join(os.path.dirname(HERE), "include")
+
+_F = ctypes.POINTER(ctypes.c_float)
+_I = ctypes.POINTER(ctypes.c_int)
+_V = ctypes.c_void_p
+
+
+class GPT2Config(ctypes.Structure):
+    """paged_infer.c:397-403"""
+    _fields_ = [("max_seq_len", ctypes.c_int), ("vocab_size", ctypes.c_int),
+                ("num_layers", ctypes.c_int), ("num_heads", ctypes.c_int),
+                ("channels", ctypes.c_int)]
+
+    def as_dict(self):
+        return dict(maxT=self.max_seq_len, V=self.vocab_size, L=self.num_layers,
+                    NH=self.num_heads, C=self.channels)
+
+
+class KVBlock(ctypes.Structure):
+    """block_manager.c:9-15"""
+    _fields_ = [("keys", _F), ("values", _F), ("filled", ctypes.c_int),
+                ("prompt_id", ctypes.c_int), ("lru_counter", ctypes.c_int)]
+
+
+class HpaKVPool(ctypes.Structure):
+    _fields_ = [("base", _V), ("num_layers", ctypes.c_int), ("num_heads", ctypes.c_int),
+                ("head_size", ctypes.c_int), ("page_size", ctypes.c_int),
+                ("num_pages", ctypes.c_int), ("dtype", ctypes.c_int),
+                ("elem_bytes", ctypes.c_size_t), ("page_elems", ctypes.c_size_t),
+                ("layer_elems", ctypes.c_size_t), ("bytes", ctypes.c_size_t),
+                ("managed", ctypes.c_int)]
+
+
+GPT2_124M = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
+GPT2_XL = dict(maxT=1024, V=50257, L=48, NH=25, C=1600)
+
+HPA_EPI_PARTIAL, HPA_EPI_BIAS, HPA_EPI_BIAS_GELU = 0, 1, 2
+
+
+def config(d):
+    return GPT2Config(d["maxT"], d["V"], d["L"], d["NH"], d["C"])
+
+
+def build(force=False):
+    """Compile libpaged_hip.so in-tree (hipcc --offload-arch=gfx950)."""
+    cmd = ["make", "-s", "-C", HERE, "-j8"]
+    if force:
+        cmd.insert(2, "-B")
+    subprocess.run(cmd, check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def _sig(L, name, res, args):
+    f = getattr(L, name)
+    f.restype = res
+    f.argtypes = args
+
+
+def lib():
+    """Load libpaged_hip.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    i, v, f, sz = ctypes.c_int, _V, ctypes.c_float, ctypes.c_size_t
+    P = ctypes.POINTER(HpaKVPool)
+    # runtime
+    _sig(L, "hpa_init", i, [i])
+    _sig(L, "hpa_device_count", i, [])
+    _sig(L, "hpa_get_device", i, [])
+    _sig(L, "hpa_set_stream", i, [v])
+    _sig(L, "hpa_get_stream", v, [])
+    _sig(L, "hpa_synchronize", i, [])
+    _sig(L, "hpa_malloc", v, [sz])
+    _sig(L, "hpa_malloc_managed", v, [sz])
+    _sig(L, "hpa_host_alloc", v, [sz])
+    _sig(L, "hpa_free", i, [v])
+    _sig(L, "hpa_memcpy", i, [v, v, sz])
+    _sig(L, "hpa_memcpy_async", i, [v, v, sz])
+    _sig(L, "hpa_memset_async", i, [v, i, sz])
+    _sig(L, "hpa_is_device_accessible", i, [v])
+    _sig(L, "hpa_event_create", v, [])
+    _sig(L, "hpa_event_record", i, [v])
+    _sig(L, "hpa_event_elapsed_ms", f, [v, v])
+    _sig(L, "hpa_event_destroy", i, [v])
+    _sig(L, "hpa_last_error", ctypes.c_char_p, [])
+    _sig(L, "hpa_device_info", i, [ctypes.c_char_p, i, _I, ctypes.POINTER(sz)])
+    _sig(L, "hpa_set_attention_waves", i, [i])
+    # pool + kernels
+    _sig(L, "hpa_pool_create", i, [P, i, i, i, i, i, i, i])
+    _sig(L, "hpa_pool_destroy", None, [P])
+    _sig(L, "hpa_pool_tile", v, [P, i, i, i, i])
+    _sig(L, "hpa_pool_k_index", sz, [P, i, i, i, i, i])
+    _sig(L, "hpa_pool_v_index", sz, [P, i, i, i, i, i])
+    _sig(L, "hpa_pool_fill_random", i, [P, v, i, i, i, ctypes.c_uint64])
+    _sig(L, "hpa_paged_attention_decode", i, [v, P, i, v, i, v, v, i])
+    _sig(L, "hpa_gemm_f32", i, [v, i, v, v, v, i, i, i, i, i, i])
+    _sig(L, "hpa_gemm_pick_splitk", i, [i, i, i])
+    _sig(L, "hpa_qkv_append", i, [v, i, v, v, P, i, v, i, v, i, i])
+    _sig(L, "hpa_embed_ln", i, [v, v, v, v, v, v, v, v, i, i])
+    _sig(L, "hpa_residual_ln", i, [v, i, v, v, v, v, v, v, i, i])
+    _sig(L, "hpa_bias_gelu", i, [v, i, v, v, i, i])
+    _sig(L, "hpa_argmax_advance", i, [v, i, i, v, v, v])
+    _sig(L, "hpa_ref_attention_paged", i, [v, v, v, v, v, v, i, i, i, i, i, i])
+    _sig(L, "hpa_ref_matmul", i, [v, v, v, v, i, i, i, i, i])
+    # block manager (block_manager.c API)
+    _sig(L, "create_block_manager", v, [i])
+    _sig(L, "create_block_manager_ex", v, [i, i, i, i, i])
+    _sig(L, "destroy_block_manager", None, [v])
+    _sig(L, "request_block", ctypes.POINTER(KVBlock), [v, i])
+    _sig(L, "get_current_block", ctypes.POINTER(KVBlock), [v, i])
+    _sig(L, "free_blocks_for_prompt", None, [v, i])
+    _sig(L, "find_least_recently_used_block", i, [v])
+    _sig(L, "page_out_lru_block", None, [v])
+    _sig(L, "get_next_block_id", i, [v, i, i])
+    _sig(L, "collect_kv_blocks", v, [v, i, _I])
+    _sig(L, "bm_block_index", i, [v, v])
+    _sig(L, "bm_free_pages", i, [v])
+    _sig(L, "bm_use_host_pages", None, [v])
+    _sig(L, "bm_default_backend_kind", i, [])
+    # model + decode engine
+    _sig(L, "gpt2_alloc", v, [])
+    _sig(L, "gpt2_release", None, [v])
+    _sig(L, "gpt2_set_manager", None, [v, v])
+    _sig(L, "gpt2_acts_logits", _F, [v])
+    _sig(L, "gpt2_acts_probs", _F, [v])
+    _sig(L, "gpt2_num_parameters", sz, [GPT2Config])
+    _sig(L, "gpt2_synthetic_params", i, [GPT2Config, ctypes.c_ulonglong, _F])
+    _sig(L, "gpt2_write_checkpoint", i, [ctypes.c_char_p, GPT2Config, _F])
+    _sig(L, "gpt2_build_from_params", i, [v, GPT2Config, _F])
+    _sig(L, "gpt2_build_synthetic", i, [v, GPT2Config, ctypes.c_ulonglong])
+    _sig(L, "gpt2_build_from_checkpoint", None, [v, ctypes.c_char_p])
+    _sig(L, "gpt2_forward", None, [v, _I, _I, sz, sz, sz, i])
+    _sig(L, "gpt2_decode_init", i, [v, i, i, i])
+    _sig(L, "gpt2_decode_step", i, [v, _I, _I])
+    _sig(L, "gpt2_decode_step_async", i, [v, _I])
+    _sig(L, "gpt2_decode_reset", i, [v])
+    _sig(L, "gpt2_decode_fill_random", i, [v, i, ctypes.c_ulonglong])
+    _sig(L, "gpt2_decode_set_graph", i, [v, i])
+    _sig(L, "gpt2_decode_reserve", i, [v, i])
+    _sig(L, "gpt2_decode_set_positions", i, [v, _I])
+    _sig(L, "gpt2_decode_logits", v, [v])
+    _sig(L, "gpt2_decode_next", v, [v])
+    _sig(L, "gpt2_decode_positions", i, [v, _I])
+    _sig(L, "gpt2_decode_splits", i, [v, _I])
+    _sig(L, "gpt2_decode_step_bytes", ctypes.c_double, [v, ctypes.POINTER(ctypes.c_double)])
+    _sig(L, "random_u32", ctypes.c_uint, [ctypes.POINTER(ctypes.c_ulonglong)])
+    _sig(L, "random_f32", f, [ctypes.POINTER(ctypes.c_ulonglong)])
+    _lib = L
+    return L
+
+
+def check(rc, what=""):
+    if rc != 0:
+        err = lib().hpa_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed: {err}")
+
+
+def init(device=0):
+    L = lib()
+    if L.hpa_device_count() <= 0:
+        raise RuntimeError("no HIP device visible: the MI355X path has no CPU fallback")
+    check(L.hpa_init(device), "hpa_init")
+
+
+def device_info():
+    L = lib()
+    name = ctypes.create_string_buffer(256)
+    cus = ctypes.c_int()
+    mem = ctypes.c_size_t()
+    check(L.hpa_device_info(name, 256, ctypes.byref(cus), ctypes.byref(mem)), "device_info")
+    return name.value.decode(), cus.value, mem.value
+
+
+# ---------------------------------------------------------------- device buffers
+class DeviceBuffer:
+    """hpa_malloc'd memory with numpy-typed upload/download helpers."""
+
+    def __init__(self, nbytes, managed=False):
+        L = lib()
+        self.nbytes = int(nbytes)
+        self.ptr = L.hpa_malloc_managed(self.nbytes) if managed else L.hpa_malloc(self.nbytes)
+        if not self.ptr:
+            raise MemoryError(f"device allocation of {nbytes} bytes failed")
+
+    @classmethod
+    def from_array(cls, a, managed=False):
+        a = np.ascontiguousarray(a)
+        b = cls(a.nbytes, managed)
+        b.upload(a)
+        return b
+
+    def upload(self, a, offset=0):
+        a = np.ascontiguousarray(a)
+        assert offset + a.nbytes <= self.nbytes
+        check(lib().hpa_memcpy(self.ptr + offset, a.ctypes.data, a.nbytes), "upload")
+
+    def download(self, shape, dtype=np.float32, offset=0):
+        out = np.empty(shape, dtype)
+        assert offset + out.nbytes <= self.nbytes
+        check(lib().hpa_memcpy(out.ctypes.data, self.ptr + offset, out.nbytes), "download")
+        return out
+
+    def free(self):
+        if self.ptr:
+            lib().hpa_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Pool:
+    """HpaKVPool: the HBM page pool in the fast layout."""
+
+    def __init__(self, num_layers, num_heads, page_size, num_pages, head_size=64, managed=False):
+        self.s = HpaKVPool()
+        check(lib().hpa_pool_create(ctypes.byref(self.s), num_layers, num_heads, head_size, page_size,
+                                    num_pages, 0, int(managed)), "pool_create")
+
+    @property
+    def ref(self):
+        return ctypes.byref(self.s)
+
+    def write_tokens(self, layer, pages, k, v):
+        """host helper: k, v (ntok, C) -> logical positions 0..ntok-1 of the
+        sequence whose page list is `pages` (uploads whole pages)."""
+        s = self.s
+        P, NH, HS = s.page_size, s.num_heads, s.head_size
+        ntok = k.shape[0]
+        for lp, page in enumerate(pages):
+            t0 = lp * P
+            if t0 >= ntok:
+                break
+            n = min(P, ntok - t0)
+            kt = np.zeros((NH, HS // 4, P, 4), np.float32)
+            vt = np.zeros((NH, P, HS), np.float32)
+            kk = k[t0:t0 + n].reshape(n, NH, HS // 4, 4).transpose(1, 2, 0, 3)
+            kt[:, :, :n, :] = kk
+            vt[:, :n, :] = v[t0:t0 + n].reshape(n, NH, HS).transpose(1, 0, 2)
+            page_k = lib().hpa_pool_tile(self.ref, layer, int(page), 0, 0)
+            page_v = lib().hpa_pool_tile(self.ref, layer, int(page), 1, 0)
+            check(lib().hpa_memcpy(page_k, kt.ctypes.data, kt.nbytes), "pool write K")
+            check(lib().hpa_memcpy(page_v, vt.ctypes.data, vt.nbytes), "pool write V")
+
+    def read_tokens(self, layer, pages, ntok):
+        s = self.s
+        P, NH, HS = s.page_size, s.num_heads, s.head_size
+        k = np.zeros((ntok, NH * HS), np.float32)
+        v = np.zeros((ntok, NH * HS), np.float32)
+        for lp, page in enumerate(pages):
+            t0 = lp * P
+            if t0 >= ntok:
+                break
+            n = min(P, ntok - t0)
+            kt = np.empty((NH, HS // 4, P, 4), np.float32)
+            vt = np.empty((NH, P, HS), np.float32)
+            check(lib().hpa_memcpy(kt.ctypes.data, lib().hpa_pool_tile(self.ref, layer, int(page), 0, 0),
+                                   kt.nbytes), "pool read K")
+            check(lib().hpa_memcpy(vt.ctypes.data, lib().hpa_pool_tile(self.ref, layer, int(page), 1, 0),
+                                   vt.nbytes), "pool read V")
+            k[t0:t0 + n] = kt[:, :, :n, :].transpose(2, 0, 1, 3).reshape(n, NH * HS)
+            v[t0:t0 + n] = vt[:, :n, :].transpose(1, 0, 2).reshape(n, NH * HS)
+        return k, v
+
+    def destroy(self):
+        if self.s.base:
+            lib().hpa_pool_destroy(self.ref)
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+# ---------------------------------------------------------------- block manager
+class BlockManager:
+    """block_manager.c API (create_block_manager, request_block, ...)."""
+
+    def __init__(self, channels, max_prompts=None, max_blocks=None, block_size=None,
+                 max_blocks_per_prompt=None, host_pages=False):
+        L = lib()
+        if max_prompts is None:
+            self.h = L.create_block_manager(channels)
+        else:
+            self.h = L.create_block_manager_ex(channels, max_prompts, max_blocks, block_size,
+                                               max_blocks_per_prompt or max_blocks)
+        if not self.h:
+            raise MemoryError("create_block_manager failed")
+        if host_pages:
+            L.bm_use_host_pages(self.h)
+
+    def request_block(self, prompt):
+        blk = lib().request_block(self.h, prompt)
+        return lib().bm_block_index(self.h, blk) if blk else -1
+
+    def block(self, index):
+        base = ctypes.cast(self.h, ctypes.POINTER(ctypes.c_void_p))
+        blocks = ctypes.cast(base[1], ctypes.POINTER(KVBlock))  # BlockManager.blocks
+        return blocks[index]
+
+    def close(self):
+        if self.h:
+            lib().destroy_block_manager(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ---------------------------------------------------------------- model / decode engine
+class Model:
+    """GPT2 + the decode engine (gpt2_decode_*), i.e. the hot path."""
+
+    def __init__(self, cfg, params=None, seed=1337, checkpoint=None):
+        L = lib()
+        self.cfg = cfg if isinstance(cfg, GPT2Config) else config(cfg)
+        self.h = L.gpt2_alloc()
+        if checkpoint is not None:
+            L.gpt2_build_from_checkpoint(self.h, checkpoint.encode())
+        elif params is not None:
+            p = np.ascontiguousarray(params, np.float32)
+            assert p.size == L.gpt2_num_parameters(self.cfg)
+            check(L.gpt2_build_from_params(self.h, self.cfg, p.ctypes.data_as(_F)), "build_from_params")
+        else:
+            check(L.gpt2_build_synthetic(self.h, self.cfg, seed), "build_synthetic")
+        self.B = 0
+
+    def decode_init(self, B, page_size=16, max_ctx=None):
+        max_ctx = max_ctx or self.cfg.max_seq_len
+        check(lib().gpt2_decode_init(self.h, B, page_size, max_ctx), "gpt2_decode_init")
+        self.B = B
+
+    def set_graph(self, on):
+        check(lib().gpt2_decode_set_graph(self.h, int(on)), "set_graph")
+
+    def step(self, tokens=None, want_next=True):
+        nxt = np.zeros(self.B, np.int32) if want_next else None
+        tp = None
+        if tokens is not None:
+            tokens = np.ascontiguousarray(tokens, np.int32)
+            assert tokens.shape == (self.B,)
+            tp = tokens.ctypes.data_as(_I)
+        check(lib().gpt2_decode_step(self.h, tp, nxt.ctypes.data_as(_I) if want_next else None),
+              "gpt2_decode_step")
+        return nxt
+
+    def step_async(self, tokens=None):
+        tp = None
+        if tokens is not None:
+            tokens = np.ascontiguousarray(tokens, np.int32)
+            tp = tokens.ctypes.data_as(_I)
+        check(lib().gpt2_decode_step_async(self.h, tp), "gpt2_decode_step_async")
+
+    def logits(self):
+        ptr = lib().gpt2_decode_logits(self.h)
+        out = np.empty((self.B, self.cfg.vocab_size), np.float32)
+        check(lib().hpa_memcpy(out.ctypes.data, ptr, out.nbytes), "logits download")
+        return out
+
+    def logits_ptr(self):
+        return lib().gpt2_decode_logits(self.h)
+
+    def next_ptr(self):
+        return lib().gpt2_decode_next(self.h)
+
+    def positions(self):
+        out = np.zeros(self.B, np.int32)
+        check(lib().gpt2_decode_positions(self.h, out.ctypes.data_as(_I)), "positions")
+        return out
+
+    def splits(self):
+        out = np.zeros(4, np.int32)
+        check(lib().gpt2_decode_splits(self.h, out.ctypes.data_as(_I)), "splits")
+        return out
+
+    def step_bytes(self):
+        att = ctypes.c_double()
+        tot = lib().gpt2_decode_step_bytes(self.h, ctypes.byref(att))
+        return tot, att.value
+
+    def reset(self):
+        check(lib().gpt2_decode_reset(self.h), "reset")
+
+    def reserve(self, ctx):
+        check(lib().gpt2_decode_reserve(self.h, ctx), "reserve")
+
+    def set_positions(self, pos):
+        pos = np.ascontiguousarray(pos, np.int32)
+        check(lib().gpt2_decode_set_positions(self.h, pos.ctypes.data_as(_I)), "set_positions")
+
+    def fill_random(self, ctx, seed=1):
+        check(lib().gpt2_decode_fill_random(self.h, ctx, seed), "fill_random")
+
+    def close(self):
+        if self.h:
+            lib().hpa_synchronize()
+            lib().gpt2_release(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def synthetic_params(cfg, seed=1337):
+    L = lib()
+    c = cfg if isinstance(cfg, GPT2Config) else config(cfg)
+    n = L.gpt2_num_parameters(c)
+    p = np.empty(n, np.float32)
+    check(L.gpt2_synthetic_params(c, seed, p.ctypes.data_as(_F)), "synthetic_params")
+    return p
+
+
+class Timer:
+    """HIP events on the library's stream (where the kernels run)."""
+
+    def __init__(self):
+        self.a = lib().hpa_event_create()
+        self.b = lib().hpa_event_create()
+
+    def start(self):
+        check(lib().hpa_event_record(self.a), "event_record")
+
+    def stop(self):
+        check(lib().hpa_event_record(self.b), "event_record")
+        return lib().hpa_event_elapsed_ms(self.a, self.b)
+
+    def __del__(self):
+        try:
+            lib().hpa_event_destroy(self.a)
+            lib().hpa_event_destroy(self.b)
+        except Exception:
+            pass

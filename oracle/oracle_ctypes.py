@@ -46,6 +46,7 @@ def lib(fast=False):
     L.oracle_num_params.argtypes = [OracleConfig]
     L.oracle_param_offsets.argtypes = [OracleConfig, ctypes.POINTER(ctypes.c_size_t)]
     L.oracle_attention_paged.argtypes = [_F, _F, _F, _F, _PF, _PF] + [ctypes.c_int] * 6
+    L.oracle_attention_decode.argtypes = [_F, _F, _PF, _PF] + [ctypes.c_int] * 4
     L.oracle_attention_forward.argtypes = [_F, _F, _F, _F] + [ctypes.c_int] * 4
     L.oracle_matmul_forward.argtypes = [_F, _F, _F, _F] + [ctypes.c_int] * 4
     L.oracle_matmul_cached.argtypes = [_F, _F, _F, _F] + [ctypes.c_int] * 4
@@ -98,6 +99,20 @@ def attention_paged(inp, kpool, vpool, page_order, B, T, C, NH, offset, block_si
     L.oracle_attention_paged(fp(out), fp(preatt), fp(att), fp(inp), kb, vb, B, T, C, NH, offset,
                              block_size)
     return out, preatt, att
+
+
+def attention_decode(q, kpages, vpages, ctx, NH):
+    """oracle_attention_decode: q (C,), kpages/vpages lists of (block_size, C)
+    float32 arrays in logical order; returns out (C,)."""
+    L = lib()
+    C = q.shape[0]
+    bs = kpages[0].shape[0]
+    out = np.zeros(C, np.float32)
+    n = len(kpages)
+    kb = (_F * n)(*[fp(p) for p in kpages])
+    vb = (_F * n)(*[fp(p) for p in vpages])
+    L.oracle_attention_decode(fp(out), fp(np.ascontiguousarray(q, np.float32)), kb, vb, ctx, C, NH, bs)
+    return out
 
 
 def gpt2_forward(params, c, tokens, fast=False):

@@ -510,3 +510,20 @@ int oracle_paged_step(OraclePaged* o, const int* tokens, float* logits, int* nex
     }
     return 0;
 }
+
+/* one decode query row per sequence: q (C) attends logical positions
+ * 0..ctx-1 through key_blocks/value_blocks (pages of block_size tokens,
+ * token-major [block_size][C]) with attention_paged's per-row arithmetic
+ * (paged_infer.c:186-236); out (C). */
+void oracle_attention_decode(float* out, const float* q, float* const* key_blocks,
+                             float* const* value_blocks, int ctx, int C, int NH, int block_size) {
+    int hs = C / NH;
+    float* pre = malloc((size_t)(ctx > 0 ? ctx : 1) * 4);
+    float* att = malloc((size_t)(ctx > 0 ? ctx : 1) * 4);
+    for (int h = 0; h < NH; h++) {
+        paged_ctx px = {key_blocks, value_blocks, block_size, C, h, hs};
+        attn_row(out + h * hs, pre, att, ctx, q + h * hs, paged_k, paged_v, &px, 0, ctx, hs);
+    }
+    free(pre);
+    free(att);
+}

@@ -70,6 +70,10 @@ void oracle_attention_paged(float* out, float* preatt, float* att, const float* 
                             float* const* key_blocks, float* const* value_blocks,
                             int B, int T, int C, int NH, int offset, int block_size);
 
+/* one decode query (C floats) over positions 0..ctx-1 of a sequence's pages */
+void oracle_attention_decode(float* out, const float* q, float* const* key_blocks,
+                             float* const* value_blocks, int ctx, int C, int NH, int block_size);
+
 /* full-recompute GPT-2 forward with all L layers, train_scratch.c:658-798
  * (the model-level oracle; logits only).  logits: (B,T,V). */
 void oracle_gpt2_forward(const float* params, OracleConfig cfg, const int* tokens,

@@ -1,0 +1,128 @@
+"""The CPU oracle against the reference's own outputs (tests/golden/, made by
+tests/golden/gen_golden.py from the reference sources) and against its own
+properties.  These pin the oracle before it is trusted as the GPU checker.
+
+Tolerance: exact (0.0 max-abs).  The oracle is built -O2 -fno-fast-math
+-ffp-contract=off like the golden generator, with the reference's arithmetic
+order, so any difference is a restatement bug.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as oc
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(GOLD, name))  # allow_pickle=False (default)
+
+
+def test_attention_paged_matches_reference_golden():
+    g = load("attn_paged_golden.npz")
+    for ci in range(int(g["ncases"])):
+        B, T, C, NH, off, bs = [int(x) for x in g[f"c{ci}_shape"]]
+        out, pre, att = oc.attention_paged(g[f"c{ci}_inp"], g[f"c{ci}_kpool"], g[f"c{ci}_vpool"],
+                                           g[f"c{ci}_order"], B, T, C, NH, off, bs)
+        assert np.array_equal(out, g[f"c{ci}_out"]), ci
+        assert np.array_equal(pre, g[f"c{ci}_preatt"]), ci
+        assert np.array_equal(att, g[f"c{ci}_att"]), ci
+
+
+def test_matmul_forward_and_cached_match_reference_golden():
+    g = load("matmul_golden.npz")
+    B, T, C, OC = [int(x) for x in g["shape"]]
+    L = oc.lib()
+    out = np.zeros((B, T, OC), np.float32)
+    L.oracle_matmul_forward(oc.fp(out), oc.fp(g["inp"]), oc.fp(g["w"]), oc.fp(g["b"]), B, T, C, OC)
+    assert np.array_equal(out, g["fwd"])
+    out = np.zeros((B, T, OC), np.float32)
+    L.oracle_matmul_cached(oc.fp(out), oc.fp(g["inp"]), oc.fp(g["w"]), oc.fp(g["b"]), B, T, C, OC)
+    assert np.array_equal(out, g["cached"])
+    # matmul_cached == matmul_forward on Q of every row and K,V of the last row
+    # (the reference's test_matmul.c property)
+    assert np.array_equal(g["cached"][:, :, :C], g["fwd"][:, :, :C])
+    assert np.array_equal(g["cached"][:, -1, C:], g["fwd"][:, -1, C:])
+
+
+def test_full_forward_matches_reference_train_scratch():
+    g = load("forward_golden.npz")
+    c = oc.cfg(*[int(x) for x in g["cfg"]])
+    logits = oc.gpt2_forward(g["params"], c, g["tokens"])
+    assert np.array_equal(logits, g["logits"])
+
+
+@pytest.mark.parametrize("page_size", [4, 8, 16, 32])
+def test_paged_decode_equals_full_recompute(page_size):
+    """incremental paged decode (absolute positions, all
+    layers, per-sequence permuted block tables) == full recompute, every step."""
+    g = load("forward_golden.npz")
+    c = oc.cfg(*[int(x) for x in g["cfg"]])
+    tokens = g["tokens"]
+    B, T = tokens.shape
+    d = oc.PagedDecoder(g["params"], c, B, page_size, 64, page_seed=page_size + 1)
+    for t in range(T):
+        nxt, logits = d.step(tokens[:, t])
+        assert np.array_equal(logits, g["logits"][:, t]), t
+        assert np.array_equal(nxt, g["logits"][:, t].argmax(-1)), t
+    d.close()
+
+
+@pytest.mark.parametrize("block_size", [1, 2, 5, 8, 16])
+def test_paged_equals_contiguous_attention(block_size):
+    """test_paged_attn.c's property (paged == contiguous attention), seeded,
+    exact, over several page sizes and permuted page placement."""
+    rng = np.random.default_rng(block_size)
+    B, T, C, NH = 2, 20, 12, 3
+    inp = rng.uniform(0, 100, (B, T, 3 * C)).astype(np.float32)
+    # the reference test shares pages across b: use b = 0's K/V for all b
+    inp[1, :, C:] = inp[0, :, C:]
+    npages = (T + block_size - 1) // block_size
+    kpool = np.zeros((npages, block_size, C), np.float32)
+    vpool = np.zeros((npages, block_size, C), np.float32)
+    order = rng.permutation(npages).astype(np.int32)
+    for t in range(T):
+        kpool[order[t // block_size], t % block_size] = inp[0, t, C:2 * C]
+        vpool[order[t // block_size], t % block_size] = inp[0, t, 2 * C:]
+    out_p, pre_p, att_p = oc.attention_paged(inp, kpool, vpool, order, B, T, C, NH, 0, block_size)
+    out_c = np.zeros((B, T, C), np.float32)
+    pre = np.zeros((B, NH, T, T), np.float32)
+    att = np.zeros((B, NH, T, T), np.float32)
+    oc.lib().oracle_attention_forward(oc.fp(out_c), oc.fp(pre), oc.fp(att), oc.fp(inp), B, T, C, NH)
+    assert np.array_equal(out_p, out_c)
+    assert np.array_equal(att_p, att)
+
+
+def test_attention_decode_row_equals_paged_last_row():
+    rng = np.random.default_rng(3)
+    C, NH, bs, ctx = 64, 4, 8, 37
+    npages = (ctx + bs - 1) // bs
+    kp = [rng.uniform(-1, 1, (bs, C)).astype(np.float32) for _ in range(npages)]
+    vp = [rng.uniform(-1, 1, (bs, C)).astype(np.float32) for _ in range(npages)]
+    q = rng.uniform(-1, 1, C).astype(np.float32)
+    out = oc.attention_decode(q, kp, vp, ctx, NH)
+    # the same row through attention_paged: T = ctx rows at offset 0, row ctx-1
+    inp = np.zeros((1, ctx, 3 * C), np.float32)
+    inp[0, ctx - 1, :C] = q
+    kpool = np.stack(kp)
+    vpool = np.stack(vp)
+    o2, _, _ = oc.attention_paged(inp, kpool, vpool, np.arange(npages, dtype=np.int32), 1, ctx, C,
+                                  NH, 0, bs)
+    assert np.array_equal(out, o2[0, ctx - 1])
+
+
+def test_argmax_first_max_wins():
+    x = np.array([0.5, 2.0, -1.0, 2.0, 2.0], np.float32)
+    assert oc.lib().oracle_argmax(oc.fp(x), 5) == 1
+
+
+def test_reference_all_negative_scores_give_zero_output():
+    """expsum == 0 branch of paged_infer.c:213: scores below -10000 -> 0."""
+    C, NH, bs, ctx = 64, 1, 8, 9
+    kp = [np.full((bs, C), 10.0, np.float32) for _ in range(2)]
+    vp = [np.ones((bs, C), np.float32) for _ in range(2)]
+    q = np.full(C, -1000.0, np.float32)
+    out = oc.attention_decode(q, kp, vp, ctx, NH)
+    assert np.all(out == 0.0)
