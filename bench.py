@@ -57,6 +57,10 @@ def parse():
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--attn-waves", type=int, default=4)
+    ap.add_argument("--unfused", action="store_true", help="row-major GEMMs + separate row kernels")
+    ap.add_argument("--lanes", type=int, default=1, help="micro-batch lanes (concurrent row groups)")
+    ap.add_argument("--gemm-waves", default="", help="fused GEMM waves qkv,attproj,fc,fcproj,logits (0 = auto)")
+    ap.add_argument("--gemm-rows", default="", help="fused GEMM 16-row blocks per workgroup, same order")
     return ap.parse_args()
 
 
@@ -136,6 +140,12 @@ def main():
 
     model = pagedattn.Model(cfgd, seed=1337)
     model.decode_init(B_local, P, ctx)
+    model.set_fused(not args.unfused)
+    if not args.unfused:
+        model.set_lanes(args.lanes)
+    if args.gemm_waves or args.gemm_rows:
+        model.gemm_config([int(x) for x in args.gemm_waves.split(",")] if args.gemm_waves else None,
+                          [int(x) for x in args.gemm_rows.split(",")] if args.gemm_rows else None)
     model.reserve(ctx)
     rng = np.random.default_rng(1000 + rank)
     if args.prefill == "synthetic":
@@ -218,8 +228,10 @@ def main():
         n = pagedattn.ctypes.c_long()
         ms = L.gpt2_decode_profile_read(model.h, pagedattn.ctypes.byref(n))
         pagedattn.check(L.gpt2_decode_profile(model.h, 0), "profile off")
-        # per launch: K+V of every sequence's context for one layer (+ q in, out)
-        per_launch_bytes = attn_bytes / (args.prof_steps * cfgd["L"]) + 2 * B_local * cfgd["C"] * 4
+        # per launch: K+V of the launch's sequences' contexts for one layer (+ q in, out);
+        # with lanes, each layer is one launch per lane
+        total_bytes = attn_bytes + args.prof_steps * cfgd["L"] * 2 * B_local * cfgd["C"] * 4
+        per_launch_bytes = total_bytes / max(n.value, 1)
         avg_ms = ms / max(n.value, 1)
         achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
         attn = dict(avg_ms=avg_ms, launches=n.value, per_launch_bytes=per_launch_bytes,
@@ -262,7 +274,10 @@ def main():
                        "decode_positions": f"{start}..{start + args.warmup + args.steps - 1}",
                        "parallelism": f"seq-shard x{world}" + (f" + RCCL all_gather({args.gather})"
                                                                if world > 1 else ""),
-                       "hip_graph": not args.no_graph, "device": name},
+                       "hip_graph": not args.no_graph, "gemm_path": "unfused" if args.unfused else "fused",
+                       "lanes": 1 if args.unfused else L.gpt2_decode_lanes(model.h),
+                       "gemm_waves": [int(x) for x in model.gemm_config()[0]],
+                       "gemm_row_blocks": [int(x) for x in model.gemm_config()[1]], "device": name},
             "step_roofline": {"bytes_per_step_rank0": int(step_bytes),
                               "achieved_GBps": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
                               "frac_of_8TBps": round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},

@@ -52,6 +52,14 @@ void* hpa_event_create(void);
 int   hpa_event_record(void* ev);
 float hpa_event_elapsed_ms(void* start, void* stop); /* syncs on stop */
 int   hpa_event_destroy(void* ev);
+void* hpa_event_create_nt(void);          /* no timing: fork/join ordering only */
+/* extra streams for concurrent work (the decode engine's micro-batch lanes);
+ * hpa_stream_wait_event: the CURRENT stream waits for `ev` (recorded on any
+ * stream).  Inside a capture, fork/join through events pulls the other
+ * stream into the same graph as parallel branches. */
+void* hpa_stream_create(void);
+int   hpa_stream_destroy(void* stream);
+int   hpa_stream_wait_event(void* ev);
 const char* hpa_last_error(void);
 /* hipGraph capture of everything enqueued on the current stream between
  * begin and end (the decode step: ~9 launches per layer); replay with
@@ -149,6 +157,67 @@ int hpa_argmax_advance(const float* logits, int B, int V, int* next, int* tokens
  * from a counter-based hash (attention microbench / bench synthetic prefill) */
 int hpa_pool_fill_random(const HpaKVPool* pool, const int* block_table, int bt_stride, int B,
                          int ctx, uint64_t seed);
+
+/* ---------------- fused decode-layer GEMMs (the engine's path) ----------------
+ * "frag" layout: a [rows][K] fp32 matrix with rows padded to a multiple of 16
+ * stored so that the v_mfma_f32_16x16x4_f32 operand fragment of (16-row
+ * block, 16-deep k-step) is 1 KiB contiguous: element (m,k) at
+ * ((m/16 * K/16 + k/16) * 64 + m%16 + 16*((k%16)/4)) * 4 + k%4.  Weights are
+ * packed once at load; activations that feed a GEMM are written in it. */
+size_t hpa_frag_elems(int rows, int K);           /* padded element count */
+int hpa_pack_frag(const float* src, int rows, int K, int ld, float* dst); /* device -> device */
+int hpa_unpack_frag(const float* src, int rows, int K, float* dst, int ld);
+
+/* per-row LayerNorm statistics travel between kernels as partial sums
+ * (sum x, sum x^2) over 16-column tiles: stats[tile][Mp][2]; a consumer sums
+ * the `ntiles` partials of a row in order: mean = S1/C, var = S2/C - mean^2,
+ * rstd = 1/sqrtf(var + 1e-5) (layernorm_forward, paged_infer.c:49-89, in its
+ * one-pass form) and applies (x - mean) * rstd * w + b to its A fragments. */
+enum { HPA_FEPI_QKV = 0, HPA_FEPI_RESID = 1, HPA_FEPI_GELU = 2, HPA_FEPI_LOGITS = 3 };
+typedef struct {
+    /* A = x (frag layout, M rows, K cols), optionally LayerNorm'ed on the fly */
+    const float* x;
+    int M, K;
+    const float* ln_stats; /* NULL: no LN */
+    int ln_ntiles;
+    const float* ln_w;
+    const float* ln_b;
+    /* B = W^T, W (frag layout, N rows of K) */
+    const float* w;
+    int N;
+    const float* bias;    /* [N] or NULL */
+    int epilogue;         /* HPA_FEPI_* */
+    /* QKV: out = q [M][C] row-major; K/V rows appended to pool pages at pos[m] */
+    /* RESID: out = res_in + acc + bias (frag layout [M][N]); stats_out[N/16][Mp][2] */
+    /* GELU: out = gelu(acc + bias) (frag layout [M][N]) */
+    /* LOGITS: out = acc [M][N] row-major (ld = N); part_out[N/16 tiles][Mp][2] = (max, argmax) */
+    float* out;
+    const float* res_in;
+    float* stats_out;
+    float* part_out;
+    const HpaKVPool* pool;
+    int layer;
+    const int* block_table;
+    int bt_stride;
+    const int* pos;
+    int waves;            /* waves per workgroup sharing the K range: 4, 8 or 16; 0 = by shape */
+    int row_blocks;       /* 16-row blocks per workgroup: 1, 2 or 4; 0 = by shape */
+} HpaFusedGemm;
+int hpa_gemm_fused(const HpaFusedGemm* g);
+/* the launch shape hpa_gemm_fused picks when waves / row_blocks are 0:
+ * out2 = {waves, row_blocks} */
+void hpa_fused_pick(int M, int N, int K, int* out2);
+int hpa_fused_pick_waves(int M, int N, int K);
+/* residual = wte[tok] + wpe[pos] in frag layout [Mp][C], stats (1 tile) */
+int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const float* wpe,
+                   float* res_frag, float* stats, int B, int C);
+/* greedy id from the logits GEMM's per-tile (max, argmax) partials:
+ * lowest index wins ties; next[b], tokens[b] = next[b], pos[b] += 1 */
+int hpa_argmax_final(const float* part, int ntiles, int Mp, int B, int* next, int* tokens, int* pos);
+/* paged decode attention writing its output in frag layout ([B][C]) */
+int hpa_paged_attention_decode_frag(const float* q, const HpaKVPool* pool, int layer,
+                                    const int* block_table, int bt_stride, const int* pos,
+                                    float* out_frag, int B);
 
 /* ---------------- reference-layout kernels (drop-in compat) ----------------
  * Pages in the reference layout: token-major [block_size][C] per page

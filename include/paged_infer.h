@@ -145,6 +145,9 @@ int  gpt2_decode_fill_random(GPT2* model, int ctx, unsigned long long seed);
 int  gpt2_decode_reserve(GPT2* model, int ctx);
 /* rewind/advance positions (pages kept) */
 int  gpt2_decode_set_positions(GPT2* model, const int* pos);
+/* 1 (default): fused frag-layout kernels (5 launches per layer);
+ * 0: unfused split-K path (9 per layer), kept for A/B and as a cross-check */
+int  gpt2_decode_set_fused(GPT2* model, int enable);
 /* capture the step into a hipGraph and replay it (1) or launch eagerly (0) */
 int  gpt2_decode_set_graph(GPT2* model, int enable);
 /* attention-kernel timing with HIP events around every layer's attention
@@ -158,6 +161,16 @@ int*   gpt2_decode_next(GPT2* model);
 int    gpt2_decode_positions(GPT2* model, int* host_pos);
 /* the per-GEMM split-K chosen for this model/batch (qkv, attproj, fc, fcproj) */
 int    gpt2_decode_splits(GPT2* model, int* splits4);
+/* fused GEMM launch shapes [qkv, attproj, fc, fcproj, logits]: waves per
+ * workgroup (4/8/16) and 16-row blocks per workgroup (1/2/4).  set = 0
+ * copies them out; set = 1 applies the nonzero entries (NULL = keep) */
+int    gpt2_decode_gemm_config(GPT2* model, int* waves5, int* row_blocks5, int set);
+/* micro-batch lanes (fused path): the batch is cut into `lanes` groups of
+ * whole 16-row blocks, each running the step on its own stream so one
+ * group's attention overlaps another's GEMMs; results are identical to
+ * lanes = 1 row for row.  Returns nonzero for lanes outside 1..8. */
+int    gpt2_decode_set_lanes(GPT2* model, int lanes);
+int    gpt2_decode_lanes(GPT2* model);
 /* algorithmic HBM bytes one step reads+writes at the current positions
  * (SURVEY.md 8d formula) and the attention kernel's share of them */
 double gpt2_decode_step_bytes(GPT2* model, double* attention_bytes);

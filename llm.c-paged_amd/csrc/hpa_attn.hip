@@ -34,7 +34,7 @@ namespace {
 
 constexpr int HS = 64;
 
-template <int P, int NW>
+template <int P, int NW, bool FRAG>
 __global__ __launch_bounds__(NW * 64, 3) void paged_attn_decode_f32(
     const float* __restrict__ q, const float* __restrict__ layer_base, size_t page_elems, int NH,
     const int* __restrict__ block_table, int bt_stride, const int* __restrict__ pos,
@@ -132,12 +132,15 @@ __global__ __launch_bounds__(NW * 64, 3) void paged_attn_decode_f32(
     }
     l = hpa::wave_sum(l);
 
-    float* o = out + (size_t)b * NH * HS + h * HS;
+    // out[b][h*64 + 4*lane .. +3]: row-major, or the frag layout the next
+    // GEMM reads (4 consecutive columns stay one contiguous float4 there)
+    const size_t oi = FRAG ? hpa::frag_index(b, h * HS + 4 * (lane & 15), NH * HS)
+                           : ((size_t)b * NH + h) * HS + 4 * (lane & 15);
+    float4* o = reinterpret_cast<float4*>(out + oi);
     if constexpr (NW == 1) {
         if (lane < 16) {
             const float inv = l == 0.f ? 0.f : 1.f / l;
-            reinterpret_cast<float4*>(o)[lane] =
-                make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+            *o = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
         }
     } else {
         if (lane == 0) {
@@ -163,12 +166,12 @@ __global__ __launch_bounds__(NW * 64, 3) void paged_attn_decode_f32(
                 O.w = fmaf(a.w, f, O.w);
             }
             const float inv = L == 0.f ? 0.f : 1.f / L;
-            reinterpret_cast<float4*>(o)[lane] = make_float4(O.x * inv, O.y * inv, O.z * inv, O.w * inv);
+            *o = make_float4(O.x * inv, O.y * inv, O.z * inv, O.w * inv);
         }
     }
 }
 
-template <int P>
+template <int P, bool FRAG>
 int launch_decode(const float* q, const HpaKVPool* pool, int layer, const int* bt, int bt_stride,
                   const int* pos, float* out, int B, int nw) {
     const float* base = (const float*)pool->base + (size_t)layer * pool->layer_elems;
@@ -178,19 +181,19 @@ int launch_decode(const float* q, const HpaKVPool* pool, int layer, const int* b
     dim3 grid(B * pool->num_heads);
     switch (nw) {
         case 1:
-            paged_attn_decode_f32<P, 1><<<grid, 64, 0, hpa_stream()>>>(
+            paged_attn_decode_f32<P, 1, FRAG><<<grid, 64, 0, hpa_stream()>>>(
                 q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init);
             break;
         case 2:
-            paged_attn_decode_f32<P, 2><<<grid, 128, 0, hpa_stream()>>>(
+            paged_attn_decode_f32<P, 2, FRAG><<<grid, 128, 0, hpa_stream()>>>(
                 q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init);
             break;
         case 8:
-            paged_attn_decode_f32<P, 8><<<grid, 512, 0, hpa_stream()>>>(
+            paged_attn_decode_f32<P, 8, FRAG><<<grid, 512, 0, hpa_stream()>>>(
                 q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init);
             break;
         default:
-            paged_attn_decode_f32<P, 4><<<grid, 256, 0, hpa_stream()>>>(
+            paged_attn_decode_f32<P, 4, FRAG><<<grid, 256, 0, hpa_stream()>>>(
                 q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init);
             break;
     }
@@ -211,22 +214,40 @@ int hpa_set_attention_waves(int nw) {
     return 0;
 }
 
-int hpa_paged_attention_decode(const float* q, const HpaKVPool* pool, int layer,
-                               const int* block_table, int bt_stride, const int* pos, float* out,
-                               int B) {
+static int attn_dispatch(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
+                         int bt_stride, const int* pos, float* out, int B, bool frag) {
     HPA_REQUIRE(pool && pool->base, "pool not created");
     HPA_REQUIRE(pool->dtype == HPA_F32, "decode attention: fp32 pool expected");
     HPA_REQUIRE(pool->head_size == HS, "decode attention requires head_size 64");
     HPA_REQUIRE(layer >= 0 && layer < pool->num_layers, "layer out of range");
     HPA_REQUIRE(B > 0 && q && out && block_table && pos, "bad arguments");
     HPA_REQUIRE(((uintptr_t)q & 15) == 0 && ((uintptr_t)out & 15) == 0, "q/out must be 16-byte aligned");
+#define HPA_ATTN_CASE(PS)                                                                        \
+    case PS:                                                                                      \
+        return frag ? launch_decode<PS, true>(q, pool, layer, block_table, bt_stride, pos, out, B, \
+                                              g_attn_waves)                                        \
+                    : launch_decode<PS, false>(q, pool, layer, block_table, bt_stride, pos, out, B, \
+                                               g_attn_waves);
     switch (pool->page_size) {
-        case 8: return launch_decode<8>(q, pool, layer, block_table, bt_stride, pos, out, B, g_attn_waves);
-        case 16: return launch_decode<16>(q, pool, layer, block_table, bt_stride, pos, out, B, g_attn_waves);
-        case 32: return launch_decode<32>(q, pool, layer, block_table, bt_stride, pos, out, B, g_attn_waves);
-        case 64: return launch_decode<64>(q, pool, layer, block_table, bt_stride, pos, out, B, g_attn_waves);
+        HPA_ATTN_CASE(8)
+        HPA_ATTN_CASE(16)
+        HPA_ATTN_CASE(32)
+        HPA_ATTN_CASE(64)
         default: return hpa_fail(__FILE__, __LINE__, "page size must be 8, 16, 32 or 64");
     }
+#undef HPA_ATTN_CASE
+}
+
+int hpa_paged_attention_decode(const float* q, const HpaKVPool* pool, int layer,
+                               const int* block_table, int bt_stride, const int* pos, float* out,
+                               int B) {
+    return attn_dispatch(q, pool, layer, block_table, bt_stride, pos, out, B, false);
+}
+
+int hpa_paged_attention_decode_frag(const float* q, const HpaKVPool* pool, int layer,
+                                    const int* block_table, int bt_stride, const int* pos,
+                                    float* out_frag, int B) {
+    return attn_dispatch(q, pool, layer, block_table, bt_stride, pos, out_frag, B, true);
 }
 
 }  // extern "C"

@@ -1,0 +1,579 @@
+// hpa_fused.hip -- the decode layer's GEMMs with everything around them fused.
+//
+// One launch per weight GEMM of a GPT-2 block (reference gpt2_forward,
+// paged_infer.c:696-722, for one decode row per sequence):
+//   QKV     : LN1(x) . Wqkv^T + b -> q (row-major) and K/V appended into the
+//             sequence's page at pos[b]        (layernorm_forward :696,
+//             matmul_cached :706, add_to_cache :710 fused)
+//   ATTPROJ : res2 = res + att . Wap^T + b, LN2 row statistics   (:716-718)
+//   FC      : gelu(LN2(res2) . Wfc^T + b)                        (:718-720)
+//   FCPROJ  : res = res2 + fch . Wfp^T + b, next-LN row statistics (:721-722)
+//   LOGITS  : LNf(res) . wte^T, per-tile (max, argmax) for greedy (:725-727)
+//
+// Shape of the kernel (measured on MI355X, see DESIGN.md "GEMMs"):
+//  * At decode M = batch <= 64, each layer GEMM is 75..300 MFLOP.  fp32 MFMA
+//    runs at 256 FLOP/clk per CU, so a GEMM spread over only N/16 = 48 CUs
+//    is MFMA-bound per CU (fcproj: ~10 us) while 200 CUs idle.  The grid is
+//    therefore (16-column tile) x (16-row block): 4x the workgroups at
+//    M = 64, with no inter-workgroup reduction (an agent-scope hand-off costs
+//    an L2 writeback on this multi-XCD part); the K range is split over the
+//    workgroup's 4..16 waves and folded in LDS in a fixed order.
+//  * v_mfma_f32_16x16x4_f32 (exact fp32) on operands in the "frag" layout
+//    (hpa_internal.h frag_index): every fragment load is one 1 KiB
+//    contiguous dwordx4 burst; two trips of U k-steps in flight per wave;
+//    one accumulator chain per row block (summation order independent of
+//    the row split), MFMA dependency latency hidden by 4+ waves per SIMD.
+//  * LayerNorm is applied to the A fragments on load from per-row partial
+//    sums written by the previous kernel's epilogue; the epilogue's own
+//    operands (bias, residual) are loaded before the LDS fold so their
+//    latency overlaps it.
+#include <math.h>
+
+#include "hpa_internal.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int HPA_FUSED_LN_KMAX = 2048;  // LN'ed A operands: K <= 2048 (GPT-2 C <= 1600)
+
+struct FG {
+    const float* x;
+    int M, Mp, K, K16;
+    const float* ln_stats;
+    int ln_ntiles;
+    const float* ln_w;
+    const float* ln_b;
+    const float* w;
+    int N, ntn;
+    const float* bias;
+    float* out;
+    const float* res_in;
+    float* stats_out;
+    float* part_out;
+    float* kv_base;
+    size_t page_elems;
+    int NH, P;
+    const int* bt;
+    int bt_stride;
+    const int* pos;
+};
+
+__device__ __forceinline__ float4 ln4(float4 a, float mu, float rs, float4 g, float4 b) {
+    // paged_infer.c:80-81: n = s * (x - m); o = n * w + b
+    a.x = (rs * (a.x - mu)) * g.x + b.x;
+    a.y = (rs * (a.y - mu)) * g.y + b.y;
+    a.z = (rs * (a.z - mu)) * g.z + b.z;
+    a.w = (rs * (a.w - mu)) * g.w + b.w;
+    return a;
+}
+
+// MT = 16-row blocks per workgroup (1, 2 or 4), NW = waves sharing the K
+// range.  Grid (ntn, Mp/16/MT): one workgroup per (16-column tile, MT-block
+// row group).  MT = 1 spreads the MFMA work of a 64-row GEMM over 4x the
+// workgroups -- the per-CU fp32 MFMA rate, not bandwidth, bounds these
+// GEMMs when only N/16 CUs are busy.
+template <int NW, int EPI, int MT>
+__global__ __launch_bounds__(NW * 64) void gemm16_kernel(FG p) {
+    constexpr int NT = NW * 64;
+    constexpr int R = MT * 16;                 // rows per workgroup
+    // k-steps per trip (two trips in flight; register budget at 16 waves)
+    constexpr int U = NW >= 16 ? (MT == 4 ? 1 : 2) : (MT == 4 ? 2 : 4);
+    __shared__ __attribute__((aligned(16))) float smem[2 * HPA_FUSED_LN_KMAX + NW * MT * 256 + R * 17 + 10 * R];
+    float* lngb = smem;                  // LN weight [K], bias [K]
+    float* red = smem + 2 * HPA_FUSED_LN_KMAX;  // [NW][MT rb x 4 reg][64 lanes]
+    float* tile = red + NW * MT * 256;   // [R rows][17]
+    float* lnst = tile + R * 17;         // [R][2] mean, rstd
+    float* lnscr = lnst + 2 * R;         // [4R][2]
+
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int nt = blockIdx.x;
+    const int rb0 = blockIdx.y * MT;
+    const int row0 = rb0 * 16;
+    const int q4 = lane >> 4;  // which 4-k group of the 16-k step
+
+    // ---- this wave's contiguous k-step range
+    const int per = (p.K16 + NW - 1) / NW;
+    const int kb0 = w * per;
+    const int nsteps = max(0, min(p.K16, kb0 + per) - kb0);
+    const float4* __restrict__ wf = reinterpret_cast<const float4*>(p.w) + (size_t)nt * p.K16 * 64 + lane;
+    const float4* __restrict__ xf = reinterpret_cast<const float4*>(p.x) + (size_t)rb0 * p.K16 * 64 + lane;
+    const size_t rbs = (size_t)p.K16 * 64;  // float4 stride between row blocks
+    const bool use_ln = p.ln_stats != nullptr;
+    const float4* sg = reinterpret_cast<const float4*>(lngb) + q4;
+    const float4* sb = reinterpret_cast<const float4*>(lngb + HPA_FUSED_LN_KMAX) + q4;
+
+    struct Buf {
+        float4 w[U], x[U][MT];
+    };
+    Buf A, Bb;
+    auto load = [&](Buf& f, int t) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = kb0 + min(t * U + u, max(nsteps - 1, 0));  // clamped, unconditional
+            f.w[u] = wf[(size_t)k * 64];
+#pragma unroll
+            for (int r = 0; r < MT; ++r) f.x[u][r] = xf[r * rbs + (size_t)k * 64];
+        }
+    };
+    const int trips = (nsteps + U - 1) / U;
+    if (trips > 0) load(A, 0);  // first operands in flight during the LN prologue
+
+    // ---- LayerNorm statistics of this workgroup's R rows (4 threads per row)
+    float mu[MT], rs[MT];
+#pragma unroll
+    for (int r = 0; r < MT; ++r) mu[r] = rs[r] = 0.f;
+    if (use_ln) {
+        for (int i = threadIdx.x; i < p.K / 4; i += NT) {
+            reinterpret_cast<float4*>(lngb)[i] = reinterpret_cast<const float4*>(p.ln_w)[i];
+            reinterpret_cast<float4*>(lngb + HPA_FUSED_LN_KMAX)[i] = reinterpret_cast<const float4*>(p.ln_b)[i];
+        }
+        if (threadIdx.x < 4 * R) {
+            const int r = threadIdx.x >> 2, q = threadIdx.x & 3;
+            const int row = row0 + r;
+            float s1 = 0.f, s2 = 0.f;
+            if (row < p.M) {
+                for (int t0 = q; t0 < p.ln_ntiles; t0 += 32) {
+                    float a[8], b[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int t = min(t0 + 4 * j, p.ln_ntiles - 1);
+                        a[j] = p.ln_stats[((size_t)t * p.Mp + row) * 2];
+                        b[j] = p.ln_stats[((size_t)t * p.Mp + row) * 2 + 1];
+                    }
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        if (t0 + 4 * j < p.ln_ntiles) {
+                            s1 += a[j];
+                            s2 += b[j];
+                        }
+                }
+            }
+            lnscr[2 * threadIdx.x] = s1;
+            lnscr[2 * threadIdx.x + 1] = s2;
+        }
+        __syncthreads();
+        if (threadIdx.x < R) {
+            const float* t = lnscr + 8 * threadIdx.x;
+            const float s1 = (t[0] + t[2]) + (t[4] + t[6]);
+            const float s2 = (t[1] + t[3]) + (t[5] + t[7]);
+            const float m = s1 / p.K;
+            const float v = fmaxf(s2 / p.K - m * m, 0.f);
+            lnst[2 * threadIdx.x] = m;
+            lnst[2 * threadIdx.x + 1] = 1.0f / sqrtf(v + 1e-5f);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < MT; ++r) {
+            mu[r] = lnst[2 * (16 * r + (lane & 15))];
+            rs[r] = lnst[2 * (16 * r + (lane & 15)) + 1];
+        }
+    }
+
+    // one accumulator chain per row block: a row's summation order depends
+    // only on NW (the per-wave K ranges), never on MT or M -- so results are
+    // bit-identical across row splits and micro-batch lanes.  The dependent
+    // MFMA latency is covered by the other waves resident on the SIMD.
+    f32x4 acc[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto comp = [&](Buf& f, int t) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (t * U + u < nsteps) {
+                float4 xa[MT];
+                float4 g, b;
+                if (use_ln) {
+                    const int k = kb0 + t * U + u;
+                    g = sg[4 * k];
+                    b = sb[4 * k];
+                }
+#pragma unroll
+                for (int r = 0; r < MT; ++r) {
+                    xa[r] = f.x[u][r];
+                    if (use_ln) xa[r] = ln4(xa[r], mu[r], rs[r], g, b);
+                }
+                const float4 wv = f.w[u];
+#pragma unroll
+                for (int r = 0; r < MT; ++r)
+                    acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[r].x, wv.x, acc[r], 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < MT; ++r)
+                    acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[r].y, wv.y, acc[r], 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < MT; ++r)
+                    acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[r].z, wv.z, acc[r], 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < MT; ++r)
+                    acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[r].w, wv.w, acc[r], 0, 0, 0);
+            }
+        }
+    };
+    for (int t = 0; t < trips; t += 2) {
+        if (t + 1 < trips) load(Bb, t + 1);
+        comp(A, t);
+        if (t + 1 >= trips) break;
+        if (t + 2 < trips) load(A, t + 2);
+        comp(Bb, t + 1);
+    }
+
+    // ---- prefetch the epilogue operands of the elements this thread owns
+    // element e: rb = e>>8, reg = (e>>6)&3, l = e&63 -> row rb*16 + (l>>4)*4 + reg, col l&15
+    // (16x16 C/D map: col = lane & 15, row = 4*(lane >> 4) + reg)
+    constexpr int EPT = (MT * 256 + NT - 1) / NT;  // tile elements per thread
+    float pre_bias[EPT], pre_res[EPT];
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+        const int e = threadIdx.x + i * NT;
+        const int l = e & 63;
+        const int lrow = (e >> 8) * 16 + (l >> 4) * 4 + ((e >> 6) & 3);
+        const int row = row0 + lrow;
+        const int col = nt * 16 + (l & 15);
+        const bool in = e < MT * 256;
+        pre_bias[i] = (EPI != HPA_FEPI_LOGITS && in && p.bias && col < p.N) ? p.bias[col] : 0.f;
+        pre_res[i] = 0.f;
+        if (EPI == HPA_FEPI_RESID && in && row < p.M && col < p.N)
+            pre_res[i] = p.res_in[hpa::frag_index(row, col, p.N)];
+    }
+
+    // ---- fold the waves' accumulators (fixed order)
+#pragma unroll
+    for (int r = 0; r < MT; ++r)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) red[w * MT * 256 + (r * 4 + g) * 64 + lane] = acc[r][g];
+    __syncthreads();
+
+    constexpr bool rowstat = EPI == HPA_FEPI_RESID || EPI == HPA_FEPI_LOGITS;
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+        const int e = threadIdx.x + i * NT;
+        if (e < MT * 256) {
+            float val = red[e];
+#pragma unroll
+            for (int ww = 1; ww < NW; ++ww) val += red[ww * MT * 256 + e];
+            const int l = e & 63;
+            const int lrow = (e >> 8) * 16 + (l >> 4) * 4 + ((e >> 6) & 3);
+            const int lcol = l & 15;
+            const int row = row0 + lrow;
+            const int col = nt * 16 + lcol;
+            const bool live = row < p.M && col < p.N;
+            val += pre_bias[i];
+            if (EPI == HPA_FEPI_QKV) {
+                if (live) {
+                    const int C = p.N / 3;
+                    if (col < C) {
+                        p.out[(size_t)row * C + col] = val;
+                    } else {
+                        const int kv = col >= 2 * C;
+                        const int c = col - (kv ? 2 * C : C);
+                        const int hh = c >> 6, d = c & 63;
+                        const int ps = p.pos[row];
+                        const int page = p.bt[(size_t)row * p.bt_stride + ps / p.P];
+                        const int slot = ps % p.P;
+                        float* kvt = p.kv_base + (size_t)page * p.page_elems + ((size_t)kv * p.NH + hh) * p.P * 64;
+                        if (kv == 0)
+                            kvt[((d >> 2) * p.P + slot) * 4 + (d & 3)] = val;  // K: [chunk][slot][4]
+                        else
+                            kvt[slot * 64 + d] = val;  // V: [slot][64]
+                    }
+                }
+            } else if (EPI == HPA_FEPI_GELU) {
+                if (row < p.Mp && col < p.N) p.out[hpa::frag_index(row, col, p.N)] = live ? hpa::gelu_ref(val) : 0.f;
+            } else if (EPI == HPA_FEPI_RESID) {
+                val = live ? pre_res[i] + val : 0.f;  // residual_forward(out, res, proj)
+                if (row < p.Mp && col < p.N) p.out[hpa::frag_index(row, col, p.N)] = val;
+                tile[lrow * 17 + lcol] = val;
+            } else {  // LOGITS
+                if (live) p.out[(size_t)row * p.N + col] = val;
+                tile[lrow * 17 + lcol] = live ? val : -INFINITY;
+            }
+        }
+    }
+    if (rowstat) {
+        __syncthreads();
+        if (threadIdx.x < R) {
+            const int row = row0 + threadIdx.x;
+            const float* tr = tile + threadIdx.x * 17;
+            if (row < p.Mp) {
+                if (EPI == HPA_FEPI_RESID) {
+                    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) {
+                        s1 += tr[c];
+                        s2 += tr[c] * tr[c];
+                    }
+                    p.stats_out[((size_t)nt * p.Mp + row) * 2] = s1;
+                    p.stats_out[((size_t)nt * p.Mp + row) * 2 + 1] = s2;
+                } else {
+                    float bv = tr[0];
+                    int bi = 0;
+#pragma unroll
+                    for (int c = 1; c < 16; ++c)
+                        if (tr[c] > bv) {  // first max wins (paged_infer.c:937-951)
+                            bv = tr[c];
+                            bi = c;
+                        }
+                    p.part_out[((size_t)nt * p.Mp + row) * 2] = bv;
+                    p.part_out[((size_t)nt * p.Mp + row) * 2 + 1] = __int_as_float(nt * 16 + bi);
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- frag packing
+__global__ void pack_frag_kernel(const float* __restrict__ src, int rows, int K, int ld,
+                                 float4* __restrict__ dst, size_t n4) {
+    const size_t o = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (o >= n4) return;
+    const int lane = (int)(o & 63);
+    const size_t blk = o >> 6;  // rb * K16 + kb
+    const int K16 = K >> 4;
+    const int kb = (int)(blk % K16);
+    const int rb = (int)(blk / K16);
+    const int m = rb * 16 + (lane & 15);
+    const int k = kb * 16 + 4 * (lane >> 4);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (m < rows) v = *reinterpret_cast<const float4*>(src + (size_t)m * ld + k);
+    dst[o] = v;
+}
+
+__global__ void unpack_frag_kernel(const float4* __restrict__ src, int rows, int K,
+                                   float* __restrict__ dst, int ld, size_t n4) {
+    const size_t o = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (o >= n4) return;
+    const int lane = (int)(o & 63);
+    const size_t blk = o >> 6;
+    const int K16 = K >> 4;
+    const int kb = (int)(blk % K16);
+    const int rb = (int)(blk / K16);
+    const int m = rb * 16 + (lane & 15);
+    const int k = kb * 16 + 4 * (lane >> 4);
+    if (m < rows) *reinterpret_cast<float4*>(dst + (size_t)m * ld + k) = src[o];
+}
+
+// ---------------------------------------------------------------- embedding
+__global__ __launch_bounds__(256) void embed_frag_kernel(const int* __restrict__ tokens,
+                                                         const int* __restrict__ pos,
+                                                         const float* __restrict__ wte,
+                                                         const float* __restrict__ wpe,
+                                                         float* __restrict__ res, float* __restrict__ stats,
+                                                         int C) {
+    __shared__ float sc[8];
+    const int b = blockIdx.x;
+    const float* te = wte + (size_t)tokens[b] * C;
+    const float* pe = wpe + (size_t)pos[b] * C;
+    float s1 = 0.f, s2 = 0.f;
+    for (int c = threadIdx.x; c < C; c += 256) {
+        const float x = te[c] + pe[c];  // encoder_forward (paged_infer.c:43), absolute position
+        res[hpa::frag_index(b, c, C)] = x;
+        s1 += x;
+        s2 += x * x;
+    }
+    s1 = hpa::wave_sum(s1);
+    s2 = hpa::wave_sum(s2);
+    if ((threadIdx.x & 63) == 0) {
+        sc[threadIdx.x >> 6] = s1;
+        sc[4 + (threadIdx.x >> 6)] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        stats[(size_t)b * 2] = (sc[0] + sc[1]) + (sc[2] + sc[3]);
+        stats[(size_t)b * 2 + 1] = (sc[4] + sc[5]) + (sc[6] + sc[7]);
+    }
+}
+
+// ---------------------------------------------------------------- greedy
+__global__ __launch_bounds__(256) void argmax_final_kernel(const float* __restrict__ part, int ntiles,
+                                                           int Mp, int* __restrict__ next,
+                                                           int* __restrict__ tokens,
+                                                           int* __restrict__ pos) {
+    __shared__ float sv[4];
+    __shared__ int si[4];
+    const int b = blockIdx.x;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int t = threadIdx.x; t < ntiles; t += 256) {
+        const float v = part[((size_t)t * Mp + b) * 2];
+        const int i = __float_as_int(part[((size_t)t * Mp + b) * 2 + 1]);
+        if (v > bv) {  // tiles visited in increasing index order per thread
+            bv = v;
+            bi = i;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float v2 = __shfl_xor(bv, o, 64);
+        const int i2 = __shfl_xor(bi, o, 64);
+        if (v2 > bv || (v2 == bv && i2 < bi)) {
+            bv = v2;
+            bi = i2;
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+        sv[threadIdx.x >> 6] = bv;
+        si[threadIdx.x >> 6] = bi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float v = sv[0];
+        int i = si[0];
+        for (int k = 1; k < 4; ++k)
+            if (sv[k] > v || (sv[k] == v && si[k] < i)) {
+                v = sv[k];
+                i = si[k];
+            }
+        if (i == 0x7fffffff) i = 0;
+        next[b] = i;
+        if (tokens) tokens[b] = i;
+        if (pos) pos[b] += 1;
+    }
+}
+
+template <int NW, int MT>
+int launch16(const FG& p, int epi) {
+    dim3 grid(p.ntn, p.Mp / 16 / MT), block(NW * 64);
+    switch (epi) {
+        case HPA_FEPI_QKV: gemm16_kernel<NW, HPA_FEPI_QKV, MT><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_RESID: gemm16_kernel<NW, HPA_FEPI_RESID, MT><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_GELU: gemm16_kernel<NW, HPA_FEPI_GELU, MT><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_LOGITS: gemm16_kernel<NW, HPA_FEPI_LOGITS, MT><<<grid, block, 0, hpa_stream()>>>(p); break;
+        default: return hpa_fail(__FILE__, __LINE__, "gemm_fused: unknown epilogue");
+    }
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int NW>
+int launch16_mt(const FG& p, int epi, int mt) {
+    switch (mt) {
+        case 1: return launch16<NW, 1>(p, epi);
+        case 2: return launch16<NW, 2>(p, epi);
+        case 4: return launch16<NW, 4>(p, epi);
+        default: return hpa_fail(__FILE__, __LINE__, "gemm_fused: row_blocks must be 1, 2 or 4");
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t hpa_frag_elems(int rows, int K) { return (size_t)((rows + 15) / 16) * 16 * (size_t)K; }
+
+int hpa_pack_frag(const float* src, int rows, int K, int ld, float* dst) {
+    HPA_REQUIRE(src && dst && rows > 0 && K > 0 && K % 16 == 0 && ld >= K && ld % 4 == 0,
+                "pack_frag: bad shape (K % 16, ld % 4)");
+    const size_t n4 = hpa_frag_elems(rows, K) / 4;
+    pack_frag_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, hpa_stream()>>>(
+        src, rows, K, ld, reinterpret_cast<float4*>(dst), n4);
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+int hpa_unpack_frag(const float* src, int rows, int K, float* dst, int ld) {
+    HPA_REQUIRE(src && dst && rows > 0 && K > 0 && K % 16 == 0 && ld >= K && ld % 4 == 0,
+                "unpack_frag: bad shape");
+    const size_t n4 = hpa_frag_elems(rows, K) / 4;
+    unpack_frag_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, hpa_stream()>>>(
+        reinterpret_cast<const float4*>(src), rows, K, dst, ld, n4);
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+// launch shape by GEMM shape: one 16-row block per workgroup for the layer
+// GEMMs (spreads the fp32 MFMA work over >= 4 * N/16 workgroups), four for
+// logits (3142 column tiles already fill the chip; amortises the A reads);
+// waves sharing the K range: enough k-steps per wave to amortise the fold
+void hpa_fused_pick(int M, int N, int K, int* out2) {
+    (void)M;
+    const int ntn = (N + 15) / 16;
+    const int k16 = K / 16;
+    if (ntn >= 1024) {
+        out2[0] = 4;
+        out2[1] = 4;
+        return;
+    }
+    out2[1] = 1;
+    out2[0] = k16 >= 96 ? 8 : 4;
+}
+
+int hpa_fused_pick_waves(int M, int N, int K) {
+    int p[2];
+    hpa_fused_pick(M, N, K, p);
+    return p[0];
+}
+
+int hpa_gemm_fused(const HpaFusedGemm* g) {
+    HPA_REQUIRE(g && g->x && g->w && g->out, "gemm_fused: null operand");
+    HPA_REQUIRE(g->M > 0 && g->N > 0 && g->K > 0 && g->K % 16 == 0, "gemm_fused: K % 16 != 0");
+    HPA_REQUIRE(!g->ln_stats || (g->ln_w && g->ln_b && g->ln_ntiles > 0), "gemm_fused: LN params");
+    HPA_REQUIRE(!g->ln_stats || g->K <= HPA_FUSED_LN_KMAX, "gemm_fused: LN over K > 2048");
+    FG p;
+    p.x = g->x;
+    p.M = g->M;
+    p.Mp = (g->M + 15) / 16 * 16;
+    p.K = g->K;
+    p.K16 = g->K / 16;
+    p.ln_stats = g->ln_stats;
+    p.ln_ntiles = g->ln_ntiles;
+    p.ln_w = g->ln_w;
+    p.ln_b = g->ln_b;
+    p.w = g->w;
+    p.N = g->N;
+    p.ntn = (g->N + 15) / 16;
+    p.bias = g->bias;
+    p.out = g->out;
+    p.res_in = g->res_in;
+    p.stats_out = g->stats_out;
+    p.part_out = g->part_out;
+    p.kv_base = nullptr;
+    p.page_elems = 0;
+    p.NH = 0;
+    p.P = 1;
+    p.bt = g->block_table;
+    p.bt_stride = g->bt_stride;
+    p.pos = g->pos;
+    if (g->epilogue == HPA_FEPI_QKV) {
+        const HpaKVPool* pool = g->pool;
+        HPA_REQUIRE(pool && pool->base && pool->dtype == HPA_F32 && pool->head_size == 64,
+                    "gemm_fused QKV: fp32 pool with head_size 64");
+        HPA_REQUIRE(g->N == 3 * pool->num_heads * 64, "gemm_fused QKV: N != 3*C");
+        HPA_REQUIRE(g->layer >= 0 && g->layer < pool->num_layers, "gemm_fused QKV: layer");
+        HPA_REQUIRE(g->block_table && g->pos, "gemm_fused QKV: block table / positions");
+        p.kv_base = (float*)pool->base + (size_t)g->layer * pool->layer_elems;
+        p.page_elems = pool->page_elems;
+        p.NH = pool->num_heads;
+        p.P = pool->page_size;
+    }
+    if (g->epilogue == HPA_FEPI_RESID) HPA_REQUIRE(g->res_in && g->stats_out, "gemm_fused RESID");
+    if (g->epilogue == HPA_FEPI_LOGITS) HPA_REQUIRE(g->part_out, "gemm_fused LOGITS: part_out");
+    int pick[2];
+    hpa_fused_pick(g->M, g->N, g->K, pick);
+    const int nw = g->waves ? g->waves : pick[0];
+    int mt = g->row_blocks ? g->row_blocks : pick[1];
+    HPA_REQUIRE(mt == 1 || mt == 2 || mt == 4, "gemm_fused: row_blocks must be 1, 2 or 4");
+    while ((p.Mp / 16) % mt) mt >>= 1;  // row blocks of this M
+    switch (nw) {
+        case 4: return launch16_mt<4>(p, g->epilogue, mt);
+        case 8: return launch16_mt<8>(p, g->epilogue, mt);
+        case 16: return launch16_mt<16>(p, g->epilogue, mt);
+        default: return hpa_fail(__FILE__, __LINE__, "gemm_fused: waves must be 4, 8 or 16");
+    }
+}
+
+int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const float* wpe,
+                   float* res_frag, float* stats, int B, int C) {
+    HPA_REQUIRE(B > 0 && C > 0 && C % 16 == 0, "embed_frag: bad shape");
+    embed_frag_kernel<<<B, 256, 0, hpa_stream()>>>(tokens, pos, wte, wpe, res_frag, stats, C);
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+int hpa_argmax_final(const float* part, int ntiles, int Mp, int B, int* next, int* tokens, int* pos) {
+    HPA_REQUIRE(part && next && B > 0 && ntiles > 0 && Mp >= B, "argmax_final: bad arguments");
+    argmax_final_kernel<<<B, 256, 0, hpa_stream()>>>(part, ntiles, Mp, next, tokens, pos);
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+}  // extern "C"

@@ -40,6 +40,20 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
+// "frag" layout of a [rows][K] fp32 matrix (rows padded to 16, K % 16 == 0),
+// the operand layout of v_mfma_f32_16x16x4_f32 loaded 16 bytes per lane:
+// element (m, k) sits at lane (m%16) + 16*((k%16)/4), float (k%4) of the
+// 1 KiB fragment of (16-row block m/16, 16-deep k-step k/16); fragment
+// (rb, kb) starts at ((rb * K/16 + kb) * 64) float4s.  A wave loads one
+// fragment as one contiguous 1 KiB dwordx4 burst.  Used for streamed weights
+// and for every activation that feeds a GEMM.
+__device__ __host__ __forceinline__ size_t frag_index(int m, int k, int K) {
+    return ((((size_t)(m >> 4) * (size_t)(K >> 4) + (size_t)(k >> 4)) * 64 +
+             (size_t)((m & 15) + 16 * ((k >> 2) & 3)))
+            << 2) +
+           (size_t)(k & 3);
+}
+
 // GELU of the reference (paged_infer.c:243-251): 0.5 x (1 + tanh(sqrt(2/pi)(x + 0.044715 x^3)))
 __device__ __forceinline__ float gelu_ref(float x) {
     // sqrtf(2.0f / M_PI) as the reference computes it: float(2/pi) then sqrtf

@@ -146,6 +146,34 @@ void* hpa_event_create(void) {
     return (void*)e;
 }
 
+void* hpa_event_create_nt(void) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+        hpa_fail(__FILE__, __LINE__, "hipEventCreateWithFlags failed");
+        return nullptr;
+    }
+    return (void*)e;
+}
+
+void* hpa_stream_create(void) {
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        hpa_fail(__FILE__, __LINE__, "hipStreamCreateWithFlags failed");
+        return nullptr;
+    }
+    return (void*)s;
+}
+
+int hpa_stream_destroy(void* s) {
+    if (s) HPA_CHECK(hipStreamDestroy((hipStream_t)s));
+    return 0;
+}
+
+int hpa_stream_wait_event(void* ev) {
+    HPA_CHECK(hipStreamWaitEvent(g_stream, (hipEvent_t)ev, 0));
+    return 0;
+}
+
 int hpa_event_record(void* ev) {
     HPA_CHECK(hipEventRecord((hipEvent_t)ev, g_stream));
     return 0;

@@ -407,6 +407,23 @@ int gpt2_write_checkpoint(const char* path, GPT2Config c, const float* host_para
 /* ------------------------------------------------------------------------ */
 /* decode engine                                                            */
 /* ------------------------------------------------------------------------ */
+/* a micro-batch lane: a contiguous group of the batch's sequences (rows
+ * r0..r0+B-1) that runs the whole fused step on its own stream with its own
+ * activations, so one lane's HBM-bound attention overlaps another lane's
+ * latency-bound GEMMs.  Lane 0 runs on the launch stream; the others fork from
+ * it and join back (captured into the same graph as parallel branches). */
+#define DEC_MAX_LANES 8
+typedef struct {
+    int r0, B, Mp;
+    float *res, *res2, *att, *fch, *st1, *st2, *part;
+    void* stream; /* NULL for lane 0 (the launch stream) */
+    void* ev_join;
+} DecLane;
+
+struct GPT2Decode;
+/* attention profiling events of (layer, lane): k = 0 start, 1 stop */
+#define PROF_EV(d, l, lane, k) ((d)->prof_ev[(((size_t)(l) * DEC_MAX_LANES + (lane)) << 1) + (k)])
+
 struct GPT2Decode {
     int B, P, max_ctx, max_pages;
     HpaKVPool pool;
@@ -422,9 +439,17 @@ struct GPT2Decode {
     int* h_bt_stage;  /* pinned staging for block-table rows */
     float *d_res, *d_res2, *d_ln, *d_q, *d_att, *d_fch, *d_part, *d_logits;
     int split[4];     /* qkv, attproj, fc, fcproj */
+    /* fused path (hpa_gemm_fused): frag-layout weights and activations */
+    int fused;
+    float* d_wpack;   /* packed qkvw, attprojw, fcw, fcprojw of every layer, then wte */
+    size_t wpack_off[5]; /* per-layer strides (0..3) and wte offset (4) */
+    int fwaves[5];    /* waves per workgroup: qkv, attproj, fc, fcproj, logits */
+    int frb[5];       /* 16-row blocks per workgroup, same order */
+    DecLane lanes[DEC_MAX_LANES];
+    int nlanes;
+    void* ev_fork;
     int use_graph;
     void* graph;
-    int graph_valid;
     /* per-layer HIP events around the attention launch (eager profiling) */
     void** prof_ev;   /* [L][2] or NULL */
     double prof_ms;   /* accumulated attention kernel time */
@@ -444,9 +469,61 @@ static void pool_view_release(void* ctx, int page, int kv, void* p) {
 
 static void dec_prof_free(GPT2Decode* d, int L) {
     if (!d->prof_ev) return;
-    for (int i = 0; i < 2 * L; i++) hpa_event_destroy(d->prof_ev[i]);
+    for (size_t i = 0; i < 2 * (size_t)L * DEC_MAX_LANES; i++) hpa_event_destroy(d->prof_ev[i]);
     free(d->prof_ev);
     d->prof_ev = NULL;
+}
+
+static void dec_lanes_free(GPT2Decode* d) {
+    for (int i = 0; i < d->nlanes; i++) {
+        DecLane* ln = &d->lanes[i];
+        hpa_free(ln->res); hpa_free(ln->res2); hpa_free(ln->att); hpa_free(ln->fch);
+        hpa_free(ln->st1); hpa_free(ln->st2); hpa_free(ln->part);
+        hpa_stream_destroy(ln->stream);
+        hpa_event_destroy(ln->ev_join);
+        memset(ln, 0, sizeof(*ln));
+    }
+    d->nlanes = 0;
+}
+
+/* split the batch into up to `n` lanes of whole 16-row blocks */
+static int dec_lanes_alloc(GPT2Decode* d, int n, int C, int V) {
+    dec_lanes_free(d);
+    int blocks = (d->B + 15) / 16;
+    if (n < 1) n = 1;
+    if (n > DEC_MAX_LANES) n = DEC_MAX_LANES;
+    if (n > blocks) n = blocks;
+    const int per = (blocks + n - 1) / n; /* 16-row blocks per lane */
+    const int ct = C / 16;
+    int r0 = 0;
+    for (int i = 0; i < n && r0 < d->B; i++) {
+        DecLane* ln = &d->lanes[i];
+        ln->r0 = r0;
+        ln->B = d->B - r0 < per * 16 ? d->B - r0 : per * 16;
+        ln->Mp = (ln->B + 15) / 16 * 16;
+        r0 += ln->B;
+        d->nlanes = i + 1;
+        const size_t Mp = ln->Mp;
+        ln->res = (float*)hpa_malloc(Mp * C * 4);
+        ln->res2 = (float*)hpa_malloc(Mp * C * 4);
+        ln->att = (float*)hpa_malloc(Mp * C * 4);
+        ln->fch = (float*)hpa_malloc(Mp * 4 * C * 4);
+        ln->st1 = (float*)hpa_malloc((size_t)ct * Mp * 2 * 4);
+        ln->st2 = (float*)hpa_malloc((size_t)ct * Mp * 2 * 4);
+        ln->part = (float*)hpa_malloc((size_t)((V + 15) / 16) * Mp * 2 * 4);
+        ln->ev_join = hpa_event_create_nt();
+        if (i > 0) ln->stream = hpa_stream_create();
+        if (!ln->res || !ln->res2 || !ln->att || !ln->fch || !ln->st1 || !ln->st2 || !ln->part ||
+            !ln->ev_join || (i > 0 && !ln->stream))
+            return 1;
+        /* padded rows stay zero forever */
+        if (hpa_memset_async(ln->res, 0, Mp * C * 4) || hpa_memset_async(ln->res2, 0, Mp * C * 4) ||
+            hpa_memset_async(ln->att, 0, Mp * C * 4) || hpa_memset_async(ln->fch, 0, Mp * 4 * C * 4) ||
+            hpa_memset_async(ln->st1, 0, (size_t)ct * Mp * 2 * 4) ||
+            hpa_memset_async(ln->st2, 0, (size_t)ct * Mp * 2 * 4))
+            return 1;
+    }
+    return hpa_synchronize();
 }
 
 static void dec_free(GPT2Decode* d) {
@@ -457,6 +534,9 @@ static void dec_free(GPT2Decode* d) {
     hpa_free(d->d_bt); hpa_free(d->d_pos); hpa_free(d->d_tokens); hpa_free(d->d_next);
     hpa_free(d->d_res); hpa_free(d->d_res2); hpa_free(d->d_ln); hpa_free(d->d_q);
     hpa_free(d->d_att); hpa_free(d->d_fch); hpa_free(d->d_part); hpa_free(d->d_logits);
+    hpa_free(d->d_wpack);
+    dec_lanes_free(d);
+    hpa_event_destroy(d->ev_fork);
     hpa_host_free(d->h_stage);
     hpa_host_free(d->h_bt_stage);
     free(d->h_pos);
@@ -470,6 +550,47 @@ void gpt2_decode_free(GPT2* model) {
         dec_free(model->decode);
         model->decode = NULL;
     }
+}
+
+/* fused path state: frag-packed weights (packed once; the weights stay also
+ * in checkpoint layout for the embedding gather and the reference API),
+ * frag-layout activations and LN statistics */
+static int dec_init_fused(GPT2* model, GPT2Decode* d) {
+    const GPT2Config c = model->config;
+    const int B = d->B, C = c.channels, L = c.num_layers, V = c.vocab_size;
+    const ParameterTensors* w = &model->params;
+    d->fused = 1;
+    size_t e_qkv = hpa_frag_elems(3 * C, C), e_ap = hpa_frag_elems(C, C);
+    size_t e_fc = hpa_frag_elems(4 * C, C), e_fp = hpa_frag_elems(C, 4 * C);
+    size_t e_layer = e_qkv + e_ap + e_fc + e_fp;
+    d->wpack_off[0] = 0;
+    d->wpack_off[1] = e_qkv;
+    d->wpack_off[2] = e_qkv + e_ap;
+    d->wpack_off[3] = e_qkv + e_ap + e_fc;
+    d->wpack_off[4] = e_layer * L; /* wte */
+    size_t total = d->wpack_off[4] + hpa_frag_elems(V, C);
+    d->d_wpack = (float*)hpa_malloc(total * 4);
+    if (!d->d_wpack) return 1;
+    for (int l = 0; l < L; l++) {
+        float* base = d->d_wpack + e_layer * l;
+        const size_t lc = (size_t)l * C;
+        if (hpa_pack_frag(w->qkvw + lc * 3 * C, 3 * C, C, C, base + d->wpack_off[0]) ||
+            hpa_pack_frag(w->attprojw + lc * C, C, C, C, base + d->wpack_off[1]) ||
+            hpa_pack_frag(w->fcw + lc * 4 * C, 4 * C, C, C, base + d->wpack_off[2]) ||
+            hpa_pack_frag(w->fcprojw + lc * 4 * C, C, 4 * C, 4 * C, base + d->wpack_off[3]))
+            return 1;
+    }
+    if (hpa_pack_frag(w->wte, V, C, C, d->d_wpack + d->wpack_off[4])) return 1;
+    const int shp[5][2] = {{3 * C, C}, {C, C}, {4 * C, C}, {C, 4 * C}, {V, C}};
+    for (int i = 0; i < 5; i++) {
+        int pk[2];
+        hpa_fused_pick(B, shp[i][0], shp[i][1], pk);
+        d->fwaves[i] = pk[0];
+        d->frb[i] = pk[1];
+    }
+    d->ev_fork = hpa_event_create_nt();
+    if (!d->ev_fork) return 1;
+    return dec_lanes_alloc(d, 1, C, V);
 }
 
 int gpt2_decode_init(GPT2* model, int B, int page_size, int max_ctx) {
@@ -562,6 +683,10 @@ int gpt2_decode_init(GPT2* model, int B, int page_size, int max_ctx) {
         dec_free(d);
         return 1;
     }
+    if (dec_init_fused(model, d)) {
+        dec_free(d);
+        return 1;
+    }
     for (size_t i = 0; i < btn; i++) d->h_bt_stage[i] = -1;
     if (hpa_memcpy(d->d_bt, d->h_bt_stage, btn * sizeof(int)) ||
         hpa_memset_async(d->d_pos, 0, B * sizeof(int)) ||
@@ -614,7 +739,7 @@ static int dec_ensure_pages(GPT2Decode* d) {
     return 0;
 }
 
-static int dec_launch(GPT2* model) {
+static int dec_launch_unfused(GPT2* model) {
     GPT2Decode* d = model->decode;
     const GPT2Config c = model->config;
     const int B = d->B, C = c.channels, L = c.num_layers, V = c.vocab_size;
@@ -630,10 +755,10 @@ static int dec_launch(GPT2* model) {
         rc |= hpa_qkv_append(d->d_part, s, s > 1 ? w->qkvb + 3 * lc : NULL, d->d_q, &d->pool, l,
                              d->d_bt, d->bt_stride, d->d_pos, B, C);
         /* paged attention over 0..pos[b] */
-        if (d->prof_ev) rc |= hpa_event_record(d->prof_ev[2 * l]);
+        if (d->prof_ev) rc |= hpa_event_record(PROF_EV(d, l, 0, 0));
         rc |= hpa_paged_attention_decode(d->d_q, &d->pool, l, d->d_bt, d->bt_stride, d->d_pos,
                                          d->d_att, B);
-        if (d->prof_ev) rc |= hpa_event_record(d->prof_ev[2 * l + 1]);
+        if (d->prof_ev) rc |= hpa_event_record(PROF_EV(d, l, 0, 1));
         /* attn proj + residual + LN2 */
         s = d->split[1];
         rc |= hpa_gemm_f32(d->d_att, C, w->attprojw + lc * C, w->attprojb + lc, d->d_part, C, B, C, C,
@@ -664,6 +789,125 @@ static int dec_launch(GPT2* model) {
     rc |= hpa_argmax_advance(d->d_logits, B, V, d->d_next, d->d_tokens, d->d_pos);
     return rc;
 }
+
+static int fgemm(GPT2Decode* d, const DecLane* ln, const float* x, int K, const float* st, int st_tiles,
+                 const float* lw, const float* lb, const float* wpk, int N, const float* bias, int gi,
+                 int epi, float* out, const float* res_in, float* stats_out, float* part_out, int layer) {
+    HpaFusedGemm g;
+    memset(&g, 0, sizeof(g));
+    g.x = x;
+    g.M = ln->B;
+    g.K = K;
+    g.ln_stats = st;
+    g.ln_ntiles = st_tiles;
+    g.ln_w = lw;
+    g.ln_b = lb;
+    g.w = wpk;
+    g.N = N;
+    g.bias = bias;
+    g.waves = d->fwaves[gi];
+    g.row_blocks = d->frb[gi];
+    g.epilogue = epi;
+    g.out = out;
+    g.res_in = res_in;
+    g.stats_out = stats_out;
+    g.part_out = part_out;
+    g.pool = &d->pool;
+    g.layer = layer;
+    g.block_table = d->d_bt + (size_t)ln->r0 * d->bt_stride;
+    g.bt_stride = d->bt_stride;
+    g.pos = d->d_pos + ln->r0;
+    return hpa_gemm_fused(&g);
+}
+
+/* one lane's fused step on the current stream: embed, then per layer
+ * QKV(+LN1, +KV append) -> attention -> attproj(+residual, LN2 stats) ->
+ * fc(+LN2, +GELU) -> fcproj(+residual, next LN stats), then logits(+LNf,
+ * argmax partials) and the greedy pick: 5 launches per layer + 3 */
+static int dec_launch_lane(GPT2* model, int li) {
+    GPT2Decode* d = model->decode;
+    const DecLane* ln = &d->lanes[li];
+    const GPT2Config c = model->config;
+    const int C = c.channels, L = c.num_layers, V = c.vocab_size;
+    const ParameterTensors* w = &model->params;
+    const int ct = C / 16, r0 = ln->r0;
+    const size_t e_layer = d->wpack_off[3] + hpa_frag_elems(C, 4 * C);
+    int* pos = d->d_pos + r0;
+    const int* bt = d->d_bt + (size_t)r0 * d->bt_stride;
+    float* q = d->d_q + (size_t)r0 * C;
+    int rc = hpa_embed_frag(d->d_tokens + r0, pos, w->wte, w->wpe, ln->res, ln->st1, ln->B, C);
+    int st_tiles = 1;
+    for (int l = 0; l < L && !rc; l++) {
+        const size_t lc = (size_t)l * C;
+        const float* wl = d->d_wpack + e_layer * l;
+        rc |= fgemm(d, ln, ln->res, C, ln->st1, st_tiles, w->ln1w + lc, w->ln1b + lc, wl + d->wpack_off[0],
+                    3 * C, w->qkvb + 3 * lc, 0, HPA_FEPI_QKV, q, NULL, NULL, NULL, l);
+        if (d->prof_ev) rc |= hpa_event_record(PROF_EV(d, l, li, 0));
+        rc |= hpa_paged_attention_decode_frag(q, &d->pool, l, bt, d->bt_stride, pos, ln->att, ln->B);
+        if (d->prof_ev) rc |= hpa_event_record(PROF_EV(d, l, li, 1));
+        rc |= fgemm(d, ln, ln->att, C, NULL, 0, NULL, NULL, wl + d->wpack_off[1], C, w->attprojb + lc,
+                    1, HPA_FEPI_RESID, ln->res2, ln->res, ln->st2, NULL, l);
+        rc |= fgemm(d, ln, ln->res2, C, ln->st2, ct, w->ln2w + lc, w->ln2b + lc, wl + d->wpack_off[2],
+                    4 * C, w->fcb + 4 * lc, 2, HPA_FEPI_GELU, ln->fch, NULL, NULL, NULL, l);
+        rc |= fgemm(d, ln, ln->fch, 4 * C, NULL, 0, NULL, NULL, wl + d->wpack_off[3], C, w->fcprojb + lc,
+                    3, HPA_FEPI_RESID, ln->res, ln->res2, ln->st1, NULL, l);
+        st_tiles = ct;
+    }
+    rc |= fgemm(d, ln, ln->res, C, ln->st1, st_tiles, w->lnfw, w->lnfb, d->d_wpack + d->wpack_off[4], V,
+                NULL, 4, HPA_FEPI_LOGITS, d->d_logits + (size_t)r0 * V, NULL, NULL, ln->part, 0);
+    rc |= hpa_argmax_final(ln->part, (V + 15) / 16, ln->Mp, ln->B, d->d_next + r0, d->d_tokens + r0, pos);
+    return rc;
+}
+
+/* all lanes: lanes 1.. fork from the launch stream, run concurrently with
+ * lane 0, and join back before the step completes */
+static int dec_launch_fused(GPT2* model) {
+    GPT2Decode* d = model->decode;
+    if (d->nlanes == 1) return dec_launch_lane(model, 0);
+    void* main_stream = hpa_get_stream();
+    int rc = hpa_event_record(d->ev_fork);
+    for (int i = 1; i < d->nlanes && !rc; i++) {
+        hpa_set_stream(d->lanes[i].stream);
+        rc |= hpa_stream_wait_event(d->ev_fork);
+        rc |= dec_launch_lane(model, i);
+        rc |= hpa_event_record(d->lanes[i].ev_join);
+    }
+    hpa_set_stream(main_stream);
+    if (rc) return rc;
+    rc |= dec_launch_lane(model, 0);
+    for (int i = 1; i < d->nlanes; i++) rc |= hpa_stream_wait_event(d->lanes[i].ev_join);
+    return rc;
+}
+
+static int dec_launch(GPT2* model) {
+    return model->decode->fused ? dec_launch_fused(model) : dec_launch_unfused(model);
+}
+
+/* 1: fused frag-layout path (default); 0: the unfused split-K path */
+int gpt2_decode_set_fused(GPT2* model, int enable) {
+    GPT2Decode* d = model->decode;
+    if (!d) return 1;
+    if (d->graph) {
+        hpa_graph_destroy(d->graph);
+        d->graph = NULL;
+    }
+    d->fused = enable ? 1 : 0;
+    return 0;
+}
+
+/* micro-batch lanes of the fused path (1..8; rounded to whole 16-row blocks) */
+int gpt2_decode_set_lanes(GPT2* model, int lanes) {
+    GPT2Decode* d = model->decode;
+    if (!d || lanes < 1 || lanes > DEC_MAX_LANES) return 1;
+    if (hpa_synchronize()) return 1;
+    if (d->graph) {
+        hpa_graph_destroy(d->graph);
+        d->graph = NULL;
+    }
+    return dec_lanes_alloc(d, lanes, model->config.channels, model->config.vocab_size);
+}
+
+int gpt2_decode_lanes(GPT2* model) { return model->decode ? model->decode->nlanes : 0; }
 
 int gpt2_decode_set_graph(GPT2* model, int enable) {
     GPT2Decode* d = model->decode;
@@ -767,6 +1011,34 @@ int gpt2_decode_splits(GPT2* model, int* s4) {
     GPT2Decode* d = model->decode;
     if (!d) return 1;
     memcpy(s4, d->split, sizeof(d->split));
+    return 0;
+}
+
+/* launch shapes of the fused GEMMs (qkv, attproj, fc, fcproj, logits):
+ * set = 0 copies them out; set = 1 applies the nonzero entries */
+int gpt2_decode_gemm_config(GPT2* model, int* waves5, int* row_blocks5, int set) {
+    GPT2Decode* d = model->decode;
+    if (!d) return 1;
+    if (!set) {
+        if (waves5) memcpy(waves5, d->fwaves, sizeof(d->fwaves));
+        if (row_blocks5) memcpy(row_blocks5, d->frb, sizeof(d->frb));
+        return 0;
+    }
+    for (int i = 0; i < 5; i++) {
+        if (waves5 && waves5[i] != 0 && waves5[i] != 4 && waves5[i] != 8 && waves5[i] != 16) return 1;
+        if (row_blocks5 && row_blocks5[i] != 0 && row_blocks5[i] != 1 && row_blocks5[i] != 2 &&
+            row_blocks5[i] != 4)
+            return 1;
+    }
+    for (int i = 0; i < 5; i++) {
+        if (waves5 && waves5[i]) d->fwaves[i] = waves5[i];
+        if (row_blocks5 && row_blocks5[i]) d->frb[i] = row_blocks5[i];
+    }
+    if (d->graph) { /* recapture with the new launch shapes */
+        hpa_synchronize();
+        hpa_graph_destroy(d->graph);
+        d->graph = NULL;
+    }
     return 0;
 }
 
@@ -931,8 +1203,8 @@ int gpt2_decode_profile(GPT2* model, int enable) {
         return 0;
     }
     if (!d->prof_ev) {
-        d->prof_ev = (void**)calloc(2 * (size_t)L, sizeof(void*));
-        for (int i = 0; i < 2 * L; i++) {
+        d->prof_ev = (void**)calloc(2 * (size_t)L * DEC_MAX_LANES, sizeof(void*));
+        for (size_t i = 0; i < 2 * (size_t)L * DEC_MAX_LANES; i++) {
             d->prof_ev[i] = hpa_event_create();
             if (!d->prof_ev[i]) return 1;
         }
@@ -947,12 +1219,14 @@ int gpt2_decode_profile_collect(GPT2* model) {
     GPT2Decode* d = model->decode;
     if (!d || !d->prof_ev) return 1;
     int L = model->config.num_layers;
-    for (int l = 0; l < L; l++) {
-        float ms = hpa_event_elapsed_ms(d->prof_ev[2 * l], d->prof_ev[2 * l + 1]);
-        if (ms < 0) return 1;
-        d->prof_ms += ms;
-        d->prof_launches++;
-    }
+    const int nl = d->fused ? d->nlanes : 1;
+    for (int l = 0; l < L; l++)
+        for (int i = 0; i < nl; i++) {
+            float ms = hpa_event_elapsed_ms(PROF_EV(d, l, i, 0), PROF_EV(d, l, i, 1));
+            if (ms < 0) return 1;
+            d->prof_ms += ms;
+            d->prof_launches++;
+        }
     return 0;
 }
 

@@ -50,6 +50,41 @@ class HpaKVPool(ctypes.Structure):
                 ("managed", ctypes.c_int)]
 
 
+class HpaFusedGemm(ctypes.Structure):
+    _fields_ = [("x", _V), ("M", ctypes.c_int), ("K", ctypes.c_int), ("ln_stats", _V),
+                ("ln_ntiles", ctypes.c_int), ("ln_w", _V), ("ln_b", _V), ("w", _V),
+                ("N", ctypes.c_int), ("bias", _V), ("epilogue", ctypes.c_int), ("out", _V),
+                ("res_in", _V), ("stats_out", _V), ("part_out", _V),
+                ("pool", ctypes.POINTER(HpaKVPool)), ("layer", ctypes.c_int), ("block_table", _V),
+                ("bt_stride", ctypes.c_int), ("pos", _V), ("waves", ctypes.c_int),
+                ("row_blocks", ctypes.c_int)]
+
+
+HPA_FEPI_QKV, HPA_FEPI_RESID, HPA_FEPI_GELU, HPA_FEPI_LOGITS = 0, 1, 2, 3
+
+
+def frag_index(m, k, K):
+    """numpy mirror of hpa_internal.h frag_index (vectorised over m, k)"""
+    m = np.asarray(m)
+    k = np.asarray(k)
+    return ((((m >> 4) * (K >> 4) + (k >> 4)) * 64 + ((m & 15) + 16 * ((k >> 2) & 3))) << 2) + (k & 3)
+
+
+def to_frag(a, pad=16):
+    """host [rows][K] -> frag-layout flat array (rows padded to `pad`)"""
+    rows, K = a.shape
+    rp = (rows + pad - 1) // pad * pad
+    out = np.zeros(rp * K, np.float32)
+    m, k = np.meshgrid(np.arange(rows), np.arange(K), indexing="ij")
+    out[frag_index(m, k, K)] = a
+    return out
+
+
+def from_frag(f, rows, K):
+    m, k = np.meshgrid(np.arange(rows), np.arange(K), indexing="ij")
+    return f[frag_index(m, k, K)]
+
+
 GPT2_124M = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
 GPT2_XL = dict(maxT=1024, V=50257, L=48, NH=25, C=1600)
 
@@ -107,6 +142,10 @@ def lib():
     _sig(L, "hpa_event_record", i, [v])
     _sig(L, "hpa_event_elapsed_ms", f, [v, v])
     _sig(L, "hpa_event_destroy", i, [v])
+    _sig(L, "hpa_event_create_nt", v, [])
+    _sig(L, "hpa_stream_create", v, [])
+    _sig(L, "hpa_stream_destroy", i, [v])
+    _sig(L, "hpa_stream_wait_event", i, [v])
     _sig(L, "hpa_last_error", ctypes.c_char_p, [])
     _sig(L, "hpa_device_info", i, [ctypes.c_char_p, i, _I, ctypes.POINTER(sz)])
     _sig(L, "hpa_set_attention_waves", i, [i])
@@ -162,11 +201,24 @@ def lib():
     _sig(L, "gpt2_decode_fill_random", i, [v, i, ctypes.c_ulonglong])
     _sig(L, "gpt2_decode_set_graph", i, [v, i])
     _sig(L, "gpt2_decode_reserve", i, [v, i])
+    _sig(L, "gpt2_decode_set_fused", i, [v, i])
+    _sig(L, "hpa_frag_elems", sz, [i, i])
+    _sig(L, "hpa_pack_frag", i, [v, i, i, i, v])
+    _sig(L, "hpa_unpack_frag", i, [v, i, i, v, i])
+    _sig(L, "hpa_gemm_fused", i, [ctypes.POINTER(HpaFusedGemm)])
+    _sig(L, "hpa_fused_pick_waves", i, [i, i, i])
+    _sig(L, "hpa_fused_pick", None, [i, i, i, _I])
+    _sig(L, "hpa_embed_frag", i, [v, v, v, v, v, v, i, i])
+    _sig(L, "hpa_argmax_final", i, [v, i, i, i, v, v, v])
+    _sig(L, "hpa_paged_attention_decode_frag", i, [v, P, i, v, i, v, v, i])
     _sig(L, "gpt2_decode_set_positions", i, [v, _I])
     _sig(L, "gpt2_decode_logits", v, [v])
     _sig(L, "gpt2_decode_next", v, [v])
     _sig(L, "gpt2_decode_positions", i, [v, _I])
     _sig(L, "gpt2_decode_splits", i, [v, _I])
+    _sig(L, "gpt2_decode_gemm_config", i, [v, _I, _I, i])
+    _sig(L, "gpt2_decode_set_lanes", i, [v, i])
+    _sig(L, "gpt2_decode_lanes", i, [v])
     _sig(L, "gpt2_decode_step_bytes", ctypes.c_double, [v, ctypes.POINTER(ctypes.c_double)])
     _sig(L, "random_u32", ctypes.c_uint, [ctypes.POINTER(ctypes.c_ulonglong)])
     _sig(L, "random_f32", f, [ctypes.POINTER(ctypes.c_ulonglong)])
@@ -362,6 +414,9 @@ class Model:
         check(lib().gpt2_decode_init(self.h, B, page_size, max_ctx), "gpt2_decode_init")
         self.B = B
 
+    def set_fused(self, on):
+        check(lib().gpt2_decode_set_fused(self.h, int(on)), "set_fused")
+
     def set_graph(self, on):
         check(lib().gpt2_decode_set_graph(self.h, int(on)), "set_graph")
 
@@ -404,6 +459,25 @@ class Model:
         out = np.zeros(4, np.int32)
         check(lib().gpt2_decode_splits(self.h, out.ctypes.data_as(_I)), "splits")
         return out
+
+    def set_lanes(self, lanes):
+        check(lib().gpt2_decode_set_lanes(self.h, int(lanes)), "set_lanes")
+        return lib().gpt2_decode_lanes(self.h)
+
+    def gemm_config(self, waves=None, row_blocks=None):
+        """fused GEMM launch shapes [qkv, attproj, fc, fcproj, logits]:
+        (waves per workgroup, 16-row blocks per workgroup); applies the
+        nonzero entries of the given lists first"""
+        if waves is not None or row_blocks is not None:
+            w = np.ascontiguousarray(waves if waves is not None else [0] * 5, np.int32)
+            r = np.ascontiguousarray(row_blocks if row_blocks is not None else [0] * 5, np.int32)
+            check(lib().gpt2_decode_gemm_config(self.h, w.ctypes.data_as(_I), r.ctypes.data_as(_I), 1),
+                  "gemm_config")
+        w = np.zeros(5, np.int32)
+        r = np.zeros(5, np.int32)
+        check(lib().gpt2_decode_gemm_config(self.h, w.ctypes.data_as(_I), r.ctypes.data_as(_I), 0),
+              "gemm_config")
+        return w, r
 
     def step_bytes(self):
         att = ctypes.c_double()

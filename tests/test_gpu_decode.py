@@ -25,10 +25,11 @@ def _margins(logits):
     return s[:, -1] - s[:, -2]
 
 
-def _compare_run(hip, cfgd, B, P, steps, seed, graph=False, feed_greedy=False):
+def _compare_run(hip, cfgd, B, P, steps, seed, graph=False, feed_greedy=False, fused=True):
     params = synth.params(cfgd, seed=seed)
     model = hip.Model(cfgd, params=params)
     model.decode_init(B, P, cfgd["maxT"])
+    model.set_fused(fused)
     model.set_graph(graph)
     c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
     orc = oc.PagedDecoder(params, c, B, P, cfgd["maxT"], page_seed=seed + 3)
@@ -53,8 +54,14 @@ def _compare_run(hip, cfgd, B, P, steps, seed, graph=False, feed_greedy=False):
 
 
 @pytest.mark.parametrize("P", [8, 16, 32])
-def test_decode_small_model_matches_oracle(hip, P):
-    _compare_run(hip, SMALL, B=3, P=P, steps=70, seed=P)
+@pytest.mark.parametrize("fused", [True, False])
+def test_decode_small_model_matches_oracle(hip, P, fused):
+    _compare_run(hip, SMALL, B=3, P=P, steps=70, seed=P, fused=fused)
+
+
+def test_decode_batch_over_64_rows(hip):
+    """B > 64: two 64-row groups in every GEMM, padded rows in the second"""
+    _compare_run(hip, SMALL, B=70, P=16, steps=12, seed=70)
 
 
 def test_decode_graph_replay_matches_oracle_greedy(hip):
@@ -79,10 +86,11 @@ def test_graph_and_eager_bit_identical(hip):
         assert np.array_equal(a, b)
 
 
-def test_decode_gpt2_124m_shapes(hip):
+@pytest.mark.parametrize("fused", [True, False])
+def test_decode_gpt2_124m_shapes(hip, fused):
     """GPT-2 124M shapes (L=12, C=768, NH=12, V=50257), B=4, 24 steps"""
     cfgd = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
-    worst, ties = _compare_run(hip, cfgd, B=4, P=16, steps=24, seed=21)
+    worst, ties = _compare_run(hip, cfgd, B=4, P=16, steps=24, seed=21, fused=fused)
     print(f"124M: worst logit diff {worst:.3e}, near-ties {ties}")
 
 
@@ -123,4 +131,60 @@ def test_context_full_is_an_error(hip):
         m.step(np.zeros(2, np.int32))
     with pytest.raises(RuntimeError):
         m.step(np.zeros(2, np.int32))
+    m.close()
+
+
+@pytest.mark.parametrize("lanes,B,graph", [(2, 64, False), (4, 64, True), (3, 70, True), (8, 20, False)])
+def test_lanes_bit_identical_to_one_lane(hip, lanes, B, graph):
+    """micro-batch lanes run row groups concurrently on their own streams;
+    every row's arithmetic is unchanged, so ids and logits equal lanes=1
+    bit for bit (B=20 with 8 lanes: only 2 lanes of 16-row blocks exist)"""
+    params = synth.params(SMALL, seed=31)
+    outs = []
+    for nl in (1, lanes):
+        m = hip.Model(SMALL, params=params)
+        m.decode_init(B, 16, 128)
+        got = m.set_lanes(nl)
+        assert got == min(nl, (B + 15) // 16)
+        m.set_graph(graph)
+        rng = np.random.default_rng(5)
+        seq = [m.step(rng.integers(0, 1000, B).astype(np.int32))]
+        for _ in range(12):
+            seq.append(m.step(None))
+        seq.append(m.logits())
+        seq.append(m.positions())
+        outs.append(seq)
+        m.close()
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+
+
+def test_lanes_match_oracle(hip):
+    params = synth.params(SMALL, seed=8)
+    B = 40
+    model = hip.Model(SMALL, params=params)
+    model.decode_init(B, 16, SMALL["maxT"])
+    assert model.set_lanes(3) == 3
+    model.set_graph(True)
+    c = oc.cfg(SMALL["maxT"], SMALL["V"], SMALL["L"], SMALL["NH"], SMALL["C"])
+    orc = oc.PagedDecoder(params, c, B, 16, SMALL["maxT"], page_seed=11)
+    rng = np.random.default_rng(8)
+    for t in range(20):
+        tok = rng.integers(0, SMALL["V"], B).astype(np.int32)
+        o_next, o_logits = orc.step(tok)
+        g_next = model.step(tok)
+        assert np.abs(model.logits() - o_logits).max() <= LOGIT_TOL
+        clear = _margins(o_logits) > TIE_MARGIN
+        assert np.array_equal(g_next[clear], o_next[clear])
+    model.close()
+    orc.close()
+
+
+def test_set_lanes_rejects_out_of_range(hip):
+    m = hip.Model(SMALL)
+    m.decode_init(4, 16, 64)
+    with pytest.raises(RuntimeError):
+        m.set_lanes(0)
+    with pytest.raises(RuntimeError):
+        m.set_lanes(9)
     m.close()

@@ -1,0 +1,225 @@
+"""The fused decode-layer GEMM (hpa_gemm_fused) and frag-layout helpers vs
+float64 numpy references of the same ops, each epilogue, at every
+waves-per-workgroup setting (the K range split over 4/8/16 waves and folded
+in LDS).
+
+Tolerance: |gpu - f64| <= 4e-6 * sum_k |a||w| + 2e-6 (fp32 MFMA chains; the
+LayerNorm on the A operand uses one-pass statistics, so LN'ed cases compare
+against the f64 LN of the same inputs).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _ln(x, w, b):
+    m = x.mean(-1, keepdims=True)
+    v = ((x - m) ** 2).mean(-1, keepdims=True)
+    return (x - m) / np.sqrt(v + 1e-5) * w + b
+
+
+def _stats_tiles(x, Mp):
+    """per-row partial (sum, sum of squares) over 16-column tiles: [tiles][Mp][2]"""
+    M, C = x.shape
+    t = C // 16
+    st = np.zeros((t, Mp, 2), np.float32)
+    for i in range(t):
+        blk = x[:, 16 * i:16 * (i + 1)].astype(np.float64)
+        st[i, :M, 0] = blk.sum(1)
+        st[i, :M, 1] = (blk * blk).sum(1)
+    return st
+
+
+def test_pack_unpack_roundtrip(hip):
+    L = hip.lib()
+    rng = np.random.default_rng(0)
+    a = rng.standard_normal((70, 96)).astype(np.float32)
+    d_a = hip.DeviceBuffer.from_array(a)
+    n = L.hpa_frag_elems(70, 96)
+    d_f = hip.DeviceBuffer(n * 4)
+    hip.check(L.hpa_pack_frag(d_a.ptr, 70, 96, 96, d_f.ptr))
+    f = d_f.download(n)
+    assert np.array_equal(f, hip.to_frag(a))
+    d_b = hip.DeviceBuffer(a.nbytes)
+    hip.check(L.hpa_unpack_frag(d_f.ptr, 70, 96, d_b.ptr, 96))
+    assert np.array_equal(d_b.download(a.shape), a)
+
+
+def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixed=None):
+    L = hip.lib()
+    x = rng.uniform(-1, 1, (M, K)).astype(np.float32)
+    W = rng.uniform(-0.05, 0.05, (N, K)).astype(np.float32)
+    bias = rng.uniform(-0.1, 0.1, N).astype(np.float32)
+    if fixed is not None:  # caller-provided operands (rows of x: the first M)
+        x, W, bias = fixed["x"][:M], fixed["W"], fixed["bias"]
+    Mp = (M + 15) // 16 * 16
+    keep = []
+
+    def dev(a):
+        b = hip.DeviceBuffer.from_array(np.ascontiguousarray(a))
+        keep.append(b)
+        return b.ptr
+
+    g = hip.HpaFusedGemm()
+    g.x = dev(hip.to_frag(x))
+    g.M, g.K, g.N = M, K, N
+    if ln:
+        lw = rng.uniform(0.8, 1.2, K).astype(np.float32)
+        lb = rng.uniform(-0.1, 0.1, K).astype(np.float32)
+        if fixed is not None:
+            lw, lb = fixed["lw"], fixed["lb"]
+        g.ln_stats = dev(_stats_tiles(x, Mp))
+        g.ln_ntiles = K // 16
+        g.ln_w, g.ln_b = dev(lw), dev(lb)
+        a = _ln(x.astype(np.float64), lw, lb)
+    else:
+        a = x.astype(np.float64)
+    g.w = dev(hip.to_frag(W))
+    g.bias = dev(bias) if epi != hip.HPA_FEPI_LOGITS else None
+    g.waves = waves
+    g.row_blocks = rb
+    g.epilogue = epi
+    acc = a @ W.astype(np.float64).T
+    bound = 4e-6 * (np.abs(a) @ np.abs(W.astype(np.float64)).T) + 2e-6
+    if epi != hip.HPA_FEPI_LOGITS:
+        acc = acc + bias
+    if epi == hip.HPA_FEPI_RESID:
+        g.res_in = dev(hip.to_frag(res))
+        out = hip.DeviceBuffer(Mp * N * 4)
+        st = hip.DeviceBuffer(N // 16 * Mp * 2 * 4)
+        g.out, g.stats_out = out.ptr, st.ptr
+        keep.append(st)
+    elif epi == hip.HPA_FEPI_GELU:
+        out = hip.DeviceBuffer(Mp * N * 4)
+        g.out = out.ptr
+    elif epi == hip.HPA_FEPI_LOGITS:
+        out = hip.DeviceBuffer(M * N * 4)
+        part = hip.DeviceBuffer((N + 15) // 16 * Mp * 2 * 4)
+        g.out, g.part_out = out.ptr, part.ptr
+        keep.append(part)
+    else:
+        out = hip.DeviceBuffer(M * (N // 3) * 4)
+        g.out = out.ptr
+        pool, bt, pos = pool_args
+        g.pool = ctypes.pointer(pool.s)
+        g.layer = 0
+        g.block_table, g.bt_stride, g.pos = dev(bt), bt.shape[1], dev(pos)
+    keep.append(out)
+    hip.check(L.hpa_gemm_fused(ctypes.byref(g)), "gemm_fused")
+    hip.check(L.hpa_synchronize())
+    return out, acc, bound, keep
+
+
+@pytest.mark.parametrize("M,K,N,waves,rb", [(64, 256, 128, 4, 4), (64, 256, 128, 16, 1), (8, 768, 768, 16, 2),
+                                            (40, 3072, 768, 8, 1), (100, 512, 96, 16, 4), (3, 48, 32, 16, 1),
+                                            (130, 768, 768, 0, 0), (64, 3072, 768, 4, 2), (48, 1600, 1600, 8, 4)])
+def test_fused_resid_with_stats(hip, M, K, N, waves, rb):
+    rng = np.random.default_rng(M + waves + rb)
+    res = rng.uniform(-1, 1, (M, N)).astype(np.float32)
+    out, acc, bound, keep = _run(hip, hip.HPA_FEPI_RESID, M, K, N, waves, ln=(K == N), rng=rng, res=res, rb=rb)
+    Mp = (M + 15) // 16 * 16
+    got = hip.from_frag(out.download(Mp * N), M, N)
+    ref = res + acc
+    assert np.all(np.abs(got - ref) <= bound + 1e-6)
+    # padded rows stay zero
+    full = out.download(Mp * N)
+    if Mp > M:
+        assert np.all(hip.from_frag(full, Mp, N)[M:] == 0)
+
+
+@pytest.mark.parametrize("waves,rb", [(4, 1), (8, 2), (16, 4), (16, 1)])
+def test_fused_gelu_with_ln(hip, waves, rb):
+    import torch
+    rng = np.random.default_rng(waves + rb)
+    M, K, N = 64, 768, 3072
+    out, acc, bound, keep = _run(hip, hip.HPA_FEPI_GELU, M, K, N, waves, ln=True, rng=rng, rb=rb)
+    got = hip.from_frag(out.download(M * N), M, N)
+    ref = torch.nn.functional.gelu(torch.from_numpy(acc), approximate="tanh").numpy()
+    assert np.abs(got - ref).max() <= 2e-5
+
+
+@pytest.mark.parametrize("M,waves,rb", [(64, 4, 4), (37, 8, 1), (64, 16, 2)])
+def test_fused_logits_argmax(hip, M, waves, rb):
+    L = hip.lib()
+    rng = np.random.default_rng(3)
+    K, N = 768, 50257
+    out, acc, bound, keep = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, waves, ln=True, rng=rng, rb=rb)
+    got = out.download((M, N))
+    assert np.all(np.abs(got - acc) <= bound)
+    part = keep[-2]
+    nxt = hip.DeviceBuffer(M * 4)
+    Mp = (M + 15) // 16 * 16
+    hip.check(L.hpa_argmax_final(part.ptr, (N + 15) // 16, Mp, M, nxt.ptr, None, None))
+    ids = nxt.download(M, np.int32)
+    assert np.array_equal(ids, got.argmax(-1))
+
+
+def test_fused_qkv_appends_into_pages(hip):
+    rng = np.random.default_rng(9)
+    NH, P = 2, 16
+    C = NH * 64
+    M, K, N = 5, C, 3 * C
+    pool = hip.Pool(1, NH, P, 20)
+    bt = rng.permutation(20).astype(np.int32)[:20].reshape(5, 4)
+    pos = np.array([0, 15, 16, 33, 63], np.int32)
+    out, acc, bound, keep = _run(hip, hip.HPA_FEPI_QKV, M, K, N, 8, ln=True, rng=rng,
+                                 pool_args=(pool, bt, pos))
+    q = out.download((M, C))
+    assert np.all(np.abs(q - acc[:, :C]) <= bound[:, :C])
+    for b in range(M):
+        k, v = pool.read_tokens(0, bt[b], pos[b] + 1)
+        assert np.all(np.abs(k[pos[b]] - acc[b, C:2 * C]) <= bound[b, C:2 * C])
+        assert np.all(np.abs(v[pos[b]] - acc[b, 2 * C:]) <= bound[b, 2 * C:])
+
+
+def test_fused_fold_deterministic(hip):
+    """the LDS fold sums the waves' partials in wave order: bit-identical
+    across repeated launches"""
+    rng = np.random.default_rng(4)
+    res = rng.uniform(-1, 1, (64, 768)).astype(np.float32)
+    outs = []
+    for _ in range(3):
+        out, acc, bound, keep = _run(hip, hip.HPA_FEPI_RESID, 64, 3072, 768, 16, ln=False,
+                                     rng=np.random.default_rng(4), res=res)
+        outs.append(out.download(64 * 768))
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[1], outs[2])
+
+
+def test_fused_rejects_bad_launch_shape(hip):
+    rng = np.random.default_rng(5)
+    with pytest.raises(RuntimeError):
+        _run(hip, hip.HPA_FEPI_GELU, 16, 64, 64, 2, ln=False, rng=rng)
+    with pytest.raises(RuntimeError):
+        _run(hip, hip.HPA_FEPI_GELU, 16, 64, 64, 4, ln=False, rng=rng, rb=3)
+    with pytest.raises(RuntimeError):  # LN'ed A operand wider than the LDS copy of w, b
+        _run(hip, hip.HPA_FEPI_GELU, 16, 2064, 64, 4, ln=True, rng=rng)
+
+
+@pytest.mark.parametrize("epi", ["RESID", "LOGITS"])
+def test_fused_rows_independent_of_split(hip, epi):
+    """a row's result depends only on the waves (per-wave K ranges): equal
+    bit for bit across row_blocks 1/2/4 and across M (the micro-batch lanes
+    rely on this)"""
+    e = getattr(hip, "HPA_FEPI_" + epi)
+    N = 768 if epi == "RESID" else 4000
+    r = np.random.default_rng(7)
+    K = 768
+    fixed = dict(x=r.uniform(-1, 1, (64, K)).astype(np.float32),
+                 W=r.uniform(-0.05, 0.05, (N, K)).astype(np.float32),
+                 bias=r.uniform(-0.1, 0.1, N).astype(np.float32),
+                 lw=r.uniform(0.8, 1.2, K).astype(np.float32), lb=r.uniform(-0.1, 0.1, K).astype(np.float32))
+    res = r.uniform(-1, 1, (64, N)).astype(np.float32)
+    outs = []
+    for M, rb in [(64, 1), (64, 2), (64, 4), (16, 1), (32, 2)]:
+        out, _, _, keep = _run(hip, e, M, K, N, 8, ln=True, rng=np.random.default_rng(7),
+                               res=res[:M], rb=rb, fixed=fixed)
+        if epi == "RESID":
+            got = hip.from_frag(out.download(((M + 15) // 16 * 16) * N), M, N)
+        else:
+            got = out.download((M, N))
+        outs.append(got[:16])
+    for o in outs[1:]:
+        assert np.array_equal(outs[0], o)
