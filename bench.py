@@ -2,8 +2,12 @@
 """Decode throughput benchmark of the MI355X paged-attention decode path.
 
 Metric (BASELINE.json): decode tokens/sec, GPT-2 124M paged attention,
-B=64, ctx 1024, page 16, fp32, on 1/2/4/8 MI355X (configs[1]; the global
-batch of 64 sequences is sharded by sequence across ranks -> strong scaling).
+B=64, ctx 1024, page 16, fp32, on 1/2/4/8 MI355X (configs[1] at N=1).  For
+N>1 the decode shards by sequence (SURVEY.md 8e, configs[3]): every rank
+decodes its own 64 sequences out of its own page pool with replicated
+weights -> weak scaling; the one collective is the end-of-step RCCL gather
+of the logits to rank 0 (--gather ids: greedy ids only).  --scaling strong
+splits a fixed global batch instead.
 
 One "step" = one decode step of the whole batch: every sequence gets one new
 token at its absolute position, all 12 layers (LN, QKV + KV append into the
@@ -33,11 +37,22 @@ METRIC = "decode tokens/sec GPT-2 124M paged-attn, B=64 T=1024, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def shard_range(B, world, rank):
-    """contiguous sequence range of `rank` (B_local = B / n)"""
-    base, rem = divmod(B, world)
-    lo = rank * base + min(rank, rem)
-    return lo, lo + base + (1 if rank < rem else 0)
+def pmc_traffic(kernel_prefix, batch_per_gpu, ctx, page_size):
+    """HBM bytes per launch of the dominant kernel from the committed PMC
+    summary (tools/pmc_traffic.sh, profiles/r1/pmc_traffic.json) when it was
+    taken on this workload; None otherwise"""
+    path = os.path.join(REPO, "profiles", "r1", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    c = d.get("config") or {}
+    if (c.get("batch_per_gpu"), c.get("seq_len"), c.get("page_size")) != (batch_per_gpu, ctx, page_size):
+        return None, None
+    for name, k in d["kernels"].items():
+        if name.startswith(kernel_prefix):
+            return k["hbm_bytes"], f"profiles/r1/pmc_traffic.json: {name}, {k['launches']} launches"
+    return None, None
 
 
 def parse():
@@ -45,15 +60,18 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=64, help="global batch (sequences)")
+    ap.add_argument("--batch", type=int, default=64,
+                    help="sequences per GPU (weak scaling) or in total (--scaling strong)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--ctx", type=int, default=1024)
     ap.add_argument("--page-size", type=int, default=16)
     ap.add_argument("--model", default="124M", choices=["124M", "XL"])
     ap.add_argument("--prefill", default="synthetic", choices=["synthetic", "decode"])
-    ap.add_argument("--gather", default="ids", choices=["ids", "logits", "none"])
+    ap.add_argument("--gather", default="logits", choices=["ids", "logits", "none"],
+                    help="end-of-step gather to rank 0 (N>1)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--prof-steps", type=int, default=4,
-                    help="extra eager steps with HIP events around each attention launch")
+                    help="attention roofline timing: prof_steps x L back-to-back launches (0 = off)")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--attn-waves", type=int, default=4)
@@ -75,7 +93,8 @@ def cpu_baseline(cfgd, B, P, ctx, budget_s):
     params = pagedattn.synthetic_params(cfgd, seed=1337)
     c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
     dec = oc.PagedDecoder(params, c, B, P, cfgd["maxT"], page_seed=3, fast=True)
-    start_ctx = ctx - 16
+    max_steps = 96
+    start_ctx = ctx - max_steps
     dec.fill_random(start_ctx, seed=5)
     rng = np.random.default_rng(0)
     tok = rng.integers(0, cfgd["V"], B).astype(np.int32)
@@ -84,7 +103,7 @@ def cpu_baseline(cfgd, B, P, ctx, budget_s):
         tok, _ = dec.step(tok, want_logits=False)
         steps += 1
         el = time.perf_counter() - t0
-        if el >= budget_s or steps >= 16:
+        if el >= budget_s or steps >= max_steps:
             break
     dec.close()
     cpu_model = ""
@@ -116,6 +135,7 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     import pagedattn
+    import shard
     L = pagedattn.lib()
     pagedattn.init(local_rank)
     if torch.cuda.is_available():
@@ -129,12 +149,13 @@ def main():
     pagedattn.check(L.hpa_set_attention_waves(args.attn_waves), "attention waves")
 
     cfgd = dict(pagedattn.GPT2_124M if args.model == "124M" else pagedattn.GPT2_XL)
-    B = args.batch
-    lo, hi = shard_range(B, world, rank)
+    B, lo, hi = shard.batch_layout(args.batch, world, rank, args.scaling)
     B_local = hi - lo
+    counts = [shard.batch_layout(args.batch, world, r, args.scaling) for r in range(world)]
+    counts = [h - l for _, l, h in counts]
     P = args.page_size
     ctx = min(args.ctx, cfgd["maxT"])
-    need = args.warmup + args.steps + args.prof_steps
+    need = args.warmup + args.steps + 1
     window = min(need, ctx // 2)
     start = ctx - window  # positions of the first decoded token
 
@@ -157,13 +178,12 @@ def main():
     first = rng.integers(0, cfgd["V"], B_local).astype(np.int32)
     pos_now = [start]
 
-    ids = torch.zeros(B_local, dtype=torch.int32, device="cuda")
-    all_ids = torch.zeros(B_local * world, dtype=torch.int32, device="cuda") if world > 1 else None
-    logits_t = None
-    all_logits = None
-    if args.gather == "logits" and world > 1:
-        logits_t = torch.zeros(B_local, cfgd["V"], dtype=torch.float32, device="cuda")
-        all_logits = torch.zeros(B_local * world, cfgd["V"], dtype=torch.float32, device="cuda")
+    gather = None
+    if world > 1 and args.gather != "none":
+        gather = shard.StepGather(dist, world, rank, counts, cfgd["V"], args.gather, "cuda")
+        send = gather.buffer()
+        src, nbytes = ((model.logits_ptr(), B_local * cfgd["V"] * 4) if args.gather == "logits"
+                       else (model.next_ptr(), B_local * 4))
 
     def one_step(tokens=None):
         if pos_now[0] >= ctx:  # slide back: pages kept, positions rewritten
@@ -171,13 +191,9 @@ def main():
             pos_now[0] = start
         model.step_async(tokens)
         pos_now[0] += 1
-        if world > 1 and args.gather != "none":
-            if args.gather == "ids":
-                L.hpa_memcpy_async(ids.data_ptr(), model.next_ptr(), B_local * 4)
-                dist.all_gather_into_tensor(all_ids, ids)
-            else:
-                L.hpa_memcpy_async(logits_t.data_ptr(), model.logits_ptr(), logits_t.numel() * 4)
-                dist.all_gather_into_tensor(all_logits, logits_t)
+        if gather is not None:  # copy on the shared stream, then RCCL gather to rank 0
+            L.hpa_memcpy_async(send.data_ptr(), src, nbytes)
+            gather.gather()
 
     def sync():
         pagedattn.check(L.hpa_synchronize(), "sync")
@@ -207,35 +223,15 @@ def main():
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
     tokens_per_s = B * args.steps / elapsed  # whole job: every rank's sequences
 
-    # ---- live attention-kernel timing (HIP events on the launch stream)
+    # ---- live attention-kernel timing: HIP events on the launch stream around
+    # back-to-back launches of the step's attention kernel over the layers, on
+    # the engine's own pool at the last step's positions
     attn = None
     if args.prof_steps > 0:
-        L.gpt2_decode_profile.argtypes = [pagedattn._V, pagedattn.ctypes.c_int]
-        L.gpt2_decode_profile_collect.argtypes = [pagedattn._V]
-        L.gpt2_decode_profile_read.argtypes = [pagedattn._V, pagedattn.ctypes.POINTER(pagedattn.ctypes.c_long)]
-        L.gpt2_decode_profile_read.restype = pagedattn.ctypes.c_double
-        pagedattn.check(L.gpt2_decode_profile(model.h, 1), "profile on")
-        attn_bytes = 0.0
-        for _ in range(args.prof_steps):
-            if pos_now[0] >= ctx:
-                model.set_positions(np.full(B_local, start, np.int32))
-                pos_now[0] = start
-            _, ab = model.step_bytes()  # KV bytes this step will read (ctx = pos + 1)
-            attn_bytes += ab
-            model.step_async(None)
-            pos_now[0] += 1
-            pagedattn.check(L.gpt2_decode_profile_collect(model.h), "profile collect")
-        n = pagedattn.ctypes.c_long()
-        ms = L.gpt2_decode_profile_read(model.h, pagedattn.ctypes.byref(n))
-        pagedattn.check(L.gpt2_decode_profile(model.h, 0), "profile off")
-        # per launch: K+V of the launch's sequences' contexts for one layer (+ q in, out);
-        # with lanes, each layer is one launch per lane
-        total_bytes = attn_bytes + args.prof_steps * cfgd["L"] * 2 * B_local * cfgd["C"] * 4
-        per_launch_bytes = total_bytes / max(n.value, 1)
-        avg_ms = ms / max(n.value, 1)
-        achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
-        attn = dict(avg_ms=avg_ms, launches=n.value, per_launch_bytes=per_launch_bytes,
-                    achieved=achieved)
+        iters = args.prof_steps * cfgd["L"]
+        avg_ms, per_launch_bytes = model.time_attention(iters)
+        attn = dict(avg_ms=avg_ms, launches=iters, per_launch_bytes=per_launch_bytes,
+                    achieved=per_launch_bytes / (avg_ms * 1e-3) / 1e9)
 
     result = None
     if rank == 0:
@@ -249,9 +245,11 @@ def main():
         name, cus, mem = pagedattn.device_info()
         roof = None
         if attn:
+            traffic, tsrc = pmc_traffic("paged_attn_decode_f32", B_local, ctx, P)
             roof = {"bound": "hbm", "kernel": "paged_attn_decode_f32", "achieved": round(attn["achieved"], 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(attn["achieved"] / HBM_PEAK_GBS, 4),
-                    "traffic": None, "avg_launch_ms": round(attn["avg_ms"], 5),
+                    "traffic": None if traffic is None else int(traffic),
+                    "traffic_source": tsrc, "avg_launch_ms": round(attn["avg_ms"], 5),
                     "bytes_per_launch": int(attn["per_launch_bytes"]), "launches_timed": attn["launches"]}
         step_bytes = 0.5 * (bytes_before + bytes_after)
         result = {
@@ -263,17 +261,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic (seeded random GPT-2 124M weights and tokens; KV prefill: "
                     + ("synthetic U(-1,1)" if args.prefill == "synthetic" else "decode steps") + ")",
-            "config": {"workload": f"GPT-2 {args.model} fp32 paged decode, batch={B}, ctx {ctx}, "
-                                   f"page_size={P} (BASELINE.json configs[1])",
-                       "global_batch": B, "seq_len": ctx, "page_size": P,
+            "config": {"workload": f"GPT-2 {args.model} fp32 paged decode, batch={B_local} per GPU x {world} "
+                                   f"(B={B}), ctx {ctx}, page_size={P} (BASELINE.json "
+                                   + ("configs[1])" if world == 1 else "configs[3]: per-seq sharded pool)"),
+                       "global_batch": B, "batch_per_gpu": B_local, "seq_len": ctx, "page_size": P,
                        "decode_positions": f"{start}..{start + args.warmup + args.steps - 1}",
-                       "parallelism": f"seq-shard x{world}" + (f" + RCCL all_gather({args.gather})"
-                                                               if world > 1 else ""),
+                       "parallelism": f"seq-shard x{world}" + (f" + RCCL gather({args.gather}) to rank 0"
+                                                               if world > 1 and args.gather != "none" else ""),
                        "hip_graph": not args.no_graph, "gemm_path": "unfused" if args.unfused else "fused",
                        "lanes": 1 if args.unfused else L.gpt2_decode_lanes(model.h),
                        "gemm_waves": [int(x) for x in model.gemm_config()[0]],

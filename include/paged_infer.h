@@ -170,6 +170,11 @@ int    gpt2_decode_gemm_config(GPT2* model, int* waves5, int* row_blocks5, int s
  * group's attention overlaps another's GEMMs; results are identical to
  * lanes = 1 row for row.  Returns nonzero for lanes outside 1..8. */
 int    gpt2_decode_set_lanes(GPT2* model, int lanes);
+/* attention kernel timed alone: `iters` back-to-back launches on the engine's
+ * pool at the last step's positions; average ms and algorithmic bytes per
+ * launch (bench.py roofline) */
+int    gpt2_decode_time_attention(GPT2* model, int iters, double* ms_per_launch,
+                                  double* bytes_per_launch);
 int    gpt2_decode_lanes(GPT2* model);
 /* algorithmic HBM bytes one step reads+writes at the current positions
  * (SURVEY.md 8d formula) and the attention kernel's share of them */

@@ -1042,6 +1042,51 @@ int gpt2_decode_gemm_config(GPT2* model, int* waves5, int* row_blocks5, int set)
     return 0;
 }
 
+/* the decode attention kernel alone, `iters` back-to-back launches over the
+ * layers (layer = i % L) on the engine's pool, block tables and q, at the
+ * positions of the LAST completed step (ctx = pos), bracketed by HIP events on
+ * the launch stream: the roofline measurement of bench.py.  Writes the average
+ * launch time and the algorithmic bytes per launch (K+V rows read, q in, out). */
+int gpt2_decode_time_attention(GPT2* model, int iters, double* ms_per_launch, double* bytes_per_launch) {
+    GPT2Decode* d = model->decode;
+    if (!d || iters <= 0) return 1;
+    const int B = d->B, C = model->config.channels, L = model->config.num_layers;
+    for (int b = 0; b < B; b++)
+        if (d->h_pos[b] < 1) {
+            fprintf(stderr, "[paged_infer] time_attention: run a step first\n");
+            return 1;
+        }
+    int* d_p = (int*)hpa_malloc(B * sizeof(int));
+    float* out = (float*)hpa_malloc(hpa_frag_elems(B, C) * sizeof(float));
+    void* e0 = hpa_event_create();
+    void* e1 = hpa_event_create();
+    int rc = !d_p || !out || !e0 || !e1;
+    if (!rc) {
+        if (hpa_synchronize()) rc = 1;
+        for (int b = 0; b < B && !rc; b++) d->h_stage[b] = d->h_pos[b] - 1;
+        rc |= hpa_memcpy(d_p, d->h_stage, B * sizeof(int));
+        /* warm-up launch, then the timed ones */
+        rc |= hpa_paged_attention_decode_frag(d->d_q, &d->pool, 0, d->d_bt, d->bt_stride, d_p, out, B);
+        rc |= hpa_event_record(e0);
+        for (int i = 0; i < iters && !rc; i++)
+            rc |= hpa_paged_attention_decode_frag(d->d_q, &d->pool, i % L, d->d_bt, d->bt_stride, d_p, out, B);
+        rc |= hpa_event_record(e1);
+        float ms = rc ? -1.f : hpa_event_elapsed_ms(e0, e1);
+        if (ms < 0) rc = 1;
+        if (!rc) {
+            double kv = 0.0;
+            for (int b = 0; b < B; b++) kv += 2.0 * d->h_pos[b] * C * 4.0;
+            if (ms_per_launch) *ms_per_launch = ms / iters;
+            if (bytes_per_launch) *bytes_per_launch = kv + 2.0 * B * C * 4.0;
+        }
+    }
+    hpa_event_destroy(e0);
+    hpa_event_destroy(e1);
+    hpa_free(out);
+    hpa_free(d_p);
+    return rc;
+}
+
 /* weights + wpe rows + KV read (ctx = pos+1) + KV append + logits */
 double gpt2_decode_step_bytes(GPT2* model, double* attn_bytes) {
     GPT2Decode* d = model->decode;

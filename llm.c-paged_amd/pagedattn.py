@@ -218,6 +218,8 @@ def lib():
     _sig(L, "gpt2_decode_splits", i, [v, _I])
     _sig(L, "gpt2_decode_gemm_config", i, [v, _I, _I, i])
     _sig(L, "gpt2_decode_set_lanes", i, [v, i])
+    _sig(L, "gpt2_decode_time_attention", i, [v, i, ctypes.POINTER(ctypes.c_double),
+                                              ctypes.POINTER(ctypes.c_double)])
     _sig(L, "gpt2_decode_lanes", i, [v])
     _sig(L, "gpt2_decode_step_bytes", ctypes.c_double, [v, ctypes.POINTER(ctypes.c_double)])
     _sig(L, "random_u32", ctypes.c_uint, [ctypes.POINTER(ctypes.c_ulonglong)])
@@ -459,6 +461,14 @@ class Model:
         out = np.zeros(4, np.int32)
         check(lib().gpt2_decode_splits(self.h, out.ctypes.data_as(_I)), "splits")
         return out
+
+    def time_attention(self, iters=48):
+        """(avg ms, algorithmic bytes) per launch of the decode attention
+        kernel, back-to-back launches at the last step's positions"""
+        ms, by = ctypes.c_double(), ctypes.c_double()
+        check(lib().gpt2_decode_time_attention(self.h, int(iters), ctypes.byref(ms), ctypes.byref(by)),
+              "time_attention")
+        return ms.value, by.value
 
     def set_lanes(self, lanes):
         check(lib().gpt2_decode_set_lanes(self.h, int(lanes)), "set_lanes")
