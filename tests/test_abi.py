@@ -75,3 +75,21 @@ def test_no_oracle_in_product_library(built):
     assert not [s for s in ex if s.startswith("oracle_")]
     dyn = subprocess.run(["readelf", "-d", built], capture_output=True, text=True).stdout
     assert "oracle" not in dyn
+
+
+def test_c_driver_compiles_links_and_fails_cleanly_without_gpu(tmp_path):
+    """examples/decode_main.c builds against the headers and
+    libpaged_hip.so with plain gcc; on a host without a GPU it exits nonzero
+    with a message instead of computing anything on the CPU"""
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    libdir = os.path.join(repo, "llm.c-paged_amd")
+    exe = str(tmp_path / "decode_main")
+    subprocess.run(["gcc", "-O2", "-Wall", "-Werror", os.path.join(repo, "examples", "decode_main.c"),
+                    "-I" + os.path.join(repo, "include"), "-L" + libdir, "-lpaged_hip",
+                    "-Wl,-rpath," + libdir, "-o", exe], check=True)
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: the failure path is not reachable")
+    r = subprocess.run([exe, "", "2", "2"], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
