@@ -202,6 +202,9 @@ typedef struct {
     const int* pos;
     int waves;            /* waves per workgroup sharing the K range: 4, 8 or 16; 0 = by shape */
     int row_blocks;       /* 16-row blocks per workgroup: 1, 2 or 4; 0 = by shape */
+    int variant;          /* 0 = by shape; 1 = looped (two trips in flight);
+                             2 = one-shot (every operand load issued up front; one
+                             row block; (waves, K/16) in {(4,48),(8,48),(16,48),(8,192)}) */
 } HpaFusedGemm;
 int hpa_gemm_fused(const HpaFusedGemm* g);
 /* the launch shape hpa_gemm_fused picks when waves / row_blocks are 0:

@@ -34,6 +34,15 @@ namespace {
 
 constexpr int HS = 64;
 
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+// K/V rows are streamed once per step by the one workgroup of their
+// (sequence, head): non-temporal loads (MI355X_MICROARCH.md "nt-weights")
+__device__ __forceinline__ float4 load_stream(const float* ptr) {
+    const f32x4v v = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(ptr));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 template <int P, int NW, bool FRAG>
 __global__ __launch_bounds__(NW * 64, 3) void paged_attn_decode_f32(
     const float* __restrict__ q, const float* __restrict__ layer_base, size_t page_elems, int NH,
@@ -70,16 +79,40 @@ __global__ __launch_bounds__(NW * 64, 3) void paged_attn_decode_f32(
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     const int n_it = (ctx + 63) >> 6;
 
-    for (int it = w; it < n_it; it += NW) {
+    // one memory round trip per 64-token tile: the tile's page ids were
+    // fetched during the previous tile; K and V rows are issued together
+    // (both depend only on the page ids), then the next tile's page ids.
+    int it = w;
+    int pid = 0;
+    if (it < n_it) {
+        const unsigned t0 = (unsigned)it << 6, tok = t0 + lane;
+        pid = bt[(tok < (unsigned)ctx ? tok : t0) / P];
+    }
+    for (; it < n_it; it += NW) {
         const unsigned t0 = (unsigned)it << 6;
         const unsigned tok = t0 + lane;
         const bool valid = tok < (unsigned)ctx;
-        const int pid = bt[(valid ? tok : t0) / P];
-        // ---- QK^T: lane-per-token over 16 chunks of 4 dims
         const float* kt = kbase + (size_t)(unsigned)pid * page_elems + (tok % P) * 4;
-        float4 kv[16];
+        float4 kv[16], vv[16];
 #pragma unroll
-        for (int c = 0; c < 16; ++c) kv[c] = *reinterpret_cast<const float4*>(kt + c * P * 4);
+        for (int c = 0; c < 16; ++c) kv[c] = load_stream(kt + c * P * 4);
+        // PV operands: lane (g, d4) takes tokens t0 + 4i + g, dims 4*d4..+3.
+        // The row address splits into a wave-uniform part (page of tokens
+        // t0+4i..+3, slot (4i)%P; t0 % P == 0) and a per-lane offset that is
+        // the same for every i, so each load is SGPR base + one shared VGPR.
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int vpid = __builtin_amdgcn_readlane(pid, 4 * i);
+            const float* vrow = vbase + (size_t)(unsigned)vpid * page_elems + ((4 * i) % P) * HS;
+            vv[i] = (t0 + 4 * i + g) < (unsigned)ctx ? load_stream(vrow + v_lane_off)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        {   // next tile's page ids
+            const int itn = it + NW;
+            const unsigned t0n = (unsigned)itn << 6, tokn = t0n + lane;
+            if (itn < n_it) pid = bt[(tokn < (unsigned)ctx ? tokn : t0n) / P];
+        }
+        // ---- QK^T: lane-per-token over 16 chunks of 4 dims
         float s = 0.f;
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
@@ -100,18 +133,7 @@ __global__ __launch_bounds__(NW * 64, 3) void paged_attn_decode_f32(
         acc.z *= alpha;
         acc.w *= alpha;
         m = mn;
-        // ---- PV: lane (g, d4) takes tokens t0 + 4i + g, dims 4*d4..+3
-        // the row address splits into a wave-uniform part (page of tokens
-        // t0+4i..+3, slot (4i)%P; t0 % P == 0) and a per-lane offset that is
-        // the same for every i, so each load is SGPR base + one shared VGPR.
-        float4 vv[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int vpid = __builtin_amdgcn_readlane(pid, 4 * i);
-            const float* vrow = vbase + (size_t)(unsigned)vpid * page_elems + ((4 * i) % P) * HS;
-            vv[i] = (t0 + 4 * i + g) < (unsigned)ctx ? *reinterpret_cast<const float4*>(vrow + v_lane_off)
-                                           : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        // ---- PV
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const float pi = __shfl(p, 4 * i + g, 64);

@@ -67,6 +67,125 @@ __device__ __forceinline__ float4 ln4(float4 a, float mu, float rs, float4 g, fl
     return a;
 }
 
+// ---- shared epilogue ---------------------------------------------------
+// Tile element e (0 .. MT*256-1) of a workgroup: rb = e>>8, reg = (e>>6)&3,
+// l = e&63 -> row rb*16 + (l>>4)*4 + reg, col l&15 (16x16 C/D map: col =
+// lane & 15, row = 4*(lane >> 4) + reg).  Thread t owns e = t + i*NT.
+template <int NW, int EPI, int MT>
+struct Epi {
+    static constexpr int NT = NW * 64;
+    static constexpr int R = MT * 16;
+    static constexpr int EPT = (MT * 256 + NT - 1) / NT;  // tile elements per thread
+    float pre_bias[EPT], pre_res[EPT];
+
+    // bias / residual operands of the owned elements: issued early so their
+    // latency hides under the main loop
+    __device__ __forceinline__ void prefetch(const FG& p, int nt, int row0) {
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+            const int e = threadIdx.x + i * NT;
+            const int l = e & 63;
+            const int lrow = (e >> 8) * 16 + (l >> 4) * 4 + ((e >> 6) & 3);
+            const int row = row0 + lrow;
+            const int col = nt * 16 + (l & 15);
+            const bool in = e < MT * 256;
+            pre_bias[i] = (EPI != HPA_FEPI_LOGITS && in && p.bias && col < p.N) ? p.bias[col] : 0.f;
+            pre_res[i] = 0.f;
+            if (EPI == HPA_FEPI_RESID && in && row < p.M && col < p.N)
+                pre_res[i] = p.res_in[hpa::frag_index(row, col, p.N)];
+        }
+    }
+
+    // fold the waves' accumulators through LDS (fixed order) and apply the epilogue
+    __device__ __forceinline__ void finish(const FG& p, const f32x4* acc, float* red, float* tile, int nt,
+                                           int row0) {
+        const int lane = threadIdx.x & 63;
+        const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int r = 0; r < MT; ++r)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) red[w * MT * 256 + (r * 4 + g) * 64 + lane] = acc[r][g];
+    __syncthreads();
+
+    constexpr bool rowstat = EPI == HPA_FEPI_RESID || EPI == HPA_FEPI_LOGITS;
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+        const int e = threadIdx.x + i * NT;
+        if (e < MT * 256) {
+            float val = red[e];
+#pragma unroll
+            for (int ww = 1; ww < NW; ++ww) val += red[ww * MT * 256 + e];
+            const int l = e & 63;
+            const int lrow = (e >> 8) * 16 + (l >> 4) * 4 + ((e >> 6) & 3);
+            const int lcol = l & 15;
+            const int row = row0 + lrow;
+            const int col = nt * 16 + lcol;
+            const bool live = row < p.M && col < p.N;
+            val += pre_bias[i];
+            if (EPI == HPA_FEPI_QKV) {
+                if (live) {
+                    const int C = p.N / 3;
+                    if (col < C) {
+                        p.out[(size_t)row * C + col] = val;
+                    } else {
+                        const int kv = col >= 2 * C;
+                        const int c = col - (kv ? 2 * C : C);
+                        const int hh = c >> 6, d = c & 63;
+                        const int ps = p.pos[row];
+                        const int page = p.bt[(size_t)row * p.bt_stride + ps / p.P];
+                        const int slot = ps % p.P;
+                        float* kvt = p.kv_base + (size_t)page * p.page_elems + ((size_t)kv * p.NH + hh) * p.P * 64;
+                        if (kv == 0)
+                            kvt[((d >> 2) * p.P + slot) * 4 + (d & 3)] = val;  // K: [chunk][slot][4]
+                        else
+                            kvt[slot * 64 + d] = val;  // V: [slot][64]
+                    }
+                }
+            } else if (EPI == HPA_FEPI_GELU) {
+                if (row < p.Mp && col < p.N) p.out[hpa::frag_index(row, col, p.N)] = live ? hpa::gelu_ref(val) : 0.f;
+            } else if (EPI == HPA_FEPI_RESID) {
+                val = live ? pre_res[i] + val : 0.f;  // residual_forward(out, res, proj)
+                if (row < p.Mp && col < p.N) p.out[hpa::frag_index(row, col, p.N)] = val;
+                tile[lrow * 17 + lcol] = val;
+            } else {  // LOGITS
+                if (live) p.out[(size_t)row * p.N + col] = val;
+                tile[lrow * 17 + lcol] = live ? val : -INFINITY;
+            }
+        }
+    }
+    if (rowstat) {
+        __syncthreads();
+        if (threadIdx.x < R) {
+            const int row = row0 + threadIdx.x;
+            const float* tr = tile + threadIdx.x * 17;
+            if (row < p.Mp) {
+                if (EPI == HPA_FEPI_RESID) {
+                    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) {
+                        s1 += tr[c];
+                        s2 += tr[c] * tr[c];
+                    }
+                    p.stats_out[((size_t)nt * p.Mp + row) * 2] = s1;
+                    p.stats_out[((size_t)nt * p.Mp + row) * 2 + 1] = s2;
+                } else {
+                    float bv = tr[0];
+                    int bi = 0;
+#pragma unroll
+                    for (int c = 1; c < 16; ++c)
+                        if (tr[c] > bv) {  // first max wins (paged_infer.c:937-951)
+                            bv = tr[c];
+                            bi = c;
+                        }
+                    p.part_out[((size_t)nt * p.Mp + row) * 2] = bv;
+                    p.part_out[((size_t)nt * p.Mp + row) * 2 + 1] = __int_as_float(nt * 16 + bi);
+                }
+            }
+        }
+    }
+    }
+};
+
 // MT = 16-row blocks per workgroup (1, 2 or 4), NW = waves sharing the K
 // range.  Grid (ntn, Mp/16/MT): one workgroup per (16-column tile, MT-block
 // row group).  MT = 1 spreads the MFMA work of a 64-row GEMM over 4x the
@@ -217,108 +336,125 @@ __global__ __launch_bounds__(NW * 64) void gemm16_kernel(FG p) {
         comp(Bb, t + 1);
     }
 
-    // ---- prefetch the epilogue operands of the elements this thread owns
-    // element e: rb = e>>8, reg = (e>>6)&3, l = e&63 -> row rb*16 + (l>>4)*4 + reg, col l&15
-    // (16x16 C/D map: col = lane & 15, row = 4*(lane >> 4) + reg)
-    constexpr int EPT = (MT * 256 + NT - 1) / NT;  // tile elements per thread
-    float pre_bias[EPT], pre_res[EPT];
-#pragma unroll
-    for (int i = 0; i < EPT; ++i) {
-        const int e = threadIdx.x + i * NT;
-        const int l = e & 63;
-        const int lrow = (e >> 8) * 16 + (l >> 4) * 4 + ((e >> 6) & 3);
-        const int row = row0 + lrow;
-        const int col = nt * 16 + (l & 15);
-        const bool in = e < MT * 256;
-        pre_bias[i] = (EPI != HPA_FEPI_LOGITS && in && p.bias && col < p.N) ? p.bias[col] : 0.f;
-        pre_res[i] = 0.f;
-        if (EPI == HPA_FEPI_RESID && in && row < p.M && col < p.N)
-            pre_res[i] = p.res_in[hpa::frag_index(row, col, p.N)];
-    }
+    Epi<NW, EPI, MT> epi;
+    epi.prefetch(p, nt, row0);
+    epi.finish(p, acc, red, tile, nt, row0);
+}
 
-    // ---- fold the waves' accumulators (fixed order)
-#pragma unroll
-    for (int r = 0; r < MT; ++r)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) red[w * MT * 256 + (r * 4 + g) * 64 + lane] = acc[r][g];
-    __syncthreads();
+// One-shot variant for the layer GEMMs (one 16-row block per workgroup,
+// K16 = NW * S): every k-step operand of the wave -- S weight fragments and S
+// activation fragments, 2 KiB per step -- is issued up front together with
+// the LayerNorm statistics and the epilogue's bias/residual, so the kernel
+// pays ONE dependent memory round trip instead of one per trip.  These GEMMs
+// run <= 2 waves per SIMD, so the registers are there.
+template <int NW, int EPI, int S>
+__global__ __launch_bounds__(NW * 64) void gemm16_os_kernel(FG p) {
+    constexpr int NT = NW * 64;
+    __shared__ __attribute__((aligned(16))) float smem[2 * HPA_FUSED_LN_KMAX + NW * 256 + 16 * 17 + 2 * 16];
+    float* lngb = smem;                         // LN weight [K], bias [K]
+    float* red = smem + 2 * HPA_FUSED_LN_KMAX;  // [NW][4 reg][64 lanes]
+    float* tile = red + NW * 256;               // [16 rows][17]
+    float* lnst = tile + 16 * 17;               // [16][2] mean, rstd
 
-    constexpr bool rowstat = EPI == HPA_FEPI_RESID || EPI == HPA_FEPI_LOGITS;
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int nt = blockIdx.x;
+    const int row0 = blockIdx.y * 16;
+    const int q4 = lane >> 4;
+    const bool use_ln = p.ln_stats != nullptr;
+
+    // 1. LN statistics partials of the 16 rows: 4 threads per row, issued first
+    constexpr int SPT = 12;  // partial tiles per thread: ln_ntiles <= 48 (C <= 768); else looped
+    float s1 = 0.f, s2 = 0.f;
+    float sa[SPT], sb[SPT];
+    const int srow = row0 + (threadIdx.x >> 2), sq = threadIdx.x & 3;
+    const bool stat_thread = use_ln && threadIdx.x < 64 && srow < p.M;
+    if (stat_thread) {
 #pragma unroll
-    for (int i = 0; i < EPT; ++i) {
-        const int e = threadIdx.x + i * NT;
-        if (e < MT * 256) {
-            float val = red[e];
-#pragma unroll
-            for (int ww = 1; ww < NW; ++ww) val += red[ww * MT * 256 + e];
-            const int l = e & 63;
-            const int lrow = (e >> 8) * 16 + (l >> 4) * 4 + ((e >> 6) & 3);
-            const int lcol = l & 15;
-            const int row = row0 + lrow;
-            const int col = nt * 16 + lcol;
-            const bool live = row < p.M && col < p.N;
-            val += pre_bias[i];
-            if (EPI == HPA_FEPI_QKV) {
-                if (live) {
-                    const int C = p.N / 3;
-                    if (col < C) {
-                        p.out[(size_t)row * C + col] = val;
-                    } else {
-                        const int kv = col >= 2 * C;
-                        const int c = col - (kv ? 2 * C : C);
-                        const int hh = c >> 6, d = c & 63;
-                        const int ps = p.pos[row];
-                        const int page = p.bt[(size_t)row * p.bt_stride + ps / p.P];
-                        const int slot = ps % p.P;
-                        float* kvt = p.kv_base + (size_t)page * p.page_elems + ((size_t)kv * p.NH + hh) * p.P * 64;
-                        if (kv == 0)
-                            kvt[((d >> 2) * p.P + slot) * 4 + (d & 3)] = val;  // K: [chunk][slot][4]
-                        else
-                            kvt[slot * 64 + d] = val;  // V: [slot][64]
-                    }
-                }
-            } else if (EPI == HPA_FEPI_GELU) {
-                if (row < p.Mp && col < p.N) p.out[hpa::frag_index(row, col, p.N)] = live ? hpa::gelu_ref(val) : 0.f;
-            } else if (EPI == HPA_FEPI_RESID) {
-                val = live ? pre_res[i] + val : 0.f;  // residual_forward(out, res, proj)
-                if (row < p.Mp && col < p.N) p.out[hpa::frag_index(row, col, p.N)] = val;
-                tile[lrow * 17 + lcol] = val;
-            } else {  // LOGITS
-                if (live) p.out[(size_t)row * p.N + col] = val;
-                tile[lrow * 17 + lcol] = live ? val : -INFINITY;
-            }
+        for (int j = 0; j < SPT; ++j) {
+            const int t = min(sq + 4 * j, p.ln_ntiles - 1);
+            sa[j] = p.ln_stats[((size_t)t * p.Mp + srow) * 2];
+            sb[j] = p.ln_stats[((size_t)t * p.Mp + srow) * 2 + 1];
         }
     }
-    if (rowstat) {
+    // 2. LN weight / bias -> registers (stored to LDS below)
+    float4 lw4 = make_float4(0.f, 0.f, 0.f, 0.f), lb4 = lw4;
+    const int K4 = p.K / 4;
+    if (use_ln && (int)threadIdx.x < K4) {
+        lw4 = reinterpret_cast<const float4*>(p.ln_w)[threadIdx.x];
+        lb4 = reinterpret_cast<const float4*>(p.ln_b)[threadIdx.x];
+    }
+    // 3. all operand fragments of this wave's k range [w*S, w*S+S)
+    const float4* __restrict__ wf = reinterpret_cast<const float4*>(p.w) + ((size_t)nt * p.K16 + w * S) * 64 + lane;
+    const float4* __restrict__ xf = reinterpret_cast<const float4*>(p.x) + ((size_t)blockIdx.y * p.K16 + w * S) * 64 + lane;
+    float4 wv[S], xv[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        wv[s] = wf[s * 64];
+        xv[s] = xf[s * 64];
+    }
+    // 4. epilogue operands
+    Epi<NW, EPI, 1> epi;
+    epi.prefetch(p, nt, row0);
+
+    // LN: reduce the statistics (waits only for the loads of step 1)
+    float mu = 0.f, rs = 0.f;
+    if (use_ln) {
+        if (stat_thread) {
+#pragma unroll
+            for (int j = 0; j < SPT; ++j)
+                if (sq + 4 * j < p.ln_ntiles) {
+                    s1 += sa[j];
+                    s2 += sb[j];
+                }
+            for (int t0 = sq + 4 * SPT; t0 < p.ln_ntiles; t0 += 4) {  // wider C
+                s1 += p.ln_stats[((size_t)t0 * p.Mp + srow) * 2];
+                s2 += p.ln_stats[((size_t)t0 * p.Mp + srow) * 2 + 1];
+            }
+        }
+        // 4 threads of a row are adjacent lanes of wave 0: combine in a fixed order
+        if (threadIdx.x < 64) {
+            const float a1 = __shfl_xor(s1, 1, 64), a2 = __shfl_xor(s2, 1, 64);
+            const float t1 = (sq & 1) ? a1 + s1 : s1 + a1;
+            const float t2 = (sq & 1) ? a2 + s2 : s2 + a2;
+            const float b1 = __shfl_xor(t1, 2, 64), b2 = __shfl_xor(t2, 2, 64);
+            const float S1 = (sq & 2) ? b1 + t1 : t1 + b1;
+            const float S2 = (sq & 2) ? b2 + t2 : t2 + b2;
+            if (sq == 0) {
+                const float m = S1 / p.K;
+                const float v = fmaxf(S2 / p.K - m * m, 0.f);
+                lnst[2 * (threadIdx.x >> 2)] = m;
+                lnst[2 * (threadIdx.x >> 2) + 1] = 1.0f / sqrtf(v + 1e-5f);
+            }
+        }
+        if ((int)threadIdx.x < K4) {
+            reinterpret_cast<float4*>(lngb)[threadIdx.x] = lw4;
+            reinterpret_cast<float4*>(lngb + HPA_FUSED_LN_KMAX)[threadIdx.x] = lb4;
+        }
+        for (int i = threadIdx.x + NT; i < K4; i += NT) {  // K > 4*NT
+            reinterpret_cast<float4*>(lngb)[i] = reinterpret_cast<const float4*>(p.ln_w)[i];
+            reinterpret_cast<float4*>(lngb + HPA_FUSED_LN_KMAX)[i] = reinterpret_cast<const float4*>(p.ln_b)[i];
+        }
         __syncthreads();
-        if (threadIdx.x < R) {
-            const int row = row0 + threadIdx.x;
-            const float* tr = tile + threadIdx.x * 17;
-            if (row < p.Mp) {
-                if (EPI == HPA_FEPI_RESID) {
-                    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-                    for (int c = 0; c < 16; ++c) {
-                        s1 += tr[c];
-                        s2 += tr[c] * tr[c];
-                    }
-                    p.stats_out[((size_t)nt * p.Mp + row) * 2] = s1;
-                    p.stats_out[((size_t)nt * p.Mp + row) * 2 + 1] = s2;
-                } else {
-                    float bv = tr[0];
-                    int bi = 0;
-#pragma unroll
-                    for (int c = 1; c < 16; ++c)
-                        if (tr[c] > bv) {  // first max wins (paged_infer.c:937-951)
-                            bv = tr[c];
-                            bi = c;
-                        }
-                    p.part_out[((size_t)nt * p.Mp + row) * 2] = bv;
-                    p.part_out[((size_t)nt * p.Mp + row) * 2 + 1] = __int_as_float(nt * 16 + bi);
-                }
-            }
-        }
+        mu = lnst[2 * (lane & 15)];
+        rs = lnst[2 * (lane & 15) + 1];
     }
+
+    // one accumulator chain: the same k order as gemm16_kernel with NW waves
+    f32x4 acc[1];
+    acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float4* sg = reinterpret_cast<const float4*>(lngb) + q4;
+    const float4* sbv = reinterpret_cast<const float4*>(lngb + HPA_FUSED_LN_KMAX) + q4;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        float4 xa = xv[s];
+        if (use_ln) xa = ln4(xa, mu, rs, sg[4 * (w * S + s)], sbv[4 * (w * S + s)]);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.x, wv[s].x, acc[0], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.y, wv[s].y, acc[0], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.z, wv[s].z, acc[0], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.w, wv[s].w, acc[0], 0, 0, 0);
+    }
+    epi.finish(p, acc, red, tile, nt, row0);
 }
 
 // ---------------------------------------------------------------- frag packing
@@ -444,6 +580,33 @@ int launch16(const FG& p, int epi) {
     return 0;
 }
 
+template <int NW, int S>
+int launch16_os(const FG& p, int epi) {
+    dim3 grid(p.ntn, p.Mp / 16), block(NW * 64);
+    switch (epi) {
+        case HPA_FEPI_QKV: gemm16_os_kernel<NW, HPA_FEPI_QKV, S><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_RESID: gemm16_os_kernel<NW, HPA_FEPI_RESID, S><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_GELU: gemm16_os_kernel<NW, HPA_FEPI_GELU, S><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_LOGITS: gemm16_os_kernel<NW, HPA_FEPI_LOGITS, S><<<grid, block, 0, hpa_stream()>>>(p); break;
+        default: return hpa_fail(__FILE__, __LINE__, "gemm_fused: unknown epilogue");
+    }
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+// one-shot instances: (NW, S) with K16 = NW * S for K = 768 (K16 = 48) and 3072 (192)
+int launch_os(const FG& p, int epi, int nw) {
+    const int S = p.K16 / nw;
+    if (p.K16 % nw) return -1;
+    switch (nw * 100 + S) {
+        case 4 * 100 + 12: return launch16_os<4, 12>(p, epi);
+        case 8 * 100 + 6: return launch16_os<8, 6>(p, epi);
+        case 16 * 100 + 3: return launch16_os<16, 3>(p, epi);
+        case 8 * 100 + 24: return launch16_os<8, 24>(p, epi);
+        default: return -1;
+    }
+}
+
 template <int NW>
 int launch16_mt(const FG& p, int epi, int mt) {
     switch (mt) {
@@ -553,6 +716,12 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
     int mt = g->row_blocks ? g->row_blocks : pick[1];
     HPA_REQUIRE(mt == 1 || mt == 2 || mt == 4, "gemm_fused: row_blocks must be 1, 2 or 4");
     while ((p.Mp / 16) % mt) mt >>= 1;  // row blocks of this M
+    HPA_REQUIRE(g->variant >= 0 && g->variant <= 2, "gemm_fused: variant must be 0, 1 or 2");
+    if (g->variant == 2 || (g->variant == 0 && mt == 1 && p.ntn < 1024)) {
+        const int rc = launch_os(p, g->epilogue, nw);
+        if (rc >= 0) return rc;
+        HPA_REQUIRE(g->variant == 0, "gemm_fused: one-shot needs (waves, K/16) in {(4,48), (8,48), (16,48), (8,192)}");
+    }
     switch (nw) {
         case 4: return launch16_mt<4>(p, g->epilogue, mt);
         case 8: return launch16_mt<8>(p, g->epilogue, mt);

@@ -57,7 +57,7 @@ class HpaFusedGemm(ctypes.Structure):
                 ("res_in", _V), ("stats_out", _V), ("part_out", _V),
                 ("pool", ctypes.POINTER(HpaKVPool)), ("layer", ctypes.c_int), ("block_table", _V),
                 ("bt_stride", ctypes.c_int), ("pos", _V), ("waves", ctypes.c_int),
-                ("row_blocks", ctypes.c_int)]
+                ("row_blocks", ctypes.c_int), ("variant", ctypes.c_int)]
 
 
 HPA_FEPI_QKV, HPA_FEPI_RESID, HPA_FEPI_GELU, HPA_FEPI_LOGITS = 0, 1, 2, 3

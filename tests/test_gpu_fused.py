@@ -48,7 +48,7 @@ def test_pack_unpack_roundtrip(hip):
     assert np.array_equal(d_b.download(a.shape), a)
 
 
-def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixed=None):
+def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixed=None, variant=0):
     L = hip.lib()
     x = rng.uniform(-1, 1, (M, K)).astype(np.float32)
     W = rng.uniform(-0.05, 0.05, (N, K)).astype(np.float32)
@@ -81,6 +81,7 @@ def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixe
     g.bias = dev(bias) if epi != hip.HPA_FEPI_LOGITS else None
     g.waves = waves
     g.row_blocks = rb
+    g.variant = variant
     g.epilogue = epi
     acc = a @ W.astype(np.float64).T
     bound = 4e-6 * (np.abs(a) @ np.abs(W.astype(np.float64)).T) + 2e-6
@@ -223,3 +224,47 @@ def test_fused_rows_independent_of_split(hip, epi):
         outs.append(got[:16])
     for o in outs[1:]:
         assert np.array_equal(outs[0], o)
+
+
+@pytest.mark.parametrize("epi,K,N,waves", [("RESID", 768, 768, 4), ("GELU", 768, 3072, 8), ("RESID", 768, 768, 16),
+                                           ("RESID", 3072, 768, 8), ("QKV", 768, 2304, 4)])
+@pytest.mark.parametrize("M", [64, 37])
+def test_fused_oneshot_bit_identical_to_looped(hip, epi, K, N, waves, M):
+    """the one-shot kernel (all operand loads up front) keeps the looped
+    kernel's per-wave K ranges, k order and LN statistics order: equal bit
+    for bit, and within the f64 bound"""
+    e = getattr(hip, "HPA_FEPI_" + epi)
+    r = np.random.default_rng(11)
+    fixed = dict(x=r.uniform(-1, 1, (M, K)).astype(np.float32),
+                 W=r.uniform(-0.05, 0.05, (N, K)).astype(np.float32),
+                 bias=r.uniform(-0.1, 0.1, N).astype(np.float32),
+                 lw=r.uniform(0.8, 1.2, K).astype(np.float32), lb=r.uniform(-0.1, 0.1, K).astype(np.float32))
+    res = r.uniform(-1, 1, (M, N)).astype(np.float32)
+    ln = K == 768
+    outs = []
+    for variant in (1, 2):
+        pool_args = None
+        if epi == "QKV":
+            NH, P = N // 3 // 64, 16
+            pool = hip.Pool(1, NH, P, 4 * M)
+            bt = np.arange(4 * M, dtype=np.int32).reshape(M, 4)
+            pos = (np.arange(M, dtype=np.int32) * 7) % 64
+            pool_args = (pool, bt, pos)
+        out, acc, bound, keep = _run(hip, e, M, K, N, waves, ln=ln, rng=np.random.default_rng(0), res=res,
+                                     rb=1, fixed=fixed, variant=variant, pool_args=pool_args)
+        if epi == "QKV":
+            q = out.download((M, N // 3))
+            k, v = pool.read_tokens(0, bt[M - 1], pos[M - 1] + 1)
+            outs.append((q, k[pos[M - 1]].copy(), v[pos[M - 1]].copy()))
+            assert np.all(np.abs(q - acc[:, :N // 3]) <= bound[:, :N // 3])
+        else:
+            Mp = (M + 15) // 16 * 16
+            got = hip.from_frag(out.download(Mp * N), M, N)
+            outs.append((got,))
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+
+
+def test_fused_oneshot_rejects_unsupported_shape(hip):
+    with pytest.raises(RuntimeError):
+        _run(hip, hip.HPA_FEPI_GELU, 16, 512, 64, 4, ln=False, rng=np.random.default_rng(1), variant=2)

@@ -1,0 +1,26 @@
+#!/usr/bin/env python3
+"""Paged decode attention alone vs batch size and waves per workgroup:
+GPT-2 124M shapes, synthetic K/V to ctx, back-to-back launches timed with
+HIP events (gpt2_decode_time_attention).  usage: attn_scan.py [ctx]"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "llm.c-paged_amd"))
+import numpy as np  # noqa: E402
+import pagedattn as pa  # noqa: E402
+
+ctx = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+pa.init(0)
+L = pa.lib()
+cfg = dict(pa.GPT2_124M)
+m = pa.Model(cfg, seed=1)
+for B in (8, 16, 32, 64, 128):
+    m.decode_init(B, 16, ctx)
+    m.fill_random(ctx - 2, seed=3)
+    m.step(np.zeros(B, np.int32))
+    for nw in (1, 2, 4, 8):
+        pa.check(L.hpa_set_attention_waves(nw), "waves")
+        ms, by = m.time_attention(48)
+        print(f"B={B:4d} waves={nw}  {ms * 1e3:8.2f} us  {by / ms / 1e6:8.1f} GB/s", flush=True)
+    pa.check(L.hpa_set_attention_waves(4), "waves")

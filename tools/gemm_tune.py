@@ -78,6 +78,9 @@ SHAPES = [("qkv", B, C, 3 * C, pa.HPA_FEPI_GELU, True), ("attproj", B, C, C, pa.
           ("logits", B, C, V, pa.HPA_FEPI_LOGITS, True)]
 
 
+ONESHOT = {(4, 48), (8, 48), (16, 48), (8, 192)}  # hpa_fused.hip launch_os instances
+
+
 def main():
     pa.init(0)
     L = pa.lib()
@@ -90,27 +93,32 @@ def main():
         rb_eff = pk[1]
         while ((M + 15) // 16) % rb_eff:
             rb_eff //= 2
-        auto = (pk[0], rb_eff)
+        oneshot = rb_eff == 1 and (N + 15) // 16 < 1024 and (pk[0], K // 16) in ONESHOT
+        auto = (pk[0], rb_eff, 2 if oneshot else 1)
         res = []
         ref = None
         for waves in (4, 8, 16):
             for rb in (1, 2, 4):
-                if ((M + 15) // 16) % rb:
-                    continue
-                g.waves, g.row_blocks = waves, rb
-                us = time_fused(g)
-                o = out_copy(g, M, N, epi)
-                if ref is None:
-                    ref = o
-                res.append((us, (waves, rb), float(np.abs(o - ref).max())))
+                for variant in (1, 2):
+                    if ((M + 15) // 16) % rb or (variant == 2 and rb != 1):
+                        continue
+                    g.waves, g.row_blocks, g.variant = waves, rb, variant
+                    try:
+                        us = time_fused(g)
+                    except RuntimeError:
+                        continue
+                    o = out_copy(g, M, N, epi)
+                    if ref is None:
+                        ref = o
+                    res.append((us, (waves, rb, variant), float(np.abs(o - ref).max())))
         flops = 2.0 * M * K * N
         wbytes = 4.0 * N * K
         best = min(res)
         total_best += best[0]
-        total_auto += [r for r in res if r[1] == auto][0][0]
-        print(f"{name:8s} M={M} K={K} N={N} auto (waves, row_blocks)={auto}")
+        total_auto += ([r for r in res if r[1] == auto] or [best])[0][0]
+        print(f"{name:8s} M={M} K={K} N={N} auto (waves, row_blocks, variant)={auto}")
         for us, waves, err in sorted(res):
-            print(f"   {us:8.2f} us  (waves, rb)={waves}  {flops / us / 1e6:7.1f} TF/s "
+            print(f"   {us:8.2f} us  (waves, rb, variant)={waves}  {flops / us / 1e6:7.1f} TF/s "
                   f"{wbytes / us / 1e3:7.1f} GB/s(W)  maxdiff={err:.2e}")
     print(f"sum best {total_best:.1f} us   sum auto {total_auto:.1f} us")
 

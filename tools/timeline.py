@@ -37,3 +37,7 @@ for k in tot:
     d, g = durs[k], gaps[k]
     print(f"{k:60s} n={len(d):5d} avg {sum(d) / len(d) / 1e3:8.2f} us  idle-before {sum(g) / len(g) / 1e3:6.2f} us"
           f"  sum {sum(d) / 1e3:9.1f} us")
+
+# concurrency: sum of kernel durations over the union of their intervals
+tot = sum(e - s for s, e, *_ in ks)
+print(f"concurrency (sum of durations / busy time): {tot / busy:.2f}")
