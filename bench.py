@@ -79,6 +79,7 @@ def parse():
     ap.add_argument("--lanes", type=int, default=1, help="micro-batch lanes (concurrent row groups)")
     ap.add_argument("--gemm-waves", default="", help="fused GEMM waves qkv,attproj,fc,fcproj,logits (0 = auto)")
     ap.add_argument("--gemm-rows", default="", help="fused GEMM 16-row blocks per workgroup, same order")
+    ap.add_argument("--gemm-cols", default="", help="fused GEMM 16-column tiles per workgroup, same order")
     return ap.parse_args()
 
 
@@ -164,9 +165,9 @@ def main():
     model.set_fused(not args.unfused)
     if not args.unfused:
         model.set_lanes(args.lanes)
-    if args.gemm_waves or args.gemm_rows:
-        model.gemm_config([int(x) for x in args.gemm_waves.split(",")] if args.gemm_waves else None,
-                          [int(x) for x in args.gemm_rows.split(",")] if args.gemm_rows else None)
+    if args.gemm_waves or args.gemm_rows or args.gemm_cols:
+        ints = lambda a: [int(x) for x in a.split(",")] if a else None  # noqa: E731
+        model.gemm_config(ints(args.gemm_waves), ints(args.gemm_rows), ints(args.gemm_cols))
     model.reserve(ctx)
     rng = np.random.default_rng(1000 + rank)
     if args.prefill == "synthetic":
@@ -276,7 +277,8 @@ def main():
                        "hip_graph": not args.no_graph, "gemm_path": "unfused" if args.unfused else "fused",
                        "lanes": 1 if args.unfused else L.gpt2_decode_lanes(model.h),
                        "gemm_waves": [int(x) for x in model.gemm_config()[0]],
-                       "gemm_row_blocks": [int(x) for x in model.gemm_config()[1]], "device": name},
+                       "gemm_row_blocks": [int(x) for x in model.gemm_config()[1]],
+                       "gemm_col_tiles": [int(x) for x in model.gemm_config()[2]], "device": name},
             "step_roofline": {"bytes_per_step_rank0": int(step_bytes),
                               "achieved_GBps": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
                               "frac_of_8TBps": round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},

@@ -205,11 +205,14 @@ typedef struct {
     int variant;          /* 0 = by shape; 1 = looped (two trips in flight);
                              2 = one-shot (every operand load issued up front; one
                              row block; (waves, K/16) in {(4,48),(8,48),(16,48),(8,192)}) */
+    int col_tiles;        /* 16-column tiles per workgroup: 1; 2 (waves 4/8, row_blocks
+                             2/4); 4 (waves 4, row_blocks 4); 0 = by shape.  A hint:
+                             where M's row blocks or the waves cannot carry it, 1 */
 } HpaFusedGemm;
 int hpa_gemm_fused(const HpaFusedGemm* g);
-/* the launch shape hpa_gemm_fused picks when waves / row_blocks are 0:
- * out2 = {waves, row_blocks} */
-void hpa_fused_pick(int M, int N, int K, int* out2);
+/* the launch shape hpa_gemm_fused picks when waves / row_blocks / col_tiles
+ * are 0: out3 = {waves, row_blocks, col_tiles} */
+void hpa_fused_pick(int M, int N, int K, int* out3);
 int hpa_fused_pick_waves(int M, int N, int K);
 /* residual = wte[tok] + wpe[pos] in frag layout [Mp][C], stats (1 tile) */
 int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const float* wpe,

@@ -162,9 +162,10 @@ int    gpt2_decode_positions(GPT2* model, int* host_pos);
 /* the per-GEMM split-K chosen for this model/batch (qkv, attproj, fc, fcproj) */
 int    gpt2_decode_splits(GPT2* model, int* splits4);
 /* fused GEMM launch shapes [qkv, attproj, fc, fcproj, logits]: waves per
- * workgroup (4/8/16) and 16-row blocks per workgroup (1/2/4).  set = 0
- * copies them out; set = 1 applies the nonzero entries (NULL = keep) */
-int    gpt2_decode_gemm_config(GPT2* model, int* waves5, int* row_blocks5, int set);
+ * workgroup (4/8/16), 16-row blocks (1/2/4) and 16-column tiles (1/2/4) per
+ * workgroup.  set = 0 copies them out; set = 1 applies the nonzero entries
+ * (NULL = keep).  Invalid combinations fail at the next step's launch. */
+int    gpt2_decode_gemm_config(GPT2* model, int* waves5, int* row_blocks5, int* col_tiles5, int set);
 /* micro-batch lanes (fused path): the batch is cut into `lanes` groups of
  * whole 16-row blocks, each running the step on its own stream so one
  * group's attention overlaps another's GEMMs; results are identical to

@@ -56,7 +56,22 @@ struct FG {
     const int* bt;
     int bt_stride;
     const int* pos;
+    int gx, gy;  // column-tile groups x row groups of the launch
 };
+
+// XCD-aware workgroup order (MI355X_MICROARCH.md "Workgroup dispatch":
+// blocks b and b+8 share an XCD -- used for L2 affinity only).  The 1-D grid
+// of ceil(gx/8)*8*gy blocks is dealt so that the gy row groups of one column
+// group run back to back on ONE XCD: its weight tile is fetched from HBM once
+// and re-read from that XCD's L2.  Returns false for the padding blocks.
+__device__ __forceinline__ bool xcd_tile(const FG& p, int& cx, int& ry) {
+    const int bid = blockIdx.x;
+    const int xg = bid & 7, s = bid >> 3;
+    const int q = s / p.gy;
+    ry = s - q * p.gy;
+    cx = q * 8 + xg;
+    return cx < p.gx;
+}
 
 __device__ __forceinline__ float4 ln4(float4 a, float mu, float rs, float4 g, float4 b) {
     // paged_infer.c:80-81: n = s * (x - m); o = n * w + b
@@ -68,27 +83,39 @@ __device__ __forceinline__ float4 ln4(float4 a, float mu, float rs, float4 g, fl
 }
 
 // ---- shared epilogue ---------------------------------------------------
-// Tile element e (0 .. MT*256-1) of a workgroup: rb = e>>8, reg = (e>>6)&3,
-// l = e&63 -> row rb*16 + (l>>4)*4 + reg, col l&15 (16x16 C/D map: col =
-// lane & 15, row = 4*(lane >> 4) + reg).  Thread t owns e = t + i*NT.
-template <int NW, int EPI, int MT>
+// A workgroup's output is NTW 16-column tiles x MT 16-row blocks.  Element e
+// (0 .. NTW*MT*256-1): column tile j = e / (MT*256); within it e' = e % (MT*256):
+// rb = e'>>8, reg = (e'>>6)&3, l = e'&63 -> row rb*16 + (l>>4)*4 + reg,
+// col l&15 (16x16 C/D map: col = lane & 15, row = 4*(lane >> 4) + reg).
+// Thread t owns e = t + i*NT.  Accumulator acc[j*MT + r] holds (tile j, block r).
+template <int NW, int EPI, int MT, int NTW = 1>
 struct Epi {
     static constexpr int NT = NW * 64;
     static constexpr int R = MT * 16;
-    static constexpr int EPT = (MT * 256 + NT - 1) / NT;  // tile elements per thread
+    static constexpr int TE = MT * 256;                    // elements per column tile
+    static constexpr int EPT = (NTW * TE + NT - 1) / NT;   // elements per thread
     float pre_bias[EPT], pre_res[EPT];
+
+    __device__ __forceinline__ static void where(int e, int nt0, int row0, int& j, int& lrow, int& lcol,
+                                                 int& row, int& col) {
+        j = e / TE;
+        const int e2 = e - j * TE;
+        const int l = e2 & 63;
+        lrow = (e2 >> 8) * 16 + (l >> 4) * 4 + ((e2 >> 6) & 3);
+        lcol = l & 15;
+        row = row0 + lrow;
+        col = (nt0 + j) * 16 + lcol;
+    }
 
     // bias / residual operands of the owned elements: issued early so their
     // latency hides under the main loop
-    __device__ __forceinline__ void prefetch(const FG& p, int nt, int row0) {
+    __device__ __forceinline__ void prefetch(const FG& p, int nt0, int row0) {
 #pragma unroll
         for (int i = 0; i < EPT; ++i) {
             const int e = threadIdx.x + i * NT;
-            const int l = e & 63;
-            const int lrow = (e >> 8) * 16 + (l >> 4) * 4 + ((e >> 6) & 3);
-            const int row = row0 + lrow;
-            const int col = nt * 16 + (l & 15);
-            const bool in = e < MT * 256;
+            int j, lrow, lcol, row, col;
+            where(e, nt0, row0, j, lrow, lcol, row, col);
+            const bool in = e < NTW * TE;
             pre_bias[i] = (EPI != HPA_FEPI_LOGITS && in && p.bias && col < p.N) ? p.bias[col] : 0.f;
             pre_res[i] = 0.f;
             if (EPI == HPA_FEPI_RESID && in && row < p.M && col < p.N)
@@ -97,117 +124,125 @@ struct Epi {
     }
 
     // fold the waves' accumulators through LDS (fixed order) and apply the epilogue
-    __device__ __forceinline__ void finish(const FG& p, const f32x4* acc, float* red, float* tile, int nt,
+    __device__ __forceinline__ void finish(const FG& p, const f32x4* acc, float* red, float* tile, int nt0,
                                            int row0) {
         const int lane = threadIdx.x & 63;
         const int w = threadIdx.x >> 6;
 #pragma unroll
-    for (int r = 0; r < MT; ++r)
+        for (int j = 0; j < NTW; ++j)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) red[w * MT * 256 + (r * 4 + g) * 64 + lane] = acc[r][g];
-    __syncthreads();
-
-    constexpr bool rowstat = EPI == HPA_FEPI_RESID || EPI == HPA_FEPI_LOGITS;
+            for (int r = 0; r < MT; ++r)
 #pragma unroll
-    for (int i = 0; i < EPT; ++i) {
-        const int e = threadIdx.x + i * NT;
-        if (e < MT * 256) {
-            float val = red[e];
-#pragma unroll
-            for (int ww = 1; ww < NW; ++ww) val += red[ww * MT * 256 + e];
-            const int l = e & 63;
-            const int lrow = (e >> 8) * 16 + (l >> 4) * 4 + ((e >> 6) & 3);
-            const int lcol = l & 15;
-            const int row = row0 + lrow;
-            const int col = nt * 16 + lcol;
-            const bool live = row < p.M && col < p.N;
-            val += pre_bias[i];
-            if (EPI == HPA_FEPI_QKV) {
-                if (live) {
-                    const int C = p.N / 3;
-                    if (col < C) {
-                        p.out[(size_t)row * C + col] = val;
-                    } else {
-                        const int kv = col >= 2 * C;
-                        const int c = col - (kv ? 2 * C : C);
-                        const int hh = c >> 6, d = c & 63;
-                        const int ps = p.pos[row];
-                        const int page = p.bt[(size_t)row * p.bt_stride + ps / p.P];
-                        const int slot = ps % p.P;
-                        float* kvt = p.kv_base + (size_t)page * p.page_elems + ((size_t)kv * p.NH + hh) * p.P * 64;
-                        if (kv == 0)
-                            kvt[((d >> 2) * p.P + slot) * 4 + (d & 3)] = val;  // K: [chunk][slot][4]
-                        else
-                            kvt[slot * 64 + d] = val;  // V: [slot][64]
-                    }
-                }
-            } else if (EPI == HPA_FEPI_GELU) {
-                if (row < p.Mp && col < p.N) p.out[hpa::frag_index(row, col, p.N)] = live ? hpa::gelu_ref(val) : 0.f;
-            } else if (EPI == HPA_FEPI_RESID) {
-                val = live ? pre_res[i] + val : 0.f;  // residual_forward(out, res, proj)
-                if (row < p.Mp && col < p.N) p.out[hpa::frag_index(row, col, p.N)] = val;
-                tile[lrow * 17 + lcol] = val;
-            } else {  // LOGITS
-                if (live) p.out[(size_t)row * p.N + col] = val;
-                tile[lrow * 17 + lcol] = live ? val : -INFINITY;
-            }
-        }
-    }
-    if (rowstat) {
+                for (int g = 0; g < 4; ++g)
+                    red[w * NTW * TE + j * TE + (r * 4 + g) * 64 + lane] = acc[j * MT + r][g];
         __syncthreads();
-        if (threadIdx.x < R) {
-            const int row = row0 + threadIdx.x;
-            const float* tr = tile + threadIdx.x * 17;
-            if (row < p.Mp) {
-                if (EPI == HPA_FEPI_RESID) {
-                    float s1 = 0.f, s2 = 0.f;
+
+        constexpr bool rowstat = EPI == HPA_FEPI_RESID || EPI == HPA_FEPI_LOGITS;
 #pragma unroll
-                    for (int c = 0; c < 16; ++c) {
-                        s1 += tr[c];
-                        s2 += tr[c] * tr[c];
-                    }
-                    p.stats_out[((size_t)nt * p.Mp + row) * 2] = s1;
-                    p.stats_out[((size_t)nt * p.Mp + row) * 2 + 1] = s2;
-                } else {
-                    float bv = tr[0];
-                    int bi = 0;
+        for (int i = 0; i < EPT; ++i) {
+            const int e = threadIdx.x + i * NT;
+            if (e < NTW * TE) {
+                float val = red[e];
 #pragma unroll
-                    for (int c = 1; c < 16; ++c)
-                        if (tr[c] > bv) {  // first max wins (paged_infer.c:937-951)
-                            bv = tr[c];
-                            bi = c;
+                for (int ww = 1; ww < NW; ++ww) val += red[ww * NTW * TE + e];
+                int j, lrow, lcol, row, col;
+                where(e, nt0, row0, j, lrow, lcol, row, col);
+                const bool live = row < p.M && col < p.N;
+                val += pre_bias[i];
+                if (EPI == HPA_FEPI_QKV) {
+                    if (live) {
+                        const int C = p.N / 3;
+                        if (col < C) {
+                            p.out[(size_t)row * C + col] = val;
+                        } else {
+                            const int kv = col >= 2 * C;
+                            const int c = col - (kv ? 2 * C : C);
+                            const int hh = c >> 6, d = c & 63;
+                            const int ps = p.pos[row];
+                            const int page = p.bt[(size_t)row * p.bt_stride + ps / p.P];
+                            const int slot = ps % p.P;
+                            float* kvt = p.kv_base + (size_t)page * p.page_elems + ((size_t)kv * p.NH + hh) * p.P * 64;
+                            if (kv == 0)
+                                kvt[((d >> 2) * p.P + slot) * 4 + (d & 3)] = val;  // K: [chunk][slot][4]
+                            else
+                                kvt[slot * 64 + d] = val;  // V: [slot][64]
                         }
-                    p.part_out[((size_t)nt * p.Mp + row) * 2] = bv;
-                    p.part_out[((size_t)nt * p.Mp + row) * 2 + 1] = __int_as_float(nt * 16 + bi);
+                    }
+                } else if (EPI == HPA_FEPI_GELU) {
+                    if (row < p.Mp && col < p.N)
+                        p.out[hpa::frag_index(row, col, p.N)] = live ? hpa::gelu_ref(val) : 0.f;
+                } else if (EPI == HPA_FEPI_RESID) {
+                    val = live ? pre_res[i] + val : 0.f;  // residual_forward(out, res, proj)
+                    if (row < p.Mp && col < p.N) p.out[hpa::frag_index(row, col, p.N)] = val;
+                    tile[(j * R + lrow) * 17 + lcol] = val;
+                } else {  // LOGITS
+                    if (live) p.out[(size_t)row * p.N + col] = val;
+                    tile[(j * R + lrow) * 17 + lcol] = live ? val : -INFINITY;
                 }
             }
         }
-    }
+        if (rowstat) {
+            __syncthreads();
+            for (int t = threadIdx.x; t < NTW * R; t += NT) {
+                const int j = t / R, lr = t - j * R;
+                const int row = row0 + lr, nt = nt0 + j;
+                const float* tr = tile + t * 17;
+                if (row < p.Mp && nt < p.ntn) {
+                    if (EPI == HPA_FEPI_RESID) {
+                        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                        for (int c = 0; c < 16; ++c) {
+                            s1 += tr[c];
+                            s2 += tr[c] * tr[c];
+                        }
+                        p.stats_out[((size_t)nt * p.Mp + row) * 2] = s1;
+                        p.stats_out[((size_t)nt * p.Mp + row) * 2 + 1] = s2;
+                    } else {
+                        float bv = tr[0];
+                        int bi = 0;
+#pragma unroll
+                        for (int c = 1; c < 16; ++c)
+                            if (tr[c] > bv) {  // first max wins (paged_infer.c:937-951)
+                                bv = tr[c];
+                                bi = c;
+                            }
+                        p.part_out[((size_t)nt * p.Mp + row) * 2] = bv;
+                        p.part_out[((size_t)nt * p.Mp + row) * 2 + 1] = __int_as_float(nt * 16 + bi);
+                    }
+                }
+            }
+        }
     }
 };
 
-// MT = 16-row blocks per workgroup (1, 2 or 4), NW = waves sharing the K
-// range.  Grid (ntn, Mp/16/MT): one workgroup per (16-column tile, MT-block
-// row group).  MT = 1 spreads the MFMA work of a 64-row GEMM over 4x the
-// workgroups -- the per-CU fp32 MFMA rate, not bandwidth, bounds these
-// GEMMs when only N/16 CUs are busy.
-template <int NW, int EPI, int MT>
+// MT = 16-row blocks per workgroup (1, 2 or 4), NTW = 16-column tiles per
+// workgroup (every wave computes all of them over its K range), NW = waves
+// sharing the K range.  Grid (ceil(ntn/NTW), Mp/16/MT).  MT = 1 spreads the
+// MFMA work of a 64-row GEMM over 4x the workgroups -- the per-CU fp32 MFMA
+// rate, not bandwidth, bounds these GEMMs when only N/16 CUs are busy.  NTW > 1
+// (logits) reuses every activation fragment for NTW weight fragments: with
+// NTW = 1 a k-step loads 5 KiB for 16 MFMAs, more than the CU's L2->L1 port
+// feeds at three waves per SIMD.
+template <int NW, int EPI, int MT, int NTW>
 __global__ __launch_bounds__(NW * 64) void gemm16_kernel(FG p) {
     constexpr int NT = NW * 64;
-    constexpr int R = MT * 16;                 // rows per workgroup
-    // k-steps per trip (two trips in flight; register budget at 16 waves)
-    constexpr int U = NW >= 16 ? (MT == 4 ? 1 : 2) : (MT == 4 ? 2 : 4);
-    __shared__ __attribute__((aligned(16))) float smem[2 * HPA_FUSED_LN_KMAX + NW * MT * 256 + R * 17 + 10 * R];
-    float* lngb = smem;                  // LN weight [K], bias [K]
-    float* red = smem + 2 * HPA_FUSED_LN_KMAX;  // [NW][MT rb x 4 reg][64 lanes]
-    float* tile = red + NW * MT * 256;   // [R rows][17]
-    float* lnst = tile + R * 17;         // [R][2] mean, rstd
-    float* lnscr = lnst + 2 * R;         // [4R][2]
+    constexpr int R = MT * 16;  // rows per workgroup
+    // k-steps per trip (two trips in flight; register budget)
+    constexpr int U = NTW > 1 ? 1 : (NW >= 16 ? (MT == 4 ? 1 : 2) : (MT == 4 ? 2 : 4));
+    __shared__ __attribute__((aligned(16))) float smem[2 * HPA_FUSED_LN_KMAX + NW * MT * NTW * 256 +
+                                                       NTW * R * 17 + 10 * R];
+    float* lngb = smem;                              // LN weight [K], bias [K]
+    float* red = smem + 2 * HPA_FUSED_LN_KMAX;       // [NW][NTW][MT rb x 4 reg][64 lanes]
+    float* tile = red + NW * MT * NTW * 256;         // [NTW][R rows][17]
+    float* lnst = tile + NTW * R * 17;               // [R][2] mean, rstd
+    float* lnscr = lnst + 2 * R;                     // [4R][2]
 
+    int cx, ry;
+    if (!xcd_tile(p, cx, ry)) return;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    const int nt = blockIdx.x;
-    const int rb0 = blockIdx.y * MT;
+    const int nt0 = cx * NTW;
+    const int rb0 = ry * MT;
     const int row0 = rb0 * 16;
     const int q4 = lane >> 4;  // which 4-k group of the 16-k step
 
@@ -215,7 +250,10 @@ __global__ __launch_bounds__(NW * 64) void gemm16_kernel(FG p) {
     const int per = (p.K16 + NW - 1) / NW;
     const int kb0 = w * per;
     const int nsteps = max(0, min(p.K16, kb0 + per) - kb0);
-    const float4* __restrict__ wf = reinterpret_cast<const float4*>(p.w) + (size_t)nt * p.K16 * 64 + lane;
+    const float4* __restrict__ wf[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)  // tail tiles past ntn re-read the last tile (never stored)
+        wf[j] = reinterpret_cast<const float4*>(p.w) + (size_t)min(nt0 + j, p.ntn - 1) * p.K16 * 64 + lane;
     const float4* __restrict__ xf = reinterpret_cast<const float4*>(p.x) + (size_t)rb0 * p.K16 * 64 + lane;
     const size_t rbs = (size_t)p.K16 * 64;  // float4 stride between row blocks
     const bool use_ln = p.ln_stats != nullptr;
@@ -223,14 +261,15 @@ __global__ __launch_bounds__(NW * 64) void gemm16_kernel(FG p) {
     const float4* sb = reinterpret_cast<const float4*>(lngb + HPA_FUSED_LN_KMAX) + q4;
 
     struct Buf {
-        float4 w[U], x[U][MT];
+        float4 w[U][NTW], x[U][MT];
     };
     Buf A, Bb;
     auto load = [&](Buf& f, int t) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int k = kb0 + min(t * U + u, max(nsteps - 1, 0));  // clamped, unconditional
-            f.w[u] = wf[(size_t)k * 64];
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) f.w[u][j] = wf[j][(size_t)k * 64];
 #pragma unroll
             for (int r = 0; r < MT; ++r) f.x[u][r] = xf[r * rbs + (size_t)k * 64];
         }
@@ -289,13 +328,13 @@ __global__ __launch_bounds__(NW * 64) void gemm16_kernel(FG p) {
         }
     }
 
-    // one accumulator chain per row block: a row's summation order depends
-    // only on NW (the per-wave K ranges), never on MT or M -- so results are
-    // bit-identical across row splits and micro-batch lanes.  The dependent
-    // MFMA latency is covered by the other waves resident on the SIMD.
-    f32x4 acc[MT];
+    // one accumulator chain per (column tile, row block): a row's summation
+    // order depends only on NW (the per-wave K ranges), never on MT, NTW or M
+    // -- results are bit-identical across launch shapes and micro-batch lanes.
+    // The dependent MFMA latency is covered by the other chains / waves.
+    f32x4 acc[MT * NTW];
 #pragma unroll
-    for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < MT * NTW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     auto comp = [&](Buf& f, int t) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -312,19 +351,17 @@ __global__ __launch_bounds__(NW * 64) void gemm16_kernel(FG p) {
                     xa[r] = f.x[u][r];
                     if (use_ln) xa[r] = ln4(xa[r], mu[r], rs[r], g, b);
                 }
-                const float4 wv = f.w[u];
 #pragma unroll
-                for (int r = 0; r < MT; ++r)
-                    acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[r].x, wv.x, acc[r], 0, 0, 0);
+                for (int q = 0; q < 4; ++q)
 #pragma unroll
-                for (int r = 0; r < MT; ++r)
-                    acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[r].y, wv.y, acc[r], 0, 0, 0);
+                    for (int j = 0; j < NTW; ++j)
 #pragma unroll
-                for (int r = 0; r < MT; ++r)
-                    acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[r].z, wv.z, acc[r], 0, 0, 0);
-#pragma unroll
-                for (int r = 0; r < MT; ++r)
-                    acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[r].w, wv.w, acc[r], 0, 0, 0);
+                        for (int r = 0; r < MT; ++r) {
+                            const float xs = q == 0 ? xa[r].x : q == 1 ? xa[r].y : q == 2 ? xa[r].z : xa[r].w;
+                            const float4 wv = f.w[u][j];
+                            const float ws = q == 0 ? wv.x : q == 1 ? wv.y : q == 2 ? wv.z : wv.w;
+                            acc[j * MT + r] = __builtin_amdgcn_mfma_f32_16x16x4f32(xs, ws, acc[j * MT + r], 0, 0, 0);
+                        }
             }
         }
     };
@@ -336,9 +373,9 @@ __global__ __launch_bounds__(NW * 64) void gemm16_kernel(FG p) {
         comp(Bb, t + 1);
     }
 
-    Epi<NW, EPI, MT> epi;
-    epi.prefetch(p, nt, row0);
-    epi.finish(p, acc, red, tile, nt, row0);
+    Epi<NW, EPI, MT, NTW> epi;
+    epi.prefetch(p, nt0, row0);
+    epi.finish(p, acc, red, tile, nt0, row0);
 }
 
 // One-shot variant for the layer GEMMs (one 16-row block per workgroup,
@@ -356,10 +393,11 @@ __global__ __launch_bounds__(NW * 64) void gemm16_os_kernel(FG p) {
     float* tile = red + NW * 256;               // [16 rows][17]
     float* lnst = tile + 16 * 17;               // [16][2] mean, rstd
 
+    int nt, ry;
+    if (!xcd_tile(p, nt, ry)) return;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    const int nt = blockIdx.x;
-    const int row0 = blockIdx.y * 16;
+    const int row0 = ry * 16;
     const int q4 = lane >> 4;
     const bool use_ln = p.ln_stats != nullptr;
 
@@ -386,7 +424,7 @@ __global__ __launch_bounds__(NW * 64) void gemm16_os_kernel(FG p) {
     }
     // 3. all operand fragments of this wave's k range [w*S, w*S+S)
     const float4* __restrict__ wf = reinterpret_cast<const float4*>(p.w) + ((size_t)nt * p.K16 + w * S) * 64 + lane;
-    const float4* __restrict__ xf = reinterpret_cast<const float4*>(p.x) + ((size_t)blockIdx.y * p.K16 + w * S) * 64 + lane;
+    const float4* __restrict__ xf = reinterpret_cast<const float4*>(p.x) + ((size_t)ry * p.K16 + w * S) * 64 + lane;
     float4 wv[S], xv[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -566,14 +604,20 @@ __global__ __launch_bounds__(256) void argmax_final_kernel(const float* __restri
     }
 }
 
-template <int NW, int MT>
-int launch16(const FG& p, int epi) {
-    dim3 grid(p.ntn, p.Mp / 16 / MT), block(NW * 64);
+inline dim3 xcd_grid(FG& p, int gx, int gy) {
+    p.gx = gx;
+    p.gy = gy;
+    return dim3((unsigned)(((gx + 7) / 8) * 8 * gy));
+}
+
+template <int NW, int MT, int NTW = 1>
+int launch16(FG p, int epi) {
+    dim3 grid = xcd_grid(p, (p.ntn + NTW - 1) / NTW, p.Mp / 16 / MT), block(NW * 64);
     switch (epi) {
-        case HPA_FEPI_QKV: gemm16_kernel<NW, HPA_FEPI_QKV, MT><<<grid, block, 0, hpa_stream()>>>(p); break;
-        case HPA_FEPI_RESID: gemm16_kernel<NW, HPA_FEPI_RESID, MT><<<grid, block, 0, hpa_stream()>>>(p); break;
-        case HPA_FEPI_GELU: gemm16_kernel<NW, HPA_FEPI_GELU, MT><<<grid, block, 0, hpa_stream()>>>(p); break;
-        case HPA_FEPI_LOGITS: gemm16_kernel<NW, HPA_FEPI_LOGITS, MT><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_QKV: gemm16_kernel<NW, HPA_FEPI_QKV, MT, NTW><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_RESID: gemm16_kernel<NW, HPA_FEPI_RESID, MT, NTW><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_GELU: gemm16_kernel<NW, HPA_FEPI_GELU, MT, NTW><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_LOGITS: gemm16_kernel<NW, HPA_FEPI_LOGITS, MT, NTW><<<grid, block, 0, hpa_stream()>>>(p); break;
         default: return hpa_fail(__FILE__, __LINE__, "gemm_fused: unknown epilogue");
     }
     HPA_LAUNCH_CHECK();
@@ -581,8 +625,8 @@ int launch16(const FG& p, int epi) {
 }
 
 template <int NW, int S>
-int launch16_os(const FG& p, int epi) {
-    dim3 grid(p.ntn, p.Mp / 16), block(NW * 64);
+int launch16_os(FG p, int epi) {
+    dim3 grid = xcd_grid(p, p.ntn, p.Mp / 16), block(NW * 64);
     switch (epi) {
         case HPA_FEPI_QKV: gemm16_os_kernel<NW, HPA_FEPI_QKV, S><<<grid, block, 0, hpa_stream()>>>(p); break;
         case HPA_FEPI_RESID: gemm16_os_kernel<NW, HPA_FEPI_RESID, S><<<grid, block, 0, hpa_stream()>>>(p); break;
@@ -607,8 +651,20 @@ int launch_os(const FG& p, int epi, int nw) {
     }
 }
 
+// multi-column-tile instances: (waves, row_blocks, col_tiles) in
+// {(4|8, 4, 2), (4|8, 2, 2), (4, 4, 4)} -- the rest exceed LDS or registers
 template <int NW>
-int launch16_mt(const FG& p, int epi, int mt) {
+int launch16_mt(const FG& p, int epi, int mt, int ntw) {
+    if constexpr (NW <= 8) {
+        if (ntw == 2 && mt == 4) return launch16<NW, 4, 2>(p, epi);
+        if (ntw == 2 && mt == 2) return launch16<NW, 2, 2>(p, epi);
+    }
+    if constexpr (NW == 4) {
+        if (ntw == 4 && mt == 4) return launch16<NW, 4, 4>(p, epi);
+    }
+    if (ntw != 1)
+        return hpa_fail(__FILE__, __LINE__,
+                        "gemm_fused: col_tiles 2 needs waves 4/8 and row_blocks 2/4; 4 needs waves 4, row_blocks 4");
     switch (mt) {
         case 1: return launch16<NW, 1>(p, epi);
         case 2: return launch16<NW, 2>(p, epi);
@@ -647,21 +703,23 @@ int hpa_unpack_frag(const float* src, int rows, int K, float* dst, int ld) {
 // GEMMs (spreads the fp32 MFMA work over >= 4 * N/16 workgroups), four for
 // logits (3142 column tiles already fill the chip; amortises the A reads);
 // waves sharing the K range: enough k-steps per wave to amortise the fold
-void hpa_fused_pick(int M, int N, int K, int* out2) {
+void hpa_fused_pick(int M, int N, int K, int* out3) {
     (void)M;
     const int ntn = (N + 15) / 16;
     const int k16 = K / 16;
-    if (ntn >= 1024) {
-        out2[0] = 4;
-        out2[1] = 4;
+    if (ntn >= 1024) {  // logits (profiles/r1/gemm_tune_b64_*.log)
+        out3[0] = 4;
+        out3[1] = 2;
+        out3[2] = 2;
         return;
     }
-    out2[1] = 1;
-    out2[0] = k16 >= 96 ? 8 : 4;
+    out3[1] = 1;
+    out3[0] = k16 >= 96 ? 8 : 4;
+    out3[2] = 1;
 }
 
 int hpa_fused_pick_waves(int M, int N, int K) {
-    int p[2];
+    int p[3];
     hpa_fused_pick(M, N, K, p);
     return p[0];
 }
@@ -710,22 +768,30 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
     }
     if (g->epilogue == HPA_FEPI_RESID) HPA_REQUIRE(g->res_in && g->stats_out, "gemm_fused RESID");
     if (g->epilogue == HPA_FEPI_LOGITS) HPA_REQUIRE(g->part_out, "gemm_fused LOGITS: part_out");
-    int pick[2];
+    int pick[3];
     hpa_fused_pick(g->M, g->N, g->K, pick);
     const int nw = g->waves ? g->waves : pick[0];
     int mt = g->row_blocks ? g->row_blocks : pick[1];
     HPA_REQUIRE(mt == 1 || mt == 2 || mt == 4, "gemm_fused: row_blocks must be 1, 2 or 4");
     while ((p.Mp / 16) % mt) mt >>= 1;  // row blocks of this M
     HPA_REQUIRE(g->variant >= 0 && g->variant <= 2, "gemm_fused: variant must be 0, 1 or 2");
-    if (g->variant == 2 || (g->variant == 0 && mt == 1 && p.ntn < 1024)) {
+    HPA_REQUIRE(g->col_tiles == 0 || g->col_tiles == 1 || g->col_tiles == 2 || g->col_tiles == 4,
+                "gemm_fused: col_tiles must be 1, 2 or 4");
+    if (g->variant == 2 || (g->variant == 0 && mt == 1 && p.ntn < 1024 && g->col_tiles <= 1)) {
         const int rc = launch_os(p, g->epilogue, nw);
         if (rc >= 0) return rc;
         HPA_REQUIRE(g->variant == 0, "gemm_fused: one-shot needs (waves, K/16) in {(4,48), (8,48), (16,48), (8,192)}");
     }
+    int ntw = g->col_tiles ? g->col_tiles : pick[2];
+    // a launch-shape hint: where this M's row blocks (or the waves) cannot
+    // carry it, fall back to one column tile (results are identical)
+    if ((ntw == 2 && (mt == 1 || nw == 16)) || (ntw == 4 && (mt != 4 || nw != 4))) ntw = 1;
     switch (nw) {
-        case 4: return launch16_mt<4>(p, g->epilogue, mt);
-        case 8: return launch16_mt<8>(p, g->epilogue, mt);
-        case 16: return launch16_mt<16>(p, g->epilogue, mt);
+        case 4: return launch16_mt<4>(p, g->epilogue, mt, ntw);
+        case 8: return launch16_mt<8>(p, g->epilogue, mt, ntw);
+        case 16:
+            HPA_REQUIRE(ntw == 1, "gemm_fused: col_tiles > 1 needs waves 4 or 8");
+            return launch16_mt<16>(p, g->epilogue, mt, ntw);
         default: return hpa_fail(__FILE__, __LINE__, "gemm_fused: waves must be 4, 8 or 16");
     }
 }

@@ -445,6 +445,7 @@ struct GPT2Decode {
     size_t wpack_off[5]; /* per-layer strides (0..3) and wte offset (4) */
     int fwaves[5];    /* waves per workgroup: qkv, attproj, fc, fcproj, logits */
     int frb[5];       /* 16-row blocks per workgroup, same order */
+    int fct[5];       /* 16-column tiles per workgroup, same order */
     DecLane lanes[DEC_MAX_LANES];
     int nlanes;
     void* ev_fork;
@@ -583,10 +584,11 @@ static int dec_init_fused(GPT2* model, GPT2Decode* d) {
     if (hpa_pack_frag(w->wte, V, C, C, d->d_wpack + d->wpack_off[4])) return 1;
     const int shp[5][2] = {{3 * C, C}, {C, C}, {4 * C, C}, {C, 4 * C}, {V, C}};
     for (int i = 0; i < 5; i++) {
-        int pk[2];
+        int pk[3];
         hpa_fused_pick(B, shp[i][0], shp[i][1], pk);
         d->fwaves[i] = pk[0];
         d->frb[i] = pk[1];
+        d->fct[i] = pk[2];
     }
     d->ev_fork = hpa_event_create_nt();
     if (!d->ev_fork) return 1;
@@ -807,6 +809,7 @@ static int fgemm(GPT2Decode* d, const DecLane* ln, const float* x, int K, const 
     g.bias = bias;
     g.waves = d->fwaves[gi];
     g.row_blocks = d->frb[gi];
+    g.col_tiles = d->fct[gi];
     g.epilogue = epi;
     g.out = out;
     g.res_in = res_in;
@@ -1016,12 +1019,13 @@ int gpt2_decode_splits(GPT2* model, int* s4) {
 
 /* launch shapes of the fused GEMMs (qkv, attproj, fc, fcproj, logits):
  * set = 0 copies them out; set = 1 applies the nonzero entries */
-int gpt2_decode_gemm_config(GPT2* model, int* waves5, int* row_blocks5, int set) {
+int gpt2_decode_gemm_config(GPT2* model, int* waves5, int* row_blocks5, int* col_tiles5, int set) {
     GPT2Decode* d = model->decode;
     if (!d) return 1;
     if (!set) {
         if (waves5) memcpy(waves5, d->fwaves, sizeof(d->fwaves));
         if (row_blocks5) memcpy(row_blocks5, d->frb, sizeof(d->frb));
+        if (col_tiles5) memcpy(col_tiles5, d->fct, sizeof(d->fct));
         return 0;
     }
     for (int i = 0; i < 5; i++) {
@@ -1029,10 +1033,13 @@ int gpt2_decode_gemm_config(GPT2* model, int* waves5, int* row_blocks5, int set)
         if (row_blocks5 && row_blocks5[i] != 0 && row_blocks5[i] != 1 && row_blocks5[i] != 2 &&
             row_blocks5[i] != 4)
             return 1;
+        if (col_tiles5 && col_tiles5[i] != 0 && col_tiles5[i] != 1 && col_tiles5[i] != 2 && col_tiles5[i] != 4)
+            return 1;
     }
     for (int i = 0; i < 5; i++) {
         if (waves5 && waves5[i]) d->fwaves[i] = waves5[i];
         if (row_blocks5 && row_blocks5[i]) d->frb[i] = row_blocks5[i];
+        if (col_tiles5 && col_tiles5[i]) d->fct[i] = col_tiles5[i];
     }
     if (d->graph) { /* recapture with the new launch shapes */
         hpa_synchronize();

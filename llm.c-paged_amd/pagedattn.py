@@ -57,7 +57,7 @@ class HpaFusedGemm(ctypes.Structure):
                 ("res_in", _V), ("stats_out", _V), ("part_out", _V),
                 ("pool", ctypes.POINTER(HpaKVPool)), ("layer", ctypes.c_int), ("block_table", _V),
                 ("bt_stride", ctypes.c_int), ("pos", _V), ("waves", ctypes.c_int),
-                ("row_blocks", ctypes.c_int), ("variant", ctypes.c_int)]
+                ("row_blocks", ctypes.c_int), ("variant", ctypes.c_int), ("col_tiles", ctypes.c_int)]
 
 
 HPA_FEPI_QKV, HPA_FEPI_RESID, HPA_FEPI_GELU, HPA_FEPI_LOGITS = 0, 1, 2, 3
@@ -216,7 +216,7 @@ def lib():
     _sig(L, "gpt2_decode_next", v, [v])
     _sig(L, "gpt2_decode_positions", i, [v, _I])
     _sig(L, "gpt2_decode_splits", i, [v, _I])
-    _sig(L, "gpt2_decode_gemm_config", i, [v, _I, _I, i])
+    _sig(L, "gpt2_decode_gemm_config", i, [v, _I, _I, _I, i])
     _sig(L, "gpt2_decode_set_lanes", i, [v, i])
     _sig(L, "gpt2_decode_time_attention", i, [v, i, ctypes.POINTER(ctypes.c_double),
                                               ctypes.POINTER(ctypes.c_double)])
@@ -474,20 +474,18 @@ class Model:
         check(lib().gpt2_decode_set_lanes(self.h, int(lanes)), "set_lanes")
         return lib().gpt2_decode_lanes(self.h)
 
-    def gemm_config(self, waves=None, row_blocks=None):
+    def gemm_config(self, waves=None, row_blocks=None, col_tiles=None):
         """fused GEMM launch shapes [qkv, attproj, fc, fcproj, logits]:
-        (waves per workgroup, 16-row blocks per workgroup); applies the
+        (waves, 16-row blocks, 16-column tiles) per workgroup; applies the
         nonzero entries of the given lists first"""
-        if waves is not None or row_blocks is not None:
-            w = np.ascontiguousarray(waves if waves is not None else [0] * 5, np.int32)
-            r = np.ascontiguousarray(row_blocks if row_blocks is not None else [0] * 5, np.int32)
-            check(lib().gpt2_decode_gemm_config(self.h, w.ctypes.data_as(_I), r.ctypes.data_as(_I), 1),
+        arrs = [np.ascontiguousarray(a if a is not None else [0] * 5, np.int32)
+                for a in (waves, row_blocks, col_tiles)]
+        if any(a is not None for a in (waves, row_blocks, col_tiles)):
+            check(lib().gpt2_decode_gemm_config(self.h, *[a.ctypes.data_as(_I) for a in arrs], 1),
                   "gemm_config")
-        w = np.zeros(5, np.int32)
-        r = np.zeros(5, np.int32)
-        check(lib().gpt2_decode_gemm_config(self.h, w.ctypes.data_as(_I), r.ctypes.data_as(_I), 0),
-              "gemm_config")
-        return w, r
+        out = [np.zeros(5, np.int32) for _ in range(3)]
+        check(lib().gpt2_decode_gemm_config(self.h, *[a.ctypes.data_as(_I) for a in out], 0), "gemm_config")
+        return tuple(out)
 
     def step_bytes(self):
         att = ctypes.c_double()

@@ -48,7 +48,7 @@ def test_pack_unpack_roundtrip(hip):
     assert np.array_equal(d_b.download(a.shape), a)
 
 
-def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixed=None, variant=0):
+def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixed=None, variant=0, ct=0):
     L = hip.lib()
     x = rng.uniform(-1, 1, (M, K)).astype(np.float32)
     W = rng.uniform(-0.05, 0.05, (N, K)).astype(np.float32)
@@ -82,6 +82,7 @@ def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixe
     g.waves = waves
     g.row_blocks = rb
     g.variant = variant
+    g.col_tiles = ct
     g.epilogue = epi
     acc = a @ W.astype(np.float64).T
     bound = 4e-6 * (np.abs(a) @ np.abs(W.astype(np.float64)).T) + 2e-6
@@ -114,13 +115,17 @@ def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixe
     return out, acc, bound, keep
 
 
-@pytest.mark.parametrize("M,K,N,waves,rb", [(64, 256, 128, 4, 4), (64, 256, 128, 16, 1), (8, 768, 768, 16, 2),
-                                            (40, 3072, 768, 8, 1), (100, 512, 96, 16, 4), (3, 48, 32, 16, 1),
-                                            (130, 768, 768, 0, 0), (64, 3072, 768, 4, 2), (48, 1600, 1600, 8, 4)])
-def test_fused_resid_with_stats(hip, M, K, N, waves, rb):
+@pytest.mark.parametrize("M,K,N,waves,rb,ct", [(64, 256, 128, 4, 4, 1), (64, 256, 128, 16, 1, 1),
+                                               (8, 768, 768, 16, 2, 1), (40, 3072, 768, 8, 1, 1),
+                                               (100, 512, 96, 16, 4, 1), (3, 48, 32, 16, 1, 1),
+                                               (130, 768, 768, 0, 0, 0), (64, 3072, 768, 4, 2, 1),
+                                               (48, 1600, 1600, 8, 4, 1), (64, 768, 768, 4, 4, 2),
+                                               (64, 768, 80, 4, 4, 4)])
+def test_fused_resid_with_stats(hip, M, K, N, waves, rb, ct):
     rng = np.random.default_rng(M + waves + rb)
     res = rng.uniform(-1, 1, (M, N)).astype(np.float32)
-    out, acc, bound, keep = _run(hip, hip.HPA_FEPI_RESID, M, K, N, waves, ln=(K == N), rng=rng, res=res, rb=rb)
+    out, acc, bound, keep = _run(hip, hip.HPA_FEPI_RESID, M, K, N, waves, ln=(K == N), rng=rng, res=res, rb=rb,
+                                 ct=ct)
     Mp = (M + 15) // 16 * 16
     got = hip.from_frag(out.download(Mp * N), M, N)
     ref = res + acc
@@ -142,12 +147,13 @@ def test_fused_gelu_with_ln(hip, waves, rb):
     assert np.abs(got - ref).max() <= 2e-5
 
 
-@pytest.mark.parametrize("M,waves,rb", [(64, 4, 4), (37, 8, 1), (64, 16, 2)])
-def test_fused_logits_argmax(hip, M, waves, rb):
+@pytest.mark.parametrize("M,waves,rb,ct", [(64, 4, 4, 1), (37, 8, 1, 1), (64, 16, 2, 1), (64, 4, 4, 2),
+                                           (64, 4, 4, 4), (40, 8, 2, 2), (64, 8, 4, 2)])
+def test_fused_logits_argmax(hip, M, waves, rb, ct):
     L = hip.lib()
     rng = np.random.default_rng(3)
     K, N = 768, 50257
-    out, acc, bound, keep = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, waves, ln=True, rng=rng, rb=rb)
+    out, acc, bound, keep = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, waves, ln=True, rng=rng, rb=rb, ct=ct)
     got = out.download((M, N))
     assert np.all(np.abs(got - acc) <= bound)
     part = keep[-2]
@@ -195,6 +201,8 @@ def test_fused_rejects_bad_launch_shape(hip):
         _run(hip, hip.HPA_FEPI_GELU, 16, 64, 64, 2, ln=False, rng=rng)
     with pytest.raises(RuntimeError):
         _run(hip, hip.HPA_FEPI_GELU, 16, 64, 64, 4, ln=False, rng=rng, rb=3)
+    with pytest.raises(RuntimeError):
+        _run(hip, hip.HPA_FEPI_GELU, 64, 64, 64, 4, ln=False, rng=rng, rb=4, ct=3)
     with pytest.raises(RuntimeError):  # LN'ed A operand wider than the LDS copy of w, b
         _run(hip, hip.HPA_FEPI_GELU, 16, 2064, 64, 4, ln=True, rng=rng)
 
@@ -214,9 +222,9 @@ def test_fused_rows_independent_of_split(hip, epi):
                  lw=r.uniform(0.8, 1.2, K).astype(np.float32), lb=r.uniform(-0.1, 0.1, K).astype(np.float32))
     res = r.uniform(-1, 1, (64, N)).astype(np.float32)
     outs = []
-    for M, rb in [(64, 1), (64, 2), (64, 4), (16, 1), (32, 2)]:
+    for M, rb, ct in [(64, 1, 1), (64, 2, 1), (64, 4, 1), (16, 1, 1), (32, 2, 1), (64, 4, 2), (32, 2, 2)]:
         out, _, _, keep = _run(hip, e, M, K, N, 8, ln=True, rng=np.random.default_rng(7),
-                               res=res[:M], rb=rb, fixed=fixed)
+                               res=res[:M], rb=rb, fixed=fixed, ct=ct)
         if epi == "RESID":
             got = hip.from_frag(out.download(((M + 15) // 16 * 16) * N), M, N)
         else:

@@ -88,37 +88,40 @@ def main():
     total_best = total_auto = 0.0
     for name, M, K, N, epi, ln in SHAPES:
         g = shape_inputs(M, K, N, epi, ln)
-        pk = (ctypes.c_int * 2)()
+        pk = (ctypes.c_int * 3)()
         L.hpa_fused_pick(M, N, K, ctypes.cast(pk, pa._I))
         rb_eff = pk[1]
         while ((M + 15) // 16) % rb_eff:
             rb_eff //= 2
-        oneshot = rb_eff == 1 and (N + 15) // 16 < 1024 and (pk[0], K // 16) in ONESHOT
-        auto = (pk[0], rb_eff, 2 if oneshot else 1)
+        oneshot = rb_eff == 1 and (N + 15) // 16 < 1024 and (pk[0], K // 16) in ONESHOT and pk[2] <= 1
+        auto = (pk[0], rb_eff, 2 if oneshot else 1, pk[2])
         res = []
         ref = None
         for waves in (4, 8, 16):
             for rb in (1, 2, 4):
                 for variant in (1, 2):
-                    if ((M + 15) // 16) % rb or (variant == 2 and rb != 1):
-                        continue
-                    g.waves, g.row_blocks, g.variant = waves, rb, variant
-                    try:
-                        us = time_fused(g)
-                    except RuntimeError:
-                        continue
-                    o = out_copy(g, M, N, epi)
-                    if ref is None:
-                        ref = o
-                    res.append((us, (waves, rb, variant), float(np.abs(o - ref).max())))
+                    for ct in (1, 2, 4):
+                        if ((M + 15) // 16) % rb or (variant == 2 and (rb != 1 or ct != 1)):
+                            continue
+                        if ct > 1 and (waves == 16 or rb == 1 or (ct == 4 and (rb != 4 or waves != 4))):
+                            continue
+                        g.waves, g.row_blocks, g.variant, g.col_tiles = waves, rb, variant, ct
+                        try:
+                            us = time_fused(g)
+                        except RuntimeError:
+                            continue
+                        o = out_copy(g, M, N, epi)
+                        if ref is None:
+                            ref = o
+                        res.append((us, (waves, rb, variant, ct), float(np.abs(o - ref).max())))
         flops = 2.0 * M * K * N
         wbytes = 4.0 * N * K
         best = min(res)
         total_best += best[0]
         total_auto += ([r for r in res if r[1] == auto] or [best])[0][0]
-        print(f"{name:8s} M={M} K={K} N={N} auto (waves, row_blocks, variant)={auto}")
+        print(f"{name:8s} M={M} K={K} N={N} auto (waves, row_blocks, variant, col_tiles)={auto}")
         for us, waves, err in sorted(res):
-            print(f"   {us:8.2f} us  (waves, rb, variant)={waves}  {flops / us / 1e6:7.1f} TF/s "
+            print(f"   {us:8.2f} us  (waves, rb, variant, ct)={waves}  {flops / us / 1e6:7.1f} TF/s "
                   f"{wbytes / us / 1e3:7.1f} GB/s(W)  maxdiff={err:.2e}")
     print(f"sum best {total_best:.1f} us   sum auto {total_auto:.1f} us")
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes (one counter group per rocprofv3 run, kernel-trace only) over
-# single GEMM configurations.  usage: tools/pmc_gemm.sh outdir "shape var wn wk split" ...
+# single GEMM configurations.  usage: tools/pmc_gemm.sh outdir "shape waves row_blocks variant col_tiles" ...
 set -u
 out=$1; shift
 mkdir -p "$out"
