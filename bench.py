@@ -77,6 +77,7 @@ def parse():
     ap.add_argument("--attn-waves", type=int, default=4)
     ap.add_argument("--unfused", action="store_true", help="row-major GEMMs + separate row kernels")
     ap.add_argument("--lanes", type=int, default=1, help="micro-batch lanes (concurrent row groups)")
+    ap.add_argument("--pipeline", type=int, default=0, help="1: two lanes, attention chunks beside GEMMs")
     ap.add_argument("--gemm-waves", default="", help="fused GEMM waves qkv,attproj,fc,fcproj,logits (0 = auto)")
     ap.add_argument("--gemm-rows", default="", help="fused GEMM 16-row blocks per workgroup, same order")
     ap.add_argument("--gemm-cols", default="", help="fused GEMM 16-column tiles per workgroup, same order")
@@ -165,6 +166,8 @@ def main():
     model.set_fused(not args.unfused)
     if not args.unfused:
         model.set_lanes(args.lanes)
+        if args.pipeline:
+            model.set_pipeline(True)
     if args.gemm_waves or args.gemm_rows or args.gemm_cols:
         ints = lambda a: [int(x) for x in a.split(",")] if a else None  # noqa: E731
         model.gemm_config(ints(args.gemm_waves), ints(args.gemm_rows), ints(args.gemm_cols))
@@ -276,6 +279,7 @@ def main():
                                                                if world > 1 and args.gather != "none" else ""),
                        "hip_graph": not args.no_graph, "gemm_path": "unfused" if args.unfused else "fused",
                        "lanes": 1 if args.unfused else L.gpt2_decode_lanes(model.h),
+                       "pipeline": bool(L.gpt2_decode_pipeline(model.h)),
                        "gemm_waves": [int(x) for x in model.gemm_config()[0]],
                        "gemm_row_blocks": [int(x) for x in model.gemm_config()[1]],
                        "gemm_col_tiles": [int(x) for x in model.gemm_config()[2]], "device": name},

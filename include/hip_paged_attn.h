@@ -225,6 +225,29 @@ int hpa_paged_attention_decode_frag(const float* q, const HpaKVPool* pool, int l
                                     const int* block_table, int bt_stride, const int* pos,
                                     float* out_frag, int B);
 
+/* ---------------- pipelined decode: attention chunk + GEMM in ONE launch ----------------
+ * Chunk `chunk` of `nchunks` of the decode attention of B sequences (each
+ * sequence's 64-token tiles split evenly; the online-softmax state (m, l, acc)
+ * is carried between chunks in `state`, hpa_attn_state_elems floats; the last
+ * chunk writes the normalised output in frag layout) runs beside an
+ * independent fused GEMM `g` (NULL = none) in one launch: workgroups
+ * [0, ceil8(B*NH)) take the attention role, the rest the GEMM role (4 waves,
+ * one row block and one column tile per workgroup; one-shot when K = 768).
+ * The caller guarantees the two touch disjoint data (different sequences). */
+typedef struct {
+    const float* q;          /* [B][C] row-major */
+    const HpaKVPool* pool;
+    int layer;
+    const int* block_table;  /* [B][bt_stride] */
+    int bt_stride;
+    const int* pos;          /* [B]: context = pos + 1 */
+    float* state;            /* hpa_attn_state_elems(B, NH) floats, 16-byte aligned */
+    float* out_frag;         /* frag layout [Mp][C] */
+    int B, chunk, nchunks;
+} HpaAttnChunk;
+size_t hpa_attn_state_elems(int B, int num_heads);
+int hpa_attn_chunk_with_gemm(const HpaAttnChunk* a, const HpaFusedGemm* g);
+
 /* ---------------- reference-layout kernels (drop-in compat) ----------------
  * Pages in the reference layout: token-major [block_size][C] per page
  * (block_manager.c:145-146).  key_blocks/value_blocks: DEVICE arrays of

@@ -177,6 +177,13 @@ int    gpt2_decode_set_lanes(GPT2* model, int lanes);
 int    gpt2_decode_time_attention(GPT2* model, int iters, double* ms_per_launch,
                                   double* bytes_per_launch);
 int    gpt2_decode_lanes(GPT2* model);
+/* pipelined step (fused path): two lanes on ONE stream; each lane's layer
+ * attention runs in 4 context chunks, every chunk in the same launch as one
+ * GEMM of the other lane's chain (hpa_attn_chunk_with_gemm).  Logits within
+ * the usual fp32 tolerance of the one-lane step (different softmax summation
+ * order).  Needs B > 16 and page size 8/16/32; disabling returns to 1 lane. */
+int    gpt2_decode_set_pipeline(GPT2* model, int enable);
+int    gpt2_decode_pipeline(GPT2* model);
 /* algorithmic HBM bytes one step reads+writes at the current positions
  * (SURVEY.md 8d formula) and the attention kernel's share of them */
 double gpt2_decode_step_bytes(GPT2* model, double* attention_bytes);

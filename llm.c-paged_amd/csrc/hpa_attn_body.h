@@ -1,0 +1,231 @@
+// hpa_attn_body.h -- device pieces of the paged decode attention (design
+// notes in hpa_attn.hip), shared by the single-pass kernel and the
+// context-chunk body of the pipelined launches (hpa_combo.hip).
+#pragma once
+#include <math.h>
+
+#include "hpa_internal.h"
+
+namespace hpa_attn {
+
+constexpr int HS = 64;
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+// K/V rows are streamed once per step by the one workgroup of their
+// (sequence, head): non-temporal loads (MI355X_MICROARCH.md "nt-weights")
+__device__ __forceinline__ float4 load_stream(const float* ptr) {
+    const f32x4v v = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(ptr));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
+// The 64-token tiles it = it_begin + w, it_begin + w + NW, ... < it_end of
+// one (sequence, head), folded into this wave's online-softmax state
+// (m, l: log2 domain; acc: lane (g = lane>>4, d4 = lane&15) holds dims
+// 4*d4..+3 summed over tokens t0 + 4i + g).  One memory round trip per tile:
+// the tile's page ids were fetched during the previous tile; K and V rows are
+// issued together (both depend only on the page ids), then the next ids.
+template <int P, int NW>
+__device__ __forceinline__ void attn_tiles(const float* __restrict__ qh, const float* __restrict__ kbase,
+                                           const float* __restrict__ vbase, size_t page_elems,
+                                           const int* __restrict__ bt, int ctx, int it_begin, int it_end,
+                                           float qscale, float& m, float& l, float4& acc) {
+    static_assert(P % 4 == 0 && 64 % P == 0, "page size must divide 64 and be a multiple of 4");
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int g = lane >> 4;
+    const int d4 = lane & 15;
+    const int v_lane_off = g * HS + d4 * 4;
+    int it = it_begin + w;
+    int pid = 0;
+    if (it < it_end) {
+        const unsigned t0 = (unsigned)it << 6, tok = t0 + lane;
+        pid = bt[(tok < (unsigned)ctx ? tok : t0) / P];
+    }
+    for (; it < it_end; it += NW) {
+        const unsigned t0 = (unsigned)it << 6;
+        const unsigned tok = t0 + lane;
+        const bool valid = tok < (unsigned)ctx;
+        const float* kt = kbase + (size_t)(unsigned)pid * page_elems + (tok % P) * 4;
+        float4 kv[16], vv[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) kv[c] = load_stream(kt + c * P * 4);
+        // PV operands: the row address splits into a wave-uniform part (page
+        // of tokens t0+4i..+3, slot (4i)%P; t0 % P == 0) and a per-lane offset
+        // that is the same for every i: SGPR base + one shared VGPR per load
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int vpid = __builtin_amdgcn_readlane(pid, 4 * i);
+            const float* vrow = vbase + (size_t)(unsigned)vpid * page_elems + ((4 * i) % P) * HS;
+            vv[i] = (t0 + 4 * i + g) < (unsigned)ctx ? load_stream(vrow + v_lane_off)
+                                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        {  // next tile's page ids
+            const int itn = it + NW;
+            const unsigned t0n = (unsigned)itn << 6, tokn = t0n + lane;
+            if (itn < it_end) pid = bt[(tokn < (unsigned)ctx ? tokn : t0n) / P];
+        }
+        // QK^T: lane-per-token over 16 chunks of 4 dims (q in SGPRs)
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+            s = fmaf(qh[4 * c + 0], kv[c].x, s);
+            s = fmaf(qh[4 * c + 1], kv[c].y, s);
+            s = fmaf(qh[4 * c + 2], kv[c].z, s);
+            s = fmaf(qh[4 * c + 3], kv[c].w, s);
+        }
+        s = valid ? s * qscale : -INFINITY;
+        // online softmax (log2 domain)
+        const float mt = hpa::wave_max(s);
+        const float mn = fmaxf(m, mt);
+        const float alpha = exp2f(m - mn);
+        const float p = exp2f(s - mn);
+        l = fmaf(l, alpha, p);
+        acc.x *= alpha;
+        acc.y *= alpha;
+        acc.z *= alpha;
+        acc.w *= alpha;
+        m = mn;
+        // PV
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float pi = __shfl(p, 4 * i + g, 64);
+            acc.x = fmaf(pi, vv[i].x, acc.x);
+            acc.y = fmaf(pi, vv[i].y, acc.y);
+            acc.z = fmaf(pi, vv[i].z, acc.z);
+            acc.w = fmaf(pi, vv[i].w, acc.w);
+        }
+    }
+}
+
+// Fold the 4 token groups and the per-lane sums of every wave, then the
+// waves (fixed order, through LDS: s_m[NW], s_l[NW], s_acc[NW*16]).  The
+// combined state lands in wave 0, lanes 0..15 (returns true there): lane
+// holds dims 4*lane..+3.
+template <int NW>
+__device__ __forceinline__ bool attn_fold(float& m, float& l, float4& acc, float* s_m, float* s_l,
+                                          float4* s_acc) {
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+        acc.x += __shfl_xor(acc.x, o, 64);
+        acc.y += __shfl_xor(acc.y, o, 64);
+        acc.z += __shfl_xor(acc.z, o, 64);
+        acc.w += __shfl_xor(acc.w, o, 64);
+    }
+    l = hpa::wave_sum(l);
+    if constexpr (NW == 1) {
+        return lane < 16;
+    } else {
+        if (lane == 0) {
+            s_m[w] = m;
+            s_l[w] = l;
+        }
+        if (lane < 16) s_acc[w * 16 + lane] = acc;
+        __syncthreads();
+        if (w != 0 || lane >= 16) return false;
+        float M = s_m[0];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) M = fmaxf(M, s_m[i]);
+        float L = 0.f;
+        float4 O = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            const float f = exp2f(s_m[i] - M);
+            L = fmaf(s_l[i], f, L);
+            const float4 a = s_acc[i * 16 + lane];
+            O.x = fmaf(a.x, f, O.x);
+            O.y = fmaf(a.y, f, O.y);
+            O.z = fmaf(a.z, f, O.z);
+            O.w = fmaf(a.w, f, O.w);
+        }
+        m = M;
+        l = L;
+        acc = O;
+        return true;
+    }
+}
+
+// ---- context-chunk attention (the pipelined decode, hpa_combo.hip) ----
+// Chunk c of n covers the 64-token tiles [c*T/n, (c+1)*T/n) of each
+// (sequence, head), T = ceil(ctx/64).  The running (m, l, acc) is carried
+// between launches in `state` ([B][NH][68] floats: m, l, -, -, acc[64]);
+// chunk 0 starts from (m_init, 0, 0), later chunks merge into the carried
+// state in a fixed order, the last chunk normalises and writes the output
+// (frag layout [Mp][C]).
+struct AttnChunk {
+    const float* q;
+    const float* layer_base;
+    size_t page_elems;
+    int NH;
+    const int* bt;
+    int bt_stride;
+    const int* pos;
+    float* state;
+    float* out;
+    int B, chunk, nchunks;
+    float qscale, m_init;
+    int nblocks;  // B*NH rounded up to a multiple of 8 (keeps the GEMM role's b % 8 XCD order)
+};
+constexpr int kStateStride = 68;
+
+template <int NW>
+constexpr int attn_lds_floats() {
+    return 2 * NW + 4 * 16 * NW;
+}
+
+template <int P, int NW>
+__device__ __forceinline__ void attn_chunk_body(const AttnChunk& a, int bid, float* smem) {
+    if (bid >= a.B * a.NH) return;
+    constexpr int TILE = P * HS;
+    const int b = bid / a.NH;
+    const int h = bid - b * a.NH;
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int ctx = a.pos[b] + 1;
+    const int n_it = (ctx + 63) >> 6;
+    const int it0 = (int)((long long)a.chunk * n_it / a.nchunks);
+    const int it1 = (int)((long long)(a.chunk + 1) * n_it / a.nchunks);
+    float* st = a.state + ((size_t)b * a.NH + h) * kStateStride;
+    // carried state, loaded before the stream so its latency hides under it
+    float pm = a.m_init, pl = 0.f;
+    float4 pa = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.chunk > 0 && w == 0 && lane < 16) {
+        pm = st[0];
+        pl = st[1];
+        pa = reinterpret_cast<const float4*>(st + 4)[lane];
+    }
+    const float* qh = a.q + ((size_t)b * a.NH + h) * HS;
+    float m = a.m_init, l = 0.f;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    attn_tiles<P, NW>(qh, a.layer_base + (size_t)h * TILE, a.layer_base + (size_t)(a.NH + h) * TILE,
+                      a.page_elems, a.bt + (size_t)b * a.bt_stride, ctx, it0, it1, a.qscale, m, l, acc);
+    float* s_m = smem;
+    float* s_l = smem + NW;
+    float4* s_acc = reinterpret_cast<float4*>(smem + 2 * NW + (4 - (2 * NW) % 4) % 4);
+    if (!attn_fold<NW>(m, l, acc, s_m, s_l, s_acc)) return;
+    // merge: carried state first, then this chunk (fixed order)
+    const float M = fmaxf(pm, m);
+    const float f0 = exp2f(pm - M), f1 = exp2f(m - M);
+    const float L = fmaf(pl, f0, l * f1);
+    float4 O;
+    O.x = fmaf(pa.x, f0, acc.x * f1);
+    O.y = fmaf(pa.y, f0, acc.y * f1);
+    O.z = fmaf(pa.z, f0, acc.z * f1);
+    O.w = fmaf(pa.w, f0, acc.w * f1);
+    if (a.chunk + 1 < a.nchunks) {
+        if (lane == 0) {
+            st[0] = M;
+            st[1] = L;
+        }
+        reinterpret_cast<float4*>(st + 4)[lane] = O;
+    } else {
+        const float inv = L == 0.f ? 0.f : 1.f / L;
+        const int C = a.NH * HS;
+        *reinterpret_cast<float4*>(a.out + hpa::frag_index(b, h * HS + 4 * lane, C)) =
+            make_float4(O.x * inv, O.y * inv, O.z * inv, O.w * inv);
+    }
+}
+
+}  // namespace hpa_attn

@@ -416,6 +416,7 @@ int gpt2_write_checkpoint(const char* path, GPT2Config c, const float* host_para
 typedef struct {
     int r0, B, Mp;
     float *res, *res2, *att, *fch, *st1, *st2, *part;
+    float* astate; /* attention chunk state (pipelined step) */
     void* stream; /* NULL for lane 0 (the launch stream) */
     void* ev_join;
 } DecLane;
@@ -448,6 +449,7 @@ struct GPT2Decode {
     int fct[5];       /* 16-column tiles per workgroup, same order */
     DecLane lanes[DEC_MAX_LANES];
     int nlanes;
+    int pipeline;     /* 1: two lanes, attention chunks beside the other lane's GEMMs */
     void* ev_fork;
     int use_graph;
     void* graph;
@@ -479,7 +481,7 @@ static void dec_lanes_free(GPT2Decode* d) {
     for (int i = 0; i < d->nlanes; i++) {
         DecLane* ln = &d->lanes[i];
         hpa_free(ln->res); hpa_free(ln->res2); hpa_free(ln->att); hpa_free(ln->fch);
-        hpa_free(ln->st1); hpa_free(ln->st2); hpa_free(ln->part);
+        hpa_free(ln->st1); hpa_free(ln->st2); hpa_free(ln->part); hpa_free(ln->astate);
         hpa_stream_destroy(ln->stream);
         hpa_event_destroy(ln->ev_join);
         memset(ln, 0, sizeof(*ln));
@@ -488,7 +490,7 @@ static void dec_lanes_free(GPT2Decode* d) {
 }
 
 /* split the batch into up to `n` lanes of whole 16-row blocks */
-static int dec_lanes_alloc(GPT2Decode* d, int n, int C, int V) {
+static int dec_lanes_alloc(GPT2Decode* d, int n, int C, int V, int NH) {
     dec_lanes_free(d);
     int blocks = (d->B + 15) / 16;
     if (n < 1) n = 1;
@@ -512,9 +514,10 @@ static int dec_lanes_alloc(GPT2Decode* d, int n, int C, int V) {
         ln->st1 = (float*)hpa_malloc((size_t)ct * Mp * 2 * 4);
         ln->st2 = (float*)hpa_malloc((size_t)ct * Mp * 2 * 4);
         ln->part = (float*)hpa_malloc((size_t)((V + 15) / 16) * Mp * 2 * 4);
+        ln->astate = (float*)hpa_malloc(hpa_attn_state_elems(ln->B, NH) * 4);
         ln->ev_join = hpa_event_create_nt();
         if (i > 0) ln->stream = hpa_stream_create();
-        if (!ln->res || !ln->res2 || !ln->att || !ln->fch || !ln->st1 || !ln->st2 || !ln->part ||
+        if (!ln->res || !ln->res2 || !ln->att || !ln->fch || !ln->st1 || !ln->st2 || !ln->part || !ln->astate ||
             !ln->ev_join || (i > 0 && !ln->stream))
             return 1;
         /* padded rows stay zero forever */
@@ -592,7 +595,7 @@ static int dec_init_fused(GPT2* model, GPT2Decode* d) {
     }
     d->ev_fork = hpa_event_create_nt();
     if (!d->ev_fork) return 1;
-    return dec_lanes_alloc(d, 1, C, V);
+    return dec_lanes_alloc(d, 1, C, V, c.num_heads);
 }
 
 int gpt2_decode_init(GPT2* model, int B, int page_size, int max_ctx) {
@@ -792,35 +795,77 @@ static int dec_launch_unfused(GPT2* model) {
     return rc;
 }
 
-static int fgemm(GPT2Decode* d, const DecLane* ln, const float* x, int K, const float* st, int st_tiles,
-                 const float* lw, const float* lb, const float* wpk, int N, const float* bias, int gi,
-                 int epi, float* out, const float* res_in, float* stats_out, float* part_out, int layer) {
+/* the fused GEMMs of one layer of one lane (gemm index = the fwaves/frb/fct
+ * slot): descriptor with that lane's rows, buffers and launch shape */
+enum { G_QKV = 0, G_ATTPROJ = 1, G_FC = 2, G_FCPROJ = 3, G_LOGITS = 4 };
+static void lane_gemm(GPT2* model, int li, int l, int which, HpaFusedGemm* g) {
+    GPT2Decode* d = model->decode;
+    const DecLane* ln = &d->lanes[li];
+    const GPT2Config c = model->config;
+    const int C = c.channels, V = c.vocab_size, ct = C / 16;
+    const ParameterTensors* w = &model->params;
+    const size_t lc = (size_t)l * C;
+    const size_t e_layer = d->wpack_off[3] + hpa_frag_elems(C, 4 * C);
+    const float* wl = d->d_wpack + e_layer * l;
+    memset(g, 0, sizeof(*g));
+    g->M = ln->B;
+    g->epilogue = which == G_QKV ? HPA_FEPI_QKV : which == G_FC ? HPA_FEPI_GELU
+                : which == G_LOGITS ? HPA_FEPI_LOGITS : HPA_FEPI_RESID;
+    g->waves = d->fwaves[which];
+    g->row_blocks = d->frb[which];
+    g->col_tiles = d->fct[which];
+    g->pool = &d->pool;
+    g->layer = l;
+    g->block_table = d->d_bt + (size_t)ln->r0 * d->bt_stride;
+    g->bt_stride = d->bt_stride;
+    g->pos = d->d_pos + ln->r0;
+    switch (which) {
+        case G_QKV: /* LN1 (stats: embedding's 1 tile at layer 0, fcproj's C/16 after) */
+            g->x = ln->res; g->K = C; g->ln_stats = ln->st1; g->ln_ntiles = l == 0 ? 1 : ct;
+            g->ln_w = w->ln1w + lc; g->ln_b = w->ln1b + lc; g->w = wl + d->wpack_off[0]; g->N = 3 * C;
+            g->bias = w->qkvb + 3 * lc; g->out = d->d_q + (size_t)ln->r0 * C;
+            break;
+        case G_ATTPROJ: /* res2 = res + att . Wap^T + b, LN2 statistics */
+            g->x = ln->att; g->K = C; g->w = wl + d->wpack_off[1]; g->N = C; g->bias = w->attprojb + lc;
+            g->out = ln->res2; g->res_in = ln->res; g->stats_out = ln->st2;
+            break;
+        case G_FC: /* gelu(LN2(res2) . Wfc^T + b) */
+            g->x = ln->res2; g->K = C; g->ln_stats = ln->st2; g->ln_ntiles = ct; g->ln_w = w->ln2w + lc;
+            g->ln_b = w->ln2b + lc; g->w = wl + d->wpack_off[2]; g->N = 4 * C; g->bias = w->fcb + 4 * lc;
+            g->out = ln->fch;
+            break;
+        case G_FCPROJ: /* res = res2 + fch . Wfp^T + b, next-LN statistics */
+            g->x = ln->fch; g->K = 4 * C; g->w = wl + d->wpack_off[3]; g->N = C; g->bias = w->fcprojb + lc;
+            g->out = ln->res; g->res_in = ln->res2; g->stats_out = ln->st1;
+            break;
+        default: /* logits = LNf(res) . wte^T, argmax partials */
+            g->x = ln->res; g->K = C; g->ln_stats = ln->st1; g->ln_ntiles = c.num_layers == 0 ? 1 : ct;
+            g->ln_w = w->lnfw; g->ln_b = w->lnfb; g->w = d->d_wpack + d->wpack_off[4]; g->N = V;
+            g->out = d->d_logits + (size_t)ln->r0 * V; g->part_out = ln->part; g->layer = 0;
+            break;
+    }
+}
+
+static int lane_gemm_run(GPT2* model, int li, int l, int which) {
     HpaFusedGemm g;
-    memset(&g, 0, sizeof(g));
-    g.x = x;
-    g.M = ln->B;
-    g.K = K;
-    g.ln_stats = st;
-    g.ln_ntiles = st_tiles;
-    g.ln_w = lw;
-    g.ln_b = lb;
-    g.w = wpk;
-    g.N = N;
-    g.bias = bias;
-    g.waves = d->fwaves[gi];
-    g.row_blocks = d->frb[gi];
-    g.col_tiles = d->fct[gi];
-    g.epilogue = epi;
-    g.out = out;
-    g.res_in = res_in;
-    g.stats_out = stats_out;
-    g.part_out = part_out;
-    g.pool = &d->pool;
-    g.layer = layer;
-    g.block_table = d->d_bt + (size_t)ln->r0 * d->bt_stride;
-    g.bt_stride = d->bt_stride;
-    g.pos = d->d_pos + ln->r0;
+    lane_gemm(model, li, l, which, &g);
     return hpa_gemm_fused(&g);
+}
+
+static int lane_embed(GPT2* model, int li) {
+    GPT2Decode* d = model->decode;
+    const DecLane* ln = &d->lanes[li];
+    const ParameterTensors* w = &model->params;
+    return hpa_embed_frag(d->d_tokens + ln->r0, d->d_pos + ln->r0, w->wte, w->wpe, ln->res, ln->st1, ln->B,
+                          model->config.channels);
+}
+
+static int lane_argmax(GPT2* model, int li) {
+    GPT2Decode* d = model->decode;
+    const DecLane* ln = &d->lanes[li];
+    const int V = model->config.vocab_size;
+    return hpa_argmax_final(ln->part, (V + 15) / 16, ln->Mp, ln->B, d->d_next + ln->r0, d->d_tokens + ln->r0,
+                            d->d_pos + ln->r0);
 }
 
 /* one lane's fused step on the current stream: embed, then per layer
@@ -830,35 +875,88 @@ static int fgemm(GPT2Decode* d, const DecLane* ln, const float* x, int K, const 
 static int dec_launch_lane(GPT2* model, int li) {
     GPT2Decode* d = model->decode;
     const DecLane* ln = &d->lanes[li];
-    const GPT2Config c = model->config;
-    const int C = c.channels, L = c.num_layers, V = c.vocab_size;
-    const ParameterTensors* w = &model->params;
-    const int ct = C / 16, r0 = ln->r0;
-    const size_t e_layer = d->wpack_off[3] + hpa_frag_elems(C, 4 * C);
-    int* pos = d->d_pos + r0;
-    const int* bt = d->d_bt + (size_t)r0 * d->bt_stride;
-    float* q = d->d_q + (size_t)r0 * C;
-    int rc = hpa_embed_frag(d->d_tokens + r0, pos, w->wte, w->wpe, ln->res, ln->st1, ln->B, C);
-    int st_tiles = 1;
+    const int C = model->config.channels, L = model->config.num_layers;
+    int rc = lane_embed(model, li);
     for (int l = 0; l < L && !rc; l++) {
-        const size_t lc = (size_t)l * C;
-        const float* wl = d->d_wpack + e_layer * l;
-        rc |= fgemm(d, ln, ln->res, C, ln->st1, st_tiles, w->ln1w + lc, w->ln1b + lc, wl + d->wpack_off[0],
-                    3 * C, w->qkvb + 3 * lc, 0, HPA_FEPI_QKV, q, NULL, NULL, NULL, l);
+        rc |= lane_gemm_run(model, li, l, G_QKV);
         if (d->prof_ev) rc |= hpa_event_record(PROF_EV(d, l, li, 0));
-        rc |= hpa_paged_attention_decode_frag(q, &d->pool, l, bt, d->bt_stride, pos, ln->att, ln->B);
+        rc |= hpa_paged_attention_decode_frag(d->d_q + (size_t)ln->r0 * C, &d->pool, l,
+                                              d->d_bt + (size_t)ln->r0 * d->bt_stride, d->bt_stride,
+                                              d->d_pos + ln->r0, ln->att, ln->B);
         if (d->prof_ev) rc |= hpa_event_record(PROF_EV(d, l, li, 1));
-        rc |= fgemm(d, ln, ln->att, C, NULL, 0, NULL, NULL, wl + d->wpack_off[1], C, w->attprojb + lc,
-                    1, HPA_FEPI_RESID, ln->res2, ln->res, ln->st2, NULL, l);
-        rc |= fgemm(d, ln, ln->res2, C, ln->st2, ct, w->ln2w + lc, w->ln2b + lc, wl + d->wpack_off[2],
-                    4 * C, w->fcb + 4 * lc, 2, HPA_FEPI_GELU, ln->fch, NULL, NULL, NULL, l);
-        rc |= fgemm(d, ln, ln->fch, 4 * C, NULL, 0, NULL, NULL, wl + d->wpack_off[3], C, w->fcprojb + lc,
-                    3, HPA_FEPI_RESID, ln->res, ln->res2, ln->st1, NULL, l);
-        st_tiles = ct;
+        rc |= lane_gemm_run(model, li, l, G_ATTPROJ);
+        rc |= lane_gemm_run(model, li, l, G_FC);
+        rc |= lane_gemm_run(model, li, l, G_FCPROJ);
     }
-    rc |= fgemm(d, ln, ln->res, C, ln->st1, st_tiles, w->lnfw, w->lnfb, d->d_wpack + d->wpack_off[4], V,
-                NULL, 4, HPA_FEPI_LOGITS, d->d_logits + (size_t)r0 * V, NULL, NULL, ln->part, 0);
-    rc |= hpa_argmax_final(ln->part, (V + 15) / 16, ln->Mp, ln->B, d->d_next + r0, d->d_tokens + r0, pos);
+    rc |= lane_gemm_run(model, li, 0, G_LOGITS);
+    rc |= lane_argmax(model, li);
+    return rc;
+}
+
+/* ---- pipelined step (two lanes, one stream) ----
+ * Each lane's layer attention is cut into PIPE_CHUNKS context chunks; every
+ * chunk of lane X's attention shares its launch with one GEMM of lane Y's
+ * chain (hpa_attn_chunk_with_gemm), so the HBM-bound stream and the
+ * latency-bound GEMMs run side by side:
+ *   A: qkv(0)                                     (alone)
+ *   layer l: attn_A(l) chunks 0..3  |  B: attproj(l-1) fc(l-1) fcproj(l-1) qkv(l)
+ *            attn_B(l) chunks 0..3  |  A: attproj(l)   fc(l)   fcproj(l)   qkv(l+1)
+ *   B: attproj(L-1) fc(L-1) fcproj(L-1); logits A, B; greedy A, B  (alone)
+ * Every dependency is a launch boundary on the one stream. */
+#define PIPE_CHUNKS 4
+
+static void lane_attn(GPT2* model, int li, int l, int chunk, HpaAttnChunk* a) {
+    GPT2Decode* d = model->decode;
+    const DecLane* ln = &d->lanes[li];
+    const int C = model->config.channels;
+    a->q = d->d_q + (size_t)ln->r0 * C;
+    a->pool = &d->pool;
+    a->layer = l;
+    a->block_table = d->d_bt + (size_t)ln->r0 * d->bt_stride;
+    a->bt_stride = d->bt_stride;
+    a->pos = d->d_pos + ln->r0;
+    a->state = ln->astate;
+    a->out_frag = ln->att;
+    a->B = ln->B;
+    a->chunk = chunk;
+    a->nchunks = PIPE_CHUNKS;
+}
+
+static int pipe_launch(GPT2* model, int att_lane, int l, int chunk, int gemm_lane, int gl, int which) {
+    HpaAttnChunk a;
+    lane_attn(model, att_lane, l, chunk, &a);
+    if (which < 0) return hpa_attn_chunk_with_gemm(&a, NULL);
+    HpaFusedGemm g;
+    lane_gemm(model, gemm_lane, gl, which, &g);
+    g.waves = 4;  /* the combo's GEMM role: 4 waves, one row block, one column tile */
+    g.row_blocks = 1;
+    g.col_tiles = 1;
+    return hpa_attn_chunk_with_gemm(&a, &g);
+}
+
+static int dec_launch_pipelined(GPT2* model) {
+    const int L = model->config.num_layers;
+    const int A = 0, B = 1;
+    int rc = lane_embed(model, A);
+    rc |= lane_embed(model, B);
+    rc |= lane_gemm_run(model, A, 0, G_QKV);
+    for (int l = 0; l < L && !rc; l++) {
+        /* lane B's chain: the rest of layer l-1, then qkv(l) */
+        const int segB[PIPE_CHUNKS][2] = {{l - 1, l > 0 ? G_ATTPROJ : -1}, {l - 1, l > 0 ? G_FC : -1},
+                                          {l - 1, l > 0 ? G_FCPROJ : -1}, {l, G_QKV}};
+        for (int c = 0; c < PIPE_CHUNKS; c++) rc |= pipe_launch(model, A, l, c, B, segB[c][0], segB[c][1]);
+        /* lane A's chain: the rest of layer l, then qkv(l+1) */
+        const int segA[PIPE_CHUNKS][2] = {{l, G_ATTPROJ}, {l, G_FC}, {l, G_FCPROJ},
+                                          {l + 1, l + 1 < L ? G_QKV : -1}};
+        for (int c = 0; c < PIPE_CHUNKS; c++) rc |= pipe_launch(model, B, l, c, A, segA[c][0], segA[c][1]);
+    }
+    rc |= lane_gemm_run(model, B, L - 1, G_ATTPROJ);
+    rc |= lane_gemm_run(model, B, L - 1, G_FC);
+    rc |= lane_gemm_run(model, B, L - 1, G_FCPROJ);
+    rc |= lane_gemm_run(model, A, 0, G_LOGITS);
+    rc |= lane_gemm_run(model, B, 0, G_LOGITS);
+    rc |= lane_argmax(model, A);
+    rc |= lane_argmax(model, B);
     return rc;
 }
 
@@ -866,6 +964,7 @@ static int dec_launch_lane(GPT2* model, int li) {
  * lane 0, and join back before the step completes */
 static int dec_launch_fused(GPT2* model) {
     GPT2Decode* d = model->decode;
+    if (d->pipeline) return dec_launch_pipelined(model);
     if (d->nlanes == 1) return dec_launch_lane(model, 0);
     void* main_stream = hpa_get_stream();
     int rc = hpa_event_record(d->ev_fork);
@@ -907,10 +1006,32 @@ int gpt2_decode_set_lanes(GPT2* model, int lanes) {
         hpa_graph_destroy(d->graph);
         d->graph = NULL;
     }
-    return dec_lanes_alloc(d, lanes, model->config.channels, model->config.vocab_size);
+    d->pipeline = 0;
+    return dec_lanes_alloc(d, lanes, model->config.channels, model->config.vocab_size, model->config.num_heads);
 }
 
 int gpt2_decode_lanes(GPT2* model) { return model->decode ? model->decode->nlanes : 0; }
+
+/* pipelined step: two lanes on ONE stream, each lane's attention in context
+ * chunks beside the other lane's GEMMs (dec_launch_pipelined).  Needs two
+ * lanes of whole 16-row blocks (B > 16) and page size 8, 16 or 32. */
+int gpt2_decode_set_pipeline(GPT2* model, int enable) {
+    GPT2Decode* d = model->decode;
+    if (!d) return 1;
+    if (!enable) {
+        if (!d->pipeline) return 0;
+        return gpt2_decode_set_lanes(model, 1);
+    }
+    if (d->B <= 16 || (d->P != 8 && d->P != 16 && d->P != 32)) {
+        fprintf(stderr, "[paged_infer] pipeline needs B > 16 and page size 8/16/32\n");
+        return 1;
+    }
+    if (gpt2_decode_set_lanes(model, 2) || d->nlanes != 2) return 1;
+    d->pipeline = 1;
+    return 0;
+}
+
+int gpt2_decode_pipeline(GPT2* model) { return model->decode ? model->decode->pipeline : 0; }
 
 int gpt2_decode_set_graph(GPT2* model, int enable) {
     GPT2Decode* d = model->decode;

@@ -50,6 +50,13 @@ class HpaKVPool(ctypes.Structure):
                 ("managed", ctypes.c_int)]
 
 
+class HpaAttnChunk(ctypes.Structure):
+    """hip_paged_attn.h HpaAttnChunk"""
+    _fields_ = [("q", _V), ("pool", _V), ("layer", ctypes.c_int), ("block_table", _V), ("bt_stride", ctypes.c_int),
+                ("pos", _V), ("state", _V), ("out_frag", _V), ("B", ctypes.c_int), ("chunk", ctypes.c_int),
+                ("nchunks", ctypes.c_int)]
+
+
 class HpaFusedGemm(ctypes.Structure):
     _fields_ = [("x", _V), ("M", ctypes.c_int), ("K", ctypes.c_int), ("ln_stats", _V),
                 ("ln_ntiles", ctypes.c_int), ("ln_w", _V), ("ln_b", _V), ("w", _V),
@@ -221,6 +228,10 @@ def lib():
     _sig(L, "gpt2_decode_time_attention", i, [v, i, ctypes.POINTER(ctypes.c_double),
                                               ctypes.POINTER(ctypes.c_double)])
     _sig(L, "gpt2_decode_lanes", i, [v])
+    _sig(L, "gpt2_decode_set_pipeline", i, [v, i])
+    _sig(L, "gpt2_decode_pipeline", i, [v])
+    _sig(L, "hpa_attn_state_elems", ctypes.c_size_t, [i, i])
+    _sig(L, "hpa_attn_chunk_with_gemm", i, [ctypes.c_void_p, ctypes.c_void_p])
     _sig(L, "gpt2_decode_step_bytes", ctypes.c_double, [v, ctypes.POINTER(ctypes.c_double)])
     _sig(L, "random_u32", ctypes.c_uint, [ctypes.POINTER(ctypes.c_ulonglong)])
     _sig(L, "random_f32", f, [ctypes.POINTER(ctypes.c_ulonglong)])
@@ -469,6 +480,9 @@ class Model:
         check(lib().gpt2_decode_time_attention(self.h, int(iters), ctypes.byref(ms), ctypes.byref(by)),
               "time_attention")
         return ms.value, by.value
+
+    def set_pipeline(self, enable=True):
+        check(lib().gpt2_decode_set_pipeline(self.h, int(bool(enable))), "set_pipeline")
 
     def set_lanes(self, lanes):
         check(lib().gpt2_decode_set_lanes(self.h, int(lanes)), "set_lanes")

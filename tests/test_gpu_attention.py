@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 
-def _run_case(hip, P, ctxs, NH, waves=4, seed=0, q_scale=2.0, kv=None):
+def _run_case(hip, P, ctxs, NH, waves=4, seed=0, q_scale=2.0, kv=None, chunks=0):
     rng = np.random.default_rng(seed)
     L = hip.lib()
     C = NH * 64
@@ -44,12 +44,26 @@ def _run_case(hip, P, ctxs, NH, waves=4, seed=0, q_scale=2.0, kv=None):
     d_q = hip.DeviceBuffer.from_array(q)
     d_bt = hip.DeviceBuffer.from_array(bt)
     d_pos = hip.DeviceBuffer.from_array(pos)
-    d_out = hip.DeviceBuffer(q.nbytes)
-    hip.check(L.hpa_set_attention_waves(waves))
-    hip.check(L.hpa_paged_attention_decode(d_q.ptr, pool.ref, 0, d_bt.ptr, maxp, d_pos.ptr, d_out.ptr, B))
-    hip.check(L.hpa_synchronize())
-    hip.check(L.hpa_set_attention_waves(4))
-    out = d_out.download((B, C))
+    if chunks:  # context chunks with carried softmax state (the pipelined decode)
+        import ctypes
+        Mp = (B + 15) // 16 * 16
+        d_out = hip.DeviceBuffer(Mp * C * 4)
+        d_state = hip.DeviceBuffer(L.hpa_attn_state_elems(B, NH) * 4)
+        a = hip.HpaAttnChunk(q=d_q.ptr, pool=ctypes.addressof(pool.s), layer=0, block_table=d_bt.ptr,
+                             bt_stride=maxp, pos=d_pos.ptr, state=d_state.ptr, out_frag=d_out.ptr, B=B,
+                             nchunks=chunks)
+        for c in range(chunks):
+            a.chunk = c
+            hip.check(L.hpa_attn_chunk_with_gemm(ctypes.byref(a), None), "attn chunk")
+        hip.check(L.hpa_synchronize())
+        out = hip.from_frag(d_out.download(Mp * C), B, C)
+    else:
+        d_out = hip.DeviceBuffer(q.nbytes)
+        hip.check(L.hpa_set_attention_waves(waves))
+        hip.check(L.hpa_paged_attention_decode(d_q.ptr, pool.ref, 0, d_bt.ptr, maxp, d_pos.ptr, d_out.ptr, B))
+        hip.check(L.hpa_synchronize())
+        hip.check(L.hpa_set_attention_waves(4))
+        out = d_out.download((B, C))
     ref = np.zeros_like(out)
     for b, ctx in enumerate(ctxs):
         n = (ctx + P - 1) // P
@@ -138,3 +152,21 @@ def test_decode_attention_full_size_subset_and_determinism(hip):
         vp = [v[i * P:(i + 1) * P].copy() for i in range(maxp)]
         ref = oc.attention_decode(q[b], kp, vp, ctx, NH)
         assert np.abs(o1[b] - ref).max() <= TOL
+
+
+@pytest.mark.parametrize("P", [8, 16, 32])
+@pytest.mark.parametrize("chunks", [1, 3, 4])
+def test_chunked_attention_with_carried_state(hip, P, chunks):
+    """the pipelined decode's attention: context chunks in separate launches,
+    (m, l, acc) carried through memory; ctx 1 and 2 leave most chunks empty"""
+    ctxs = [1, 2, 5, 63, 64, 65, 200, 257, 1024]
+    out, ref = _run_case(hip, P, ctxs, NH=3, seed=P + chunks, chunks=chunks)
+    assert np.abs(out - ref).max() <= TOL
+
+
+def test_chunked_attention_all_scores_below_reference_floor(hip):
+    def kv(ctx, C):
+        return np.full((ctx, C), 10.0, np.float32), np.ones((ctx, C), np.float32)
+
+    out, ref = _run_case(hip, 16, [5, 80, 300], NH=1, seed=1, kv=kv, q_scale=1e-6, chunks=4)
+    assert np.abs(out - ref).max() <= TOL

@@ -25,11 +25,13 @@ def _margins(logits):
     return s[:, -1] - s[:, -2]
 
 
-def _compare_run(hip, cfgd, B, P, steps, seed, graph=False, feed_greedy=False, fused=True):
+def _compare_run(hip, cfgd, B, P, steps, seed, graph=False, feed_greedy=False, fused=True, pipeline=False):
     params = synth.params(cfgd, seed=seed)
     model = hip.Model(cfgd, params=params)
     model.decode_init(B, P, cfgd["maxT"])
     model.set_fused(fused)
+    if pipeline:
+        model.set_pipeline(True)
     model.set_graph(graph)
     c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
     orc = oc.PagedDecoder(params, c, B, P, cfgd["maxT"], page_seed=seed + 3)
@@ -187,4 +189,44 @@ def test_set_lanes_rejects_out_of_range(hip):
         m.set_lanes(0)
     with pytest.raises(RuntimeError):
         m.set_lanes(9)
+    m.close()
+
+
+@pytest.mark.parametrize("P,B", [(16, 40), (8, 33), (32, 64)])
+def test_pipelined_decode_matches_oracle(hip, P, B):
+    """two lanes on one stream, attention chunks beside the other lane's GEMMs"""
+    _compare_run(hip, SMALL, B=B, P=P, steps=40, seed=P + B, pipeline=True)
+
+
+def test_pipelined_decode_gpt2_124m_shapes(hip):
+    """124M shapes: the one-shot GEMM role (K = 768) and the looped one (fcproj)"""
+    cfgd = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
+    worst, ties = _compare_run(hip, cfgd, B=48, P=16, steps=12, seed=5, pipeline=True, graph=True)
+    print(f"124M pipelined: worst logit diff {worst:.3e}, near-ties {ties}")
+
+
+def test_pipelined_graph_equals_eager(hip):
+    params = synth.params(SMALL, seed=14)
+    outs = []
+    for graph in (False, True):
+        m = hip.Model(SMALL, params=params)
+        m.decode_init(40, 16, 128)
+        m.set_pipeline(True)
+        m.set_graph(graph)
+        rng = np.random.default_rng(2)
+        seq = [m.step(rng.integers(0, 1000, 40).astype(np.int32))]
+        for _ in range(10):
+            seq.append(m.step(None))
+        seq.append(m.logits())
+        outs.append(seq)
+        m.close()
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+
+
+def test_set_pipeline_needs_two_lanes(hip):
+    m = hip.Model(SMALL)
+    m.decode_init(16, 16, 64)
+    with pytest.raises(RuntimeError):
+        m.set_pipeline(True)
     m.close()
