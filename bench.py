@@ -272,7 +272,8 @@ def main():
                     + ("synthetic U(-1,1)" if args.prefill == "synthetic" else "decode steps") + ")",
             "config": {"workload": f"GPT-2 {args.model} fp32 paged decode, batch={B_local} per GPU x {world} "
                                    f"(B={B}), ctx {ctx}, page_size={P} (BASELINE.json "
-                                   + ("configs[1])" if world == 1 else "configs[3]: per-seq sharded pool)"),
+                                   + ("configs[2])" if args.model == "XL" else
+                                      "configs[1])" if world == 1 else "configs[3]: per-seq sharded pool)"),
                        "global_batch": B, "batch_per_gpu": B_local, "seq_len": ctx, "page_size": P,
                        "decode_positions": f"{start}..{start + args.warmup + args.steps - 1}",
                        "parallelism": f"seq-shard x{world}" + (f" + RCCL gather({args.gather}) to rank 0"

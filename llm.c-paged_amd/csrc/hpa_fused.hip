@@ -243,18 +243,26 @@ int hpa_unpack_frag(const float* src, int rows, int K, float* dst, int ld) {
 // logits (3142 column tiles already fill the chip; amortises the A reads);
 // waves sharing the K range: enough k-steps per wave to amortise the fold
 void hpa_fused_pick(int M, int N, int K, int* out3) {
-    (void)M;
+    (void)M;  // never by M: a row's summation order must not depend on the batch
     const int ntn = (N + 15) / 16;
     const int k16 = K / 16;
     if (ntn >= 1024) {  // logits (profiles/r1/gemm_tune_b64_*.log)
         out3[0] = 4;
         out3[1] = 2;
         out3[2] = 2;
-        return;
+    } else if (ntn >= 256 && k16 >= 96) {  // GPT-2 XL qkv / fc: MFMA-bound, reuse A over 2 tiles
+        out3[0] = 8;
+        out3[1] = 4;
+        out3[2] = 2;
+    } else if (ntn >= 96 && k16 >= 96) {  // GPT-2 XL attproj / fcproj
+        out3[0] = 8;
+        out3[1] = 2;
+        out3[2] = 1;
+    } else {  // GPT-2 124M layer GEMMs: one row block per workgroup (one-shot where K allows)
+        out3[0] = k16 >= 96 ? 8 : 4;
+        out3[1] = 1;
+        out3[2] = 1;
     }
-    out3[1] = 1;
-    out3[0] = k16 >= 96 ? 8 : 4;
-    out3[2] = 1;
 }
 
 int hpa_fused_pick_waves(int M, int N, int K) {

@@ -230,3 +230,11 @@ def test_set_pipeline_needs_two_lanes(hip):
     with pytest.raises(RuntimeError):
         m.set_pipeline(True)
     m.close()
+
+
+def test_decode_xl_width_matches_oracle(hip):
+    """GPT-2 XL layer shapes (C=1600, NH=25 -> K/16 = 100 and 400: the looped
+    GEMM path; page 32 as BASELINE config 3) on a 2-layer model"""
+    cfgd = dict(maxT=128, V=1000, L=2, NH=25, C=1600)
+    worst, ties = _compare_run(hip, cfgd, B=20, P=32, steps=20, seed=33, graph=True)
+    print(f"XL width: worst logit diff {worst:.3e}, near-ties {ties}")
