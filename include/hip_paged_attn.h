@@ -80,12 +80,16 @@ int   hpa_device_info(char* name, int name_len, int* num_cus, size_t* total_mem)
  * columns of 64 consecutive tokens = 128..512 contiguous bytes per page, the
  * lane-per-token QK^T layout); V tiles are token-major [page_size][head_size]
  * (one 256-byte row per token-head, the lane-per-dimension PV layout).
+ * bf16 pools (HPA_BF16, BASELINE config 5; storage only, all arithmetic
+ * fp32): K tiles [head_size/8][page_size][8] (one 16-byte chunk per
+ * lane-per-token load), V tiles [page_size][head_size] (128-byte rows);
+ * values are rounded to nearest-even when appended.  Page size multiple of 8.
  * A page id names the same slot in every layer's pool (vLLM-style shared
  * block table), so the block table is [seq][logical page] int32. */
 typedef struct HpaKVPool {
     void*  base;          /* device pointer */
     int    num_layers, num_heads, head_size, page_size, num_pages;
-    int    dtype;         /* HPA_F32 (round 1) */
+    int    dtype;         /* HPA_F32 or HPA_BF16 */
     size_t elem_bytes;
     size_t page_elems;    /* elements of one page of one layer (K and V, all heads) */
     size_t layer_elems;   /* num_pages * page_elems */

@@ -131,6 +131,9 @@ float* gpt2_acts_probs(GPT2* model);
  * Uses model->manager when it was set by the caller (its block_size becomes
  * the page size), otherwise creates one sized B x ceil(max_ctx/page_size). */
 int  gpt2_decode_init(GPT2* model, int B, int page_size, int max_ctx);
+/* the same with the KV pool's storage type: HPA_F32 (0, default) or HPA_BF16
+ * (1: BASELINE config 5; page size a multiple of 8; fused path only) */
+int  gpt2_decode_init_ex(GPT2* model, int B, int page_size, int max_ctx, int kv_dtype);
 /* one decode step for every sequence: tokens[b] (host) at position pos[b];
  * tokens == NULL feeds back the previous step's greedy ids (device-resident).
  * next_tokens (host, may be NULL) receives argmax(logits[b]). */

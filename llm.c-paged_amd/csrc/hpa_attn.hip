@@ -33,9 +33,9 @@
 namespace {
 using namespace hpa_attn;
 
-template <int P, int NW, bool FRAG>
+template <int P, int NW, bool FRAG, bool BF16>
 __global__ __launch_bounds__(NW * 64, 3) void paged_attn_decode_f32(
-    const float* __restrict__ q, const float* __restrict__ layer_base, size_t page_elems, int NH,
+    const float* __restrict__ q, const void* __restrict__ layer_base, size_t page_elems, int NH,
     const int* __restrict__ block_table, int bt_stride, const int* __restrict__ pos,
     float* __restrict__ out, float qscale, float m_init) {
     constexpr int TILE = P * HS;
@@ -55,42 +55,62 @@ __global__ __launch_bounds__(NW * 64, 3) void paged_attn_decode_f32(
     // 1/sqrt(hs) * log2(e) scale is applied to the finished dot (as the
     // reference applies `val *= scale` after the dot, :197).
     const float* __restrict__ qh = q + ((size_t)b * NH + h) * HS;
+    const int* bt = block_table + (size_t)b * bt_stride;
+    const int n_it = (ctx + 63) >> 6;
     float m = m_init;
     float l = 0.f;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    attn_tiles<P, NW>(qh, layer_base + (size_t)h * TILE, layer_base + (size_t)(NH + h) * TILE, page_elems,
-                      block_table + (size_t)b * bt_stride, ctx, 0, (ctx + 63) >> 6, qscale, m, l, acc);
-    if (!attn_fold<NW>(m, l, acc, s_m, s_l, s_acc)) return;
-    // out[b][h*64 + 4*lane .. +3]: row-major, or the frag layout the next
-    // GEMM reads (4 consecutive columns stay one contiguous float4 there)
-    const size_t oi = FRAG ? hpa::frag_index(b, h * HS + 4 * lane, NH * HS) : ((size_t)b * NH + h) * HS + 4 * lane;
-    const float inv = l == 0.f ? 0.f : 1.f / l;
-    *reinterpret_cast<float4*>(out + oi) = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+    if constexpr (BF16) {
+        const unsigned short* base = reinterpret_cast<const unsigned short*>(layer_base);
+        float4 acc[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+        attn_tiles_bf16<P, NW>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, page_elems, bt, ctx, 0,
+                               n_it, qscale, m, l, acc);
+        if (!attn_fold_bf16<NW>(m, l, acc, s_m, s_l, s_acc)) return;
+        const float inv = l == 0.f ? 0.f : 1.f / l;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {  // dims 8*lane + 4k .. +3
+            const int col = h * HS + 8 * lane + 4 * k;
+            const size_t oi = FRAG ? hpa::frag_index(b, col, NH * HS) : (size_t)b * NH * HS + col;
+            *reinterpret_cast<float4*>(out + oi) =
+                make_float4(acc[k].x * inv, acc[k].y * inv, acc[k].z * inv, acc[k].w * inv);
+        }
+    } else {
+        const float* base = reinterpret_cast<const float*>(layer_base);
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        attn_tiles<P, NW>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, page_elems, bt, ctx, 0,
+                          n_it, qscale, m, l, acc);
+        if (!attn_fold<NW>(m, l, acc, s_m, s_l, s_acc)) return;
+        // out[b][h*64 + 4*lane .. +3]: row-major, or the frag layout the next
+        // GEMM reads (4 consecutive columns stay one contiguous float4 there)
+        const size_t oi =
+            FRAG ? hpa::frag_index(b, h * HS + 4 * lane, NH * HS) : ((size_t)b * NH + h) * HS + 4 * lane;
+        const float inv = l == 0.f ? 0.f : 1.f / l;
+        *reinterpret_cast<float4*>(out + oi) = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+    }
 }
 
-template <int P, bool FRAG>
+template <int P, bool FRAG, bool BF16>
 int launch_decode(const float* q, const HpaKVPool* pool, int layer, const int* bt, int bt_stride,
                   const int* pos, float* out, int B, int nw) {
-    const float* base = (const float*)pool->base + (size_t)layer * pool->layer_elems;
+    const void* base = (const char*)pool->base + (size_t)layer * pool->layer_elems * pool->elem_bytes;
     const float log2e = 1.4426950408889634f;
     const float qscale = (float)(1.0 / sqrt((double)HS)) * log2e;
     const float m_init = -10000.0f * log2e;
     dim3 grid(B * pool->num_heads);
     switch (nw) {
         case 1:
-            paged_attn_decode_f32<P, 1, FRAG><<<grid, 64, 0, hpa_stream()>>>(
+            paged_attn_decode_f32<P, 1, FRAG, BF16><<<grid, 64, 0, hpa_stream()>>>(
                 q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init);
             break;
         case 2:
-            paged_attn_decode_f32<P, 2, FRAG><<<grid, 128, 0, hpa_stream()>>>(
+            paged_attn_decode_f32<P, 2, FRAG, BF16><<<grid, 128, 0, hpa_stream()>>>(
                 q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init);
             break;
         case 8:
-            paged_attn_decode_f32<P, 8, FRAG><<<grid, 512, 0, hpa_stream()>>>(
+            paged_attn_decode_f32<P, 8, FRAG, BF16><<<grid, 512, 0, hpa_stream()>>>(
                 q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init);
             break;
         default:
-            paged_attn_decode_f32<P, 4, FRAG><<<grid, 256, 0, hpa_stream()>>>(
+            paged_attn_decode_f32<P, 4, FRAG, BF16><<<grid, 256, 0, hpa_stream()>>>(
                 q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init);
             break;
     }
@@ -114,17 +134,23 @@ int hpa_set_attention_waves(int nw) {
 static int attn_dispatch(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
                          int bt_stride, const int* pos, float* out, int B, bool frag) {
     HPA_REQUIRE(pool && pool->base, "pool not created");
-    HPA_REQUIRE(pool->dtype == HPA_F32, "decode attention: fp32 pool expected");
+    HPA_REQUIRE(pool->dtype == HPA_F32 || pool->dtype == HPA_BF16, "decode attention: fp32 or bf16 pool");
     HPA_REQUIRE(pool->head_size == HS, "decode attention requires head_size 64");
     HPA_REQUIRE(layer >= 0 && layer < pool->num_layers, "layer out of range");
     HPA_REQUIRE(B > 0 && q && out && block_table && pos, "bad arguments");
     HPA_REQUIRE(((uintptr_t)q & 15) == 0 && ((uintptr_t)out & 15) == 0, "q/out must be 16-byte aligned");
-#define HPA_ATTN_CASE(PS)                                                                        \
-    case PS:                                                                                      \
-        return frag ? launch_decode<PS, true>(q, pool, layer, block_table, bt_stride, pos, out, B, \
-                                              g_attn_waves)                                        \
-                    : launch_decode<PS, false>(q, pool, layer, block_table, bt_stride, pos, out, B, \
-                                               g_attn_waves);
+    const bool bf = pool->dtype == HPA_BF16;
+#define HPA_ATTN_CASE(PS)                                                                              \
+    case PS:                                                                                            \
+        if (bf)                                                                                         \
+            return frag ? launch_decode<PS, true, true>(q, pool, layer, block_table, bt_stride, pos, out, B, \
+                                                        g_attn_waves)                                   \
+                        : launch_decode<PS, false, true>(q, pool, layer, block_table, bt_stride, pos, out, \
+                                                         B, g_attn_waves);                              \
+        return frag ? launch_decode<PS, true, false>(q, pool, layer, block_table, bt_stride, pos, out, B, \
+                                                     g_attn_waves)                                      \
+                    : launch_decode<PS, false, false>(q, pool, layer, block_table, bt_stride, pos, out, B, \
+                                                      g_attn_waves);
     switch (pool->page_size) {
         HPA_ATTN_CASE(8)
         HPA_ATTN_CASE(16)

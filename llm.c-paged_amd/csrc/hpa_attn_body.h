@@ -98,6 +98,154 @@ __device__ __forceinline__ void attn_tiles(const float* __restrict__ qh, const f
     }
 }
 
+// ---- bf16 KV pool (BASELINE config 5): storage only, every product and
+// sum in fp32.  K tile [8 chunks][P][8 dims] (a lane-per-token chunk is one
+// 16-B load), V tile [P][64] (128 B per token: 8 lanes per row, one wave
+// instruction reads 8 consecutive rows = 1 KiB).
+__device__ __forceinline__ uint4 load_stream16(const unsigned short* ptr) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(ptr));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float bf_lo(unsigned int u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf_hi(unsigned int u) { return __uint_as_float(u & 0xffff0000u); }
+
+// acc[0], acc[1]: lane (g = lane>>3, d8 = lane&7) holds dims 8*d8..+7 summed
+// over tokens t0 + 8i + g
+template <int P, int NW>
+__device__ __forceinline__ void attn_tiles_bf16(const float* __restrict__ qh,
+                                                const unsigned short* __restrict__ kbase,
+                                                const unsigned short* __restrict__ vbase, size_t page_elems,
+                                                const int* __restrict__ bt, int ctx, int it_begin, int it_end,
+                                                float qscale, float& m, float& l, float4* acc) {
+    static_assert(P % 8 == 0 && 64 % P == 0, "bf16 pages: page size 8, 16, 32 or 64");
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int g = lane >> 3;
+    const int d8 = lane & 7;
+    const int v_lane_off = g * HS + d8 * 8;
+    int it = it_begin + w;
+    int pid = 0;
+    if (it < it_end) {
+        const unsigned t0 = (unsigned)it << 6, tok = t0 + lane;
+        pid = bt[(tok < (unsigned)ctx ? tok : t0) / P];
+    }
+    for (; it < it_end; it += NW) {
+        const unsigned t0 = (unsigned)it << 6;
+        const unsigned tok = t0 + lane;
+        const bool valid = tok < (unsigned)ctx;
+        const unsigned short* kt = kbase + (size_t)(unsigned)pid * page_elems + (tok % P) * 8;
+        uint4 kv[8], vv[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) kv[c] = load_stream16(kt + c * P * 8);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int vpid = __builtin_amdgcn_readlane(pid, 8 * i);
+            const unsigned short* vrow = vbase + (size_t)(unsigned)vpid * page_elems + ((8 * i) % P) * HS;
+            vv[i] = (t0 + 8 * i + g) < (unsigned)ctx ? load_stream16(vrow + v_lane_off) : make_uint4(0, 0, 0, 0);
+        }
+        {
+            const int itn = it + NW;
+            const unsigned t0n = (unsigned)itn << 6, tokn = t0n + lane;
+            if (itn < it_end) pid = bt[(tokn < (unsigned)ctx ? tokn : t0n) / P];
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            s = fmaf(qh[8 * c + 0], bf_lo(kv[c].x), s);
+            s = fmaf(qh[8 * c + 1], bf_hi(kv[c].x), s);
+            s = fmaf(qh[8 * c + 2], bf_lo(kv[c].y), s);
+            s = fmaf(qh[8 * c + 3], bf_hi(kv[c].y), s);
+            s = fmaf(qh[8 * c + 4], bf_lo(kv[c].z), s);
+            s = fmaf(qh[8 * c + 5], bf_hi(kv[c].z), s);
+            s = fmaf(qh[8 * c + 6], bf_lo(kv[c].w), s);
+            s = fmaf(qh[8 * c + 7], bf_hi(kv[c].w), s);
+        }
+        s = valid ? s * qscale : -INFINITY;
+        const float mt = hpa::wave_max(s);
+        const float mn = fmaxf(m, mt);
+        const float alpha = exp2f(m - mn);
+        const float p = exp2f(s - mn);
+        l = fmaf(l, alpha, p);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            acc[k].x *= alpha;
+            acc[k].y *= alpha;
+            acc[k].z *= alpha;
+            acc[k].w *= alpha;
+        }
+        m = mn;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float pi = __shfl(p, 8 * i + g, 64);
+            acc[0].x = fmaf(pi, bf_lo(vv[i].x), acc[0].x);
+            acc[0].y = fmaf(pi, bf_hi(vv[i].x), acc[0].y);
+            acc[0].z = fmaf(pi, bf_lo(vv[i].y), acc[0].z);
+            acc[0].w = fmaf(pi, bf_hi(vv[i].y), acc[0].w);
+            acc[1].x = fmaf(pi, bf_lo(vv[i].z), acc[1].x);
+            acc[1].y = fmaf(pi, bf_hi(vv[i].z), acc[1].y);
+            acc[1].z = fmaf(pi, bf_lo(vv[i].w), acc[1].z);
+            acc[1].w = fmaf(pi, bf_hi(vv[i].w), acc[1].w);
+        }
+    }
+}
+
+// fold for the bf16 layout: the 8 token groups (lane bits 3..5), then the
+// waves through LDS (s_acc: [NW][8 lanes][2]); result in wave 0, lanes 0..7
+template <int NW>
+__device__ __forceinline__ bool attn_fold_bf16(float& m, float& l, float4* acc, float* s_m, float* s_l,
+                                               float4* s_acc) {
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 8; o <= 32; o <<= 1)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            acc[k].x += __shfl_xor(acc[k].x, o, 64);
+            acc[k].y += __shfl_xor(acc[k].y, o, 64);
+            acc[k].z += __shfl_xor(acc[k].z, o, 64);
+            acc[k].w += __shfl_xor(acc[k].w, o, 64);
+        }
+    l = hpa::wave_sum(l);
+    if constexpr (NW == 1) {
+        return lane < 8;
+    } else {
+        if (lane == 0) {
+            s_m[w] = m;
+            s_l[w] = l;
+        }
+        if (lane < 8) {
+            s_acc[(w * 8 + lane) * 2] = acc[0];
+            s_acc[(w * 8 + lane) * 2 + 1] = acc[1];
+        }
+        __syncthreads();
+        if (w != 0 || lane >= 8) return false;
+        float M = s_m[0];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) M = fmaxf(M, s_m[i]);
+        float L = 0.f;
+        float4 O[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            const float f = exp2f(s_m[i] - M);
+            L = fmaf(s_l[i], f, L);
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const float4 a = s_acc[(i * 8 + lane) * 2 + k];
+                O[k].x = fmaf(a.x, f, O[k].x);
+                O[k].y = fmaf(a.y, f, O[k].y);
+                O[k].z = fmaf(a.z, f, O[k].z);
+                O[k].w = fmaf(a.w, f, O[k].w);
+            }
+        }
+        m = M;
+        l = L;
+        acc[0] = O[0];
+        acc[1] = O[1];
+        return true;
+    }
+}
+
 // Fold the 4 token groups and the per-lane sums of every wave, then the
 // waves (fixed order, through LDS: s_m[NW], s_l[NW], s_acc[NW*16]).  The
 // combined state lands in wave 0, lanes 0..15 (returns true there): lane

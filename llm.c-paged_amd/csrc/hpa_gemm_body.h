@@ -25,7 +25,8 @@ struct FG {
     const float* res_in;
     float* stats_out;
     float* part_out;
-    float* kv_base;
+    float* kv_base;  // layer base of the KV pool (bf16 pools: reinterpreted)
+    int kv_bf16;
     size_t page_elems;
     int NH, P;
     const int* bt;
@@ -135,11 +136,18 @@ struct Epi {
                             const int ps = p.pos[row];
                             const int page = p.bt[(size_t)row * p.bt_stride + ps / p.P];
                             const int slot = ps % p.P;
-                            float* kvt = p.kv_base + (size_t)page * p.page_elems + ((size_t)kv * p.NH + hh) * p.P * 64;
-                            if (kv == 0)
-                                kvt[((d >> 2) * p.P + slot) * 4 + (d & 3)] = val;  // K: [chunk][slot][4]
-                            else
-                                kvt[slot * 64 + d] = val;  // V: [slot][64]
+                            const size_t toff = (size_t)page * p.page_elems + ((size_t)kv * p.NH + hh) * p.P * 64;
+                            if (p.kv_bf16) {  // bf16 pool: K [chunk of 8][slot][8], V [slot][64], RNE
+                                unsigned short* kvt = reinterpret_cast<unsigned short*>(p.kv_base) + toff;
+                                kvt[kv == 0 ? ((d >> 3) * p.P + slot) * 8 + (d & 7) : slot * 64 + d] =
+                                    hpa::f32_to_bf16(val);
+                            } else {
+                                float* kvt = p.kv_base + toff;
+                                if (kv == 0)
+                                    kvt[((d >> 2) * p.P + slot) * 4 + (d & 3)] = val;  // K: [chunk][slot][4]
+                                else
+                                    kvt[slot * 64 + d] = val;  // V: [slot][64]
+                            }
                         }
                     }
                 } else if (EPI == HPA_FEPI_GELU) {
@@ -517,6 +525,7 @@ static inline int fused_prepare(const HpaFusedGemm* g, FG* p) {
     p->stats_out = g->stats_out;
     p->part_out = g->part_out;
     p->kv_base = nullptr;
+    p->kv_bf16 = 0;
     p->page_elems = 0;
     p->NH = 0;
     p->P = 1;
@@ -525,12 +534,14 @@ static inline int fused_prepare(const HpaFusedGemm* g, FG* p) {
     p->pos = g->pos;
     if (g->epilogue == HPA_FEPI_QKV) {
         const HpaKVPool* pool = g->pool;
-        HPA_REQUIRE(pool && pool->base && pool->dtype == HPA_F32 && pool->head_size == 64,
-                    "gemm_fused QKV: fp32 pool with head_size 64");
+        HPA_REQUIRE(pool && pool->base && (pool->dtype == HPA_F32 || pool->dtype == HPA_BF16) &&
+                        pool->head_size == 64,
+                    "gemm_fused QKV: fp32/bf16 pool with head_size 64");
         HPA_REQUIRE(g->N == 3 * pool->num_heads * 64, "gemm_fused QKV: N != 3*C");
         HPA_REQUIRE(g->layer >= 0 && g->layer < pool->num_layers, "gemm_fused QKV: layer");
         HPA_REQUIRE(g->block_table && g->pos, "gemm_fused QKV: block table / positions");
-        p->kv_base = (float*)pool->base + (size_t)g->layer * pool->layer_elems;
+        p->kv_base = (float*)((char*)pool->base + (size_t)g->layer * pool->layer_elems * pool->elem_bytes);
+        p->kv_bf16 = pool->dtype == HPA_BF16;
         p->page_elems = pool->page_elems;
         p->NH = pool->num_heads;
         p->P = pool->page_size;

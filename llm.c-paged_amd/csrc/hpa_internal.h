@@ -54,6 +54,14 @@ __device__ __host__ __forceinline__ size_t frag_index(int m, int k, int K) {
            (size_t)(k & 3);
 }
 
+// fp32 -> bf16, round to nearest even (finite inputs; the KV pool's storage)
+__device__ __host__ __forceinline__ unsigned short f32_to_bf16(float f) {
+    unsigned int u;
+    __builtin_memcpy(&u, &f, 4);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (unsigned short)(u >> 16);
+}
+
 // GELU of the reference (paged_infer.c:243-251): 0.5 x (1 + tanh(sqrt(2/pi)(x + 0.044715 x^3)))
 __device__ __forceinline__ float gelu_ref(float x) {
     // sqrtf(2.0f / M_PI) as the reference computes it: float(2/pi) then sqrtf

@@ -230,7 +230,7 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
 }
 
 // grid (ctx, B, L): every (layer, sequence, position) token row of K and V
-__global__ __launch_bounds__(256) void pool_fill_random_kernel(float* __restrict__ base,
+__global__ __launch_bounds__(256) void pool_fill_random_kernel(void* __restrict__ base_v, int bf16,
                                                                size_t layer_elems, size_t page_elems,
                                                                int NH, int P, const int* __restrict__ bt,
                                                                int bt_stride, uint64_t seed) {
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void pool_fill_random_kernel(float* __restrict
     const int C = NH * 64;
     const int page = bt[(size_t)b * bt_stride + p / P];
     const int slot = p % P;
-    float* lb = base + (size_t)l * layer_elems + (size_t)page * page_elems;
+    const size_t off = (size_t)l * layer_elems + (size_t)page * page_elems;
     const uint64_t key = (((uint64_t)l * 4096u + b) * 1048576u + p) * 4u;
     for (int i = threadIdx.x; i < 2 * C; i += 256) {
         const int kv = i >= C;
@@ -246,11 +246,14 @@ __global__ __launch_bounds__(256) void pool_fill_random_kernel(float* __restrict
         const int hh = c >> 6, d = c & 63;
         const uint64_t r = splitmix64(seed ^ (key * 2654435761ull + (uint64_t)i));
         const float u = (float)(r >> 40) * (1.0f / 16777216.0f) * 2.0f - 1.0f;
-        float* tile = lb + ((size_t)kv * NH + hh) * P * 64;
-        if (kv == 0)
-            tile[((d >> 2) * P + slot) * 4 + (d & 3)] = u;
-        else
-            tile[slot * 64 + d] = u;
+        const size_t tile = off + ((size_t)kv * NH + hh) * P * 64;
+        if (bf16) {
+            unsigned short* t = reinterpret_cast<unsigned short*>(base_v) + tile;
+            t[kv == 0 ? ((d >> 3) * P + slot) * 8 + (d & 7) : slot * 64 + d] = hpa::f32_to_bf16(u);
+        } else {
+            float* t = reinterpret_cast<float*>(base_v) + tile;
+            t[kv == 0 ? ((d >> 2) * P + slot) * 4 + (d & 3) : slot * 64 + d] = u;
+        }
     }
 }
 
@@ -312,12 +315,12 @@ int hpa_argmax_advance(const float* logits, int B, int V, int* next, int* tokens
 
 int hpa_pool_fill_random(const HpaKVPool* pool, const int* block_table, int bt_stride, int B, int ctx,
                          uint64_t seed) {
-    HPA_REQUIRE(pool && pool->base && pool->dtype == HPA_F32 && pool->head_size == 64,
-                "fill_random: fp32 pool with head_size 64 expected");
+    HPA_REQUIRE(pool && pool->base && (pool->dtype == HPA_F32 || pool->dtype == HPA_BF16) && pool->head_size == 64,
+                "fill_random: fp32/bf16 pool with head_size 64 expected");
     HPA_REQUIRE(B > 0 && B < 4096 && ctx >= 0 && ctx < 1048576, "fill_random: bad shape");
     if (ctx == 0) return 0;
     dim3 grid(ctx, B, pool->num_layers);
-    pool_fill_random_kernel<<<grid, 256, 0, hpa_stream()>>>((float*)pool->base, pool->layer_elems,
+    pool_fill_random_kernel<<<grid, 256, 0, hpa_stream()>>>(pool->base, pool->dtype == HPA_BF16, pool->layer_elems,
                                                             pool->page_elems, pool->num_heads,
                                                             pool->page_size, block_table, bt_stride,
                                                             seed);

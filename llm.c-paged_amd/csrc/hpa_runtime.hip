@@ -242,8 +242,9 @@ int hpa_pool_create(HpaKVPool* pool, int num_layers, int num_heads, int head_siz
                     int num_pages, int dtype, int managed) {
     HPA_REQUIRE(pool, "pool is NULL");
     memset(pool, 0, sizeof(*pool));
-    HPA_REQUIRE(dtype == HPA_F32, "only fp32 pages are supported in this build");
-    HPA_REQUIRE(head_size % 4 == 0, "head_size must be a multiple of 4");
+    HPA_REQUIRE(dtype == HPA_F32 || dtype == HPA_BF16, "pool dtype must be HPA_F32 or HPA_BF16");
+    HPA_REQUIRE(head_size % 8 == 0, "head_size must be a multiple of 8");
+    HPA_REQUIRE(dtype == HPA_F32 || page_size % 8 == 0, "bf16 pages need a page size multiple of 8");
     HPA_REQUIRE(page_size > 0 && num_pages > 0 && num_layers > 0 && num_heads > 0, "bad pool shape");
     pool->num_layers = num_layers;
     pool->num_heads = num_heads;
@@ -251,7 +252,7 @@ int hpa_pool_create(HpaKVPool* pool, int num_layers, int num_heads, int head_siz
     pool->page_size = page_size;
     pool->num_pages = num_pages;
     pool->dtype = dtype;
-    pool->elem_bytes = 4;
+    pool->elem_bytes = dtype == HPA_BF16 ? 2 : 4;
     pool->page_elems = (size_t)2 * num_heads * page_size * head_size;
     pool->layer_elems = (size_t)num_pages * pool->page_elems;
     pool->bytes = (size_t)num_layers * pool->layer_elems * pool->elem_bytes;
@@ -281,6 +282,7 @@ void* hpa_pool_tile(const HpaKVPool* p, int layer, int page, int kv, int head) {
 size_t hpa_pool_k_index(const HpaKVPool* p, int layer, int page, int head, int slot, int d) {
     size_t tile = (size_t)p->page_size * p->head_size;
     size_t base = (size_t)layer * p->layer_elems + (size_t)page * p->page_elems + (size_t)head * tile;
+    if (p->dtype == HPA_BF16) return base + ((size_t)(d >> 3) * p->page_size + slot) * 8 + (d & 7);
     return base + ((size_t)(d >> 2) * p->page_size + slot) * 4 + (d & 3);
 }
 

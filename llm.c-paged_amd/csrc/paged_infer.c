@@ -599,7 +599,15 @@ static int dec_init_fused(GPT2* model, GPT2Decode* d) {
 }
 
 int gpt2_decode_init(GPT2* model, int B, int page_size, int max_ctx) {
+    return gpt2_decode_init_ex(model, B, page_size, max_ctx, HPA_F32);
+}
+
+int gpt2_decode_init_ex(GPT2* model, int B, int page_size, int max_ctx, int kv_dtype) {
     ensure_device();
+    if (kv_dtype != HPA_F32 && kv_dtype != HPA_BF16) {
+        fprintf(stderr, "[paged_infer] kv dtype must be HPA_F32 or HPA_BF16\n");
+        return 1;
+    }
     if (!model->params_memory) { fprintf(stderr, "[paged_infer] model not built\n"); return 1; }
     GPT2Config c = model->config;
     if (c.channels != c.num_heads * 64) {
@@ -645,7 +653,7 @@ int gpt2_decode_init(GPT2* model, int B, int page_size, int max_ctx) {
         free(d);
         return 1;
     }
-    if (hpa_pool_create(&d->pool, c.num_layers, c.num_heads, 64, page_size, num_pages, HPA_F32, 0)) {
+    if (hpa_pool_create(&d->pool, c.num_layers, c.num_heads, 64, page_size, num_pages, kv_dtype, 0)) {
         if (d->own_bm) destroy_block_manager(d->bm);
         free(d);
         return 1;
@@ -993,6 +1001,10 @@ int gpt2_decode_set_fused(GPT2* model, int enable) {
         hpa_graph_destroy(d->graph);
         d->graph = NULL;
     }
+    if (!enable && d->pool.dtype != HPA_F32) {
+        fprintf(stderr, "[paged_infer] the unfused path needs an fp32 KV pool\n");
+        return 1;
+    }
     d->fused = enable ? 1 : 0;
     return 0;
 }
@@ -1022,8 +1034,8 @@ int gpt2_decode_set_pipeline(GPT2* model, int enable) {
         if (!d->pipeline) return 0;
         return gpt2_decode_set_lanes(model, 1);
     }
-    if (d->B <= 16 || (d->P != 8 && d->P != 16 && d->P != 32)) {
-        fprintf(stderr, "[paged_infer] pipeline needs B > 16 and page size 8/16/32\n");
+    if (d->B <= 16 || (d->P != 8 && d->P != 16 && d->P != 32) || d->pool.dtype != HPA_F32) {
+        fprintf(stderr, "[paged_infer] pipeline needs B > 16, page size 8/16/32 and an fp32 KV pool\n");
         return 1;
     }
     if (gpt2_decode_set_lanes(model, 2) || d->nlanes != 2) return 1;
@@ -1203,7 +1215,7 @@ int gpt2_decode_time_attention(GPT2* model, int iters, double* ms_per_launch, do
         if (ms < 0) rc = 1;
         if (!rc) {
             double kv = 0.0;
-            for (int b = 0; b < B; b++) kv += 2.0 * d->h_pos[b] * C * 4.0;
+            for (int b = 0; b < B; b++) kv += 2.0 * d->h_pos[b] * C * (double)d->pool.elem_bytes;
             if (ms_per_launch) *ms_per_launch = ms / iters;
             if (bytes_per_launch) *bytes_per_launch = kv + 2.0 * B * C * 4.0;
         }
@@ -1221,10 +1233,11 @@ double gpt2_decode_step_bytes(GPT2* model, double* attn_bytes) {
     if (!d) return 0.0;
     const GPT2Config c = model->config;
     const double C = c.channels, L = c.num_layers, V = c.vocab_size, w = 4.0;
+    const double wkv = (double)d->pool.elem_bytes; /* fp32 or bf16 KV storage */
     double weights = (L * (12 * C * C + 13 * C) + V * C + 2 * C) * w;
     double kv = 0.0;
-    for (int b = 0; b < d->B; b++) kv += 2.0 * L * (d->h_pos[b] + 1) * C * w;
-    double append = 2.0 * L * d->B * C * w;
+    for (int b = 0; b < d->B; b++) kv += 2.0 * L * (d->h_pos[b] + 1) * C * wkv;
+    double append = 2.0 * L * d->B * C * wkv;
     double logits = (double)d->B * V * 4.0;
     if (attn_bytes) *attn_bytes = kv;
     return weights + d->B * C * w + kv + append + logits;

@@ -202,6 +202,7 @@ def lib():
     _sig(L, "gpt2_build_from_checkpoint", None, [v, ctypes.c_char_p])
     _sig(L, "gpt2_forward", None, [v, _I, _I, sz, sz, sz, i])
     _sig(L, "gpt2_decode_init", i, [v, i, i, i])
+    _sig(L, "gpt2_decode_init_ex", i, [v, i, i, i, i])
     _sig(L, "gpt2_decode_step", i, [v, _I, _I])
     _sig(L, "gpt2_decode_step_async", i, [v, _I])
     _sig(L, "gpt2_decode_reset", i, [v])
@@ -302,34 +303,59 @@ class DeviceBuffer:
             pass
 
 
-class Pool:
-    """HpaKVPool: the HBM page pool in the fast layout."""
+def to_bf16_bits(a):
+    """fp32 -> bf16 bit patterns, round to nearest even (hpa::f32_to_bf16)"""
+    u = np.ascontiguousarray(a, np.float32).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) >> 16
+    return u.astype(np.uint16)
 
-    def __init__(self, num_layers, num_heads, page_size, num_pages, head_size=64, managed=False):
+
+def from_bf16_bits(b):
+    return (np.asarray(b, np.uint16).astype(np.uint32) << 16).view(np.float32)
+
+
+def round_bf16(a):
+    """the fp32 value a bf16 KV pool stores for `a`"""
+    return from_bf16_bits(to_bf16_bits(a))
+
+
+HPA_F32, HPA_BF16 = 0, 1
+
+
+class Pool:
+    """HpaKVPool: the HBM page pool in the fast layout (fp32 or bf16)."""
+
+    def __init__(self, num_layers, num_heads, page_size, num_pages, head_size=64, managed=False, dtype=HPA_F32):
         self.s = HpaKVPool()
         check(lib().hpa_pool_create(ctypes.byref(self.s), num_layers, num_heads, head_size, page_size,
-                                    num_pages, 0, int(managed)), "pool_create")
+                                    num_pages, int(dtype), int(managed)), "pool_create")
 
     @property
     def ref(self):
         return ctypes.byref(self.s)
 
+    def _k_chunk(self):
+        return 8 if self.s.dtype == HPA_BF16 else 4
+
     def write_tokens(self, layer, pages, k, v):
         """host helper: k, v (ntok, C) -> logical positions 0..ntok-1 of the
-        sequence whose page list is `pages` (uploads whole pages)."""
+        sequence whose page list is `pages` (uploads whole pages; bf16 pools
+        store the round-to-nearest-even values)."""
         s = self.s
-        P, NH, HS = s.page_size, s.num_heads, s.head_size
+        P, NH, HS, ch = s.page_size, s.num_heads, s.head_size, self._k_chunk()
+        bf = s.dtype == HPA_BF16
         ntok = k.shape[0]
         for lp, page in enumerate(pages):
             t0 = lp * P
             if t0 >= ntok:
                 break
             n = min(P, ntok - t0)
-            kt = np.zeros((NH, HS // 4, P, 4), np.float32)
+            kt = np.zeros((NH, HS // ch, P, ch), np.float32)
             vt = np.zeros((NH, P, HS), np.float32)
-            kk = k[t0:t0 + n].reshape(n, NH, HS // 4, 4).transpose(1, 2, 0, 3)
-            kt[:, :, :n, :] = kk
+            kt[:, :, :n, :] = k[t0:t0 + n].reshape(n, NH, HS // ch, ch).transpose(1, 2, 0, 3)
             vt[:, :n, :] = v[t0:t0 + n].reshape(n, NH, HS).transpose(1, 0, 2)
+            if bf:
+                kt, vt = to_bf16_bits(kt), to_bf16_bits(vt)
             page_k = lib().hpa_pool_tile(self.ref, layer, int(page), 0, 0)
             page_v = lib().hpa_pool_tile(self.ref, layer, int(page), 1, 0)
             check(lib().hpa_memcpy(page_k, kt.ctypes.data, kt.nbytes), "pool write K")
@@ -337,7 +363,9 @@ class Pool:
 
     def read_tokens(self, layer, pages, ntok):
         s = self.s
-        P, NH, HS = s.page_size, s.num_heads, s.head_size
+        P, NH, HS, ch = s.page_size, s.num_heads, s.head_size, self._k_chunk()
+        bf = s.dtype == HPA_BF16
+        et = np.uint16 if bf else np.float32
         k = np.zeros((ntok, NH * HS), np.float32)
         v = np.zeros((ntok, NH * HS), np.float32)
         for lp, page in enumerate(pages):
@@ -345,12 +373,14 @@ class Pool:
             if t0 >= ntok:
                 break
             n = min(P, ntok - t0)
-            kt = np.empty((NH, HS // 4, P, 4), np.float32)
-            vt = np.empty((NH, P, HS), np.float32)
+            kt = np.empty((NH, HS // ch, P, ch), et)
+            vt = np.empty((NH, P, HS), et)
             check(lib().hpa_memcpy(kt.ctypes.data, lib().hpa_pool_tile(self.ref, layer, int(page), 0, 0),
                                    kt.nbytes), "pool read K")
             check(lib().hpa_memcpy(vt.ctypes.data, lib().hpa_pool_tile(self.ref, layer, int(page), 1, 0),
                                    vt.nbytes), "pool read V")
+            if bf:
+                kt, vt = from_bf16_bits(kt), from_bf16_bits(vt)
             k[t0:t0 + n] = kt[:, :, :n, :].transpose(2, 0, 1, 3).reshape(n, NH * HS)
             v[t0:t0 + n] = vt[:, :n, :].transpose(1, 0, 2).reshape(n, NH * HS)
         return k, v
@@ -422,9 +452,9 @@ class Model:
             check(L.gpt2_build_synthetic(self.h, self.cfg, seed), "build_synthetic")
         self.B = 0
 
-    def decode_init(self, B, page_size=16, max_ctx=None):
+    def decode_init(self, B, page_size=16, max_ctx=None, kv_dtype=HPA_F32):
         max_ctx = max_ctx or self.cfg.max_seq_len
-        check(lib().gpt2_decode_init(self.h, B, page_size, max_ctx), "gpt2_decode_init")
+        check(lib().gpt2_decode_init_ex(self.h, B, page_size, max_ctx, int(kv_dtype)), "gpt2_decode_init")
         self.B = B
 
     def set_fused(self, on):

@@ -10,6 +10,7 @@
 #include "paged_oracle.h"
 #include <math.h>
 #include <stdio.h>
+#include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -357,6 +358,7 @@ struct OraclePaged {
     int* pos;         /* [B] */
     int* free_perm;   /* page ids in hand-out order */
     int next_free;
+    int kv_bf16;      /* round appended K/V to bf16 (round to nearest even) */
     float *x, *ln, *qkv, *atty, *tmp, *res2, *fch, *fchg, *logits;
 };
 
@@ -401,6 +403,19 @@ void oracle_paged_free(OraclePaged* o) {
 }
 
 int oracle_paged_pos(const OraclePaged* o, int b) { return o->pos[b]; }
+
+void oracle_paged_set_kv_bf16(OraclePaged* o, int on) { o->kv_bf16 = on ? 1 : 0; }
+
+/* fp32 -> the value a bf16 store keeps: round to nearest even on the upper
+ * 16 bits (finite inputs), returned as fp32 */
+float oracle_round_bf16(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    u &= 0xffff0000u;
+    memcpy(&f, &u, 4);
+    return f;
+}
 
 static float* page_ptr(OraclePaged* o, float* pool, int layer, int page) {
     return pool + ((size_t)layer * o->num_pages + page) * o->P * o->cfg.channels;
@@ -472,6 +487,11 @@ int oracle_paged_step(OraclePaged* o, const int* tokens, float* logits, int* nex
             float* v = page_ptr(o, o->vpool, l, page) + (size_t)(p % o->P) * C;
             memcpy(k, o->qkv + (size_t)b * 3 * C + C, C * 4);
             memcpy(v, o->qkv + (size_t)b * 3 * C + 2 * C, C * 4);
+            if (o->kv_bf16)
+                for (int i = 0; i < C; i++) {
+                    k[i] = oracle_round_bf16(k[i]);
+                    v[i] = oracle_round_bf16(v[i]);
+                }
         }
         /* attention_paged arithmetic (paged_infer.c:163-240), keys 0..pos[b] */
         #pragma omp parallel for collapse(2) schedule(dynamic)

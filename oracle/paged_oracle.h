@@ -97,6 +97,10 @@ int  oracle_paged_step(OraclePaged* o, const int* tokens, float* logits, int* ne
  * (the bounded CPU-baseline sample; bench.py only). */
 void oracle_paged_fill_random(OraclePaged* o, int ctx, unsigned long long seed);
 int  oracle_paged_pos(const OraclePaged* o, int b);
+/* bf16 KV pool semantics (BASELINE config 5): appended K/V are rounded to
+ * bf16 (nearest even) and read back exactly; all arithmetic stays fp32 */
+void oracle_paged_set_kv_bf16(OraclePaged* o, int on);
+float oracle_round_bf16(float f);
 void oracle_paged_free(OraclePaged* o);
 
 #ifdef __cplusplus

@@ -15,14 +15,14 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 
-def _run_case(hip, P, ctxs, NH, waves=4, seed=0, q_scale=2.0, kv=None, chunks=0):
+def _run_case(hip, P, ctxs, NH, waves=4, seed=0, q_scale=2.0, kv=None, chunks=0, bf16=False):
     rng = np.random.default_rng(seed)
     L = hip.lib()
     C = NH * 64
     B = len(ctxs)
     maxp = max((c + P - 1) // P for c in ctxs)
     num_pages = B * maxp + 3
-    pool = hip.Pool(1, NH, P, num_pages)
+    pool = hip.Pool(1, NH, P, num_pages, dtype=hip.HPA_BF16 if bf16 else hip.HPA_F32)
     perm = rng.permutation(num_pages).astype(np.int32)
     bt = np.full((B, maxp), -1, np.int32)
     ks, vs = [], []
@@ -36,6 +36,8 @@ def _run_case(hip, P, ctxs, NH, waves=4, seed=0, q_scale=2.0, kv=None, chunks=0)
             v = rng.uniform(-1, 1, (ctx, C)).astype(np.float32)
         else:
             k, v = kv(ctx, C)
+        if bf16:  # the values a bf16 pool stores; the oracle sees exactly these
+            k, v = hip.round_bf16(k), hip.round_bf16(v)
         pool.write_tokens(0, bt[b, :n], k, v)
         ks.append(k)
         vs.append(v)
@@ -170,3 +172,23 @@ def test_chunked_attention_all_scores_below_reference_floor(hip):
 
     out, ref = _run_case(hip, 16, [5, 80, 300], NH=1, seed=1, kv=kv, q_scale=1e-6, chunks=4)
     assert np.abs(out - ref).max() <= TOL
+
+
+@pytest.mark.parametrize("P", [8, 16, 32])
+@pytest.mark.parametrize("waves", [1, 4, 8])
+def test_bf16_pool_attention(hip, P, waves):
+    """bf16 KV storage (BASELINE config 5), fp32 arithmetic: exact same
+    K/V values on both sides, so the fp32 1e-4 bar holds"""
+    ctxs = [1, 2, 7, 63, 64, 65, 200, 257, 1024]
+    out, ref = _run_case(hip, P, ctxs, NH=3, seed=P + waves, waves=waves, bf16=True)
+    assert np.abs(out - ref).max() <= TOL
+
+
+def test_bf16_pool_roundtrip(hip):
+    rng = np.random.default_rng(1)
+    pool = hip.Pool(2, 2, 8, 6, dtype=hip.HPA_BF16)
+    k = rng.standard_normal((13, 128)).astype(np.float32)
+    v = rng.standard_normal((13, 128)).astype(np.float32)
+    pool.write_tokens(1, [4, 1], k, v)
+    k2, v2 = pool.read_tokens(1, [4, 1], 13)
+    assert np.array_equal(k2, hip.round_bf16(k)) and np.array_equal(v2, hip.round_bf16(v))

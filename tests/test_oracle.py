@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 import oracle_ctypes as oc
+import synth
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -126,3 +127,33 @@ def test_reference_all_negative_scores_give_zero_output():
     q = np.full(C, -1000.0, np.float32)
     out = oc.attention_decode(q, kp, vp, ctx, NH)
     assert np.all(out == 0.0)
+
+
+def test_oracle_bf16_rounding_matches_numpy_rne():
+    """oracle_round_bf16 == round-to-nearest-even on the upper 16 bits (the
+    GPU pool's hpa::f32_to_bf16), ties to even included"""
+    L = oc.lib()
+    xs = np.array([1.0, 1.00390625, 1.01171875, -2.5e-3, 3.14159, 65504.0, 1e-30, -0.0], np.float32)
+    u = xs.view(np.uint32).astype(np.uint64)
+    want = (((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16).astype(np.uint32).view(np.float32)
+    got = np.array([L.oracle_round_bf16(float(x)) for x in xs], np.float32)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_oracle_bf16_kv_decode_is_close_to_fp32():
+    """bf16 KV storage perturbs the decode by bf16 rounding only"""
+    cfgd = dict(maxT=64, V=300, L=2, NH=2, C=128)
+    params = synth.params(cfgd, seed=2)
+    c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
+    a = oc.PagedDecoder(params, c, 3, 8, 64, page_seed=1)
+    b = oc.PagedDecoder(params, c, 3, 8, 64, page_seed=1, kv_bf16=True)
+    rng = np.random.default_rng(0)
+    worst = 0.0
+    for _ in range(10):
+        tok = rng.integers(0, 300, 3).astype(np.int32)
+        _, la = a.step(tok)
+        _, lb = b.step(tok)
+        worst = max(worst, float(np.abs(la - lb).max()))
+    a.close()
+    b.close()
+    assert 0.0 < worst < 5e-2
