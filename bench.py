@@ -37,21 +37,23 @@ METRIC = "decode tokens/sec GPT-2 124M paged-attn, B=64 T=1024, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def pmc_traffic(kernel_prefix, batch_per_gpu, ctx, page_size):
-    """HBM bytes per launch of the dominant kernel from the committed PMC
-    summary (tools/pmc_traffic.sh, profiles/r1/pmc_traffic.json) when it was
-    taken on this workload; None otherwise"""
-    path = os.path.join(REPO, "profiles", "r1", "pmc_traffic.json")
-    try:
-        d = json.load(open(path))
-    except (OSError, ValueError):
-        return None, None
-    c = d.get("config") or {}
-    if (c.get("batch_per_gpu"), c.get("seq_len"), c.get("page_size")) != (batch_per_gpu, ctx, page_size):
-        return None, None
-    for name, k in d["kernels"].items():
-        if name.startswith(kernel_prefix):
-            return k["hbm_bytes"], f"profiles/r1/pmc_traffic.json: {name}, {k['launches']} launches"
+def pmc_traffic(kernel_prefix, batch_per_gpu, ctx, page_size, dtype):
+    """HBM bytes per launch of the dominant kernel from a committed PMC
+    summary (tools/pmc_traffic.sh -> profiles/r1/pmc_traffic*.json) taken on
+    this workload; (None, None) when there is none"""
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r1", "pmc_traffic*.json"))):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        c = d.get("config") or {}
+        if (c.get("batch_per_gpu"), c.get("seq_len"), c.get("page_size"), c.get("dtype", "fp32")) != \
+                (batch_per_gpu, ctx, page_size, dtype):
+            continue
+        for name, k in d["kernels"].items():
+            if name.startswith(kernel_prefix):
+                return k["hbm_bytes"], f"profiles/r1/{os.path.basename(path)}: {name}, {k['launches']} launches"
     return None, None
 
 
@@ -65,6 +67,8 @@ def parse():
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--ctx", type=int, default=1024)
     ap.add_argument("--page-size", type=int, default=16)
+    ap.add_argument("--kv-dtype", default="f32", choices=["f32", "bf16"],
+                    help="KV pool storage (bf16: BASELINE config 5; arithmetic stays fp32)")
     ap.add_argument("--model", default="124M", choices=["124M", "XL"])
     ap.add_argument("--prefill", default="synthetic", choices=["synthetic", "decode"])
     ap.add_argument("--gather", default="logits", choices=["ids", "logits", "none"],
@@ -84,7 +88,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(cfgd, B, P, ctx, budget_s):
+def cpu_baseline(cfgd, B, P, ctx, budget_s, kv_bf16=False):
     """The oracle's OpenMP C restatement of the same paged decode, timed on the
     host cores on a bounded sample (rank 0, N=1).  Test infrastructure only."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -94,8 +98,8 @@ def cpu_baseline(cfgd, B, P, ctx, budget_s):
     os.environ["OMP_NUM_THREADS"] = str(threads)
     params = pagedattn.synthetic_params(cfgd, seed=1337)
     c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
-    dec = oc.PagedDecoder(params, c, B, P, cfgd["maxT"], page_seed=3, fast=True)
-    max_steps = 96
+    dec = oc.PagedDecoder(params, c, B, P, cfgd["maxT"], page_seed=3, fast=True, kv_bf16=kv_bf16)
+    max_steps = min(512, ctx // 2)  # the budget normally ends the sample first
     start_ctx = ctx - max_steps
     dec.fill_random(start_ctx, seed=5)
     rng = np.random.default_rng(0)
@@ -118,9 +122,9 @@ def cpu_baseline(cfgd, B, P, ctx, budget_s):
     except OSError:
         pass
     return {"value": B * steps / el, "unit": "tokens/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/liboracle_fast.so (-O3 -Ofast OpenMP C restatement), GPT-2 124M fp32, "
-                      f"B={B}, page {P}, {steps} decode steps at ctx {start_ctx}..{start_ctx + steps} "
-                      f"after a synthetic K/V fill, {el:.1f} s; cpu: {cpu_model}"}
+            "sample": f"oracle/liboracle_fast.so (-O3 -Ofast OpenMP C restatement), GPT-2 124M fp32"
+                      f"{' (bf16 KV)' if kv_bf16 else ''}, B={B}, page {P}, {steps} decode steps at ctx "
+                      f"{start_ctx}..{start_ctx + steps} after a synthetic K/V fill, {el:.1f} s; cpu: {cpu_model}"}
 
 
 def main():
@@ -151,6 +155,9 @@ def main():
     pagedattn.check(L.hpa_set_attention_waves(args.attn_waves), "attention waves")
 
     cfgd = dict(pagedattn.GPT2_124M if args.model == "124M" else pagedattn.GPT2_XL)
+    if args.ctx > cfgd["maxT"]:  # config 5: ctx 2048 -> 2048 rows of (synthetic) wpe, SURVEY.md 8d
+        cfgd["maxT"] = args.ctx
+    kv_bf16 = args.kv_dtype == "bf16"
     B, lo, hi = shard.batch_layout(args.batch, world, rank, args.scaling)
     B_local = hi - lo
     counts = [shard.batch_layout(args.batch, world, r, args.scaling) for r in range(world)]
@@ -162,7 +169,7 @@ def main():
     start = ctx - window  # positions of the first decoded token
 
     model = pagedattn.Model(cfgd, seed=1337)
-    model.decode_init(B_local, P, ctx)
+    model.decode_init(B_local, P, ctx, kv_dtype=pagedattn.HPA_BF16 if kv_bf16 else pagedattn.HPA_F32)
     model.set_fused(not args.unfused)
     if not args.unfused:
         model.set_lanes(args.lanes)
@@ -243,14 +250,21 @@ def main():
         want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
         if want_cpu and args.model == "124M":
             try:
-                cpu = cpu_baseline(cfgd, B, P, ctx, args.cpu_seconds)
+                # bounded sample: the oracle keeps an fp32 pool of B*ctx*C*L*2 floats, so
+                # beyond config 2's B*ctx the sample takes a subset of the sequences
+                cpu_B = B_local if B_local * ctx <= 65536 else max(1, 16384 // ctx)
+                cpu = cpu_baseline(cfgd, cpu_B, P, ctx, args.cpu_seconds, kv_bf16)
+                if cpu_B != B_local:
+                    cpu["sample"] += f" (a {cpu_B}-sequence subset of the {B_local}-sequence batch)"
             except Exception as e:  # reported, never fatal for the GPU number
                 cpu = {"value": None, "error": repr(e)}
         name, cus, mem = pagedattn.device_info()
         roof = None
         if attn:
-            traffic, tsrc = pmc_traffic("paged_attn_decode_f32", B_local, ctx, P)
-            roof = {"bound": "hbm", "kernel": "paged_attn_decode_f32", "achieved": round(attn["achieved"], 1),
+            traffic, tsrc = pmc_traffic("paged_attn_decode_f32", B_local, ctx, P,
+                                        "fp32 (bf16 KV storage)" if kv_bf16 else "fp32")
+            roof = {"bound": "hbm", "kernel": "paged_attn_decode_f32" + ("<bf16 KV>" if kv_bf16 else ""),
+                    "achieved": round(attn["achieved"], 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(attn["achieved"] / HBM_PEAK_GBS, 4),
                     "traffic": None if traffic is None else int(traffic),
                     "traffic_source": tsrc, "avg_launch_ms": round(attn["avg_ms"], 5),
@@ -267,12 +281,12 @@ def main():
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "fp32 (bf16 KV storage)" if kv_bf16 else "fp32",
             "data": "synthetic (seeded random GPT-2 124M weights and tokens; KV prefill: "
                     + ("synthetic U(-1,1)" if args.prefill == "synthetic" else "decode steps") + ")",
             "config": {"workload": f"GPT-2 {args.model} fp32 paged decode, batch={B_local} per GPU x {world} "
-                                   f"(B={B}), ctx {ctx}, page_size={P} (BASELINE.json "
-                                   + ("configs[2])" if args.model == "XL" else
+                                   f"(B={B}), ctx {ctx}, page_size={P}{', bf16 KV' if kv_bf16 else ''} (BASELINE.json "
+                                   + ("configs[4])" if kv_bf16 else "configs[2])" if args.model == "XL" else
                                       "configs[1])" if world == 1 else "configs[3]: per-seq sharded pool)"),
                        "global_batch": B, "batch_per_gpu": B_local, "seq_len": ctx, "page_size": P,
                        "decode_positions": f"{start}..{start + args.warmup + args.steps - 1}",

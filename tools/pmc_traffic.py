@@ -58,8 +58,10 @@ cfg = None
 try:  # the bench line printed by the profiled run names the workload
     for line in open(os.path.join(out, "FETCH_SIZE.log")):
         if line.startswith("{"):
-            c = json.loads(line)["config"]
+            j = json.loads(line)
+            c = j["config"]
             cfg = {k: c.get(k) for k in ("workload", "batch_per_gpu", "seq_len", "page_size", "gemm_path")}
+            cfg["dtype"] = j.get("dtype", "fp32")
 except (OSError, ValueError, KeyError):
     pass
 json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, --kernel-trace, eager "
