@@ -14,7 +14,9 @@ token at its absolute position, all 12 layers (LN, QKV + KV append into the
 HBM page pool, paged attention over 0..pos through the block table,
 projections, MLP, residuals), final LN, logits (B x 50257), greedy argmax.
 The KV cache is prefilled to ctx - (warmup + steps) positions with synthetic
-K/V (default; --prefill decode runs real decode steps instead); the timed
+K/V (default; --prefill real runs the one-pass prefill -- B*T-row GEMMs and
+the causal multi-query attention on MFMA -- and reports its throughput too;
+--prefill decode runs token-by-token decode steps instead); the timed
 steps then decode at positions up to ctx - 1.  Weights are seeded synthetic
 GPT-2 124M (no checkpoints offline).
 
@@ -70,7 +72,8 @@ def parse():
     ap.add_argument("--kv-dtype", default="f32", choices=["f32", "bf16"],
                     help="KV pool storage (bf16: BASELINE config 5; arithmetic stays fp32)")
     ap.add_argument("--model", default="124M", choices=["124M", "XL"])
-    ap.add_argument("--prefill", default="synthetic", choices=["synthetic", "decode"])
+    ap.add_argument("--prefill", default="synthetic", choices=["synthetic", "real", "decode"])
+    ap.add_argument("--prefill-chunk", type=int, default=256, help="tokens per sequence per prefill call")
     ap.add_argument("--gather", default="logits", choices=["ids", "logits", "none"],
                     help="end-of-step gather to rank 0 (N>1)")
     ap.add_argument("--no-graph", action="store_true")
@@ -180,8 +183,22 @@ def main():
         model.gemm_config(ints(args.gemm_waves), ints(args.gemm_rows), ints(args.gemm_cols))
     model.reserve(ctx)
     rng = np.random.default_rng(1000 + rank)
+    prefill_stats = None
     if args.prefill == "synthetic":
         model.fill_random(start, seed=77 + rank)
+    elif args.prefill == "real":
+        toks = rng.integers(0, cfgd["V"], (B_local, start)).astype(np.int32)
+        model.prefill(toks[:, :min(start, 16)])  # warm-up (kernels, workspace)
+        model.set_positions(np.zeros(B_local, np.int32))
+        pagedattn.check(L.hpa_synchronize(), "sync")
+        t0 = time.perf_counter()
+        for c0 in range(0, start, args.prefill_chunk):
+            model.prefill(toks[:, c0:c0 + args.prefill_chunk])
+        pagedattn.check(L.hpa_synchronize(), "sync")
+        el = time.perf_counter() - t0
+        prefill_stats = {"tokens": B_local * start, "seconds": round(el, 4),
+                         "tokens_per_s": round(B_local * start / el, 1), "chunk": args.prefill_chunk,
+                         "note": "one-pass prefill of positions 0..start-1, rank 0, not part of value"}
     else:
         for p in range(start):
             model.step(rng.integers(0, cfgd["V"], B_local).astype(np.int32), want_next=False)
@@ -283,7 +300,8 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32 (bf16 KV storage)" if kv_bf16 else "fp32",
             "data": "synthetic (seeded random GPT-2 124M weights and tokens; KV prefill: "
-                    + ("synthetic U(-1,1)" if args.prefill == "synthetic" else "decode steps") + ")",
+                    + {"synthetic": "synthetic U(-1,1)", "real": "one-pass prefill of random tokens",
+                       "decode": "decode steps"}[args.prefill] + ")",
             "config": {"workload": f"GPT-2 {args.model} fp32 paged decode, batch={B_local} per GPU x {world} "
                                    f"(B={B}), ctx {ctx}, page_size={P}{', bf16 KV' if kv_bf16 else ''} (BASELINE.json "
                                    + ("configs[4])" if kv_bf16 else "configs[2])" if args.model == "XL" else
@@ -304,6 +322,8 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if prefill_stats:
+            result["prefill"] = prefill_stats
         print(json.dumps(result), flush=True)
     model.close()
     if world > 1:

@@ -212,6 +212,8 @@ typedef struct {
     int col_tiles;        /* 16-column tiles per workgroup: 1; 2 (waves 4/8, row_blocks
                              2/4); 4 (waves 4, row_blocks 4); 0 = by shape.  A hint:
                              where M's row blocks or the waves cannot carry it, 1 */
+    const int* row_seq;   /* QKV: block-table row of each GEMM row (NULL = the row
+                             itself; prefill rows b*T+t -> b) */
 } HpaFusedGemm;
 int hpa_gemm_fused(const HpaFusedGemm* g);
 /* the launch shape hpa_gemm_fused picks when waves / row_blocks / col_tiles
@@ -228,6 +230,20 @@ int hpa_argmax_final(const float* part, int ntiles, int Mp, int B, int* next, in
 int hpa_paged_attention_decode_frag(const float* q, const HpaKVPool* pool, int layer,
                                     const int* block_table, int bt_stride, const int* pos,
                                     float* out_frag, int B);
+
+/* ---------------- prefill (multi-query) ----------------
+ * attention_paged (paged_infer.c:163-240) for T query rows per sequence at
+ * absolute positions start[b] + t, causal over the sequence's pages: q
+ * [B*T][C] row-major (row = b*T + t), out frag layout [ceil16(B*T)][C].
+ * S = QK^T and O += PV on v_mfma_f32_16x16x4_f32 (dense here), online
+ * softmax from the reference's -10000 floor.  The K/V of every query
+ * position must already be in the pages (the prefill QKV GEMM appends them). */
+int hpa_paged_attention_prefill(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
+                                int bt_stride, const int* start, int B, int T, float* out_frag);
+/* rows[i] of a frag-layout [src_Mp][C] matrix and of its LN statistics
+ * ([C/16][src_Mp][2]) -> row i of dst / dst_stats (n rows; prefill -> logits) */
+int hpa_gather_rows_frag(const float* src, const float* src_stats, int src_Mp, const int* rows, int n,
+                         float* dst, float* dst_stats, int dst_Mp, int C);
 
 /* ---------------- pipelined decode: attention chunk + GEMM in ONE launch ----------------
  * Chunk `chunk` of `nchunks` of the decode attention of B sequences (each

@@ -138,6 +138,12 @@ int  gpt2_decode_init_ex(GPT2* model, int B, int page_size, int max_ctx, int kv_
  * tokens == NULL feeds back the previous step's greedy ids (device-resident).
  * next_tokens (host, may be NULL) receives argmax(logits[b]). */
 int  gpt2_decode_step(GPT2* model, const int* tokens, int* next_tokens);
+/* prefill: tokens[b*T + t] (host) at positions pos[b] + t for every sequence,
+ * all T tokens in one pass (B*T-row GEMMs, causal multi-query paged
+ * attention on MFMA); afterwards logits / next ids are those of each
+ * sequence's last token and pos[b] += T, so decode continues with
+ * gpt2_decode_step(model, NULL, ...).  Fused one-lane engine. */
+int  gpt2_decode_prefill(GPT2* model, const int* tokens, int T, int* next_tokens);
 /* the same, but enqueue only (no host sync; next ids stay on device) */
 int  gpt2_decode_step_async(GPT2* model, const int* tokens);
 /* free every sequence's pages and rewind positions to 0 */

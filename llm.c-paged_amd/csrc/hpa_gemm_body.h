@@ -32,6 +32,7 @@ struct FG {
     const int* bt;
     int bt_stride;
     const int* pos;
+    const int* row_seq;  // QKV: block-table row per GEMM row (NULL: the row)
     int gx, gy;  // column-tile groups x row groups of the launch
 };
 
@@ -134,7 +135,8 @@ struct Epi {
                             const int c = col - (kv ? 2 * C : C);
                             const int hh = c >> 6, d = c & 63;
                             const int ps = p.pos[row];
-                            const int page = p.bt[(size_t)row * p.bt_stride + ps / p.P];
+                            const int seq = p.row_seq ? p.row_seq[row] : row;
+                            const int page = p.bt[(size_t)seq * p.bt_stride + ps / p.P];
                             const int slot = ps % p.P;
                             const size_t toff = (size_t)page * p.page_elems + ((size_t)kv * p.NH + hh) * p.P * 64;
                             if (p.kv_bf16) {  // bf16 pool: K [chunk of 8][slot][8], V [slot][64], RNE
@@ -532,6 +534,7 @@ static inline int fused_prepare(const HpaFusedGemm* g, FG* p) {
     p->bt = g->block_table;
     p->bt_stride = g->bt_stride;
     p->pos = g->pos;
+    p->row_seq = g->row_seq;
     if (g->epilogue == HPA_FEPI_QKV) {
         const HpaKVPool* pool = g->pool;
         HPA_REQUIRE(pool && pool->base && (pool->dtype == HPA_F32 || pool->dtype == HPA_BF16) &&

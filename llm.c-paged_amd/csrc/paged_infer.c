@@ -450,6 +450,10 @@ struct GPT2Decode {
     DecLane lanes[DEC_MAX_LANES];
     int nlanes;
     int pipeline;     /* 1: two lanes, attention chunks beside the other lane's GEMMs */
+    /* prefill workspace (gpt2_decode_prefill), rows R = B*T, grown on demand */
+    int pf_cap;       /* row capacity */
+    float *pf_res, *pf_res2, *pf_att, *pf_fch, *pf_st1, *pf_st2, *pf_q;
+    int *pf_tok, *pf_pos, *pf_seq, *pf_start, *pf_last, *h_pf;
     void* ev_fork;
     int use_graph;
     void* graph;
@@ -530,8 +534,19 @@ static int dec_lanes_alloc(GPT2Decode* d, int n, int C, int V, int NH) {
     return hpa_synchronize();
 }
 
+static void dec_prefill_free(GPT2Decode* d) {
+    hpa_free(d->pf_res); hpa_free(d->pf_res2); hpa_free(d->pf_att); hpa_free(d->pf_fch);
+    hpa_free(d->pf_st1); hpa_free(d->pf_st2); hpa_free(d->pf_q);
+    hpa_free(d->pf_tok); hpa_free(d->pf_pos); hpa_free(d->pf_seq); hpa_free(d->pf_start); hpa_free(d->pf_last);
+    free(d->h_pf);
+    d->pf_res = d->pf_res2 = d->pf_att = d->pf_fch = d->pf_st1 = d->pf_st2 = d->pf_q = NULL;
+    d->pf_tok = d->pf_pos = d->pf_seq = d->pf_start = d->pf_last = d->h_pf = NULL;
+    d->pf_cap = 0;
+}
+
 static void dec_free(GPT2Decode* d) {
     if (!d) return;
+    dec_prefill_free(d);
     dec_prof_free(d, d->pool.num_layers);
     if (d->graph) hpa_graph_destroy(d->graph);
     hpa_pool_destroy(&d->pool);
@@ -1087,6 +1102,162 @@ static int dec_enqueue(GPT2* model, const int* tokens) {
     }
     for (int b = 0; b < d->B; b++) d->h_pos[b]++;
     return 0;
+}
+
+/* ---- prefill: T tokens of every sequence in one pass ----
+ * All B*T rows go through the fused GEMMs (row r = b*T + t at absolute
+ * position pos[b] + t; the QKV epilogue appends each row's K/V through its
+ * sequence's block table), the causal multi-query attention runs on MFMA
+ * (hpa_paged_attention_prefill), and the last row of every sequence is
+ * gathered for the logits and the greedy pick.  Equivalent to T decode steps
+ * with the same tokens (tested against the oracle's token-by-token decode). */
+static int dec_prefill_reserve(GPT2* model, int R) {
+    GPT2Decode* d = model->decode;
+    if (R <= d->pf_cap) return 0;
+    dec_prefill_free(d);
+    const size_t C = model->config.channels, ct = C / 16;
+    const size_t Rp = (size_t)(R + 15) / 16 * 16;
+    d->pf_res = (float*)hpa_malloc(Rp * C * 4);
+    d->pf_res2 = (float*)hpa_malloc(Rp * C * 4);
+    d->pf_att = (float*)hpa_malloc(Rp * C * 4);
+    d->pf_fch = (float*)hpa_malloc(Rp * 4 * C * 4);
+    d->pf_st1 = (float*)hpa_malloc(ct * Rp * 2 * 4);
+    d->pf_st2 = (float*)hpa_malloc(ct * Rp * 2 * 4);
+    d->pf_q = (float*)hpa_malloc(Rp * C * 4);
+    d->pf_tok = (int*)hpa_malloc(Rp * sizeof(int));
+    d->pf_pos = (int*)hpa_malloc(Rp * sizeof(int));
+    d->pf_seq = (int*)hpa_malloc(Rp * sizeof(int));
+    d->pf_start = (int*)hpa_malloc(d->B * sizeof(int));
+    d->pf_last = (int*)hpa_malloc(d->B * sizeof(int));
+    d->h_pf = (int*)malloc((3 * Rp + 2 * d->B) * sizeof(int));
+    if (!d->pf_res || !d->pf_res2 || !d->pf_att || !d->pf_fch || !d->pf_st1 || !d->pf_st2 || !d->pf_q ||
+        !d->pf_tok || !d->pf_pos || !d->pf_seq || !d->pf_start || !d->pf_last || !d->h_pf) {
+        dec_prefill_free(d);
+        return 1;
+    }
+    /* padded rows stay zero */
+    if (hpa_memset_async(d->pf_res, 0, Rp * C * 4) || hpa_memset_async(d->pf_res2, 0, Rp * C * 4) ||
+        hpa_memset_async(d->pf_att, 0, Rp * C * 4) || hpa_memset_async(d->pf_fch, 0, Rp * 4 * C * 4))
+        return 1;
+    d->pf_cap = R;
+    return 0;
+}
+
+static int prefill_gemm(GPT2* model, int l, int which, int R) {
+    GPT2Decode* d = model->decode;
+    const GPT2Config c = model->config;
+    const int C = c.channels, ct = C / 16;
+    const ParameterTensors* w = &model->params;
+    const size_t lc = (size_t)l * C;
+    const size_t e_layer = d->wpack_off[3] + hpa_frag_elems(C, 4 * C);
+    const float* wl = d->d_wpack + e_layer * l;
+    HpaFusedGemm g;
+    memset(&g, 0, sizeof(g));
+    g.M = R;
+    /* B*T rows: reuse every activation fragment over 2 weight tiles and every
+     * weight fragment over 4 row blocks (MFMA-bound at this M) */
+    g.waves = 8;
+    g.row_blocks = 4;
+    g.col_tiles = 2;
+    g.pool = &d->pool;
+    g.layer = l;
+    g.block_table = d->d_bt;
+    g.bt_stride = d->bt_stride;
+    g.pos = d->pf_pos;
+    g.row_seq = d->pf_seq;
+    switch (which) {
+        case G_QKV:
+            g.epilogue = HPA_FEPI_QKV; g.x = d->pf_res; g.K = C; g.ln_stats = d->pf_st1;
+            g.ln_ntiles = l == 0 ? 1 : ct; g.ln_w = w->ln1w + lc; g.ln_b = w->ln1b + lc;
+            g.w = wl + d->wpack_off[0]; g.N = 3 * C; g.bias = w->qkvb + 3 * lc; g.out = d->pf_q;
+            break;
+        case G_ATTPROJ:
+            g.epilogue = HPA_FEPI_RESID; g.x = d->pf_att; g.K = C; g.w = wl + d->wpack_off[1]; g.N = C;
+            g.bias = w->attprojb + lc; g.out = d->pf_res2; g.res_in = d->pf_res; g.stats_out = d->pf_st2;
+            break;
+        case G_FC:
+            g.epilogue = HPA_FEPI_GELU; g.x = d->pf_res2; g.K = C; g.ln_stats = d->pf_st2; g.ln_ntiles = ct;
+            g.ln_w = w->ln2w + lc; g.ln_b = w->ln2b + lc; g.w = wl + d->wpack_off[2]; g.N = 4 * C;
+            g.bias = w->fcb + 4 * lc; g.out = d->pf_fch;
+            break;
+        default: /* G_FCPROJ */
+            g.epilogue = HPA_FEPI_RESID; g.x = d->pf_fch; g.K = 4 * C; g.w = wl + d->wpack_off[3]; g.N = C;
+            g.bias = w->fcprojb + lc; g.out = d->pf_res; g.res_in = d->pf_res2; g.stats_out = d->pf_st1;
+            break;
+    }
+    return hpa_gemm_fused(&g);
+}
+
+int gpt2_decode_prefill(GPT2* model, const int* tokens, int T, int* next_tokens) {
+    GPT2Decode* d = model->decode;
+    if (!d) { fprintf(stderr, "[paged_infer] gpt2_decode_init first\n"); return 1; }
+    const GPT2Config c = model->config;
+    const int B = d->B, C = c.channels, L = c.num_layers;
+    if (T <= 0) return 1;
+    if (!d->fused || d->nlanes != 1 || d->pipeline) {
+        fprintf(stderr, "[paged_infer] prefill runs on the fused one-lane engine\n");
+        return 1;
+    }
+    for (int i = 0; i < B * T; i++)
+        if (tokens[i] < 0 || tokens[i] >= c.vocab_size) {
+            fprintf(stderr, "[paged_infer] token out of range\n"); /* :591-596 */
+            return 1;
+        }
+    /* pages for positions pos[b] .. pos[b]+T-1 */
+    for (int b = 0; b < B; b++) {
+        if (d->h_pos[b] + T > d->max_ctx) {
+            fprintf(stderr, "[paged_infer] prefill of %d tokens overflows sequence %d\n", T, b);
+            return 1;
+        }
+        const int need = (d->h_pos[b] + T - 1) / d->P + 1;
+        while (d->bm->prompt_block_count[b] < need)
+            if (!request_block(d->bm, b)) return 1;
+    }
+    if (dec_sync_block_table(d)) return 1;
+    const int R = B * T;
+    if (dec_prefill_reserve(model, R)) return 1;
+    /* row tables: token, absolute position, sequence; per-sequence start and last row */
+    if (hpa_synchronize()) return 1; /* h_pf staging reuse */
+    const int Rp = (R + 15) / 16 * 16;
+    int *ht = d->h_pf, *hp = ht + Rp, *hs = hp + Rp, *hst = hs + Rp, *hl = hst + B;
+    for (int b = 0; b < B; b++) {
+        for (int t = 0; t < T; t++) {
+            ht[b * T + t] = tokens[b * T + t];
+            hp[b * T + t] = d->h_pos[b] + t;
+            hs[b * T + t] = b;
+        }
+        hst[b] = d->h_pos[b];
+        hl[b] = b * T + T - 1;
+    }
+    if (hpa_memcpy(d->pf_tok, ht, R * sizeof(int)) || hpa_memcpy(d->pf_pos, hp, R * sizeof(int)) ||
+        hpa_memcpy(d->pf_seq, hs, R * sizeof(int)) || hpa_memcpy(d->pf_start, hst, B * sizeof(int)) ||
+        hpa_memcpy(d->pf_last, hl, B * sizeof(int)))
+        return 1;
+    const ParameterTensors* w = &model->params;
+    int rc = hpa_embed_frag(d->pf_tok, d->pf_pos, w->wte, w->wpe, d->pf_res, d->pf_st1, R, C);
+    for (int l = 0; l < L && !rc; l++) {
+        rc |= prefill_gemm(model, l, G_QKV, R);
+        rc |= hpa_paged_attention_prefill(d->pf_q, &d->pool, l, d->d_bt, d->bt_stride, d->pf_start, B, T,
+                                          d->pf_att);
+        rc |= prefill_gemm(model, l, G_ATTPROJ, R);
+        rc |= prefill_gemm(model, l, G_FC, R);
+        rc |= prefill_gemm(model, l, G_FCPROJ, R);
+    }
+    /* last row of every sequence -> the one-lane engine's buffers, logits, greedy;
+     * argmax_final advances pos by one: set pos = start + T - 1 first */
+    DecLane* ln = &d->lanes[0];
+    for (int b = 0; b < B; b++) hst[b] = d->h_pos[b] + T - 1;
+    rc |= hpa_memcpy(d->d_pos, hst, B * sizeof(int));
+    rc |= hpa_gather_rows_frag(d->pf_res, d->pf_st1, Rp, d->pf_last, B, ln->res, ln->st1, ln->Mp, C);
+    rc |= lane_gemm_run(model, 0, 0, G_LOGITS);
+    rc |= lane_argmax(model, 0);
+    if (rc) return 1;
+    for (int b = 0; b < B; b++) d->h_pos[b] += T;
+    if (next_tokens) {
+        if (hpa_memcpy(d->h_stage + B, d->d_next, B * sizeof(int))) return 1;
+        memcpy(next_tokens, d->h_stage + B, B * sizeof(int));
+    }
+    return hpa_synchronize();
 }
 
 int gpt2_decode_step_async(GPT2* model, const int* tokens) { return dec_enqueue(model, tokens); }

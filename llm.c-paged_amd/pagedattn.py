@@ -64,7 +64,8 @@ class HpaFusedGemm(ctypes.Structure):
                 ("res_in", _V), ("stats_out", _V), ("part_out", _V),
                 ("pool", ctypes.POINTER(HpaKVPool)), ("layer", ctypes.c_int), ("block_table", _V),
                 ("bt_stride", ctypes.c_int), ("pos", _V), ("waves", ctypes.c_int),
-                ("row_blocks", ctypes.c_int), ("variant", ctypes.c_int), ("col_tiles", ctypes.c_int)]
+                ("row_blocks", ctypes.c_int), ("variant", ctypes.c_int), ("col_tiles", ctypes.c_int),
+                ("row_seq", _V)]
 
 
 HPA_FEPI_QKV, HPA_FEPI_RESID, HPA_FEPI_GELU, HPA_FEPI_LOGITS = 0, 1, 2, 3
@@ -203,6 +204,9 @@ def lib():
     _sig(L, "gpt2_forward", None, [v, _I, _I, sz, sz, sz, i])
     _sig(L, "gpt2_decode_init", i, [v, i, i, i])
     _sig(L, "gpt2_decode_init_ex", i, [v, i, i, i, i])
+    _sig(L, "gpt2_decode_prefill", i, [v, _I, i, _I])
+    _sig(L, "hpa_paged_attention_prefill", i, [_F, v, i, _I, i, _I, i, i, _F])
+    _sig(L, "hpa_gather_rows_frag", i, [_F, _F, i, _I, i, _F, _F, i, i])
     _sig(L, "gpt2_decode_step", i, [v, _I, _I])
     _sig(L, "gpt2_decode_step_async", i, [v, _I])
     _sig(L, "gpt2_decode_reset", i, [v])
@@ -510,6 +514,16 @@ class Model:
         check(lib().gpt2_decode_time_attention(self.h, int(iters), ctypes.byref(ms), ctypes.byref(by)),
               "time_attention")
         return ms.value, by.value
+
+    def prefill(self, tokens):
+        """tokens (B, T): all T tokens of every sequence in one pass; returns
+        the greedy next ids (B,)"""
+        tokens = np.ascontiguousarray(tokens, np.int32)
+        assert tokens.ndim == 2 and tokens.shape[0] == self.B
+        nxt = np.zeros(self.B, np.int32)
+        check(lib().gpt2_decode_prefill(self.h, tokens.ctypes.data_as(_I), tokens.shape[1],
+                                        nxt.ctypes.data_as(_I)), "prefill")
+        return nxt
 
     def set_pipeline(self, enable=True):
         check(lib().gpt2_decode_set_pipeline(self.h, int(bool(enable))), "set_pipeline")
