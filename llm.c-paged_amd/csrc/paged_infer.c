@@ -1455,16 +1455,26 @@ void gpt2_forward(GPT2* model, int* inputs, int* targets, size_t B, size_t T, si
     }
     memcpy(model->inputs, inputs, B * T * sizeof(int));
     GPT2Decode* d = model->decode;
-    int* tok = (int*)malloc(B * sizeof(int));
-    /* all sequences share the window, so they advance together */
+    /* all sequences share the window, so they advance together: the
+     * uncached positions cached..offset+T-1 go through the one-pass prefill
+     * (several tokens) or a decode step (one token) */
     int cached = d->h_pos[0];
-    for (int p = cached; p < offset + (int)T; p++) {
-        int t = p - offset;
-        if (t < 0) PI_FATAL("window starts after uncached positions");
-        for (size_t b = 0; b < B; b++) tok[b] = inputs[b * T + t];
-        if (gpt2_decode_step(model, tok, NULL)) PI_FATAL("decode step failed");
+    if (cached < offset) PI_FATAL("window starts after uncached positions");
+    const int t0 = cached - offset, n = offset + (int)T - cached;
+    if (n > 1 && d->fused && d->nlanes == 1 && !d->pipeline) {
+        int* tok = (int*)malloc(B * (size_t)n * sizeof(int));
+        for (size_t b = 0; b < B; b++)
+            for (int t = 0; t < n; t++) tok[b * n + t] = inputs[b * T + t0 + t];
+        if (gpt2_decode_prefill(model, tok, n, NULL)) PI_FATAL("prefill failed");
+        free(tok);
+    } else {
+        int* tok = (int*)malloc(B * sizeof(int));
+        for (int t = t0; t < (int)T; t++) {
+            for (size_t b = 0; b < B; b++) tok[b] = inputs[b * T + t];
+            if (gpt2_decode_step(model, tok, NULL)) PI_FATAL("decode step failed");
+        }
+        free(tok);
     }
-    free(tok);
     PI_CHECK(hpa_synchronize());
     for (size_t b = 0; b < B; b++) {
         float* row = model->acts.logits + (b * T + (T - 1)) * V;
