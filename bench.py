@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--unfused", action="store_true", help="row-major GEMMs + separate row kernels")
     ap.add_argument("--lanes", type=int, default=1, help="micro-batch lanes (concurrent row groups)")
     ap.add_argument("--pipeline", type=int, default=0, help="1: two lanes, attention chunks beside GEMMs")
+    ap.add_argument("--sample", action="store_true",
+                    help="multinomial sampling as the reference driver (default: greedy argmax)")
     ap.add_argument("--gemm-waves", default="", help="fused GEMM waves qkv,attproj,fc,fcproj,logits (0 = auto)")
     ap.add_argument("--gemm-rows", default="", help="fused GEMM 16-row blocks per workgroup, same order")
     ap.add_argument("--gemm-cols", default="", help="fused GEMM 16-column tiles per workgroup, same order")
@@ -178,6 +180,8 @@ def main():
         model.set_lanes(args.lanes)
         if args.pipeline:
             model.set_pipeline(True)
+    if args.sample:
+        model.set_sampling(True, seed=1337 + rank * B_local)
     if args.gemm_waves or args.gemm_rows or args.gemm_cols:
         ints = lambda a: [int(x) for x in a.split(",")] if a else None  # noqa: E731
         model.gemm_config(ints(args.gemm_waves), ints(args.gemm_rows), ints(args.gemm_cols))
@@ -313,6 +317,7 @@ def main():
                        "hip_graph": not args.no_graph, "gemm_path": "unfused" if args.unfused else "fused",
                        "lanes": 1 if args.unfused else L.gpt2_decode_lanes(model.h),
                        "pipeline": bool(L.gpt2_decode_pipeline(model.h)),
+                       "token_choice": "multinomial (reference sample_mult)" if args.sample else "greedy",
                        "gemm_waves": [int(x) for x in model.gemm_config()[0]],
                        "gemm_row_blocks": [int(x) for x in model.gemm_config()[1]],
                        "gemm_col_tiles": [int(x) for x in model.gemm_config()[2]], "device": name},

@@ -186,6 +186,10 @@ int    gpt2_decode_set_lanes(GPT2* model, int lanes);
 int    gpt2_decode_time_attention(GPT2* model, int iters, double* ms_per_launch,
                                   double* bytes_per_launch);
 int    gpt2_decode_lanes(GPT2* model);
+/* token choice: 0 = greedy argmax (default); 1 = multinomial sampling as the
+ * reference driver (softmax_forward + sample_mult with random_f32 coins),
+ * sequence b seeded with seed + b; the coins stay on the device */
+int    gpt2_decode_set_sampling(GPT2* model, int enable, unsigned long long seed);
 /* pipelined step (fused path): two lanes on ONE stream; each lane's layer
  * attention runs in 4 context chunks, every chunk in the same launch as one
  * GEMM of the other lane's chain (hpa_attn_chunk_with_gemm).  Logits within

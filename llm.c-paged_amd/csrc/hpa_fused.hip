@@ -143,6 +143,85 @@ __global__ __launch_bounds__(256) void argmax_final_kernel(const float* __restri
     }
 }
 
+// ---------------------------------------------------------------- sampling
+// Multinomial draw from softmax(logits[b]) in the REFERENCE's arithmetic
+// order (softmax_forward paged_infer.c:259-286, sample_mult :837-848, coin =
+// random_f32 :826-835), so draws match it: the fp32 running sums over ~50k
+// probabilities drift by more than one probability's width, so any other
+// summation order picks neighbouring ids near CDF boundaries.  One wave per
+// row: the wave computes 64 expf / divisions at a time in parallel, lane 0
+// performs the order-dependent additions sequentially.  Each sequence has its
+// own xorshift state, advanced once per draw on the device.
+__device__ __forceinline__ unsigned int xorshift_u32(unsigned long long& s) {
+    s ^= s >> 12;
+    s ^= s << 25;
+    s ^= s >> 27;
+    return (unsigned int)((s * 0x2545F4914F6CDD1Dull) >> 32);
+}
+
+__global__ __launch_bounds__(64) void sample_final_kernel(const float* __restrict__ logits, int V,
+                                                          float* __restrict__ scratch,
+                                                          unsigned long long* __restrict__ state,
+                                                          int* __restrict__ next, int* __restrict__ tokens,
+                                                          int* __restrict__ pos) {
+    __shared__ float sh[64];
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const float* lg = logits + (size_t)b * V;
+    float* pr = scratch + (size_t)b * V;
+    // maxval = -10000; if (x > maxval) maxval = x  (exact in any order)
+    float mx = -10000.0f;
+    for (int i = lane; i < V; i += 64) mx = fmaxf(mx, lg[i]);
+    mx = hpa::wave_max(mx);
+    // probs[i] = expf(x - maxval); sum += probs[i]  (sum in index order)
+    float sum = 0.f;
+    for (int base = 0; base < V; base += 64) {
+        const int i = base + lane;
+        const float e = i < V ? expf(lg[i] - mx) : 0.f;
+        if (i < V) pr[i] = e;
+        sh[lane] = e;
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+            const int n = min(64, V - base);
+            for (int k = 0; k < n; ++k) sum += sh[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    sum = __shfl(sum, 0, 64);
+    // coin; cdf += probs[i] / sum; if (coin < cdf) return i   (index order)
+    unsigned long long st = state[b];
+    const float coin = (xorshift_u32(st) >> 8) / 16777216.0f;
+    int pick = V - 1;
+    float cdf = 0.f;
+    for (int base = 0; base < V; base += 64) {
+        const int i = base + lane;
+        sh[lane] = i < V ? pr[i] / sum : 0.f;
+        __builtin_amdgcn_wave_barrier();
+        int found = -1;
+        if (lane == 0) {
+            const int n = min(64, V - base);
+            for (int k = 0; k < n; ++k) {
+                cdf += sh[k];
+                if (coin < cdf) {
+                    found = base + k;
+                    break;
+                }
+            }
+        }
+        found = __shfl(found, 0, 64);
+        __builtin_amdgcn_wave_barrier();
+        if (found >= 0) {
+            pick = found;
+            break;
+        }
+    }
+    if (lane == 0) {
+        state[b] = st;
+        next[b] = pick;
+        if (tokens) tokens[b] = pick;
+        if (pos) pos[b] += 1;
+    }
+}
+
 inline dim3 xcd_grid(FG& p, int gx, int gy) {
     p.gx = gx;
     p.gy = gy;
@@ -306,6 +385,14 @@ int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const fl
                    float* res_frag, float* stats, int B, int C) {
     HPA_REQUIRE(B > 0 && C > 0 && C % 16 == 0, "embed_frag: bad shape");
     embed_frag_kernel<<<B, 256, 0, hpa_stream()>>>(tokens, pos, wte, wpe, res_frag, stats, C);
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+int hpa_sample_final(const float* logits, int B, int V, float* scratch, unsigned long long* state, int* next,
+                     int* tokens, int* pos) {
+    HPA_REQUIRE(logits && scratch && state && next && B > 0 && V > 0, "sample_final: bad arguments");
+    sample_final_kernel<<<B, 64, 0, hpa_stream()>>>(logits, V, scratch, state, next, tokens, pos);
     HPA_LAUNCH_CHECK();
     return 0;
 }

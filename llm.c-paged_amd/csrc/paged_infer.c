@@ -450,6 +450,9 @@ struct GPT2Decode {
     DecLane lanes[DEC_MAX_LANES];
     int nlanes;
     int pipeline;     /* 1: two lanes, attention chunks beside the other lane's GEMMs */
+    int sample;       /* 0: greedy argmax; 1: multinomial with per-sequence xorshift */
+    unsigned long long* d_rng; /* [B] sampler states */
+    float* d_probs;   /* [B][V] sampler scratch */
     /* prefill workspace (gpt2_decode_prefill), rows R = B*T, grown on demand */
     int pf_cap;       /* row capacity */
     float *pf_res, *pf_res2, *pf_att, *pf_fch, *pf_st1, *pf_st2, *pf_q;
@@ -554,6 +557,8 @@ static void dec_free(GPT2Decode* d) {
     hpa_free(d->d_res); hpa_free(d->d_res2); hpa_free(d->d_ln); hpa_free(d->d_q);
     hpa_free(d->d_att); hpa_free(d->d_fch); hpa_free(d->d_part); hpa_free(d->d_logits);
     hpa_free(d->d_wpack);
+    hpa_free(d->d_rng);
+    hpa_free(d->d_probs);
     dec_lanes_free(d);
     hpa_event_destroy(d->ev_fork);
     hpa_host_free(d->h_stage);
@@ -887,6 +892,9 @@ static int lane_argmax(GPT2* model, int li) {
     GPT2Decode* d = model->decode;
     const DecLane* ln = &d->lanes[li];
     const int V = model->config.vocab_size;
+    if (d->sample)
+        return hpa_sample_final(d->d_logits + (size_t)ln->r0 * V, ln->B, V, d->d_probs + (size_t)ln->r0 * V,
+                                d->d_rng + ln->r0, d->d_next + ln->r0, d->d_tokens + ln->r0, d->d_pos + ln->r0);
     return hpa_argmax_final(ln->part, (V + 15) / 16, ln->Mp, ln->B, d->d_next + ln->r0, d->d_tokens + ln->r0,
                             d->d_pos + ln->r0);
 }
@@ -1038,6 +1046,37 @@ int gpt2_decode_set_lanes(GPT2* model, int lanes) {
 }
 
 int gpt2_decode_lanes(GPT2* model) { return model->decode ? model->decode->nlanes : 0; }
+
+/* token choice: greedy argmax (enable = 0, the north star's), or the
+ * reference driver's multinomial sampling (softmax_forward + sample_mult,
+ * paged_infer.c:259-286, :837-848) with sequence b drawing its coins from
+ * xorshift state seed + b (B = 1 reproduces the reference's single stream) */
+int gpt2_decode_set_sampling(GPT2* model, int enable, unsigned long long seed) {
+    GPT2Decode* d = model->decode;
+    if (!d) return 1;
+    if (hpa_synchronize()) return 1;
+    if (!d->d_rng) {
+        d->d_rng = (unsigned long long*)hpa_malloc(d->B * sizeof(unsigned long long));
+        d->d_probs = (float*)hpa_malloc((size_t)d->B * model->config.vocab_size * sizeof(float));
+        if (!d->d_rng || !d->d_probs) return 1;
+    }
+    unsigned long long* h = (unsigned long long*)malloc(d->B * sizeof(unsigned long long));
+    if (!h) return 1;
+    for (int b = 0; b < d->B; b++) h[b] = seed + (unsigned long long)b;
+    int rc = hpa_memcpy(d->d_rng, h, d->B * sizeof(unsigned long long));
+    free(h);
+    if (rc) return 1;
+    if (enable && !d->fused) {
+        fprintf(stderr, "[paged_infer] sampling runs on the fused path\n");
+        return 1;
+    }
+    d->sample = enable ? 1 : 0;
+    if (d->graph) { /* recapture with the other token-choice kernel */
+        hpa_graph_destroy(d->graph);
+        d->graph = NULL;
+    }
+    return 0;
+}
 
 /* pipelined step: two lanes on ONE stream, each lane's attention in context
  * chunks beside the other lane's GEMMs (dec_launch_pipelined).  Needs two

@@ -205,6 +205,7 @@ def lib():
     _sig(L, "gpt2_decode_init", i, [v, i, i, i])
     _sig(L, "gpt2_decode_init_ex", i, [v, i, i, i, i])
     _sig(L, "gpt2_decode_prefill", i, [v, _I, i, _I])
+    _sig(L, "gpt2_decode_set_sampling", i, [v, i, ctypes.c_ulonglong])
     _sig(L, "hpa_paged_attention_prefill", i, [_F, v, i, _I, i, _I, i, i, _F])
     _sig(L, "hpa_gather_rows_frag", i, [_F, _F, i, _I, i, _F, _F, i, i])
     _sig(L, "gpt2_decode_step", i, [v, _I, _I])
@@ -524,6 +525,9 @@ class Model:
         check(lib().gpt2_decode_prefill(self.h, tokens.ctypes.data_as(_I), tokens.shape[1],
                                         nxt.ctypes.data_as(_I)), "prefill")
         return nxt
+
+    def set_sampling(self, enable=True, seed=1337):
+        check(lib().gpt2_decode_set_sampling(self.h, int(bool(enable)), int(seed)), "set_sampling")
 
     def set_pipeline(self, enable=True):
         check(lib().gpt2_decode_set_pipeline(self.h, int(bool(enable))), "set_pipeline")

@@ -65,6 +65,11 @@ def lib(fast=False):
     L.oracle_paged_set_kv_bf16.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.oracle_round_bf16.argtypes = [ctypes.c_float]
     L.oracle_round_bf16.restype = ctypes.c_float
+    L.oracle_softmax_forward.argtypes = [_F, _F, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    L.oracle_random_f32.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+    L.oracle_random_f32.restype = ctypes.c_float
+    L.oracle_sample_mult.argtypes = [_F, ctypes.c_int, ctypes.c_float]
+    L.oracle_sample_mult.restype = ctypes.c_int
     L.oracle_argmax.argtypes = [_F, ctypes.c_int]
     L.oracle_argmax.restype = ctypes.c_int
     _libs[key] = L
@@ -166,3 +171,24 @@ class PagedDecoder:
             self.close()
         except Exception:
             pass
+
+
+class Sampler:
+    """the reference driver's token choice (softmax_forward :259-286 +
+    sample_mult :837-848 with random_f32 coins :826-835), one xorshift stream
+    per sequence seeded seed + b (as gpt2_decode_set_sampling)"""
+
+    def __init__(self, B, seed=1337):
+        self.states = [ctypes.c_ulonglong(seed + b) for b in range(B)]
+
+    def sample(self, logits):
+        L = lib()
+        B, V = logits.shape
+        logits = np.ascontiguousarray(logits, np.float32)
+        probs = np.empty_like(logits)
+        L.oracle_softmax_forward(fp(probs), fp(logits), B, 1, V)
+        out = np.empty(B, np.int32)
+        for b in range(B):
+            coin = L.oracle_random_f32(ctypes.byref(self.states[b]))
+            out[b] = L.oracle_sample_mult(fp(probs[b]), V, coin)
+        return out
