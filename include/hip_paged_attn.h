@@ -229,10 +229,9 @@ int hpa_argmax_final(const float* part, int ntiles, int Mp, int B, int* next, in
 /* multinomial draw per row from softmax(logits) with the reference's
  * generator and arithmetic order (softmax_forward :259-286, sample_mult
  * :837-848, random_f32 :826-835), one xorshift state per row advanced on the
- * device; scratch: B*V floats (the probabilities); next[b], tokens[b] =
- * next[b], pos[b] += 1 (tokens/pos may be NULL) */
-int hpa_sample_final(const float* logits, int B, int V, float* scratch, unsigned long long* state, int* next,
-                     int* tokens, int* pos);
+ * device; next[b], tokens[b] = next[b], pos[b] += 1 (tokens/pos may be NULL) */
+int hpa_sample_final(const float* logits, int B, int V, unsigned long long* state, int* next, int* tokens,
+                     int* pos);
 /* paged decode attention writing its output in frag layout ([B][C]) */
 int hpa_paged_attention_decode_frag(const float* q, const HpaKVPool* pool, int layer,
                                     const int* block_table, int bt_stride, const int* pos,

@@ -148,10 +148,10 @@ __global__ __launch_bounds__(256) void argmax_final_kernel(const float* __restri
 // order (softmax_forward paged_infer.c:259-286, sample_mult :837-848, coin =
 // random_f32 :826-835), so draws match it: the fp32 running sums over ~50k
 // probabilities drift by more than one probability's width, so any other
-// summation order picks neighbouring ids near CDF boundaries.  One wave per
-// row: the wave computes 64 expf / divisions at a time in parallel, lane 0
-// performs the order-dependent additions sequentially.  Each sequence has its
-// own xorshift state, advanced once per draw on the device.
+// summation order picks neighbouring ids near CDF boundaries.  The additions
+// stay sequential (one lane), everything else is parallel (see the kernel).
+// Each sequence has its own xorshift state, advanced once per draw on the
+// device.
 __device__ __forceinline__ unsigned int xorshift_u32(unsigned long long& s) {
     s ^= s >> 12;
     s ^= s << 25;
@@ -159,62 +159,143 @@ __device__ __forceinline__ unsigned int xorshift_u32(unsigned long long& s) {
     return (unsigned int)((s * 0x2545F4914F6CDD1Dull) >> 32);
 }
 
-__global__ __launch_bounds__(64) void sample_final_kernel(const float* __restrict__ logits, int V,
-                                                          float* __restrict__ scratch,
-                                                          unsigned long long* __restrict__ state,
-                                                          int* __restrict__ next, int* __restrict__ tokens,
-                                                          int* __restrict__ pos) {
-    __shared__ float sh[64];
-    const int b = blockIdx.x, lane = threadIdx.x;
+constexpr int kSampPer = 16;                 // elements per lane per block
+constexpr int kSampBlk = 64 * kSampPer;     // 1024 elements per block
+
+// a block of logits, coalesced: element base + j*64 + lane -> v[j]
+__device__ __forceinline__ void samp_load(const float* lg, int V, int base, int lane, float* v) {
+#pragma unroll
+    for (int j = 0; j < kSampPer; ++j) {
+        const int i = base + j * 64 + lane;
+        v[j] = i < V ? lg[i] : -INFINITY;
+    }
+}
+
+// lane 0 of the consumer wave: acc += v[k] for nb*64 values of an LDS
+// buffer, in index order, branch-free (batches of 16 x 16-B LDS reads).
+// Pads beyond V hold +0 and leave the sum unchanged.  The chain runs at the
+// dependent-add latency (~4 ns per add, tools/micro/chain.hip); prefetching
+// the next batch's LDS reads measured slower (465 vs 416 us per launch).
+__device__ __forceinline__ float samp_chain(const float* buf, int nb, float acc) {
+    const float4* s4 = reinterpret_cast<const float4*>(buf);
+    for (int q0 = 0; q0 < nb * 16; q0 += 16) {
+        float4 r[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) r[q] = s4[q0 + q];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            acc += r[q].x;
+            acc += r[q].y;
+            acc += r[q].z;
+            acc += r[q].w;
+        }
+    }
+    return acc;
+}
+
+// Two waves per row.  Wave 1 produces: it streams the logits (one block of
+// 1024 ahead) and writes expf(x - max) (pass 1) or expf(x - max) / sum
+// (pass 2) into one of two LDS buffers.  Wave 0's lane 0 consumes the other
+// buffer with the order-dependent additions, so the serial chain never waits
+// for a load or an exp.  Pass 2 checks coin < cdf once per 64 values: cdf is
+// non-decreasing, so when the batch-end cdf exceeds the coin the batch is
+// replayed from its start with the per-element test (same additions, same
+// roundings), which yields the first index where coin < cdf.
+__global__ __launch_bounds__(128) void sample_final_kernel(const float* __restrict__ logits, int V,
+                                                           unsigned long long* __restrict__ state,
+                                                           int* __restrict__ next, int* __restrict__ tokens,
+                                                           int* __restrict__ pos) {
+    __shared__ __attribute__((aligned(16))) float sh[2][kSampBlk];
+    __shared__ float s_red[2];
+    __shared__ int s_found;
+    const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const float* lg = logits + (size_t)b * V;
-    float* pr = scratch + (size_t)b * V;
     // maxval = -10000; if (x > maxval) maxval = x  (exact in any order)
     float mx = -10000.0f;
-    for (int i = lane; i < V; i += 64) mx = fmaxf(mx, lg[i]);
+    for (int i = threadIdx.x; i < V; i += 128) mx = fmaxf(mx, lg[i]);
     mx = hpa::wave_max(mx);
-    // probs[i] = expf(x - maxval); sum += probs[i]  (sum in index order)
+    if (lane == 0) s_red[w] = mx;
+    __syncthreads();
+    mx = fmaxf(s_red[0], s_red[1]);
+    const int nblk = (V + kSampBlk - 1) / kSampBlk;
+    float cur[kSampPer], nxt[kSampPer];
+    // pass 1: sum += expf(x - maxval) in index order
     float sum = 0.f;
-    for (int base = 0; base < V; base += 64) {
-        const int i = base + lane;
-        const float e = i < V ? expf(lg[i] - mx) : 0.f;
-        if (i < V) pr[i] = e;
-        sh[lane] = e;
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) {
-            const int n = min(64, V - base);
-            for (int k = 0; k < n; ++k) sum += sh[k];
+    if (w == 1) samp_load(lg, V, 0, lane, cur);
+    for (int it = 0; it <= nblk; ++it) {
+        if (w == 1 && it < nblk) {
+            if (it + 1 < nblk) samp_load(lg, V, (it + 1) * kSampBlk, lane, nxt);
+            float* dst = sh[it & 1];
+#pragma unroll
+            for (int j = 0; j < kSampPer; ++j) dst[j * 64 + lane] = expf(cur[j] - mx);  // expf(-inf) = +0 pads
+#pragma unroll
+            for (int j = 0; j < kSampPer; ++j) cur[j] = nxt[j];
         }
-        __builtin_amdgcn_wave_barrier();
+        if (w == 0 && lane == 0 && it > 0) {
+            const int blk = it - 1;
+            sum = samp_chain(sh[blk & 1], (min(kSampBlk, V - blk * kSampBlk) + 63) / 64, sum);
+        }
+        __syncthreads();
     }
-    sum = __shfl(sum, 0, 64);
-    // coin; cdf += probs[i] / sum; if (coin < cdf) return i   (index order)
+    if (threadIdx.x == 0) s_red[0] = sum;
+    if (threadIdx.x == 0) s_found = -1;
+    __syncthreads();
+    sum = s_red[0];
+    // pass 2: coin; cdf += expf(x - maxval) / sum; if (coin < cdf) return i
+    // (the exps recomputed: expf is deterministic)
     unsigned long long st = state[b];
     const float coin = (xorshift_u32(st) >> 8) / 16777216.0f;
     int pick = V - 1;
     float cdf = 0.f;
-    for (int base = 0; base < V; base += 64) {
-        const int i = base + lane;
-        sh[lane] = i < V ? pr[i] / sum : 0.f;
-        __builtin_amdgcn_wave_barrier();
-        int found = -1;
-        if (lane == 0) {
-            const int n = min(64, V - base);
-            for (int k = 0; k < n; ++k) {
-                cdf += sh[k];
+    if (w == 1) samp_load(lg, V, 0, lane, cur);
+    for (int it = 0; it <= nblk; ++it) {
+        if (w == 1 && it < nblk) {
+            if (it + 1 < nblk) samp_load(lg, V, (it + 1) * kSampBlk, lane, nxt);
+            float* dst = sh[it & 1];
+#pragma unroll
+            for (int j = 0; j < kSampPer; ++j) dst[j * 64 + lane] = expf(cur[j] - mx) / sum;
+#pragma unroll
+            for (int j = 0; j < kSampPer; ++j) cur[j] = nxt[j];
+        }
+        if (w == 0 && lane == 0 && it > 0) {
+            const int blk = it - 1;
+            const int n = min(kSampBlk, V - blk * kSampBlk);
+            const float* buf = sh[blk & 1];
+            for (int q0 = 0; q0 < n; q0 += 64) {
+                // cdf is non-decreasing: test once per 64 values, and replay
+                // the batch that crosses the coin from its start with the
+                // per-element test (same additions, same roundings)
+                const float4* s4 = reinterpret_cast<const float4*>(buf + q0);
+                float4 r[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) r[q] = s4[q];
+                const float c0 = cdf;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    cdf += r[q].x;
+                    cdf += r[q].y;
+                    cdf += r[q].z;
+                    cdf += r[q].w;
+                }
                 if (coin < cdf) {
-                    found = base + k;
+                    float c = c0;
+                    int k = q0;
+                    for (; k < q0 + 63; ++k) {
+                        c += buf[k];
+                        if (coin < c) break;
+                    }
+                    s_found = min(blk * kSampBlk + k, V - 1);
                     break;
                 }
             }
         }
-        found = __shfl(found, 0, 64);
-        __builtin_amdgcn_wave_barrier();
-        if (found >= 0) {
-            pick = found;
+        __syncthreads();
+        if (s_found >= 0) {
+            pick = s_found;
             break;
         }
     }
-    if (lane == 0) {
+    if (threadIdx.x == 0) {
         state[b] = st;
         next[b] = pick;
         if (tokens) tokens[b] = pick;
@@ -389,10 +470,10 @@ int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const fl
     return 0;
 }
 
-int hpa_sample_final(const float* logits, int B, int V, float* scratch, unsigned long long* state, int* next,
-                     int* tokens, int* pos) {
-    HPA_REQUIRE(logits && scratch && state && next && B > 0 && V > 0, "sample_final: bad arguments");
-    sample_final_kernel<<<B, 64, 0, hpa_stream()>>>(logits, V, scratch, state, next, tokens, pos);
+int hpa_sample_final(const float* logits, int B, int V, unsigned long long* state, int* next, int* tokens,
+                     int* pos) {
+    HPA_REQUIRE(logits && state && next && B > 0 && V > 0, "sample_final: bad arguments");
+    sample_final_kernel<<<B, 128, 0, hpa_stream()>>>(logits, V, state, next, tokens, pos);
     HPA_LAUNCH_CHECK();
     return 0;
 }

@@ -452,7 +452,6 @@ struct GPT2Decode {
     int pipeline;     /* 1: two lanes, attention chunks beside the other lane's GEMMs */
     int sample;       /* 0: greedy argmax; 1: multinomial with per-sequence xorshift */
     unsigned long long* d_rng; /* [B] sampler states */
-    float* d_probs;   /* [B][V] sampler scratch */
     /* prefill workspace (gpt2_decode_prefill), rows R = B*T, grown on demand */
     int pf_cap;       /* row capacity */
     float *pf_res, *pf_res2, *pf_att, *pf_fch, *pf_st1, *pf_st2, *pf_q;
@@ -558,7 +557,6 @@ static void dec_free(GPT2Decode* d) {
     hpa_free(d->d_att); hpa_free(d->d_fch); hpa_free(d->d_part); hpa_free(d->d_logits);
     hpa_free(d->d_wpack);
     hpa_free(d->d_rng);
-    hpa_free(d->d_probs);
     dec_lanes_free(d);
     hpa_event_destroy(d->ev_fork);
     hpa_host_free(d->h_stage);
@@ -893,8 +891,8 @@ static int lane_argmax(GPT2* model, int li) {
     const DecLane* ln = &d->lanes[li];
     const int V = model->config.vocab_size;
     if (d->sample)
-        return hpa_sample_final(d->d_logits + (size_t)ln->r0 * V, ln->B, V, d->d_probs + (size_t)ln->r0 * V,
-                                d->d_rng + ln->r0, d->d_next + ln->r0, d->d_tokens + ln->r0, d->d_pos + ln->r0);
+        return hpa_sample_final(d->d_logits + (size_t)ln->r0 * V, ln->B, V, d->d_rng + ln->r0, d->d_next + ln->r0,
+                                d->d_tokens + ln->r0, d->d_pos + ln->r0);
     return hpa_argmax_final(ln->part, (V + 15) / 16, ln->Mp, ln->B, d->d_next + ln->r0, d->d_tokens + ln->r0,
                             d->d_pos + ln->r0);
 }
@@ -1057,8 +1055,7 @@ int gpt2_decode_set_sampling(GPT2* model, int enable, unsigned long long seed) {
     if (hpa_synchronize()) return 1;
     if (!d->d_rng) {
         d->d_rng = (unsigned long long*)hpa_malloc(d->B * sizeof(unsigned long long));
-        d->d_probs = (float*)hpa_malloc((size_t)d->B * model->config.vocab_size * sizeof(float));
-        if (!d->d_rng || !d->d_probs) return 1;
+        if (!d->d_rng) return 1;
     }
     unsigned long long* h = (unsigned long long*)malloc(d->B * sizeof(unsigned long long));
     if (!h) return 1;
