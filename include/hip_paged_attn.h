@@ -224,14 +224,17 @@ int hpa_fused_pick_waves(int M, int N, int K);
 int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const float* wpe,
                    float* res_frag, float* stats, int B, int C);
 /* greedy id from the logits GEMM's per-tile (max, argmax) partials:
- * lowest index wins ties; next[b], tokens[b] = next[b], pos[b] += 1 */
-int hpa_argmax_final(const float* part, int ntiles, int Mp, int B, int* next, int* tokens, int* pos);
+ * lowest index wins ties; next[b], tokens[b] = next[b], pos[b] += 1.
+ * active (nullable, [B]): rows with active[b] <= 0 are left untouched */
+int hpa_argmax_final(const float* part, int ntiles, int Mp, int B, int* next, int* tokens, int* pos,
+                     const int* active);
 /* multinomial draw per row from softmax(logits) with the reference's
  * generator and arithmetic order (softmax_forward :259-286, sample_mult
  * :837-848, random_f32 :826-835), one xorshift state per row advanced on the
- * device; next[b], tokens[b] = next[b], pos[b] += 1 (tokens/pos may be NULL) */
+ * device; next[b], tokens[b] = next[b], pos[b] += 1 (tokens/pos may be NULL);
+ * active as hpa_argmax_final (an inactive row's state does not advance) */
 int hpa_sample_final(const float* logits, int B, int V, unsigned long long* state, int* next, int* tokens,
-                     int* pos);
+                     int* pos, const int* active);
 /* paged decode attention writing its output in frag layout ([B][C]) */
 int hpa_paged_attention_decode_frag(const float* q, const HpaKVPool* pool, int layer,
                                     const int* block_table, int bt_stride, const int* pos,
@@ -246,8 +249,15 @@ int hpa_paged_attention_decode_frag(const float* q, const HpaKVPool* pool, int l
  * position must already be in the pages (the prefill QKV GEMM appends them). */
 int hpa_paged_attention_prefill(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
                                 int bt_stride, const int* start, int B, int T, float* out_frag);
+/* ragged form (continuous batching): sequence b has len[b] >= 0 query rows
+ * starting at row row0[b] of q / out (device arrays, given together);
+ * T = max(len).  row0 = len = NULL is the uniform form above. */
+int hpa_paged_attention_prefill_ragged(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
+                                       int bt_stride, const int* start, const int* row0, const int* len, int B,
+                                       int T, float* out_frag);
 /* rows[i] of a frag-layout [src_Mp][C] matrix and of its LN statistics
- * ([C/16][src_Mp][2]) -> row i of dst / dst_stats (n rows; prefill -> logits) */
+ * ([C/16][src_Mp][2]) -> row i of dst / dst_stats (n rows; prefill -> logits);
+ * rows[i] < 0 leaves row i of dst as it is */
 int hpa_gather_rows_frag(const float* src, const float* src_stats, int src_Mp, const int* rows, int n,
                          float* dst, float* dst_stats, int dst_Mp, int C);
 

@@ -144,6 +144,15 @@ int  gpt2_decode_step(GPT2* model, const int* tokens, int* next_tokens);
  * sequence's last token and pos[b] += T, so decode continues with
  * gpt2_decode_step(model, NULL, ...).  Fused one-lane engine. */
 int  gpt2_decode_prefill(GPT2* model, const int* tokens, int T, int* next_tokens);
+/* continuous batching: one pass over lens[b] >= 0 new tokens per sequence
+ * (tokens packed in sequence order, sum(lens) of them): prompts of newly
+ * admitted sequences and single decode tokens of running ones go through
+ * the same call.  Sequences with lens[b] = 0 are untouched (position, next
+ * id, sampler state).  next_tokens[b] is each sequence's next id. */
+int  gpt2_decode_prefill_ragged(GPT2* model, const int* tokens, const int* lens, int* next_tokens);
+/* retire sequence seq: its pages go back to the pool (block_manager.c:78-90),
+ * its position restarts at 0, so the slot can admit a new prompt */
+int  gpt2_decode_release(GPT2* model, int seq);
 /* the same, but enqueue only (no host sync; next ids stay on device) */
 int  gpt2_decode_step_async(GPT2* model, const int* tokens);
 /* free every sequence's pages and rewind positions to 0 */

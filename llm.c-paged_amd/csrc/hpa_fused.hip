@@ -100,10 +100,12 @@ __global__ __launch_bounds__(256) void embed_frag_kernel(const int* __restrict__
 __global__ __launch_bounds__(256) void argmax_final_kernel(const float* __restrict__ part, int ntiles,
                                                            int Mp, int* __restrict__ next,
                                                            int* __restrict__ tokens,
-                                                           int* __restrict__ pos) {
+                                                           int* __restrict__ pos,
+                                                           const int* __restrict__ active) {
     __shared__ float sv[4];
     __shared__ int si[4];
     const int b = blockIdx.x;
+    if (active && active[b] <= 0) return;  // row left as it is
     float bv = -INFINITY;
     int bi = 0x7fffffff;
     for (int t = threadIdx.x; t < ntiles; t += 256) {
@@ -204,11 +206,12 @@ __device__ __forceinline__ float samp_chain(const float* buf, int nb, float acc)
 __global__ __launch_bounds__(128) void sample_final_kernel(const float* __restrict__ logits, int V,
                                                            unsigned long long* __restrict__ state,
                                                            int* __restrict__ next, int* __restrict__ tokens,
-                                                           int* __restrict__ pos) {
+                                                           int* __restrict__ pos, const int* __restrict__ active) {
     __shared__ __attribute__((aligned(16))) float sh[2][kSampBlk];
     __shared__ float s_red[2];
     __shared__ int s_found;
     const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (active && active[b] <= 0) return;  // row left as it is (its RNG state too)
     const float* lg = logits + (size_t)b * V;
     // maxval = -10000; if (x > maxval) maxval = x  (exact in any order)
     float mx = -10000.0f;
@@ -471,16 +474,17 @@ int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const fl
 }
 
 int hpa_sample_final(const float* logits, int B, int V, unsigned long long* state, int* next, int* tokens,
-                     int* pos) {
+                     int* pos, const int* active) {
     HPA_REQUIRE(logits && state && next && B > 0 && V > 0, "sample_final: bad arguments");
-    sample_final_kernel<<<B, 128, 0, hpa_stream()>>>(logits, V, state, next, tokens, pos);
+    sample_final_kernel<<<B, 128, 0, hpa_stream()>>>(logits, V, state, next, tokens, pos, active);
     HPA_LAUNCH_CHECK();
     return 0;
 }
 
-int hpa_argmax_final(const float* part, int ntiles, int Mp, int B, int* next, int* tokens, int* pos) {
+int hpa_argmax_final(const float* part, int ntiles, int Mp, int B, int* next, int* tokens, int* pos,
+                     const int* active) {
     HPA_REQUIRE(part && next && B > 0 && ntiles > 0 && Mp >= B, "argmax_final: bad arguments");
-    argmax_final_kernel<<<B, 256, 0, hpa_stream()>>>(part, ntiles, Mp, next, tokens, pos);
+    argmax_final_kernel<<<B, 256, 0, hpa_stream()>>>(part, ntiles, Mp, next, tokens, pos, active);
     HPA_LAUNCH_CHECK();
     return 0;
 }

@@ -137,6 +137,7 @@ struct Epi {
                             const int ps = p.pos[row];
                             const int seq = p.row_seq ? p.row_seq[row] : row;
                             const int page = p.bt[(size_t)seq * p.bt_stride + ps / p.P];
+                            if (page < 0) continue;  // no page (host bug): never write below the pool
                             const int slot = ps % p.P;
                             const size_t toff = (size_t)page * p.page_elems + ((size_t)kv * p.NH + hh) * p.P * 64;
                             if (p.kv_bf16) {  // bf16 pool: K [chunk of 8][slot][8], V [slot][64], RNE

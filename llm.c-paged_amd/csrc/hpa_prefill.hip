@@ -35,13 +35,15 @@ constexpr int LD = 68;    // padded LDS row (floats)
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct PrefillArgs {
-    const float* q;        // [B*T][C] row-major (row = b*T + t)
+    const float* q;        // [rows][C] row-major (row = row0[b] + t)
     const void* layer_base;
     size_t page_elems;
     int NH, P, bf16;
     const int* bt;
     int bt_stride;
     const int* start;      // [B] position of row t = 0
+    const int* row0;       // [B] first row of sequence b (nullptr: b*T)
+    const int* len;        // [B] query rows of sequence b (nullptr: T); T = max
     int T;
     float* out;            // frag layout [Rp][C]
     float qscale, m_init;
@@ -78,6 +80,9 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(PrefillArgs a) {
     const int qb = blockIdx.x % nqb;
     const int bh = blockIdx.x / nqb;
     const int b = bh / NH, h = bh - b * NH;
+    const int Tb = a.len ? a.len[b] : a.T;  // ragged: this sequence's query rows
+    if (qb * QB >= Tb) return;              // whole workgroup past them (uniform, before any barrier)
+    const int rb0 = a.row0 ? a.row0[b] : b * a.T;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     const int g = lane >> 4;     // C-layout row group: rows 4g .. 4g+3
@@ -86,7 +91,7 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(PrefillArgs a) {
     const int* bt = a.bt + (size_t)b * a.bt_stride;
     const int start = a.start[b];
     const int t0 = qb * QB + 16 * w;                  // this wave's first query (row offset in the sequence)
-    const int last_t = min(a.T - 1, qb * QB + QB - 1);
+    const int last_t = min(Tb - 1, qb * QB + QB - 1);
     const int kmax = start + last_t;                  // last key any query of the block sees
     const int ntiles = kmax / KT + 1;
 
@@ -94,8 +99,8 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(PrefillArgs a) {
     // qa[s] = q[row t0 + (lane&15)][h*64 + 4s + (lane>>4)], pre-scaled
     float qa[16];
     {
-        const int t = min(t0 + c16, a.T - 1);
-        const float* qr = a.q + ((size_t)b * a.T + t) * C + h * HS;
+        const int t = min(t0 + c16, Tb - 1);
+        const float* qr = a.q + ((size_t)rb0 + t) * C + h * HS;
 #pragma unroll
         for (int s = 0; s < 16; ++s) qa[s] = qr[4 * s + g] * a.qscale;
     }
@@ -121,7 +126,7 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(PrefillArgs a) {
         __syncthreads();
         if (it + 1 < ntiles) load_kv4(a, bt, h, min((it + 1) * KT + skey, kmax), sc, rk, rv);
         const int k0 = it * KT;
-        if (k0 <= start + min(t0 + 15, a.T - 1)) {  // any key of the tile visible to this wave's queries
+        if (k0 <= start + min(t0 + 15, Tb - 1)) {  // any key of the tile visible to this wave's queries
             // S = Q K^T  (B operand: B[k = lane>>4][n = key lane&15] = K[key][4s + k])
             f32x4 s4 = f32x4{0.f, 0.f, 0.f, 0.f};
             const float* kr = &sK[buf][c16 * LD + g];
@@ -176,9 +181,9 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(PrefillArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int t = t0 + 4 * g + r;
-        if (t < a.T) {
+        if (t < Tb) {
             const float inv = l[r] == 0.f ? 0.f : 1.f / l[r];
-            const int row = b * a.T + t;
+            const int row = rb0 + t;
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt) a.out[hpa::frag_index(row, h * HS + 16 * dt + c16, C)] = o[dt][r] * inv;
         }
@@ -195,6 +200,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restric
                                                           int src_Mp, const int* __restrict__ idx, float* __restrict__ dst,
                                                           float* __restrict__ dst_st, int dst_Mp, int C, int ct) {
     const int i = blockIdx.x, r = idx[i];
+    if (r < 0) return;  // row i left as it is
     for (int c = threadIdx.x * 4; c < C; c += 1024)
         *reinterpret_cast<float4*>(dst + hpa::frag_index(i, c, C)) =
             *reinterpret_cast<const float4*>(src + hpa::frag_index(r, c, C));
@@ -208,13 +214,15 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restric
 
 extern "C" {
 
-int hpa_paged_attention_prefill(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
-                                int bt_stride, const int* start, int B, int T, float* out_frag) {
+int hpa_paged_attention_prefill_ragged(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
+                                       int bt_stride, const int* start, const int* row0, const int* len, int B,
+                                       int T, float* out_frag) {
     HPA_REQUIRE(pool && pool->base && pool->head_size == HS, "prefill attention: pool with head_size 64");
     HPA_REQUIRE(pool->dtype == HPA_F32 || pool->dtype == HPA_BF16, "prefill attention: fp32 or bf16 pool");
     HPA_REQUIRE(pool->dtype == HPA_F32 || pool->page_size % 8 == 0, "prefill attention: bf16 pages need P % 8");
     HPA_REQUIRE(layer >= 0 && layer < pool->num_layers, "prefill attention: layer out of range");
     HPA_REQUIRE(q && block_table && start && out_frag && B > 0 && T > 0, "prefill attention: bad arguments");
+    HPA_REQUIRE(!row0 == !len, "prefill attention: row0 and len go together");
     PrefillArgs a;
     a.q = q;
     a.layer_base = (const char*)pool->base + (size_t)layer * pool->layer_elems * pool->elem_bytes;
@@ -225,6 +233,8 @@ int hpa_paged_attention_prefill(const float* q, const HpaKVPool* pool, int layer
     a.bt = block_table;
     a.bt_stride = bt_stride;
     a.start = start;
+    a.row0 = row0;
+    a.len = len;
     a.T = T;
     a.out = out_frag;
     const float log2e = 1.4426950408889634f;
@@ -234,6 +244,12 @@ int hpa_paged_attention_prefill(const float* q, const HpaKVPool* pool, int layer
     prefill_attn_kernel<<<(unsigned)(B * a.NH * nqb), 256, 0, hpa_stream()>>>(a);
     HPA_LAUNCH_CHECK();
     return 0;
+}
+
+int hpa_paged_attention_prefill(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
+                                int bt_stride, const int* start, int B, int T, float* out_frag) {
+    return hpa_paged_attention_prefill_ragged(q, pool, layer, block_table, bt_stride, start, nullptr, nullptr, B, T,
+                                              out_frag);
 }
 
 int hpa_gather_rows_frag(const float* src, const float* src_stats, int src_Mp, const int* rows, int n,

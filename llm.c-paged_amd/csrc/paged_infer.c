@@ -745,29 +745,47 @@ static int dec_sync_block_table(GPT2Decode* d) {
     return 0;
 }
 
-/* make sure every sequence owns the page its next token lands in */
-static int dec_ensure_pages(GPT2Decode* d) {
-    for (int b = 0; b < d->B; b++) {
-        int p = d->h_pos[b];
-        if (p >= d->max_ctx) {
-            fprintf(stderr, "[paged_infer] sequence %d is full (%d tokens)\n", b, p);
+/* pages for positions pos[b] .. pos[b]+n-1 of sequence b.  The reference
+ * policy may evict a whole LRU sequence to make room (block_manager.c:104-162);
+ * the evicted sequence restarts at position 0.  `busy` (nullable) marks the
+ * sequences of the current batch: evicting one of those fails the call. */
+static int dec_grow(GPT2Decode* d, int b, int n, const int* busy, int* evicted) {
+    for (;;) {
+        const int need = (d->h_pos[b] + n - 1) / d->P + 1;
+        if (d->bm->prompt_block_count[b] >= need) return 0;
+        if (!request_block(d->bm, b)) return 1;
+        const int ev = d->bm->last_evicted_prompt; /* may be b itself */
+        if (ev < 0 || ev >= d->B) continue;
+        fprintf(stderr, "[paged_infer] page pool full: sequence %d evicted (LRU)\n", ev);
+        if (evicted) ++*evicted;
+        d->h_pos[ev] = 0;
+        if (hpa_memcpy(d->d_pos + ev, &d->h_pos[ev], sizeof(int))) return 1;
+        if (busy && busy[ev]) {
+            fprintf(stderr, "[paged_infer] sequence %d of this batch was evicted: pool too small\n", ev);
             return 1;
         }
-        int need = p / d->P + 1;
-        while (d->bm->prompt_block_count[b] < need) {
-            KVBlock* blk = request_block(d->bm, b);
-            if (!blk) return 1;
-            int ev = d->bm->last_evicted_prompt;
-            if (ev >= 0 && ev < d->B && ev != b) {
-                /* the reference policy evicted a whole live sequence: it restarts */
-                fprintf(stderr, "[paged_infer] page pool full: sequence %d evicted (LRU)\n", ev);
-                d->h_pos[ev] = 0;
-                if (hpa_memcpy_async(d->d_pos + ev, &d->h_pos[ev], sizeof(int))) return 1;
-                if (hpa_synchronize()) return 1;
-            }
-        }
     }
-    return 0;
+}
+
+/* make sure every sequence owns the page its next token lands in.  An LRU
+ * eviction (dec_grow) restarts the evicted sequence at position 0, which
+ * needs a page again: repeat until a pass evicts nobody (bounded). */
+static int dec_ensure_pages(GPT2Decode* d) {
+    for (int pass = 0; pass <= d->B; pass++) {
+        int evictions = 0;
+        for (int b = 0; b < d->B; b++) {
+            const int p = d->h_pos[b];
+            if (p >= d->max_ctx) {
+                fprintf(stderr, "[paged_infer] sequence %d is full (%d tokens)\n", b, p);
+                return 1;
+            }
+            if (d->bm->prompt_block_count[b] >= p / d->P + 1) continue;
+            if (dec_grow(d, b, 1, NULL, &evictions)) return 1;
+        }
+        if (!evictions) return 0;
+    }
+    fprintf(stderr, "[paged_infer] page pool thrashing: every pass evicts a sequence\n");
+    return 1;
 }
 
 static int dec_launch_unfused(GPT2* model) {
@@ -886,15 +904,17 @@ static int lane_embed(GPT2* model, int li) {
                           model->config.channels);
 }
 
-static int lane_argmax(GPT2* model, int li) {
+/* greedy or sampled next token of the lane's rows; active (nullable):
+ * rows with active[b] <= 0 are left untouched */
+static int lane_pick(GPT2* model, int li, const int* active) {
     GPT2Decode* d = model->decode;
     const DecLane* ln = &d->lanes[li];
     const int V = model->config.vocab_size;
     if (d->sample)
         return hpa_sample_final(d->d_logits + (size_t)ln->r0 * V, ln->B, V, d->d_rng + ln->r0, d->d_next + ln->r0,
-                                d->d_tokens + ln->r0, d->d_pos + ln->r0);
+                                d->d_tokens + ln->r0, d->d_pos + ln->r0, active);
     return hpa_argmax_final(ln->part, (V + 15) / 16, ln->Mp, ln->B, d->d_next + ln->r0, d->d_tokens + ln->r0,
-                            d->d_pos + ln->r0);
+                            d->d_pos + ln->r0, active);
 }
 
 /* one lane's fused step on the current stream: embed, then per layer
@@ -918,7 +938,7 @@ static int dec_launch_lane(GPT2* model, int li) {
         rc |= lane_gemm_run(model, li, l, G_FCPROJ);
     }
     rc |= lane_gemm_run(model, li, 0, G_LOGITS);
-    rc |= lane_argmax(model, li);
+    rc |= lane_pick(model, li, NULL);
     return rc;
 }
 
@@ -984,8 +1004,8 @@ static int dec_launch_pipelined(GPT2* model) {
     rc |= lane_gemm_run(model, B, L - 1, G_FCPROJ);
     rc |= lane_gemm_run(model, A, 0, G_LOGITS);
     rc |= lane_gemm_run(model, B, 0, G_LOGITS);
-    rc |= lane_argmax(model, A);
-    rc |= lane_argmax(model, B);
+    rc |= lane_pick(model, A, NULL);
+    rc |= lane_pick(model, B, NULL);
     return rc;
 }
 
@@ -1163,9 +1183,9 @@ static int dec_prefill_reserve(GPT2* model, int R) {
     d->pf_tok = (int*)hpa_malloc(Rp * sizeof(int));
     d->pf_pos = (int*)hpa_malloc(Rp * sizeof(int));
     d->pf_seq = (int*)hpa_malloc(Rp * sizeof(int));
-    d->pf_start = (int*)hpa_malloc(d->B * sizeof(int));
+    d->pf_start = (int*)hpa_malloc(3 * (size_t)d->B * sizeof(int)); /* start[B], row0[B], len[B] */
     d->pf_last = (int*)hpa_malloc(d->B * sizeof(int));
-    d->h_pf = (int*)malloc((3 * Rp + 2 * d->B) * sizeof(int));
+    d->h_pf = (int*)malloc((3 * Rp + 4 * (size_t)d->B) * sizeof(int));
     if (!d->pf_res || !d->pf_res2 || !d->pf_att || !d->pf_fch || !d->pf_st1 || !d->pf_st2 || !d->pf_q ||
         !d->pf_tok || !d->pf_pos || !d->pf_seq || !d->pf_start || !d->pf_last || !d->h_pf) {
         dec_prefill_free(d);
@@ -1224,76 +1244,121 @@ static int prefill_gemm(GPT2* model, int l, int which, int R) {
     return hpa_gemm_fused(&g);
 }
 
-int gpt2_decode_prefill(GPT2* model, const int* tokens, int T, int* next_tokens) {
+/* One pass over lens[b] >= 0 new tokens of every sequence b (tokens packed
+ * in sequence order): all rows through the fused GEMMs (the QKV epilogue
+ * appends each row's K/V through its own sequence's block table), causal
+ * multi-query paged attention per sequence, then the last row of every
+ * sequence with lens[b] > 0 through the logits and the greedy / sampled
+ * pick.  Sequences with lens[b] = 0 are untouched (position, next token,
+ * sampler state). */
+static int dec_prefill_rows(GPT2* model, const int* tokens, const int* lens, int* next_tokens) {
     GPT2Decode* d = model->decode;
     if (!d) { fprintf(stderr, "[paged_infer] gpt2_decode_init first\n"); return 1; }
     const GPT2Config c = model->config;
     const int B = d->B, C = c.channels, L = c.num_layers;
-    if (T <= 0) return 1;
     if (!d->fused || d->nlanes != 1 || d->pipeline) {
         fprintf(stderr, "[paged_infer] prefill runs on the fused one-lane engine\n");
         return 1;
     }
-    for (int i = 0; i < B * T; i++)
+    long R = 0;
+    int T = 0;
+    for (int b = 0; b < B; b++) {
+        if (lens[b] < 0) { fprintf(stderr, "[paged_infer] negative length for sequence %d\n", b); return 1; }
+        if (d->h_pos[b] + lens[b] > d->max_ctx) {
+            fprintf(stderr, "[paged_infer] prefill of %d tokens overflows sequence %d\n", lens[b], b);
+            return 1;
+        }
+        R += lens[b];
+        if (lens[b] > T) T = lens[b];
+    }
+    if (R == 0) return 0;
+    if (R > (1L << 24)) { fprintf(stderr, "[paged_infer] prefill too large\n"); return 1; }
+    for (long i = 0; i < R; i++)
         if (tokens[i] < 0 || tokens[i] >= c.vocab_size) {
             fprintf(stderr, "[paged_infer] token out of range\n"); /* :591-596 */
             return 1;
         }
-    /* pages for positions pos[b] .. pos[b]+T-1 */
-    for (int b = 0; b < B; b++) {
-        if (d->h_pos[b] + T > d->max_ctx) {
-            fprintf(stderr, "[paged_infer] prefill of %d tokens overflows sequence %d\n", T, b);
-            return 1;
-        }
-        const int need = (d->h_pos[b] + T - 1) / d->P + 1;
-        while (d->bm->prompt_block_count[b] < need)
-            if (!request_block(d->bm, b)) return 1;
-    }
+    for (int b = 0; b < B; b++)
+        if (lens[b] > 0 && dec_grow(d, b, lens[b], lens, NULL)) return 1;
     if (dec_sync_block_table(d)) return 1;
-    const int R = B * T;
-    if (dec_prefill_reserve(model, R)) return 1;
-    /* row tables: token, absolute position, sequence; per-sequence start and last row */
+    if (dec_prefill_reserve(model, (int)R)) return 1;
+    /* row tables: token, absolute position, sequence; per-sequence start,
+     * first row, length, last row (-1: skipped) */
     if (hpa_synchronize()) return 1; /* h_pf staging reuse */
-    const int Rp = (R + 15) / 16 * 16;
-    int *ht = d->h_pf, *hp = ht + Rp, *hs = hp + Rp, *hst = hs + Rp, *hl = hst + B;
+    const int Rp = (int)((R + 15) / 16 * 16);
+    int *ht = d->h_pf, *hp = ht + Rp, *hs = hp + Rp, *hst = hs + Rp, *hr0 = hst + B, *hln = hr0 + B, *hl = hln + B;
+    int r = 0;
     for (int b = 0; b < B; b++) {
-        for (int t = 0; t < T; t++) {
-            ht[b * T + t] = tokens[b * T + t];
-            hp[b * T + t] = d->h_pos[b] + t;
-            hs[b * T + t] = b;
-        }
         hst[b] = d->h_pos[b];
-        hl[b] = b * T + T - 1;
+        hr0[b] = r;
+        hln[b] = lens[b];
+        for (int t = 0; t < lens[b]; t++, r++) {
+            ht[r] = tokens[r];
+            hp[r] = d->h_pos[b] + t;
+            hs[r] = b;
+        }
+        hl[b] = lens[b] > 0 ? r - 1 : -1;
     }
     if (hpa_memcpy(d->pf_tok, ht, R * sizeof(int)) || hpa_memcpy(d->pf_pos, hp, R * sizeof(int)) ||
-        hpa_memcpy(d->pf_seq, hs, R * sizeof(int)) || hpa_memcpy(d->pf_start, hst, B * sizeof(int)) ||
+        hpa_memcpy(d->pf_seq, hs, R * sizeof(int)) || hpa_memcpy(d->pf_start, hst, 3 * (size_t)B * sizeof(int)) ||
         hpa_memcpy(d->pf_last, hl, B * sizeof(int)))
         return 1;
+    const int* d_row0 = d->pf_start + B;
+    const int* d_len = d->pf_start + 2 * B;
     const ParameterTensors* w = &model->params;
-    int rc = hpa_embed_frag(d->pf_tok, d->pf_pos, w->wte, w->wpe, d->pf_res, d->pf_st1, R, C);
+    int rc = hpa_embed_frag(d->pf_tok, d->pf_pos, w->wte, w->wpe, d->pf_res, d->pf_st1, (int)R, C);
     for (int l = 0; l < L && !rc; l++) {
-        rc |= prefill_gemm(model, l, G_QKV, R);
-        rc |= hpa_paged_attention_prefill(d->pf_q, &d->pool, l, d->d_bt, d->bt_stride, d->pf_start, B, T,
-                                          d->pf_att);
-        rc |= prefill_gemm(model, l, G_ATTPROJ, R);
-        rc |= prefill_gemm(model, l, G_FC, R);
-        rc |= prefill_gemm(model, l, G_FCPROJ, R);
+        rc |= prefill_gemm(model, l, G_QKV, (int)R);
+        rc |= hpa_paged_attention_prefill_ragged(d->pf_q, &d->pool, l, d->d_bt, d->bt_stride, d->pf_start, d_row0,
+                                                 d_len, B, T, d->pf_att);
+        rc |= prefill_gemm(model, l, G_ATTPROJ, (int)R);
+        rc |= prefill_gemm(model, l, G_FC, (int)R);
+        rc |= prefill_gemm(model, l, G_FCPROJ, (int)R);
     }
-    /* last row of every sequence -> the one-lane engine's buffers, logits, greedy;
-     * argmax_final advances pos by one: set pos = start + T - 1 first */
+    /* last row of every active sequence -> the one-lane engine's buffers,
+     * logits, pick; the pick advances pos by one: set pos = start + len - 1 */
     DecLane* ln = &d->lanes[0];
-    for (int b = 0; b < B; b++) hst[b] = d->h_pos[b] + T - 1;
+    for (int b = 0; b < B; b++) hst[b] = d->h_pos[b] + (lens[b] > 0 ? lens[b] - 1 : 0);
     rc |= hpa_memcpy(d->d_pos, hst, B * sizeof(int));
     rc |= hpa_gather_rows_frag(d->pf_res, d->pf_st1, Rp, d->pf_last, B, ln->res, ln->st1, ln->Mp, C);
     rc |= lane_gemm_run(model, 0, 0, G_LOGITS);
-    rc |= lane_argmax(model, 0);
+    rc |= lane_pick(model, 0, d_len);
     if (rc) return 1;
-    for (int b = 0; b < B; b++) d->h_pos[b] += T;
+    for (int b = 0; b < B; b++) d->h_pos[b] += lens[b];
     if (next_tokens) {
         if (hpa_memcpy(d->h_stage + B, d->d_next, B * sizeof(int))) return 1;
         memcpy(next_tokens, d->h_stage + B, B * sizeof(int));
     }
     return hpa_synchronize();
+}
+
+int gpt2_decode_prefill(GPT2* model, const int* tokens, int T, int* next_tokens) {
+    GPT2Decode* d = model->decode;
+    if (!d) { fprintf(stderr, "[paged_infer] gpt2_decode_init first\n"); return 1; }
+    if (T <= 0) return 1;
+    int* lens = (int*)malloc(d->B * sizeof(int));
+    if (!lens) return 1;
+    for (int b = 0; b < d->B; b++) lens[b] = T;
+    const int rc = dec_prefill_rows(model, tokens, lens, next_tokens);
+    free(lens);
+    return rc;
+}
+
+int gpt2_decode_prefill_ragged(GPT2* model, const int* tokens, const int* lens, int* next_tokens) {
+    if (!model->decode) { fprintf(stderr, "[paged_infer] gpt2_decode_init first\n"); return 1; }
+    if (!lens || !tokens) return 1;
+    return dec_prefill_rows(model, tokens, lens, next_tokens);
+}
+
+int gpt2_decode_release(GPT2* model, int seq) {
+    GPT2Decode* d = model->decode;
+    if (!d) { fprintf(stderr, "[paged_infer] gpt2_decode_init first\n"); return 1; }
+    if (seq < 0 || seq >= d->B) { fprintf(stderr, "[paged_infer] no sequence %d\n", seq); return 1; }
+    if (hpa_synchronize()) return 1; /* the pages may still be read by queued work */
+    if (d->bm->prompt_block_count[seq]) free_blocks_for_prompt(d->bm, seq);
+    d->h_pos[seq] = 0;
+    if (hpa_memcpy(d->d_pos + seq, &d->h_pos[seq], sizeof(int))) return 1;
+    return dec_sync_block_table(d);
 }
 
 int gpt2_decode_step_async(GPT2* model, const int* tokens) { return dec_enqueue(model, tokens); }

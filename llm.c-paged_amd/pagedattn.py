@@ -205,8 +205,11 @@ def lib():
     _sig(L, "gpt2_decode_init", i, [v, i, i, i])
     _sig(L, "gpt2_decode_init_ex", i, [v, i, i, i, i])
     _sig(L, "gpt2_decode_prefill", i, [v, _I, i, _I])
+    _sig(L, "gpt2_decode_prefill_ragged", i, [v, _I, _I, _I])
+    _sig(L, "gpt2_decode_release", i, [v, i])
     _sig(L, "gpt2_decode_set_sampling", i, [v, i, ctypes.c_ulonglong])
     _sig(L, "hpa_paged_attention_prefill", i, [_F, v, i, _I, i, _I, i, i, _F])
+    _sig(L, "hpa_paged_attention_prefill_ragged", i, [_F, v, i, _I, i, _I, _I, _I, i, i, _F])
     _sig(L, "hpa_gather_rows_frag", i, [_F, _F, i, _I, i, _F, _F, i, i])
     _sig(L, "gpt2_decode_step", i, [v, _I, _I])
     _sig(L, "gpt2_decode_step_async", i, [v, _I])
@@ -222,7 +225,7 @@ def lib():
     _sig(L, "hpa_fused_pick_waves", i, [i, i, i])
     _sig(L, "hpa_fused_pick", None, [i, i, i, _I])
     _sig(L, "hpa_embed_frag", i, [v, v, v, v, v, v, i, i])
-    _sig(L, "hpa_argmax_final", i, [v, i, i, i, v, v, v])
+    _sig(L, "hpa_argmax_final", i, [v, i, i, i, v, v, v, v])
     _sig(L, "hpa_paged_attention_decode_frag", i, [v, P, i, v, i, v, v, i])
     _sig(L, "gpt2_decode_set_positions", i, [v, _I])
     _sig(L, "gpt2_decode_logits", v, [v])
@@ -457,6 +460,12 @@ class Model:
             check(L.gpt2_build_synthetic(self.h, self.cfg, seed), "build_synthetic")
         self.B = 0
 
+    def set_manager(self, bm):
+        """model.manager = bm (paged_infer.c:986-987): the engine's pages come
+        from this manager's capacity, with its LRU policy"""
+        self._bm = bm
+        lib().gpt2_set_manager(self.h, bm.h)
+
     def decode_init(self, B, page_size=16, max_ctx=None, kv_dtype=HPA_F32):
         max_ctx = max_ctx or self.cfg.max_seq_len
         check(lib().gpt2_decode_init_ex(self.h, B, page_size, max_ctx, int(kv_dtype)), "gpt2_decode_init")
@@ -525,6 +534,22 @@ class Model:
         check(lib().gpt2_decode_prefill(self.h, tokens.ctypes.data_as(_I), tokens.shape[1],
                                         nxt.ctypes.data_as(_I)), "prefill")
         return nxt
+
+    def prefill_ragged(self, seqs):
+        """seqs: B token lists (empty = sequence untouched); one pass over
+        all of them (continuous batching); returns the next ids (B,)"""
+        assert len(seqs) == self.B
+        lens = np.array([len(t) for t in seqs], np.int32)
+        flat = np.ascontiguousarray(np.concatenate([np.asarray(t, np.int32).reshape(-1) for t in seqs])
+                                    if lens.sum() else np.zeros(1, np.int32), np.int32)
+        nxt = np.zeros(self.B, np.int32)
+        check(lib().gpt2_decode_prefill_ragged(self.h, flat.ctypes.data_as(_I), lens.ctypes.data_as(_I),
+                                               nxt.ctypes.data_as(_I)), "prefill_ragged")
+        return nxt
+
+    def release(self, seq):
+        """retire sequence seq: pages back to the pool, position 0"""
+        check(lib().gpt2_decode_release(self.h, int(seq)), "release")
 
     def set_sampling(self, enable=True, seed=1337):
         check(lib().gpt2_decode_set_sampling(self.h, int(bool(enable)), int(seed)), "set_sampling")

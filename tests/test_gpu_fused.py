@@ -159,7 +159,7 @@ def test_fused_logits_argmax(hip, M, waves, rb, ct):
     part = keep[-2]
     nxt = hip.DeviceBuffer(M * 4)
     Mp = (M + 15) // 16 * 16
-    hip.check(L.hpa_argmax_final(part.ptr, (N + 15) // 16, Mp, M, nxt.ptr, None, None))
+    hip.check(L.hpa_argmax_final(part.ptr, (N + 15) // 16, Mp, M, nxt.ptr, None, None, None))
     ids = nxt.download(M, np.int32)
     assert np.array_equal(ids, got.argmax(-1))
 
