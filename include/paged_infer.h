@@ -19,6 +19,7 @@
 #ifndef PAGED_INFER_H
 #define PAGED_INFER_H
 #include <stddef.h>
+#include <stdint.h>
 
 #include "block_manager.h"
 #ifdef __cplusplus
@@ -103,6 +104,19 @@ unsigned int random_u32(unsigned long long* state);
 float random_f32(unsigned long long* state);
 int sample_mult(float* probabilities, int n, float coin);
 int* generate_tokens_from_logits(float* probs, int B, int T, int V);
+void print_generated_sequence(int* tokens, int B, int T);   /* :930-935 */
+
+/* tokenizer, decode only (paged_infer.c:852-928); file written by
+ * train_gpt2.py:350-363 */
+typedef struct {
+    uint32_t vocab_size;
+    char** token_table;
+    int init_ok;
+} Tokenizer;
+void safe_printf(const char* piece);
+void tokenizer_init(Tokenizer* tokenizer, const char* filename);
+const char* tokenizer_decode(Tokenizer* tokenizer, uint32_t token_id);
+void tokenizer_free(Tokenizer* tokenizer);
 
 /* attention_paged with the page size as an argument (the reference fixes
  * BLOCK_SIZE = 32); attention_paged() uses BLOCK_SIZE */
@@ -118,6 +132,15 @@ int gpt2_build_synthetic(GPT2* model, GPT2Config config, unsigned long long seed
 size_t gpt2_num_parameters(GPT2Config config);
 int gpt2_synthetic_params(GPT2Config config, unsigned long long seed, float* host_params);
 int gpt2_write_checkpoint(const char* path, GPT2Config config, const float* host_params);
+/* version 1 (fp32) or 2 (bf16 weights, LN fp32 and last: train_gpt2.py:267-293,
+ * rounded to nearest even as torch .to(bfloat16)) */
+int gpt2_write_checkpoint_ex(const char* path, GPT2Config config, const float* host_params, int version);
+/* host-only reader of v1 and v2 checkpoints: config (nullable) from the
+ * header; host_params (nullable: header only) receives the parameters in
+ * ParameterTensors order as fp32 (bf16 widened exactly).  Nonzero + stderr
+ * on a bad file (gpt2_build_from_checkpoint prints and exits instead, as
+ * the reference :436-502). */
+int gpt2_read_checkpoint(const char* path, GPT2Config* config, float* host_params);
 
 /* heap handle for FFI callers (ctypes / cgo) that cannot size GPT2 */
 GPT2* gpt2_alloc(void);

@@ -13,6 +13,7 @@
 
 #include <math.h>
 #include <stdint.h>
+#include <ctype.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -335,24 +336,83 @@ int gpt2_build_from_params(GPT2* model, GPT2Config c, const float* host_params) 
 }
 
 /* paged_infer.c:436-502: 256 x int32 header, magic 20240326, version 1 (fp32) */
-void gpt2_build_from_checkpoint(GPT2* model, const char* checkpoint_path) {
-    FILE* f = fopen(checkpoint_path, "rb");
-    if (!f) { printf("Error opening model file\n"); exit(1); }
+/* Checkpoint formats (train_gpt2.py:295-320 write_model; 256-int32 header
+ * magic 20240326, version, maxT, V, L, NH, C):
+ *   v1: the 16 tensors in ParameterTensors order, fp32 (:242-265);
+ *   v2: wte wpe qkvw qkvb attprojw attprojb fcw fcb fcprojw fcprojb as bf16,
+ *       then ln1w ln1b ln2w ln2b lnfw lnfb as fp32 (:267-293).
+ * The reference loader (paged_infer.c:436-502) reads v1 only; v2 loads
+ * here with an exact bf16 -> fp32 widening, so compute stays fp32. */
+static const int kV2Order[NUM_PARAMETER_TENSORS] = {0, 1, 4, 5, 6, 7, 10, 11, 12, 13, /* bf16 */
+                                                    2, 3, 8, 9, 14, 15};               /* fp32 */
+#define CKPT_V2_NBF16 10
+
+static unsigned short f32_to_bf16_rne(float f) {
+    unsigned int u;
+    memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40); /* quiet NaN */
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (unsigned short)(u >> 16);
+}
+
+int gpt2_read_checkpoint(const char* path, GPT2Config* config, float* host_params) {
+    FILE* f = fopen(path, "rb");
+    if (!f) { fprintf(stderr, "[paged_infer] cannot open checkpoint %s\n", path); return 1; }
     int hdr[256];
-    if (fread(hdr, sizeof(int), 256, f) != 256) { printf("Bad model file\n"); exit(1); }
-    if (hdr[0] != 20240326) { printf("Bad magic model file"); exit(1); }
-    if (hdr[1] != 1) { printf("Bad version in model file"); exit(1); }
+    int rc = 1;
+    if (fread(hdr, sizeof(int), 256, f) != 256) { fprintf(stderr, "[paged_infer] short checkpoint header\n"); goto out; }
+    if (hdr[0] != 20240326) { fprintf(stderr, "[paged_infer] bad magic in checkpoint\n"); goto out; }
+    if (hdr[1] != 1 && hdr[1] != 2) { fprintf(stderr, "[paged_infer] checkpoint version %d (1 or 2)\n", hdr[1]); goto out; }
     GPT2Config c;
     c.max_seq_len = hdr[2];
     c.vocab_size = hdr[3];
     c.num_layers = hdr[4];
     c.num_heads = hdr[5];
     c.channels = hdr[6];
+    if (c.max_seq_len <= 0 || c.vocab_size <= 0 || c.num_layers <= 0 || c.num_heads <= 0 || c.channels <= 0 ||
+        c.channels % c.num_heads) {
+        fprintf(stderr, "[paged_infer] bad checkpoint config\n");
+        goto out;
+    }
+    if (config) *config = c;
+    if (!host_params) { rc = 0; goto out; }
+    size_t s[NUM_PARAMETER_TENSORS], off[NUM_PARAMETER_TENSORS], n = 0;
+    param_sizes(c, s);
+    for (int t = 0; t < NUM_PARAMETER_TENSORS; t++) { off[t] = n; n += s[t]; }
+    if (hdr[1] == 1) {
+        if (fread(host_params, sizeof(float), n, f) != n) { fprintf(stderr, "[paged_infer] truncated checkpoint\n"); goto out; }
+    } else {
+        for (int k = 0; k < NUM_PARAMETER_TENSORS; k++) {
+            const int t = kV2Order[k];
+            float* dst = host_params + off[t];
+            if (k < CKPT_V2_NBF16) {
+                /* read the bf16 halves into the upper half of the tensor's
+                 * own fp32 slot, then widen front to back (never overtakes) */
+                unsigned short* src = (unsigned short*)(dst + s[t]) - s[t];
+                if (fread(src, 2, s[t], f) != s[t]) { fprintf(stderr, "[paged_infer] truncated checkpoint\n"); goto out; }
+                for (size_t i = 0; i < s[t]; i++) {
+                    unsigned int u = (unsigned int)src[i] << 16;
+                    memcpy(dst + i, &u, 4);
+                }
+            } else if (fread(dst, sizeof(float), s[t], f) != s[t]) {
+                fprintf(stderr, "[paged_infer] truncated checkpoint\n");
+                goto out;
+            }
+        }
+    }
+    rc = 0;
+out:
+    fclose(f);
+    return rc;
+}
+
+void gpt2_build_from_checkpoint(GPT2* model, const char* checkpoint_path) {
+    GPT2Config c;
+    if (gpt2_read_checkpoint(checkpoint_path, &c, NULL)) { printf("Error opening model file\n"); exit(1); }
     size_t n = gpt2_num_parameters(c);
     float* host = (float*)malloc(n * sizeof(float));
     if (!host) { printf("Out of host memory for parameters\n"); exit(1); }
-    if (fread(host, sizeof(float), n, f) != n) { printf("Truncated model file\n"); exit(1); }
-    fclose(f);
+    if (gpt2_read_checkpoint(checkpoint_path, &c, host)) { printf("Bad model file\n"); exit(1); }
     if (gpt2_build_from_params(model, c, host) != 0) { printf("Parameter upload failed\n"); exit(1); }
     free(host);
 }
@@ -391,17 +451,118 @@ int gpt2_build_synthetic(GPT2* model, GPT2Config c, unsigned long long seed) {
     return rc;
 }
 
-int gpt2_write_checkpoint(const char* path, GPT2Config c, const float* host_params) {
+int gpt2_write_checkpoint_ex(const char* path, GPT2Config c, const float* host_params, int version) {
+    if (version != 1 && version != 2) return 1;
     FILE* f = fopen(path, "wb");
     if (!f) return 1;
     int hdr[256];
     memset(hdr, 0, sizeof(hdr));
-    hdr[0] = 20240326; hdr[1] = 1; hdr[2] = c.max_seq_len; hdr[3] = c.vocab_size;
+    hdr[0] = 20240326; hdr[1] = version; hdr[2] = c.max_seq_len; hdr[3] = c.vocab_size;
     hdr[4] = c.num_layers; hdr[5] = c.num_heads; hdr[6] = c.channels;
-    size_t n = gpt2_num_parameters(c);
-    int ok = fwrite(hdr, sizeof(int), 256, f) == 256 && fwrite(host_params, sizeof(float), n, f) == n;
+    size_t s[NUM_PARAMETER_TENSORS], off[NUM_PARAMETER_TENSORS], n = 0;
+    param_sizes(c, s);
+    for (int t = 0; t < NUM_PARAMETER_TENSORS; t++) { off[t] = n; n += s[t]; }
+    int ok = fwrite(hdr, sizeof(int), 256, f) == 256;
+    if (version == 1) {
+        ok = ok && fwrite(host_params, sizeof(float), n, f) == n;
+    } else {
+        unsigned short buf[4096];
+        for (int k = 0; k < NUM_PARAMETER_TENSORS && ok; k++) {
+            const int t = kV2Order[k];
+            const float* src = host_params + off[t];
+            if (k >= CKPT_V2_NBF16) { ok = fwrite(src, sizeof(float), s[t], f) == s[t]; continue; }
+            for (size_t i = 0; i < s[t] && ok; i += 4096) { /* torch .to(bfloat16): round to nearest even */
+                const size_t m = s[t] - i < 4096 ? s[t] - i : 4096;
+                for (size_t j = 0; j < m; j++) buf[j] = f32_to_bf16_rne(src[i + j]);
+                ok = fwrite(buf, 2, m, f) == m;
+            }
+        }
+    }
     fclose(f);
     return ok ? 0 : 1;
+}
+
+int gpt2_write_checkpoint(const char* path, GPT2Config c, const float* host_params) {
+    return gpt2_write_checkpoint_ex(path, c, host_params, 1);
+}
+
+/* ------------------------------------------------------------------------ */
+/* tokenizer (paged_infer.c:852-928): the decode-only byte table written by
+ * train_gpt2.py:350-363 (header magic 20240328, version 1, vocab size; then
+ * per token a length byte and the bytes)                                    */
+/* ------------------------------------------------------------------------ */
+void safe_printf(const char* piece) {
+    if (piece == NULL || piece[0] == '\0') return;
+    if (piece[1] == '\0') { /* a lone byte: printable or whitespace only */
+        unsigned char b = (unsigned char)piece[0];
+        if (!(isprint(b) || isspace(b))) return;
+    }
+    printf("%s", piece);
+}
+
+static void tokenizer_release(Tokenizer* tk, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) free(tk->token_table[i]);
+    free(tk->token_table);
+    tk->token_table = NULL;
+}
+
+void tokenizer_init(Tokenizer* tokenizer, const char* filename) {
+    tokenizer->init_ok = 0;
+    tokenizer->vocab_size = 0;
+    tokenizer->token_table = NULL;
+    FILE* f = fopen(filename, "rb");
+    if (!f) {
+        printf("---\nWARNING: Failed to open the tokenizer file %s\n---\n", filename);
+        return;
+    }
+    uint32_t hdr[256];
+    if (fread(hdr, sizeof(uint32_t), 256, f) != 256 || hdr[0] != 20240328 || hdr[1] != 1) {
+        fprintf(stderr, "[paged_infer] bad tokenizer file %s\n", filename);
+        fclose(f);
+        return;
+    }
+    const uint32_t n = hdr[2];
+    tokenizer->token_table = (char**)calloc(n ? n : 1, sizeof(char*));
+    if (!tokenizer->token_table) { fclose(f); return; }
+    for (uint32_t i = 0; i < n; i++) {
+        unsigned char len;
+        char* piece = NULL;
+        if (fread(&len, 1, 1, f) != 1 || len == 0 || !(piece = (char*)malloc(len + 1u)) ||
+            fread(piece, 1, len, f) != len) {
+            fprintf(stderr, "[paged_infer] truncated tokenizer file %s\n", filename);
+            free(piece);
+            tokenizer_release(tokenizer, i);
+            fclose(f);
+            return;
+        }
+        piece[len] = '\0';
+        tokenizer->token_table[i] = piece;
+    }
+    fclose(f);
+    tokenizer->vocab_size = n;
+    tokenizer->init_ok = 1;
+}
+
+const char* tokenizer_decode(Tokenizer* tokenizer, uint32_t token_id) {
+    if (!tokenizer->init_ok) return NULL;
+    if (token_id >= tokenizer->vocab_size) {
+        printf("invalid token id %u!\n", token_id);
+        return NULL;
+    }
+    return tokenizer->token_table[token_id];
+}
+
+void tokenizer_free(Tokenizer* tokenizer) {
+    if (tokenizer->init_ok) tokenizer_release(tokenizer, tokenizer->vocab_size);
+    tokenizer->init_ok = 0;
+}
+
+/* paged_infer.c:930-935 */
+void print_generated_sequence(int* tokens, int B, int T) {
+    for (int i = 0; i < B * T; i++) {
+        printf("%d ", tokens[i]);
+        if ((i + 1) % T == 0) printf("\n");
+    }
 }
 
 /* ------------------------------------------------------------------------ */

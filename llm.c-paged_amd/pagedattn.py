@@ -198,6 +198,12 @@ def lib():
     _sig(L, "gpt2_num_parameters", sz, [GPT2Config])
     _sig(L, "gpt2_synthetic_params", i, [GPT2Config, ctypes.c_ulonglong, _F])
     _sig(L, "gpt2_write_checkpoint", i, [ctypes.c_char_p, GPT2Config, _F])
+    _sig(L, "gpt2_write_checkpoint_ex", i, [ctypes.c_char_p, GPT2Config, _F, i])
+    _sig(L, "gpt2_read_checkpoint", i, [ctypes.c_char_p, ctypes.POINTER(GPT2Config), _F])
+    _sig(L, "tokenizer_init", None, [v, ctypes.c_char_p])
+    _sig(L, "tokenizer_decode", ctypes.c_char_p, [v, ctypes.c_uint32])
+    _sig(L, "tokenizer_free", None, [v])
+    _sig(L, "safe_printf", None, [ctypes.c_char_p])
     _sig(L, "gpt2_build_from_params", i, [v, GPT2Config, _F])
     _sig(L, "gpt2_build_synthetic", i, [v, GPT2Config, ctypes.c_ulonglong])
     _sig(L, "gpt2_build_from_checkpoint", None, [v, ctypes.c_char_p])
@@ -404,6 +410,40 @@ class Pool:
             pass
 
 
+# ---------------------------------------------------------------- on-disk formats
+def read_checkpoint(path):
+    """gpt2_read_checkpoint (host only): (GPT2Config, fp32 params in
+    ParameterTensors order) from a v1 or v2 checkpoint"""
+    c = GPT2Config()
+    check(lib().gpt2_read_checkpoint(str(path).encode(), ctypes.byref(c), None), "read_checkpoint header")
+    p = np.empty(lib().gpt2_num_parameters(c), np.float32)
+    check(lib().gpt2_read_checkpoint(str(path).encode(), ctypes.byref(c), p.ctypes.data_as(_F)), "read_checkpoint")
+    return c, p
+
+
+def write_checkpoint(path, c, params, version=1):
+    p = np.ascontiguousarray(params, np.float32)
+    check(lib().gpt2_write_checkpoint_ex(str(path).encode(), c, p.ctypes.data_as(_F), int(version)),
+          "write_checkpoint")
+
+
+class Tokenizer(ctypes.Structure):
+    """paged_infer.c:852-856"""
+    _fields_ = [("vocab_size", ctypes.c_uint32), ("token_table", ctypes.POINTER(ctypes.c_char_p)),
+                ("init_ok", ctypes.c_int)]
+
+    def __init__(self, path):
+        super().__init__()
+        lib().tokenizer_init(ctypes.byref(self), str(path).encode())
+
+    def decode(self, token_id):
+        """the token's bytes, or None (not initialised / out of range)"""
+        return lib().tokenizer_decode(ctypes.byref(self), int(token_id))
+
+    def free(self):
+        lib().tokenizer_free(ctypes.byref(self))
+
+
 # ---------------------------------------------------------------- block manager
 class BlockManager:
     """block_manager.c API (create_block_manager, request_block, ...)."""
@@ -448,10 +488,13 @@ class Model:
 
     def __init__(self, cfg, params=None, seed=1337, checkpoint=None):
         L = lib()
+        if checkpoint is not None:  # config from the file's header
+            cfg = GPT2Config()
+            check(L.gpt2_read_checkpoint(str(checkpoint).encode(), ctypes.byref(cfg), None), "checkpoint header")
         self.cfg = cfg if isinstance(cfg, GPT2Config) else config(cfg)
         self.h = L.gpt2_alloc()
         if checkpoint is not None:
-            L.gpt2_build_from_checkpoint(self.h, checkpoint.encode())
+            L.gpt2_build_from_checkpoint(self.h, str(checkpoint).encode())
         elif params is not None:
             p = np.ascontiguousarray(params, np.float32)
             assert p.size == L.gpt2_num_parameters(self.cfg)
