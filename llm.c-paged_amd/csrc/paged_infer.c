@@ -573,6 +573,12 @@ void print_generated_sequence(int* tokens, int B, int T) {
  * activations, so one lane's HBM-bound attention overlaps another lane's
  * latency-bound GEMMs.  Lane 0 runs on the launch stream; the others fork from
  * it and join back (captured into the same graph as parallel branches). */
+/* manager page index -> pool slot (page_map_create) */
+typedef struct {
+    HpaKVPool* pool;
+    int* map;
+} PageView;
+
 #define DEC_MAX_LANES 8
 typedef struct {
     int r0, B, Mp;
@@ -599,6 +605,7 @@ struct GPT2Decode {
     int* h_pos;       /* host mirror of d_pos */
     int* h_stage;     /* pinned staging: tokens / next */
     int* h_bt_stage;  /* pinned staging for block-table rows */
+    PageView pv;      /* manager page index -> pool slot (page_map_create) */
     float *d_res, *d_res2, *d_ln, *d_q, *d_att, *d_fch, *d_part, *d_logits;
     int split[4];     /* qkv, attproj, fc, fcproj */
     /* fused path (hpa_gemm_fused): frag-layout weights and activations */
@@ -627,11 +634,31 @@ struct GPT2Decode {
 };
 
 /* the pool view backend: page payload pointers are layer-0 tiles in HBM */
+/* the manager's page index -> pool slot: a fixed pseudo-random permutation,
+ * so that whatever order pages are allocated in (first-fit hands each
+ * sequence a contiguous run) the K/V streams of concurrent workgroups spread
+ * over the HBM channels instead of walking them in lockstep at a
+ * power-of-two stride (measured: attention 68.5 us with contiguous runs of
+ * 64 pages vs 62.5 us scattered, config 2) */
+static int* page_map_create(int n) {
+    int* map = (int*)malloc((size_t)n * sizeof(int));
+    if (!map) return NULL;
+    for (int i = 0; i < n; i++) map[i] = i;
+    unsigned long long st = 0x9E3779B97F4A7C15ull;
+    for (int i = n - 1; i > 0; i--) { /* Fisher-Yates with the reference's xorshift */
+        const int j = (int)(random_u32(&st) % (unsigned)(i + 1));
+        const int t = map[i];
+        map[i] = map[j];
+        map[j] = t;
+    }
+    return map;
+}
+
 static void* pool_view_alloc(void* ctx, int page, int kv, size_t bytes) {
     (void)bytes;
-    HpaKVPool* pool = (HpaKVPool*)ctx;
-    if (page < 0 || page >= pool->num_pages) return NULL;
-    return hpa_pool_tile(pool, 0, page, kv, 0);
+    PageView* v = (PageView*)ctx;
+    if (page < 0 || page >= v->pool->num_pages) return NULL;
+    return hpa_pool_tile(v->pool, 0, v->map[page], kv, 0);
 }
 static void pool_view_release(void* ctx, int page, int kv, void* p) {
     (void)ctx; (void)page; (void)kv; (void)p;
@@ -722,6 +749,7 @@ static void dec_free(GPT2Decode* d) {
     hpa_event_destroy(d->ev_fork);
     hpa_host_free(d->h_stage);
     hpa_host_free(d->h_bt_stage);
+    free(d->pv.map);
     free(d->h_pos);
     if (d->own_bm) destroy_block_manager(d->bm);
     free(d);
@@ -840,7 +868,15 @@ int gpt2_decode_init_ex(GPT2* model, int B, int page_size, int max_ctx, int kv_d
     /* pages of this manager are views into the pool from now on */
     for (int p = 0; p < d->bm->max_prompts; p++)
         if (d->bm->prompt_block_count[p]) free_blocks_for_prompt(d->bm, p);
-    BMPageBackend be = {pool_view_alloc, pool_view_release, &d->pool};
+    d->pv.pool = &d->pool;
+    d->pv.map = page_map_create(num_pages);
+    if (!d->pv.map) {
+        hpa_pool_destroy(&d->pool);
+        if (d->own_bm) destroy_block_manager(d->bm);
+        free(d);
+        return 1;
+    }
+    BMPageBackend be = {pool_view_alloc, pool_view_release, &d->pv};
     bm_set_backend(d->bm, &be);
     d->bt_stride = d->bm->max_blocks_per_prompt;
     int C = c.channels, V = c.vocab_size;
@@ -900,7 +936,10 @@ static int dec_sync_block_table(GPT2Decode* d) {
     /* the staging copy must not be overwritten while a previous async copy
      * may still read it: wait for the stream's earlier work first */
     if (hpa_synchronize()) return 1;
-    memcpy(d->h_bt_stage + lo, m->block_table + lo, n * sizeof(int));
+    for (size_t i = 0; i < n; i++) {
+        const int v = m->block_table[lo + i];
+        d->h_bt_stage[lo + i] = v >= 0 ? d->pv.map[v] : -1;
+    }
     if (hpa_memcpy_async(d->d_bt + lo, d->h_bt_stage + lo, n * sizeof(int))) return 1;
     bm_clear_dirty(m);
     return 0;
