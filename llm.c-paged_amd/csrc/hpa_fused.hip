@@ -312,14 +312,14 @@ inline dim3 xcd_grid(FG& p, int gx, int gy) {
     return dim3((unsigned)(((gx + 7) / 8) * 8 * gy));
 }
 
-template <int NW, int MT, int NTW = 1>
+template <int NW, int MT, int NTW = 1, int UD = 0>
 int launch16(FG p, int epi) {
     dim3 grid = xcd_grid(p, (p.ntn + NTW - 1) / NTW, p.Mp / 16 / MT), block(NW * 64);
     switch (epi) {
-        case HPA_FEPI_QKV: gemm16_kernel<NW, HPA_FEPI_QKV, MT, NTW><<<grid, block, 0, hpa_stream()>>>(p); break;
-        case HPA_FEPI_RESID: gemm16_kernel<NW, HPA_FEPI_RESID, MT, NTW><<<grid, block, 0, hpa_stream()>>>(p); break;
-        case HPA_FEPI_GELU: gemm16_kernel<NW, HPA_FEPI_GELU, MT, NTW><<<grid, block, 0, hpa_stream()>>>(p); break;
-        case HPA_FEPI_LOGITS: gemm16_kernel<NW, HPA_FEPI_LOGITS, MT, NTW><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_QKV: gemm16_kernel<NW, HPA_FEPI_QKV, MT, NTW, UD><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_RESID: gemm16_kernel<NW, HPA_FEPI_RESID, MT, NTW, UD><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_GELU: gemm16_kernel<NW, HPA_FEPI_GELU, MT, NTW, UD><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_LOGITS: gemm16_kernel<NW, HPA_FEPI_LOGITS, MT, NTW, UD><<<grid, block, 0, hpa_stream()>>>(p); break;
         default: return hpa_fail(__FILE__, __LINE__, "gemm_fused: unknown epilogue");
     }
     HPA_LAUNCH_CHECK();
@@ -356,10 +356,11 @@ int launch_os(const FG& p, int epi, int nw) {
 // multi-column-tile instances: (waves, row_blocks, col_tiles) in
 // {(4|8, 4, 2), (4|8, 2, 2), (4, 4, 4)} -- the rest exceed LDS or registers
 template <int NW>
-int launch16_mt(const FG& p, int epi, int mt, int ntw) {
+int launch16_mt(const FG& p, int epi, int mt, int ntw, bool deep) {
+    if constexpr (NW > 8) deep = false;  // 1024-thread groups: no registers for larger trips
     if constexpr (NW <= 8) {
-        if (ntw == 2 && mt == 4) return launch16<NW, 4, 2>(p, epi);
-        if (ntw == 2 && mt == 2) return launch16<NW, 2, 2>(p, epi);
+        if (ntw == 2 && mt == 4) return deep ? launch16<NW, 4, 2, 2>(p, epi) : launch16<NW, 4, 2>(p, epi);
+        if (ntw == 2 && mt == 2) return deep ? launch16<NW, 2, 2, 4>(p, epi) : launch16<NW, 2, 2>(p, epi);
     }
     if constexpr (NW == 4) {
         if (ntw == 4 && mt == 4) return launch16<NW, 4, 4>(p, epi);
@@ -368,9 +369,9 @@ int launch16_mt(const FG& p, int epi, int mt, int ntw) {
         return hpa_fail(__FILE__, __LINE__,
                         "gemm_fused: col_tiles 2 needs waves 4/8 and row_blocks 2/4; 4 needs waves 4, row_blocks 4");
     switch (mt) {
-        case 1: return launch16<NW, 1>(p, epi);
-        case 2: return launch16<NW, 2>(p, epi);
-        case 4: return launch16<NW, 4>(p, epi);
+        case 1: return deep ? launch16<NW, 1, 1, 8>(p, epi) : launch16<NW, 1>(p, epi);
+        case 2: return deep ? launch16<NW, 2, 1, 8>(p, epi) : launch16<NW, 2>(p, epi);
+        case 4: return deep ? launch16<NW, 4, 1, 4>(p, epi) : launch16<NW, 4>(p, epi);
         default: return hpa_fail(__FILE__, __LINE__, "gemm_fused: row_blocks must be 1, 2 or 4");
     }
 }
@@ -443,7 +444,8 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
     int mt = g->row_blocks ? g->row_blocks : pick[1];
     HPA_REQUIRE(mt == 1 || mt == 2 || mt == 4, "gemm_fused: row_blocks must be 1, 2 or 4");
     while ((p.Mp / 16) % mt) mt >>= 1;  // row blocks of this M
-    HPA_REQUIRE(g->variant >= 0 && g->variant <= 2, "gemm_fused: variant must be 0, 1 or 2");
+    HPA_REQUIRE(g->variant >= 0 && g->variant <= 4, "gemm_fused: variant must be 0 .. 4");
+    if (g->variant == 4 && logits_resident_eligible(p, g->epilogue)) return launch_logits_resident(p);
     HPA_REQUIRE(g->col_tiles == 0 || g->col_tiles == 1 || g->col_tiles == 2 || g->col_tiles == 4,
                 "gemm_fused: col_tiles must be 1, 2 or 4");
     if (g->variant == 2 || (g->variant == 0 && mt == 1 && p.ntn < 1024 && g->col_tiles <= 1)) {
@@ -455,12 +457,13 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
     // a launch-shape hint: where this M's row blocks (or the waves) cannot
     // carry it, fall back to one column tile (results are identical)
     if ((ntw == 2 && (mt == 1 || nw == 16)) || (ntw == 4 && (mt != 4 || nw != 4))) ntw = 1;
+    const bool deep = g->variant == 3;  // looped with larger trips (same results as 1)
     switch (nw) {
-        case 4: return launch16_mt<4>(p, g->epilogue, mt, ntw);
-        case 8: return launch16_mt<8>(p, g->epilogue, mt, ntw);
+        case 4: return launch16_mt<4>(p, g->epilogue, mt, ntw, deep);
+        case 8: return launch16_mt<8>(p, g->epilogue, mt, ntw, deep);
         case 16:
             HPA_REQUIRE(ntw == 1, "gemm_fused: col_tiles > 1 needs waves 4 or 8");
-            return launch16_mt<16>(p, g->epilogue, mt, ntw);
+            return launch16_mt<16>(p, g->epilogue, mt, ntw, deep);
         default: return hpa_fail(__FILE__, __LINE__, "gemm_fused: waves must be 4, 8 or 16");
     }
 }

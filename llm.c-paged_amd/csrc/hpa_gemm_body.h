@@ -216,12 +216,14 @@ constexpr int gemm16_lds_floats() {
 
 // body of the looped GEMM workgroup `bid` of the XCD-ordered 1-D grid
 // (gemm16_kernel, and the GEMM role of the pipelined combo launches)
-template <int NW, int EPI, int MT, int NTW>
+template <int NW, int EPI, int MT, int NTW, int UD = 0>
 __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
     constexpr int NT = NW * 64;
     constexpr int R = MT * 16;  // rows per workgroup
-    // k-steps per trip (two trips in flight; register budget)
-    constexpr int U = NTW > 1 ? 1 : (NW >= 16 ? (MT == 4 ? 1 : 2) : (MT == 4 ? 2 : 4));
+    // k-steps per trip (two trips in flight; register budget); UD > 0: the
+    // "deep" variant's larger trips (more bytes in flight per wave for the
+    // MFMA-bound shapes)
+    constexpr int U = UD > 0 ? UD : (NTW > 1 ? 1 : (NW >= 16 ? (MT == 4 ? 1 : 2) : (MT == 4 ? 2 : 4)));
     float* lngb = smem;                              // LN weight [K], bias [K]
     float* red = smem + 2 * HPA_FUSED_LN_KMAX;       // [NW][NTW][MT rb x 4 reg][64 lanes]
     float* tile = red + NW * MT * NTW * 256;         // [NTW][R rows][17]
@@ -369,10 +371,10 @@ __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
     epi.finish(p, acc, red, tile, nt0, row0);
 }
 
-template <int NW, int EPI, int MT, int NTW>
+template <int NW, int EPI, int MT, int NTW, int UD = 0>
 __global__ __launch_bounds__(NW * 64) void gemm16_kernel(FG p) {
     __shared__ __attribute__((aligned(16))) float smem[gemm16_lds_floats<NW, MT, NTW>()];
-    gemm16_body<NW, EPI, MT, NTW>(p, blockIdx.x, smem);
+    gemm16_body<NW, EPI, MT, NTW, UD>(p, blockIdx.x, smem);
 }
 
 // One-shot variant for the layer GEMMs (one 16-row block per workgroup,
@@ -505,6 +507,10 @@ __global__ __launch_bounds__(NW * 64) void gemm16_os_kernel(FG p) {
 
 // validate a HpaFusedGemm and build the kernel argument block (gx/gy are
 // set by the launcher); nonzero (with hpa_last_error) on a bad description
+// the activation-resident logits kernel (hpa_logits.hip, variant 4)
+bool logits_resident_eligible(const FG& p, int epi);
+int launch_logits_resident(const FG& p);
+
 static inline int fused_prepare(const HpaFusedGemm* g, FG* p) {
     HPA_REQUIRE(g && g->x && g->w && g->out, "gemm_fused: null operand");
     HPA_REQUIRE(g->M > 0 && g->N > 0 && g->K > 0 && g->K % 16 == 0, "gemm_fused: K % 16 != 0");

@@ -1086,6 +1086,7 @@ static void lane_gemm(GPT2* model, int li, int l, int which, HpaFusedGemm* g) {
             g->x = ln->res; g->K = C; g->ln_stats = ln->st1; g->ln_ntiles = c.num_layers == 0 ? 1 : ct;
             g->ln_w = w->lnfw; g->ln_b = w->lnfb; g->w = d->d_wpack + d->wpack_off[4]; g->N = V;
             g->out = d->d_logits + (size_t)ln->r0 * V; g->part_out = ln->part; g->layer = 0;
+            g->variant = 4; /* activation-resident kernel where the shape allows (hpa_logits.hip) */
             break;
     }
 }

@@ -16,7 +16,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpaged_hip.so")
+LIB_PATH = os.environ.get("HPA_LIB") or os.path.join(HERE, "libpaged_hip.so")  # HPA_LIB: tool A/B builds
 INCLUDE_DIR = os.path.join(os.path.dirname(HERE), "include")
 
 _F = ctypes.POINTER(ctypes.c_float)

@@ -164,6 +164,27 @@ def test_fused_logits_argmax(hip, M, waves, rb, ct):
     assert np.array_equal(ids, got.argmax(-1))
 
 
+@pytest.mark.parametrize("M", [64, 37, 16, 1])
+def test_logits_resident_kernel(hip, M):
+    """variant 4 (activation-resident, 16 waves, hpa_logits.hip): logits
+    within the fp32 bound of the float64 reference, argmax partials consistent,
+    and within rounding of the looped kernel"""
+    L = hip.lib()
+    rng = np.random.default_rng(11)
+    K, N = 768, 50257
+    out, acc, bound, keep = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, 0, ln=True, rng=rng, variant=4)
+    got = out.download((M, N))
+    assert np.all(np.abs(got - acc) <= bound)
+    part = keep[-2]
+    nxt = hip.DeviceBuffer(M * 4)
+    Mp = (M + 15) // 16 * 16
+    hip.check(L.hpa_argmax_final(part.ptr, (N + 15) // 16, Mp, M, nxt.ptr, None, None, None))
+    assert np.array_equal(nxt.download(M, np.int32), got.argmax(-1))
+    rng = np.random.default_rng(11)
+    out1, _, _, keep1 = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, 4, ln=True, rng=rng, rb=1, variant=1)
+    assert np.abs(out1.download((M, N)) - got).max() <= 2e-5
+
+
 def test_fused_qkv_appends_into_pages(hip):
     rng = np.random.default_rng(9)
     NH, P = 2, 16

@@ -99,10 +99,14 @@ def main():
         ref = None
         for waves in (4, 8, 16):
             for rb in (1, 2, 4):
-                for variant in (1, 2):
+                for variant in (1, 2, 3, 4):
                     for ct in (1, 2, 4):
                         if ((M + 15) // 16) % rb or (variant == 2 and (rb != 1 or ct != 1)):
                             continue
+                        if variant == 3 and (waves == 16 or ct == 4):  # deep = looped there
+                            continue
+                        if variant == 4 and (epi != pa.HPA_FEPI_LOGITS or (waves, rb, ct) != (4, 1, 1)):
+                            continue  # resident logits kernel: one launch shape
                         if ct > 1 and (waves == 16 or rb == 1 or (ct == 4 and (rb != 4 or waves != 4))):
                             continue
                         g.waves, g.row_blocks, g.variant, g.col_tiles = waves, rb, variant, ct
