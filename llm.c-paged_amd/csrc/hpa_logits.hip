@@ -43,6 +43,15 @@ __device__ __forceinline__ float4 load_nt4(const float4* ptr) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
+template <int CTRL>
+__device__ __forceinline__ void dpp_argmax(float& bv, int& bi) {
+    const float v2 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(bv), CTRL, 0xF, 0xF, false));
+    const int i2 = __builtin_amdgcn_mov_dpp(bi, CTRL, 0xF, 0xF, false);
+    const bool take = v2 > bv || (v2 == bv && i2 < bi);
+    bv = take ? v2 : bv;
+    bi = take ? i2 : bi;
+}
+
 template <int MT>
 constexpr int resident_lds_floats() {
     return 2 * kResNW * MT * 256 + 10 * MT * 16;
@@ -187,9 +196,12 @@ __global__ __launch_bounds__(kResNW * 64) void logits_resident_kernel(FG p) {
         for (int e = threadIdx.x; e < MT * 256; e += kResNW * 64) {  // whole waves (multiples of 64)
             const int frow = 16 * (e >> 8) + 4 * ((e & 63) >> 4) + ((e >> 6) & 3);
             const int fcol = e & 15;
-            float val = rb[e];
+            float part[kResNW];  // all partials in flight at once, then the fixed-order sum
 #pragma unroll
-            for (int ww = 1; ww < kResNW; ++ww) val += rb[ww * MT * 256 + e];
+            for (int ww = 0; ww < kResNW; ++ww) part[ww] = rb[ww * MT * 256 + e];
+            float val = part[0];
+#pragma unroll
+            for (int ww = 1; ww < kResNW; ++ww) val += part[ww];
             const int col = t * 16 + fcol;
             const bool live = frow < p.M && col < p.N;
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), out_rs,
@@ -197,14 +209,13 @@ __global__ __launch_bounds__(kResNW * 64) void logits_resident_kernel(FG p) {
             // per-tile (max, argmax) of the row: first max wins (paged_infer.c:937-951)
             float bv = live ? val : -INFINITY;
             int bi = fcol;
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) {
-                const float v2 = __shfl_xor(bv, o, 64);
-                const int i2 = __shfl_xor(bi, o, 64);
-                const bool take = v2 > bv || (v2 == bv && i2 < bi);
-                bv = take ? v2 : bv;
-                bi = take ? i2 : bi;
-            }
+            // butterfly over the 16 lanes of the row with DPP (no LDS): mirror
+            // within 16, mirror within 8, then quad xor 2 and xor 1 cover all
+            // 16 lanes; (max, lowest index) is order-independent
+            dpp_argmax<0x140>(bv, bi);  // row_mirror
+            dpp_argmax<0x141>(bv, bi);  // row_half_mirror
+            dpp_argmax<0x4E>(bv, bi);   // quad_perm [2,3,0,1]
+            dpp_argmax<0xB1>(bv, bi);   // quad_perm [1,0,3,2]
             typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
             const u32x2 pv = {__float_as_uint(bv), (unsigned int)(t * 16 + bi)};
             __builtin_amdgcn_raw_buffer_store_b64(pv, part_rs,
