@@ -2,9 +2,6 @@
 // hpa_fused.hip for the design notes).  Shared by hpa_fused.hip (stand-alone
 // launches) and hpa_combo.hip (the GEMM role of the pipelined launches).
 #pragma once
-#ifndef HPA_OS_NT
-#define HPA_OS_NT 0  // one-shot weight loads non-temporal (A/B builds only)
-#endif
 #include <math.h>
 
 #include "hpa_internal.h"
@@ -434,15 +431,7 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
     float4 wv[S], xv[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-#if HPA_OS_NT
-        {  // A/B experiment: non-temporal weight loads
-            typedef float v4 __attribute__((ext_vector_type(4)));
-            const v4 t = __builtin_nontemporal_load(reinterpret_cast<const v4*>(wf + s * 64));
-            wv[s] = make_float4(t.x, t.y, t.z, t.w);
-        }
-#else
-        wv[s] = wf[s * 64];
-#endif
+        wv[s] = wf[s * 64];  // default policy: nt measured no faster here (tools/ab_bench.sh)
         xv[s] = xf[s * 64];
     }
     // 4. epilogue operands
