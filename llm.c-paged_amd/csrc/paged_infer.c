@@ -639,17 +639,23 @@ struct GPT2Decode {
  * sequence a contiguous run) the K/V streams of concurrent workgroups spread
  * over the HBM channels instead of walking them in lockstep at a
  * power-of-two stride (measured: attention 68.5 us with contiguous runs of
- * 64 pages vs 62.5 us scattered, config 2) */
-static int* page_map_create(int n) {
+ * 64 pages vs 62.5 us scattered, config 2).  Small page tiles (1 KiB per
+ * head: bf16, page 8) stream better with 16 consecutive pages kept together
+ * (config 5: 0.844 of 8 TB/s grouped by 16, 0.839 by 4, 0.833 single pages;
+ * config 2: 0.813 single, 0.806 by 4, 0.787 by 16). */
+static int* page_map_create(int n, int G) {
     int* map = (int*)malloc((size_t)n * sizeof(int));
     if (!map) return NULL;
+    const int ng = n / G; /* groups of G consecutive pages move together; a tail stays in place */
     for (int i = 0; i < n; i++) map[i] = i;
     unsigned long long st = 0x9E3779B97F4A7C15ull;
-    for (int i = n - 1; i > 0; i--) { /* Fisher-Yates with the reference's xorshift */
+    for (int i = ng - 1; i > 0; i--) { /* Fisher-Yates over groups with the reference's xorshift */
         const int j = (int)(random_u32(&st) % (unsigned)(i + 1));
-        const int t = map[i];
-        map[i] = map[j];
-        map[j] = t;
+        for (int k = 0; k < G; k++) {
+            const int t = map[i * G + k];
+            map[i * G + k] = map[j * G + k];
+            map[j * G + k] = t;
+        }
     }
     return map;
 }
@@ -869,7 +875,10 @@ int gpt2_decode_init_ex(GPT2* model, int B, int page_size, int max_ctx, int kv_d
     for (int p = 0; p < d->bm->max_prompts; p++)
         if (d->bm->prompt_block_count[p]) free_blocks_for_prompt(d->bm, p);
     d->pv.pool = &d->pool;
-    d->pv.map = page_map_create(num_pages);
+    {
+        const size_t tile_bytes = (size_t)page_size * 64 * d->pool.elem_bytes; /* one head's K of a page */
+        d->pv.map = page_map_create(num_pages, tile_bytes >= 4096 ? 1 : 16);
+    }
     if (!d->pv.map) {
         hpa_pool_destroy(&d->pool);
         if (d->own_bm) destroy_block_manager(d->bm);

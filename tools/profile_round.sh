@@ -1,0 +1,25 @@
+#!/bin/bash
+# The round's evidence on one GPU box: bench lines of every single-GPU
+# BASELINE config, the rocprofv3 kernel stats of the headline bench command,
+# PMC traffic (configs 2 and 5), prefill and sampling lines.
+# usage: tools/profile_round.sh <outdir>      (then copy into profiles/rNN/)
+set -u
+out=$1; mkdir -p "$out"
+export TMPDIR=/tmp
+step() {  # name, timeout, command...
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 $lim "$@" > "$out/$name.log" 2>&1
+  local rc=$?; echo "$name rc=$rc"
+  case $rc in 0) ;; *) tail -5 "$out/$name.log"; exit $rc;; esac
+}
+step bench_c2 400 python bench.py
+grep "^{" "$out/bench_c2.log" > "$out/bench_line.json"
+step prof_c2 400 rocprofv3 --kernel-trace --stats -d "$out/prof_c2" -o run --output-format csv -- \
+  python3 bench.py --cpu-baseline off
+step pmc_c2 900 bash tools/pmc_traffic.sh "$out/pmc_c2" --steps 8 --warmup 2
+step bench_c5 500 python bench.py --batch 256 --ctx 2048 --page-size 8 --kv-dtype bf16
+step bench_xl 600 python bench.py --model XL --page-size 32 --cpu-baseline off
+step bench_prefill 400 python bench.py --prefill real --cpu-baseline off
+step bench_sample 400 python bench.py --sample --cpu-baseline off
+python3 tools/kstats.py "$out/prof_c2/run_kernel_trace.csv" > "$out/kstats_c2.txt"
+echo done
