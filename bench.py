@@ -6,7 +6,8 @@ B=64, ctx 1024, page 16, fp32, on 1/2/4/8 MI355X (configs[1] at N=1).  For
 N>1 the decode shards by sequence (SURVEY.md 8e, configs[3]): every rank
 decodes its own 64 sequences out of its own page pool with replicated
 weights -> weak scaling; the one collective is the end-of-step RCCL gather
-of the logits to rank 0 (--gather ids: greedy ids only).  --scaling strong
+of the logits to rank 0 (--gather ids: greedy ids only), double-buffered on
+its own stream so that step k's gather overlaps step k+1.  --scaling strong
 splits a fixed global batch instead.
 
 One "step" = one decode step of the whole batch: every sequence gets one new
@@ -211,9 +212,12 @@ def main():
     pos_now = [start]
 
     gather = None
+    nstep = [0]
     if world > 1 and args.gather != "none":
-        gather = shard.StepGather(dist, world, rank, counts, cfgd["V"], args.gather, "cuda")
-        send = gather.buffer()
+        # double-buffered: step k's output is copied on the compute stream,
+        # then gathered on a comm stream while step k+1 computes
+        gather = shard.StepGather(dist, world, rank, counts, cfgd["V"], args.gather, "cuda", nbuf=2)
+        comm = torch.cuda.Stream()
         src, nbytes = ((model.logits_ptr(), B_local * cfgd["V"] * 4) if args.gather == "logits"
                        else (model.next_ptr(), B_local * 4))
 
@@ -223,9 +227,14 @@ def main():
             pos_now[0] = start
         model.step_async(tokens)
         pos_now[0] += 1
-        if gather is not None:  # copy on the shared stream, then RCCL gather to rank 0
-            L.hpa_memcpy_async(send.data_ptr(), src, nbytes)
-            gather.gather()
+        if gather is not None:
+            i = nstep[0] % 2
+            gather.wait(i)  # the compute stream waits for the gather that last used buffer i
+            L.hpa_memcpy_async(gather.buffer(i).data_ptr(), src, nbytes)  # compute stream
+            comm.wait_stream(stream)
+            with torch.cuda.stream(comm):  # RCCL gather to rank 0, overlapped with the next step
+                gather.gather(i, async_op=True)
+        nstep[0] += 1
 
     def sync():
         pagedattn.check(L.hpa_synchronize(), "sync")
@@ -312,7 +321,7 @@ def main():
                                       "configs[1])" if world == 1 else "configs[3]: per-seq sharded pool)"),
                        "global_batch": B, "batch_per_gpu": B_local, "seq_len": ctx, "page_size": P,
                        "decode_positions": f"{start}..{start + args.warmup + args.steps - 1}",
-                       "parallelism": f"seq-shard x{world}" + (f" + RCCL gather({args.gather}) to rank 0"
+                       "parallelism": f"seq-shard x{world}" + (f" + RCCL gather({args.gather}) to rank 0, overlapped with the next step"
                                                                if world > 1 and args.gather != "none" else ""),
                        "hip_graph": not args.no_graph, "gemm_path": "unfused" if args.unfused else "fused",
                        "lanes": 1 if args.unfused else L.gpt2_decode_lanes(model.h),

@@ -36,9 +36,15 @@ class StepGather:
     greedy ids ("ids"); "none" skips the collective.  Ranks may hold
     different numbers of sequences (strong scaling with B % world != 0): the
     gather is over padded [max_local, ...] buffers and rank 0 trims them.
-    `src` tensors live on `device` ("cuda" for RCCL, "cpu" for gloo)."""
+    `src` tensors live on `device` ("cuda" for RCCL, "cpu" for gloo).
 
-    def __init__(self, dist, world, rank, counts, V, mode, device):
+    nbuf = 2 double-buffers the step output so the gather of step k can run
+    asynchronously (async_op) while step k+1 computes: gather(i, async_op=True)
+    returns once the collective is queued; before buffer i is refilled,
+    wait(i) orders the refill after that collective (on RCCL: the caller's
+    current stream waits for it; the host does not block)."""
+
+    def __init__(self, dist, world, rank, counts, V, mode, device, nbuf=1):
         import torch
         self.dist, self.world, self.rank, self.mode = dist, world, rank, mode
         self.counts = list(counts)
@@ -46,26 +52,37 @@ class StepGather:
         self.V = V
         width = V if mode == "logits" else 1
         dtype = torch.float32 if mode == "logits" else torch.int32
-        self.send = torch.zeros(self.max_local, width, dtype=dtype, device=device)
-        self.recv = None
+        self.send = [torch.zeros(self.max_local, width, dtype=dtype, device=device) for _ in range(nbuf)]
+        self.recv = [None] * nbuf
         if rank == 0 and mode != "none":
-            self.recv = [torch.zeros_like(self.send) for _ in range(world)]
+            self.recv = [[torch.zeros_like(self.send[0]) for _ in range(world)] for _ in range(nbuf)]
+        self.work = [None] * nbuf
 
-    def buffer(self):
-        """the [max_local, width] send buffer the step's output is copied into"""
-        return self.send
+    def buffer(self, i=0):
+        """the [max_local, width] send buffer i the step's output is copied into"""
+        return self.send[i]
 
-    def gather(self):
+    def wait(self, i=0):
+        """order the next use of buffer i after its outstanding gather"""
+        if self.work[i] is not None:
+            self.work[i].wait()
+            self.work[i] = None
+
+    def gather(self, i=0, async_op=False):
         if self.mode == "none" or self.world == 1:
             return
-        self.dist.gather(self.send, gather_list=self.recv, dst=0)
+        self.wait(i)
+        w = self.dist.gather(self.send[i], gather_list=self.recv[i], dst=0, async_op=async_op)
+        if async_op:
+            self.work[i] = w
 
-    def result(self):
-        """rank 0: the gathered [B, V] logits or [B] ids in global sequence order"""
+    def result(self, i=0):
+        """rank 0: the gathered [B, V] logits or [B] ids in global sequence
+        order (after wait(i) for an asynchronous gather)"""
         import torch
         if self.rank != 0 or self.mode == "none":
             return None
-        parts = [self.send[:self.counts[0]]] if self.world == 1 else \
-            [r[:n] for r, n in zip(self.recv, self.counts)]
+        parts = [self.send[i][:self.counts[0]]] if self.world == 1 else \
+            [r[:n] for r, n in zip(self.recv[i], self.counts)]
         out = torch.cat(parts, 0)
         return out if self.mode == "logits" else out[:, 0]

@@ -31,7 +31,7 @@ def _tokens(B, steps, V):
     return np.random.default_rng(123).integers(0, V, (steps, B)).astype(np.int32)
 
 
-def _worker(rank, world, port, batch, scaling, mode, out_path):
+def _worker(rank, world, port, batch, scaling, mode, out_path, nbuf=1):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -43,19 +43,29 @@ def _worker(rank, world, port, batch, scaling, mode, out_path):
         params = synth.params(SMALL, seed=5)
         c = oc.cfg(SMALL["maxT"], SMALL["V"], SMALL["L"], SMALL["NH"], SMALL["C"])
         dec = oc.PagedDecoder(params, c, hi - lo, 8, SMALL["maxT"], page_seed=17 + rank)
-        g = shard.StepGather(dist, world, rank, counts, SMALL["V"], mode, "cpu")
+        g = shard.StepGather(dist, world, rank, counts, SMALL["V"], mode, "cpu", nbuf=nbuf)
         toks = _tokens(B, STEPS, SMALL["V"])
         got = []
         for t in range(STEPS):
             nxt, logits = dec.step(toks[t, lo:hi])
-            buf = g.buffer()
+            i = t % nbuf
+            if nbuf > 1 and rank == 0 and t >= nbuf:  # the gather of step t - nbuf, read before reuse
+                g.wait(i)
+                got.append(g.result(i).numpy().copy())
+            g.wait(i)
+            buf = g.buffer(i)
             if mode == "logits":
                 buf[:hi - lo] = torch.from_numpy(logits)
             else:
                 buf[:hi - lo, 0] = torch.from_numpy(nxt)
-            g.gather()
-            if rank == 0:
+            g.gather(i, async_op=nbuf > 1)
+            if rank == 0 and nbuf == 1:
                 got.append(g.result().numpy().copy())
+        if nbuf > 1:  # drain: the last nbuf steps, in order
+            for t in range(STEPS - nbuf, STEPS):
+                g.wait(t % nbuf)
+                if rank == 0:
+                    got.append(g.result(t % nbuf).numpy().copy())
         dec.close()
         if rank == 0:
             np.save(out_path, np.stack(got))
@@ -76,12 +86,14 @@ def _unsharded(B, mode):
     return np.stack(out)
 
 
-@pytest.mark.parametrize("batch,scaling,mode", [(3, "weak", "logits"), (5, "strong", "logits"),
-                                                (4, "weak", "ids")])
-def test_two_rank_sharded_decode_equals_unsharded(tmp_path, batch, scaling, mode):
+@pytest.mark.parametrize("batch,scaling,mode,nbuf", [(3, "weak", "logits", 1), (5, "strong", "logits", 1),
+                                                     (4, "weak", "ids", 1), (3, "weak", "logits", 2)])
+def test_two_rank_sharded_decode_equals_unsharded(tmp_path, batch, scaling, mode, nbuf):
+    """nbuf = 2: the double-buffered asynchronous gather bench.py overlaps
+    with the next step"""
     world = 2
     out = str(tmp_path / "rank0.npy")
-    mp.start_processes(_worker, args=(world, _free_port(), batch, scaling, mode, out), nprocs=world,
+    mp.start_processes(_worker, args=(world, _free_port(), batch, scaling, mode, out, nbuf), nprocs=world,
                        join=True, start_method="spawn")
     got = np.load(out)
     B = batch * world if scaling == "weak" else batch
