@@ -86,6 +86,10 @@ def parse():
     ap.add_argument("--unfused", action="store_true", help="row-major GEMMs + separate row kernels")
     ap.add_argument("--lanes", type=int, default=1, help="micro-batch lanes (concurrent row groups)")
     ap.add_argument("--pipeline", type=int, default=0, help="1: two lanes, attention chunks beside GEMMs")
+    ap.add_argument("--overlap", type=int, default=0,
+                    help="overlapped step: chain workgroups beside the attention (0 = off)")
+    ap.add_argument("--split", type=int, default=0,
+                    help="split step: GEMM chains on this many CUs beside the attention (0 = off)")
     ap.add_argument("--sample", action="store_true",
                     help="multinomial sampling as the reference driver (default: greedy argmax)")
     ap.add_argument("--gemm-waves", default="", help="fused GEMM waves qkv,attproj,fc,fcproj,logits (0 = auto)")
@@ -207,6 +211,10 @@ def main():
     else:
         for p in range(start):
             model.step(rng.integers(0, cfgd["V"], B_local).astype(np.int32), want_next=False)
+    if args.split and not args.unfused:
+        model.set_split(args.split)
+    if args.overlap and not args.unfused:
+        model.set_overlap(args.overlap)
     model.set_graph(not args.no_graph)
     first = rng.integers(0, cfgd["V"], B_local).astype(np.int32)
     pos_now = [start]
@@ -326,6 +334,8 @@ def main():
                        "hip_graph": not args.no_graph, "gemm_path": "unfused" if args.unfused else "fused",
                        "lanes": 1 if args.unfused else L.gpt2_decode_lanes(model.h),
                        "pipeline": bool(L.gpt2_decode_pipeline(model.h)),
+                       "split_gemm_cus": 0 if args.unfused else L.gpt2_decode_split(model.h),
+                       "overlap_chain_blocks": 0 if args.unfused else L.gpt2_decode_overlap(model.h),
                        "token_choice": "multinomial (reference sample_mult)" if args.sample else "greedy",
                        "gemm_waves": [int(x) for x in model.gemm_config()[0]],
                        "gemm_row_blocks": [int(x) for x in model.gemm_config()[1]],

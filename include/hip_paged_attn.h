@@ -58,7 +58,11 @@ void* hpa_event_create_nt(void);          /* no timing: fork/join ordering only 
  * stream).  Inside a capture, fork/join through events pulls the other
  * stream into the same graph as parallel branches. */
 void* hpa_stream_create(void);
-int   hpa_stream_destroy(void* stream);
+int   hpa_stream_destroy(void* stream); /* CU-masked streams are cached per range: a no-op for them */
+/* a stream restricted to the CUs of mask bits [lo, hi) (hipExtStreamCreateWithCUMask;
+ * bits are dealt round-robin over the XCDs): the decode engine's split step
+ * runs attention and the GEMM chains on disjoint CU sets */
+void* hpa_stream_create_cumask(int lo, int hi);
 int   hpa_stream_wait_event(void* ev);
 const char* hpa_last_error(void);
 /* hipGraph capture of everything enqueued on the current stream between
@@ -286,6 +290,15 @@ typedef struct {
 } HpaAttnChunk;
 size_t hpa_attn_state_elems(int B, int num_heads);
 int hpa_attn_chunk_with_gemm(const HpaAttnChunk* a, const HpaFusedGemm* g);
+/* one launch of the overlapped decode step (hpa_lane.hip): the whole paged
+ * attention of one micro-batch lane (att, nchunks ignored; NULL = none) and
+ * the GEMM chain of the OTHER lane -- chain[0..nph-1] = attproj, fc, fcproj
+ * and optionally qkv of the next layer, 4-wave tiles -- on disjoint
+ * workgroups.  The chain's links are in-launch hand-offs counted in ctl
+ * (HPA_LANE_CTL_WORDS words, zeroed before the launch; ctl[1] != 0 after it
+ * reports an expired wait); chain_blocks persistent workgroups run it. */
+#define HPA_LANE_CTL_WORDS 32
+int hpa_lane_layer(const HpaAttnChunk* att, const HpaFusedGemm* chain, int nph, unsigned* ctl, int chain_blocks);
 
 /* ---------------- reference-layout kernels (drop-in compat) ----------------
  * Pages in the reference layout: token-major [block_size][C] per page

@@ -229,6 +229,22 @@ int    gpt2_decode_set_sampling(GPT2* model, int enable, unsigned long long seed
  * order).  Needs B > 16 and page size 8/16/32; disabling returns to 1 lane. */
 int    gpt2_decode_set_pipeline(GPT2* model, int enable);
 int    gpt2_decode_pipeline(GPT2* model);
+/* split step (fused path): two lanes on two CU-masked streams, the attention
+ * of one half of the batch beside the GEMM chains of the other, GEMMs on
+ * `gemm_cus` CUs and attention on the rest; launched eagerly (CU masks do not
+ * survive graph capture).  Rows bit-identical to one lane.  Needs B > 16;
+ * gemm_cus = 0 returns to one lane. */
+int    gpt2_decode_set_split(GPT2* model, int gemm_cus);
+int    gpt2_decode_split(GPT2* model);
+/* overlapped step (fused path, fp32 pool, 16 < B <= 128): two lanes on one
+ * stream; each launch runs one lane's attention of a layer beside the other
+ * lane's GEMM chain (hpa_lane_layer), 2 launches per layer.  chain_blocks =
+ * persistent chain workgroups; 0 returns to one lane.  Logits within the
+ * fp32 tolerance of the one-lane step (fcproj folds K over 4 waves here). */
+int    gpt2_decode_set_overlap(GPT2* model, int chain_blocks);
+int    gpt2_decode_overlap(GPT2* model);
+/* nonzero if an in-launch wait of the last overlapped step expired */
+unsigned gpt2_decode_overlap_faults(GPT2* model);
 /* algorithmic HBM bytes one step reads+writes at the current positions
  * (SURVEY.md 8d formula) and the attention kernel's share of them */
 double gpt2_decode_step_bytes(GPT2* model, double* attention_bytes);

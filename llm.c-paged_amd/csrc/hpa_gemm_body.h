@@ -6,6 +6,15 @@
 
 #include "hpa_internal.h"
 
+// phase timestamps of the one-shot body: empty in the library; the
+// tools/micro/os_trace.hip build defines it to record s_memrealtime per wave
+#ifndef HPA_TS
+#define HPA_TS(i, bid)
+#endif
+#ifndef HPA_OS_ORDER
+#define HPA_OS_ORDER 1
+#endif
+
 namespace hpa_gemm {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -49,6 +58,17 @@ __device__ __forceinline__ bool xcd_tile(const FG& p, int bid, int& cx, int& ry)
     return cx < p.gx;
 }
 
+// output store of an epilogue: WT = write-through (sc1), for outputs another
+// workgroup of the same launch consumes (hpa_lane.hip; MI355X_MICROARCH.md
+// "publish-large": sc1 stores + a drained counter instead of a release fence)
+template <bool WT>
+__device__ __forceinline__ void st_out(float* p, float v) {
+    if constexpr (WT)
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
+}
+
 __device__ __forceinline__ float4 ln4(float4 a, float mu, float rs, float4 g, float4 b) {
     // paged_infer.c:80-81: n = s * (x - m); o = n * w + b
     a.x = (rs * (a.x - mu)) * g.x + b.x;
@@ -64,7 +84,7 @@ __device__ __forceinline__ float4 ln4(float4 a, float mu, float rs, float4 g, fl
 // rb = e'>>8, reg = (e'>>6)&3, l = e'&63 -> row rb*16 + (l>>4)*4 + reg,
 // col l&15 (16x16 C/D map: col = lane & 15, row = 4*(lane >> 4) + reg).
 // Thread t owns e = t + i*NT.  Accumulator acc[j*MT + r] holds (tile j, block r).
-template <int NW, int EPI, int MT, int NTW = 1>
+template <int NW, int EPI, int MT, int NTW = 1, bool WT = false>
 struct Epi {
     static constexpr int NT = NW * 64;
     static constexpr int R = MT * 16;
@@ -155,10 +175,10 @@ struct Epi {
                     }
                 } else if (EPI == HPA_FEPI_GELU) {
                     if (row < p.Mp && col < p.N)
-                        p.out[hpa::frag_index(row, col, p.N)] = live ? hpa::gelu_ref(val) : 0.f;
+                        st_out<WT>(p.out + hpa::frag_index(row, col, p.N), live ? hpa::gelu_ref(val) : 0.f);
                 } else if (EPI == HPA_FEPI_RESID) {
                     val = live ? pre_res[i] + val : 0.f;  // residual_forward(out, res, proj)
-                    if (row < p.Mp && col < p.N) p.out[hpa::frag_index(row, col, p.N)] = val;
+                    if (row < p.Mp && col < p.N) st_out<WT>(p.out + hpa::frag_index(row, col, p.N), val);
                     tile[(j * R + lrow) * 17 + lcol] = val;
                 } else {  // LOGITS
                     if (live) p.out[(size_t)row * p.N + col] = val;
@@ -180,8 +200,8 @@ struct Epi {
                             s1 += tr[c];
                             s2 += tr[c] * tr[c];
                         }
-                        p.stats_out[((size_t)nt * p.Mp + row) * 2] = s1;
-                        p.stats_out[((size_t)nt * p.Mp + row) * 2 + 1] = s2;
+                        st_out<WT>(p.stats_out + ((size_t)nt * p.Mp + row) * 2, s1);
+                        st_out<WT>(p.stats_out + ((size_t)nt * p.Mp + row) * 2 + 1, s2);
                     } else {
                         float bv = tr[0];
                         int bi = 0;
@@ -216,7 +236,7 @@ constexpr int gemm16_lds_floats() {
 
 // body of the looped GEMM workgroup `bid` of the XCD-ordered 1-D grid
 // (gemm16_kernel, and the GEMM role of the pipelined combo launches)
-template <int NW, int EPI, int MT, int NTW, int UD = 0>
+template <int NW, int EPI, int MT, int NTW, int UD = 0, bool WT = false>
 __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
     constexpr int NT = NW * 64;
     constexpr int R = MT * 16;  // rows per workgroup
@@ -366,7 +386,7 @@ __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
         comp(Bb, t + 1);
     }
 
-    Epi<NW, EPI, MT, NTW> epi;
+    Epi<NW, EPI, MT, NTW, WT> epi;
     epi.prefetch(p, nt0, row0);
     epi.finish(p, acc, red, tile, nt0, row0);
 }
@@ -388,7 +408,7 @@ constexpr int gemm16_os_lds_floats() {
     return 2 * HPA_FUSED_LN_KMAX + NW * 256 + 16 * 17 + 2 * 16;
 }
 
-template <int NW, int EPI, int S>
+template <int NW, int EPI, int S, bool WT = false>
 __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem) {
     constexpr int NT = NW * 64;
     float* lngb = smem;                         // LN weight [K], bias [K]
@@ -398,6 +418,7 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
 
     int nt, ry;
     if (!xcd_tile(p, bid, nt, ry)) return;
+    HPA_TS(0, bid);
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     const int row0 = ry * 16;
@@ -428,15 +449,24 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
     // 3. all operand fragments of this wave's k range [w*S, w*S+S)
     const float4* __restrict__ wf = reinterpret_cast<const float4*>(p.w) + ((size_t)nt * p.K16 + w * S) * 64 + lane;
     const float4* __restrict__ xf = reinterpret_cast<const float4*>(p.x) + ((size_t)ry * p.K16 + w * S) * 64 + lane;
+    // issued strictly in k-step order (a scheduling barrier per step): the
+    // chain below then waits for each step's pair with a descending vmcnt and
+    // the MFMAs of early steps overlap the arrival of later ones (left to
+    // itself the scheduler grouped the loads by base register, and step 4
+    // waited for nearly every load of the wave)
     float4 wv[S], xv[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
         wv[s] = wf[s * 64];  // default policy: nt measured no faster here (tools/ab_bench.sh)
         xv[s] = xf[s * 64];
+#if HPA_OS_ORDER
+        __builtin_amdgcn_sched_barrier(0);
+#endif
     }
     // 4. epilogue operands
-    Epi<NW, EPI, 1> epi;
+    Epi<NW, EPI, 1, 1, WT> epi;
     epi.prefetch(p, nt, row0);
+    HPA_TS(1, bid);
 
     // LN: reduce the statistics (waits only for the loads of step 1)
     float mu = 0.f, rs = 0.f;
@@ -481,6 +511,7 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
         rs = lnst[2 * (lane & 15) + 1];
     }
 
+    HPA_TS(2, bid);
     // one accumulator chain: the same k order as gemm16_kernel with NW waves
     f32x4 acc[1];
     acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -495,7 +526,12 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
         acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.z, wv[s].z, acc[0], 0, 0, 0);
         acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.w, wv[s].w, acc[0], 0, 0, 0);
     }
+#ifdef HPA_TS_ACC
+    HPA_TS_ACC(acc[0]);
+#endif
+    HPA_TS(3, bid);
     epi.finish(p, acc, red, tile, nt, row0);
+    HPA_TS(4, bid);
 }
 
 template <int NW, int EPI, int S>

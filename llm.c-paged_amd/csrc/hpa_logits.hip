@@ -237,7 +237,8 @@ int g_num_cus = 0;
 
 template <int MT>
 int launch_resident_mt(const FG& p) {
-    logits_resident_kernel<MT><<<(unsigned)min(p.ntn, g_num_cus), kResNW * 64, 0, hpa_stream()>>>(p);
+    const int cus = hpa_stream_cus() > 0 ? hpa_stream_cus() : g_num_cus;  // one workgroup per CU of the stream
+    logits_resident_kernel<MT><<<(unsigned)min(p.ntn, cus), kResNW * 64, 0, hpa_stream()>>>(p);
     HPA_LAUNCH_CHECK();
     return 0;
 }

@@ -618,6 +618,11 @@ struct GPT2Decode {
     DecLane lanes[DEC_MAX_LANES];
     int nlanes;
     int pipeline;     /* 1: two lanes, attention chunks beside the other lane's GEMMs */
+    int split_cus;    /* > 0: split step, the GEMM chains on this many CUs (dec_launch_split) */
+    void *s_att, *s_gemm; /* CU-masked streams of the split step */
+    void** sp_ev;     /* [2][L+1][2] split-step events: kind (Q ready, attention done), layer, lane */
+    int overlap;      /* > 0: overlapped step (dec_launch_overlap) with this many chain workgroups */
+    unsigned* d_ctl;  /* [2L+2][HPA_LANE_CTL_WORDS] in-launch hand-off counters, zeroed per step */
     int sample;       /* 0: greedy argmax; 1: multinomial with per-sequence xorshift */
     unsigned long long* d_rng; /* [B] sampler states */
     /* prefill workspace (gpt2_decode_prefill), rows R = B*T, grown on demand */
@@ -675,6 +680,23 @@ static void dec_prof_free(GPT2Decode* d, int L) {
     for (size_t i = 0; i < 2 * (size_t)L * DEC_MAX_LANES; i++) hpa_event_destroy(d->prof_ev[i]);
     free(d->prof_ev);
     d->prof_ev = NULL;
+}
+
+static void dec_split_free(GPT2Decode* d, int L) {
+    if (d->sp_ev)
+        for (int i = 0; i < 4 * (L + 1); i++) hpa_event_destroy(d->sp_ev[i]);
+    free(d->sp_ev);
+    d->sp_ev = NULL;
+    hpa_stream_destroy(d->s_att);
+    hpa_stream_destroy(d->s_gemm);
+    d->s_att = d->s_gemm = NULL;
+    d->split_cus = 0;
+}
+
+static void dec_overlap_free(GPT2Decode* d) {
+    hpa_free(d->d_ctl);
+    d->d_ctl = NULL;
+    d->overlap = 0;
 }
 
 static void dec_lanes_free(GPT2Decode* d) {
@@ -744,6 +766,8 @@ static void dec_free(GPT2Decode* d) {
     if (!d) return;
     dec_prefill_free(d);
     dec_prof_free(d, d->pool.num_layers);
+    dec_split_free(d, d->pool.num_layers);
+    dec_overlap_free(d);
     if (d->graph) hpa_graph_destroy(d->graph);
     hpa_pool_destroy(&d->pool);
     hpa_free(d->d_bt); hpa_free(d->d_pos); hpa_free(d->d_tokens); hpa_free(d->d_next);
@@ -1219,11 +1243,127 @@ static int dec_launch_pipelined(GPT2* model) {
     return rc;
 }
 
+/* ---- split step (two lanes, two CU-masked streams) ----
+ * The attention stream owns most CUs, the GEMM stream the remaining
+ * split_cus; the two lanes alternate between them as a two-stage pipeline:
+ *   att  stream:  attn_A(l)            attn_B(l)            attn_A(l+1) ...
+ *   gemm stream:  chain_B(l-1)         chain_A(l)           chain_B(l)  ...
+ * where chain_X(l) = attproj, fc, fcproj of layer l and qkv of layer l+1.
+ * The HBM-bound attention of one half of the batch thus runs beside the
+ * latency-bound GEMMs of the other half on CUs of its own (a plain
+ * second stream gets no CUs while the attention grid fills them).  Events
+ * carry the dependencies; logits and the token choice run on the launch
+ * stream (all CUs).  Kernel node CU masks do not survive graph capture, so
+ * this step is launched eagerly.  Rows are bit-identical to one lane. */
+#define SP_EV(d, kind, l, lane) ((d)->sp_ev[((kind) * (model->config.num_layers + 1) + (l)) * 2 + (lane)])
+static int dec_launch_split(GPT2* model) {
+    GPT2Decode* d = model->decode;
+    const int C = model->config.channels, L = model->config.num_layers;
+    void* main_stream = hpa_get_stream();
+    int rc = hpa_event_record(d->ev_fork);
+    hpa_set_stream(d->s_att);
+    rc |= hpa_stream_wait_event(d->ev_fork);
+    hpa_set_stream(d->s_gemm);
+    rc |= hpa_stream_wait_event(d->ev_fork);
+    for (int li = 0; li < 2; li++) {
+        rc |= lane_embed(model, li);
+        rc |= lane_gemm_run(model, li, 0, G_QKV);
+        rc |= hpa_event_record(SP_EV(d, 0, 0, li));
+    }
+    for (int l = 0; l < L && !rc; l++) {
+        for (int li = 0; li < 2; li++) {
+            const DecLane* ln = &d->lanes[li];
+            hpa_set_stream(d->s_att);
+            rc |= hpa_stream_wait_event(SP_EV(d, 0, l, li));
+            rc |= hpa_paged_attention_decode_frag(d->d_q + (size_t)ln->r0 * C, &d->pool, l,
+                                                  d->d_bt + (size_t)ln->r0 * d->bt_stride, d->bt_stride,
+                                                  d->d_pos + ln->r0, ln->att, ln->B);
+            rc |= hpa_event_record(SP_EV(d, 1, l, li));
+            hpa_set_stream(d->s_gemm);
+            rc |= hpa_stream_wait_event(SP_EV(d, 1, l, li));
+            rc |= lane_gemm_run(model, li, l, G_ATTPROJ);
+            rc |= lane_gemm_run(model, li, l, G_FC);
+            rc |= lane_gemm_run(model, li, l, G_FCPROJ);
+            if (l + 1 < L) rc |= lane_gemm_run(model, li, l + 1, G_QKV);
+            rc |= hpa_event_record(SP_EV(d, 0, l + 1, li));
+        }
+    }
+    hpa_set_stream(main_stream);
+    for (int li = 0; li < 2; li++) {
+        rc |= hpa_stream_wait_event(SP_EV(d, 0, L, li));
+        rc |= lane_gemm_run(model, li, 0, G_LOGITS);
+        rc |= lane_pick(model, li, NULL);
+    }
+    return rc;
+}
+
+/* ---- overlapped step (two lanes, one stream, hpa_lane_layer) ----
+ * Lanes A and B alternate: every launch holds one lane's whole attention of
+ * a layer beside the other lane's GEMM chain (attproj, fc, fcproj of the
+ * previous attention, then qkv of the next layer), whose links are in-launch
+ * hand-offs:
+ *   embed A, B; qkv_A(0); qkv_B(0)
+ *   layer l:  [attn_A(l) | chain_B(l-1) + qkv_B(l)]   (l = 0: attn_A(0) alone)
+ *             [attn_B(l) | chain_A(l)   + qkv_A(l+1)]
+ *   [chain_B(L-1)]; logits A, B; token choice A, B
+ * Two launches per layer instead of ten. */
+static void chain_desc(GPT2* model, int li, int l, int which, HpaFusedGemm* g) {
+    lane_gemm(model, li, l, which, g);
+    g->waves = 4; /* the chain's tiles: 4 waves, one row block, one column tile */
+    g->row_blocks = 1;
+    g->col_tiles = 1;
+}
+
+static int overlap_launch(GPT2* model, int att_lane, int att_layer, int chain_lane, int chain_layer, int with_qkv,
+                          int slot) {
+    GPT2Decode* d = model->decode;
+    const int L = model->config.num_layers;
+    HpaAttnChunk a;
+    if (att_lane >= 0) {
+        lane_attn(model, att_lane, att_layer, 0, &a);
+        a.nchunks = 1;
+    }
+    HpaFusedGemm ch[4];
+    int nph = 0;
+    if (chain_lane >= 0) {
+        chain_desc(model, chain_lane, chain_layer, G_ATTPROJ, &ch[nph++]);
+        chain_desc(model, chain_lane, chain_layer, G_FC, &ch[nph++]);
+        chain_desc(model, chain_lane, chain_layer, G_FCPROJ, &ch[nph++]);
+        if (with_qkv && chain_layer + 1 < L) chain_desc(model, chain_lane, chain_layer + 1, G_QKV, &ch[nph++]);
+    }
+    unsigned* ctl = d->d_ctl + (size_t)slot * HPA_LANE_CTL_WORDS;
+    return hpa_lane_layer(att_lane >= 0 ? &a : NULL, nph ? ch : NULL, nph, ctl, d->overlap);
+}
+
+static int dec_launch_overlap(GPT2* model) {
+    GPT2Decode* d = model->decode;
+    const int L = model->config.num_layers;
+    const int A = 0, B = 1;
+    int rc = hpa_memset_async(d->d_ctl, 0, (size_t)(2 * L + 2) * HPA_LANE_CTL_WORDS * sizeof(unsigned));
+    rc |= lane_embed(model, A);
+    rc |= lane_embed(model, B);
+    rc |= lane_gemm_run(model, A, 0, G_QKV);
+    rc |= lane_gemm_run(model, B, 0, G_QKV);
+    int slot = 0;
+    for (int l = 0; l < L && !rc; l++) {
+        rc |= overlap_launch(model, A, l, l > 0 ? B : -1, l - 1, 1, slot++);
+        rc |= overlap_launch(model, B, l, A, l, 1, slot++);
+    }
+    rc |= overlap_launch(model, -1, 0, B, L - 1, 0, slot++);
+    rc |= lane_gemm_run(model, A, 0, G_LOGITS);
+    rc |= lane_gemm_run(model, B, 0, G_LOGITS);
+    rc |= lane_pick(model, A, NULL);
+    rc |= lane_pick(model, B, NULL);
+    return rc;
+}
+
 /* all lanes: lanes 1.. fork from the launch stream, run concurrently with
  * lane 0, and join back before the step completes */
 static int dec_launch_fused(GPT2* model) {
     GPT2Decode* d = model->decode;
     if (d->pipeline) return dec_launch_pipelined(model);
+    if (d->overlap) return dec_launch_overlap(model);
+    if (d->split_cus) return dec_launch_split(model);
     if (d->nlanes == 1) return dec_launch_lane(model, 0);
     void* main_stream = hpa_get_stream();
     int rc = hpa_event_record(d->ev_fork);
@@ -1270,6 +1410,8 @@ int gpt2_decode_set_lanes(GPT2* model, int lanes) {
         d->graph = NULL;
     }
     d->pipeline = 0;
+    dec_split_free(d, model->config.num_layers);
+    dec_overlap_free(d);
     return dec_lanes_alloc(d, lanes, model->config.channels, model->config.vocab_size, model->config.num_heads);
 }
 
@@ -1326,6 +1468,81 @@ int gpt2_decode_set_pipeline(GPT2* model, int enable) {
 
 int gpt2_decode_pipeline(GPT2* model) { return model->decode ? model->decode->pipeline : 0; }
 
+/* split step (dec_launch_split): gemm_cus > 0 gives the GEMM chains that many
+ * CUs and the attention the rest; 0 returns to one lane */
+int gpt2_decode_set_split(GPT2* model, int gemm_cus) {
+    GPT2Decode* d = model->decode;
+    if (!d) return 1;
+    if (gemm_cus <= 0) {
+        if (!d->split_cus) return 0;
+        return gpt2_decode_set_lanes(model, 1);
+    }
+    int ncu = 0;
+    if (hpa_device_info(NULL, 0, &ncu, NULL)) return 1;
+    if (!d->fused || d->B <= 16 || gemm_cus >= ncu) {
+        fprintf(stderr, "[paged_infer] split step needs the fused path, B > 16 and gemm_cus < %d\n", ncu);
+        return 1;
+    }
+    if (gpt2_decode_set_lanes(model, 2) || d->nlanes != 2) return 1;
+    const int L = model->config.num_layers;
+    d->sp_ev = (void**)calloc(4 * (size_t)(L + 1), sizeof(void*));
+    if (!d->sp_ev) return 1;
+    for (int i = 0; i < 4 * (L + 1); i++)
+        if (!(d->sp_ev[i] = hpa_event_create_nt())) return 1;
+    d->s_gemm = hpa_stream_create_cumask(0, gemm_cus);
+    d->s_att = hpa_stream_create_cumask(gemm_cus, ncu);
+    if (!d->s_gemm || !d->s_att) {
+        dec_split_free(d, L);
+        return 1;
+    }
+    d->split_cus = gemm_cus;
+    return 0;
+}
+
+int gpt2_decode_split(GPT2* model) { return model->decode ? model->decode->split_cus : 0; }
+
+/* overlapped step (dec_launch_overlap): chain_blocks > 0 persistent
+ * workgroups run the GEMM chains beside the attention; 0 returns to one lane */
+int gpt2_decode_set_overlap(GPT2* model, int chain_blocks) {
+    GPT2Decode* d = model->decode;
+    if (!d) return 1;
+    if (chain_blocks <= 0) {
+        if (!d->overlap) return 0;
+        return gpt2_decode_set_lanes(model, 1);
+    }
+    if (!d->fused || d->B <= 16 || d->B > 128 || (d->P != 8 && d->P != 16 && d->P != 32) ||
+        d->pool.dtype != HPA_F32) {
+        fprintf(stderr, "[paged_infer] overlapped step needs the fused path, 16 < B <= 128, page size 8/16/32 "
+                        "and an fp32 KV pool\n");
+        return 1;
+    }
+    if (gpt2_decode_set_lanes(model, 2) || d->nlanes != 2) return 1;
+    const int L = model->config.num_layers;
+    d->d_ctl = (unsigned*)hpa_malloc((size_t)(2 * L + 2) * HPA_LANE_CTL_WORDS * sizeof(unsigned));
+    if (!d->d_ctl) return 1;
+    d->overlap = chain_blocks;
+    return 0;
+}
+
+int gpt2_decode_overlap(GPT2* model) { return model->decode ? model->decode->overlap : 0; }
+
+/* timeout codes the overlapped step's in-launch waits left in the last step
+ * (0 = none): synchronises */
+unsigned gpt2_decode_overlap_faults(GPT2* model) {
+    GPT2Decode* d = model->decode;
+    if (!d || !d->overlap || !d->d_ctl) return 0;
+    const int L = model->config.num_layers;
+    const size_t n = (size_t)(2 * L + 2) * HPA_LANE_CTL_WORDS;
+    unsigned* h = (unsigned*)malloc(n * sizeof(unsigned));
+    if (!h) return ~0u;
+    unsigned f = 0;
+    if (hpa_synchronize() || hpa_memcpy(h, d->d_ctl, n * sizeof(unsigned))) f = ~0u;
+    else
+        for (int s = 0; s < 2 * L + 2; s++) f |= h[(size_t)s * HPA_LANE_CTL_WORDS + 1];
+    free(h);
+    return f;
+}
+
 int gpt2_decode_set_graph(GPT2* model, int enable) {
     GPT2Decode* d = model->decode;
     if (!d) return 1;
@@ -1354,7 +1571,7 @@ static int dec_enqueue(GPT2* model, const int* tokens) {
         memcpy(d->h_stage, tokens, d->B * sizeof(int));
         if (hpa_memcpy_async(d->d_tokens, d->h_stage, d->B * sizeof(int))) return 1;
     }
-    if (d->use_graph) {
+    if (d->use_graph && !d->split_cus) {
         if (!d->graph) {
             if (hpa_graph_begin()) return 1;
             int rc = dec_launch(model);

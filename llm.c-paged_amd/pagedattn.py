@@ -245,6 +245,12 @@ def lib():
     _sig(L, "gpt2_decode_lanes", i, [v])
     _sig(L, "gpt2_decode_set_pipeline", i, [v, i])
     _sig(L, "gpt2_decode_pipeline", i, [v])
+    _sig(L, "gpt2_decode_set_split", i, [v, i])
+    _sig(L, "gpt2_decode_set_overlap", i, [v, i])
+    _sig(L, "gpt2_decode_overlap", i, [v])
+    _sig(L, "gpt2_decode_overlap_faults", ctypes.c_uint, [v])
+    _sig(L, "gpt2_decode_split", i, [v])
+    _sig(L, "hpa_stream_create_cumask", v, [i, i])
     _sig(L, "hpa_attn_state_elems", ctypes.c_size_t, [i, i])
     _sig(L, "hpa_attn_chunk_with_gemm", i, [ctypes.c_void_p, ctypes.c_void_p])
     _sig(L, "gpt2_decode_step_bytes", ctypes.c_double, [v, ctypes.POINTER(ctypes.c_double)])
@@ -599,6 +605,20 @@ class Model:
 
     def set_pipeline(self, enable=True):
         check(lib().gpt2_decode_set_pipeline(self.h, int(bool(enable))), "set_pipeline")
+
+    def set_overlap(self, chain_blocks):
+        """overlapped step: one lane's attention beside the other lane's GEMM
+        chain in one launch per layer half (0 = off)"""
+        check(lib().gpt2_decode_set_overlap(self.h, int(chain_blocks)), "set_overlap")
+        return lib().gpt2_decode_overlap(self.h)
+
+    def overlap_faults(self):
+        return int(lib().gpt2_decode_overlap_faults(self.h))
+
+    def set_split(self, gemm_cus):
+        """split step: GEMM chains on `gemm_cus` CUs beside the attention (0 = off)"""
+        check(lib().gpt2_decode_set_split(self.h, int(gemm_cus)), "set_split")
+        return lib().gpt2_decode_split(self.h)
 
     def set_lanes(self, lanes):
         check(lib().gpt2_decode_set_lanes(self.h, int(lanes)), "set_lanes")

@@ -306,3 +306,135 @@ def test_sampling_off_is_greedy(hip):
     g = m.step(np.array([1, 2, 3], np.int32))
     assert np.array_equal(g, m.logits().argmax(-1))
     m.close()
+
+
+@pytest.mark.parametrize("gemm_cus,B", [(32, 64), (32, 40), (64, 70)])
+def test_split_step_bit_identical_to_one_lane(hip, gemm_cus, B):
+    """split step: two lanes on CU-masked streams (attention on one CU set,
+    the GEMM chains on the other); every row's arithmetic is unchanged, so
+    ids, logits and positions equal the one-lane step bit for bit"""
+    params = synth.params(SMALL, seed=41)
+    outs = []
+    for split in (0, gemm_cus):
+        m = hip.Model(SMALL, params=params)
+        m.decode_init(B, 16, 128)
+        if split:
+            assert m.set_split(split) == split
+        m.set_graph(True)  # ignored by the split step (eager)
+        rng = np.random.default_rng(6)
+        seq = [m.step(rng.integers(0, 1000, B).astype(np.int32))]
+        for _ in range(12):
+            seq.append(m.step(None))
+        seq.append(m.logits())
+        seq.append(m.positions())
+        outs.append(seq)
+        m.close()
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+
+
+def test_split_step_gpt2_124m_matches_oracle(hip):
+    """124M shapes through the split step against the oracle"""
+    cfgd = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
+    params = synth.params(cfgd, seed=9)
+    B = 48
+    model = hip.Model(cfgd, params=params)
+    model.decode_init(B, 16, cfgd["maxT"])
+    assert model.set_split(32) == 32
+    c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
+    orc = oc.PagedDecoder(params, c, B, 16, cfgd["maxT"], page_seed=12)
+    rng = np.random.default_rng(9)
+    tok = rng.integers(0, cfgd["V"], B).astype(np.int32)
+    for t in range(8):
+        o_next, o_logits = orc.step(tok)
+        g_next = model.step(tok)
+        assert np.abs(model.logits() - o_logits).max() <= LOGIT_TOL
+        clear = _margins(o_logits) > TIE_MARGIN
+        assert np.array_equal(g_next[clear], o_next[clear])
+        tok = o_next
+    model.close()
+    orc.close()
+
+
+def test_set_split_rejects_bad_shapes(hip):
+    m = hip.Model(SMALL)
+    m.decode_init(16, 16, 64)
+    with pytest.raises(RuntimeError):
+        m.set_split(32)  # B <= 16: no second lane
+    m.close()
+    m = hip.Model(SMALL)
+    m.decode_init(32, 16, 64)
+    with pytest.raises(RuntimeError):
+        m.set_split(100000)
+    assert m.set_split(0) == 0
+    m.close()
+
+
+@pytest.mark.parametrize("P,B,chain", [(16, 40, 64), (8, 64, 256), (32, 33, 16)])
+def test_overlap_step_matches_oracle(hip, P, B, chain):
+    """overlapped step: each launch runs one lane's attention beside the
+    other lane's GEMM chain with in-launch hand-offs (hpa_lane_layer)"""
+    params = synth.params(SMALL, seed=P + B)
+    model = hip.Model(SMALL, params=params)
+    model.decode_init(B, P, SMALL["maxT"])
+    assert model.set_overlap(chain) == chain
+    model.set_graph(True)
+    c = oc.cfg(SMALL["maxT"], SMALL["V"], SMALL["L"], SMALL["NH"], SMALL["C"])
+    orc = oc.PagedDecoder(params, c, B, P, SMALL["maxT"], page_seed=P)
+    rng = np.random.default_rng(P)
+    for t in range(30):
+        tok = rng.integers(0, SMALL["V"], B).astype(np.int32)
+        o_next, o_logits = orc.step(tok)
+        g_next = model.step(tok)
+        assert model.overlap_faults() == 0
+        assert np.abs(model.logits() - o_logits).max() <= LOGIT_TOL
+        clear = _margins(o_logits) > TIE_MARGIN
+        assert np.array_equal(g_next[clear], o_next[clear])
+    model.close()
+    orc.close()
+
+
+def test_overlap_step_gpt2_124m_matches_oracle(hip):
+    """124M shapes: one-shot chain tiles (K = 768) and the looped fcproj"""
+    cfgd = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
+    params = synth.params(cfgd, seed=19)
+    B = 64
+    model = hip.Model(cfgd, params=params)
+    model.decode_init(B, 16, cfgd["maxT"])
+    assert model.set_overlap(192) == 192
+    model.set_graph(True)
+    c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
+    orc = oc.PagedDecoder(params, c, B, 16, cfgd["maxT"], page_seed=19)
+    rng = np.random.default_rng(19)
+    tok = rng.integers(0, cfgd["V"], B).astype(np.int32)
+    worst = 0.0
+    for t in range(8):
+        o_next, o_logits = orc.step(tok)
+        g_next = model.step(tok)
+        assert model.overlap_faults() == 0
+        worst = max(worst, float(np.abs(model.logits() - o_logits).max()))
+        clear = _margins(o_logits) > TIE_MARGIN
+        assert np.array_equal(g_next[clear], o_next[clear])
+        tok = o_next
+    assert worst <= LOGIT_TOL, worst
+    model.close()
+    orc.close()
+
+
+def test_overlap_graph_equals_eager(hip):
+    params = synth.params(SMALL, seed=23)
+    outs = []
+    for graph in (False, True):
+        m = hip.Model(SMALL, params=params)
+        m.decode_init(48, 16, 128)
+        m.set_overlap(96)
+        m.set_graph(graph)
+        rng = np.random.default_rng(3)
+        seq = [m.step(rng.integers(0, 1000, 48).astype(np.int32))]
+        for _ in range(10):
+            seq.append(m.step(None))
+        seq.append(m.logits())
+        outs.append(seq)
+        m.close()
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
