@@ -109,7 +109,7 @@ def cpu_baseline(cfgd, B, P, ctx, budget_s, kv_bf16=False):
     params = pagedattn.synthetic_params(cfgd, seed=1337)
     c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
     dec = oc.PagedDecoder(params, c, B, P, cfgd["maxT"], page_seed=3, fast=True, kv_bf16=kv_bf16)
-    max_steps = min(512, ctx // 2)  # the budget normally ends the sample first
+    max_steps = min(256, ctx // 2)  # the budget normally ends the sample first (near ctx)
     start_ctx = ctx - max_steps
     dec.fill_random(start_ctx, seed=5)
     rng = np.random.default_rng(0)
