@@ -223,6 +223,11 @@ typedef struct {
                              itself; prefill rows b*T+t -> b) */
 } HpaFusedGemm;
 int hpa_gemm_fused(const HpaFusedGemm* g);
+/* argmax partials per row a LOGITS launch of g writes into part_out (the
+ * `ntiles` of hpa_argmax_final): N/16 tiles, or one per workgroup of the
+ * activation-resident kernel (variant 4) on the current stream; -1 if g is
+ * not a valid LOGITS descriptor */
+int hpa_logits_partials(const HpaFusedGemm* g);
 /* the launch shape hpa_gemm_fused picks when waves / row_blocks / col_tiles
  * are 0: out3 = {waves, row_blocks, col_tiles} */
 void hpa_fused_pick(int M, int N, int K, int* out3);

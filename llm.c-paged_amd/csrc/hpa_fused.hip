@@ -468,6 +468,13 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
     }
 }
 
+int hpa_logits_partials(const HpaFusedGemm* g) {
+    FG p;
+    if (!g || g->epilogue != HPA_FEPI_LOGITS || fused_prepare(g, &p)) return -1;
+    if (g->variant == 4 && logits_resident_eligible(p, g->epilogue)) return logits_resident_grid(p);
+    return p.ntn;  // one partial per 16-column tile
+}
+
 int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const float* wpe,
                    float* res_frag, float* stats, int B, int C) {
     HPA_REQUIRE(B > 0 && C > 0 && C % 16 == 0, "embed_frag: bad shape");

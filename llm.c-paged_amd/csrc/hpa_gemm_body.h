@@ -546,6 +546,7 @@ __global__ __launch_bounds__(NW * 64) void gemm16_os_kernel(FG p) {
 // the activation-resident logits kernel (hpa_logits.hip, variant 4)
 bool logits_resident_eligible(const FG& p, int epi);
 int launch_logits_resident(const FG& p);
+int logits_resident_grid(const FG& p);  // workgroups = argmax partials per row it writes
 
 static inline int fused_prepare(const HpaFusedGemm* g, FG* p) {
     HPA_REQUIRE(g && g->x && g->w && g->out, "gemm_fused: null operand");

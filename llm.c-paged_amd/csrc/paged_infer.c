@@ -1147,7 +1147,11 @@ static int lane_pick(GPT2* model, int li, const int* active) {
     if (d->sample)
         return hpa_sample_final(d->d_logits + (size_t)ln->r0 * V, ln->B, V, d->d_rng + ln->r0, d->d_next + ln->r0,
                                 d->d_tokens + ln->r0, d->d_pos + ln->r0, active);
-    return hpa_argmax_final(ln->part, (V + 15) / 16, ln->Mp, ln->B, d->d_next + ln->r0, d->d_tokens + ln->r0,
+    HpaFusedGemm g;
+    lane_gemm(model, li, 0, G_LOGITS, &g);
+    const int npart = hpa_logits_partials(&g); /* per-tile or per-workgroup partials */
+    if (npart <= 0) return 1;
+    return hpa_argmax_final(ln->part, npart, ln->Mp, ln->B, d->d_next + ln->r0, d->d_tokens + ln->r0,
                             d->d_pos + ln->r0, active);
 }
 

@@ -228,6 +228,7 @@ def lib():
     _sig(L, "hpa_pack_frag", i, [v, i, i, i, v])
     _sig(L, "hpa_unpack_frag", i, [v, i, i, v, i])
     _sig(L, "hpa_gemm_fused", i, [ctypes.POINTER(HpaFusedGemm)])
+    _sig(L, "hpa_logits_partials", i, [ctypes.POINTER(HpaFusedGemm)])
     _sig(L, "hpa_fused_pick_waves", i, [i, i, i])
     _sig(L, "hpa_fused_pick", None, [i, i, i, _I])
     _sig(L, "hpa_embed_frag", i, [v, v, v, v, v, v, i, i])

@@ -110,6 +110,7 @@ def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixe
         g.layer = 0
         g.block_table, g.bt_stride, g.pos = dev(bt), bt.shape[1], dev(pos)
     keep.append(out)
+    keep.append(g)  # the descriptor (LOGITS: hpa_logits_partials)
     hip.check(L.hpa_gemm_fused(ctypes.byref(g)), "gemm_fused")
     hip.check(L.hpa_synchronize())
     return out, acc, bound, keep
@@ -156,7 +157,7 @@ def test_fused_logits_argmax(hip, M, waves, rb, ct):
     out, acc, bound, keep = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, waves, ln=True, rng=rng, rb=rb, ct=ct)
     got = out.download((M, N))
     assert np.all(np.abs(got - acc) <= bound)
-    part = keep[-2]
+    part = keep[-3]
     nxt = hip.DeviceBuffer(M * 4)
     Mp = (M + 15) // 16 * 16
     hip.check(L.hpa_argmax_final(part.ptr, (N + 15) // 16, Mp, M, nxt.ptr, None, None, None))
@@ -175,14 +176,44 @@ def test_logits_resident_kernel(hip, M):
     out, acc, bound, keep = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, 0, ln=True, rng=rng, variant=4)
     got = out.download((M, N))
     assert np.all(np.abs(got - acc) <= bound)
-    part = keep[-2]
+    part, g = keep[-3], keep[-1]
+    # one running (max, argmax) partial per row per workgroup (grid <= CUs)
+    npart = L.hpa_logits_partials(ctypes.byref(g))
+    assert 0 < npart <= 256
     nxt = hip.DeviceBuffer(M * 4)
     Mp = (M + 15) // 16 * 16
-    hip.check(L.hpa_argmax_final(part.ptr, (N + 15) // 16, Mp, M, nxt.ptr, None, None, None))
+    hip.check(L.hpa_argmax_final(part.ptr, npart, Mp, M, nxt.ptr, None, None, None))
     assert np.array_equal(nxt.download(M, np.int32), got.argmax(-1))
     rng = np.random.default_rng(11)
     out1, _, _, keep1 = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, 4, ln=True, rng=rng, rb=1, variant=1)
-    assert np.abs(out1.download((M, N)) - got).max() <= 2e-5
+    got1 = out1.download((M, N))
+    assert np.abs(got1 - got).max() <= 2e-5
+    # the looped kernel: one partial per 16-column tile
+    assert L.hpa_logits_partials(ctypes.byref(keep1[-1])) == (N + 15) // 16
+    hip.check(L.hpa_argmax_final(keep1[-3].ptr, (N + 15) // 16, Mp, M, nxt.ptr, None, None, None))
+    assert np.array_equal(nxt.download(M, np.int32), got1.argmax(-1))
+
+
+def test_logits_resident_argmax_ties_first_index(hip):
+    """equal maxima in several column tiles and workgroups: the lowest column
+    wins, as the reference's strict-> scan (paged_infer.c:937-951)"""
+    L = hip.lib()
+    M, K, N = 16, 768, 50257
+    x = np.zeros((M, K), np.float32)
+    x[:, 0] = 1.0
+    W = np.zeros((N, K), np.float32)
+    # logit = W[:, 0] * LN(x)[0]; LN of a one-hot row is a fixed positive value at k = 0
+    cols = [7, 4000, 4001, 25000, 50256]
+    W[cols, 0] = 0.5
+    fixed = dict(x=x, W=W, bias=np.zeros(N, np.float32), lw=np.ones(K, np.float32), lb=np.zeros(K, np.float32))
+    out, acc, bound, keep = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, 0, ln=True, rng=np.random.default_rng(0),
+                                 fixed=fixed, variant=4)
+    got = out.download((M, N))
+    assert np.all(got[:, cols] == got[0, 7]) and got[0, 7] > got[0, 8]
+    npart = L.hpa_logits_partials(ctypes.byref(keep[-1]))
+    nxt = hip.DeviceBuffer(M * 4)
+    hip.check(L.hpa_argmax_final(keep[-3].ptr, npart, 16, M, nxt.ptr, None, None, None))
+    assert np.array_equal(nxt.download(M, np.int32), np.full(M, 7, np.int32))
 
 
 def test_fused_qkv_appends_into_pages(hip):
