@@ -14,6 +14,12 @@
 #ifndef HPA_OS_ORDER
 #define HPA_OS_ORDER 1
 #endif
+// one-shot body timing experiments (tools/micro/os_trace.hip only; 0 in the
+// library): 1 no LayerNorm, 2 no MFMA (VALU stand-in), 3 every workgroup reads
+// the weight/activation tiles of (0, 0) (L2-resident operands), 4 no epilogue
+#ifndef HPA_OS_EXP
+#define HPA_OS_EXP 0
+#endif
 
 namespace hpa_gemm {
 
@@ -423,7 +429,7 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
     const int w = threadIdx.x >> 6;
     const int row0 = ry * 16;
     const int q4 = lane >> 4;
-    const bool use_ln = p.ln_stats != nullptr;
+    const bool use_ln = HPA_OS_EXP != 1 && p.ln_stats != nullptr;
 
     // 1. LN statistics partials of the 16 rows: 4 threads per row, issued first
     constexpr int SPT = 12;  // partial tiles per thread: ln_ntiles <= 48 (C <= 768); else looped
@@ -447,8 +453,9 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
         lb4 = reinterpret_cast<const float4*>(p.ln_b)[threadIdx.x];
     }
     // 3. all operand fragments of this wave's k range [w*S, w*S+S)
-    const float4* __restrict__ wf = reinterpret_cast<const float4*>(p.w) + ((size_t)nt * p.K16 + w * S) * 64 + lane;
-    const float4* __restrict__ xf = reinterpret_cast<const float4*>(p.x) + ((size_t)ry * p.K16 + w * S) * 64 + lane;
+    const int nt_ld = HPA_OS_EXP == 3 ? 0 : nt, ry_ld = HPA_OS_EXP == 3 ? 0 : ry;
+    const float4* __restrict__ wf = reinterpret_cast<const float4*>(p.w) + ((size_t)nt_ld * p.K16 + w * S) * 64 + lane;
+    const float4* __restrict__ xf = reinterpret_cast<const float4*>(p.x) + ((size_t)ry_ld * p.K16 + w * S) * 64 + lane;
     // issued strictly in k-step order (a scheduling barrier per step): the
     // chain below then waits for each step's pair with a descending vmcnt and
     // the MFMAs of early steps overlap the arrival of later ones (left to
@@ -521,11 +528,20 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
     for (int s = 0; s < S; ++s) {
         float4 xa = xv[s];
         if (use_ln) xa = ln4(xa, mu, rs, sg[4 * (w * S + s)], sbv[4 * (w * S + s)]);
+#if HPA_OS_EXP == 2
+        acc[0][0] += xa.x * wv[s].x + xa.y * wv[s].y;
+        acc[0][1] += xa.z * wv[s].z + xa.w * wv[s].w;
+#else
         acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.x, wv[s].x, acc[0], 0, 0, 0);
         acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.y, wv[s].y, acc[0], 0, 0, 0);
         acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.z, wv[s].z, acc[0], 0, 0, 0);
         acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.w, wv[s].w, acc[0], 0, 0, 0);
+#endif
     }
+#if HPA_OS_EXP == 4
+    if (acc[0][0] == 1.2345f && acc[0][1] == 5.4321f) asm volatile("" ::"v"(acc[0][2]));  // no epilogue
+    return;
+#endif
 #ifdef HPA_TS_ACC
     HPA_TS_ACC(acc[0]);
 #endif
