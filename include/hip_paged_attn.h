@@ -196,7 +196,8 @@ typedef struct {
     const float* bias;    /* [N] or NULL */
     int epilogue;         /* HPA_FEPI_* */
     /* QKV: out = q [M][C] row-major; K/V rows appended to pool pages at pos[m] */
-    /* RESID: out = res_in + acc + bias (frag layout [M][N]); stats_out[N/16][Mp][2] */
+    /* RESID: out = res_in + acc + bias (frag layout [M][N]); stats_out[N/16][Mp][2]
+       (NULL: no statistics -- the consumer folds its LN and sums its own) */
     /* GELU: out = gelu(acc + bias) (frag layout [M][N]) */
     /* LOGITS: out = acc [M][N] row-major (ld = N); part_out[N/16 tiles][Mp][2] = (max, argmax) */
     float* out;
@@ -221,7 +222,23 @@ typedef struct {
                              where M's row blocks or the waves cannot carry it, 1 */
     const int* row_seq;   /* QKV: block-table row of each GEMM row (NULL = the row
                              itself; prefill rows b*T+t -> b) */
+    const float* ln_fold_c1; /* non-NULL: the LayerNorm is folded into w (packed by
+                             hpa_ln_fold_pack: w = W*ln_w per column k, bias = c2):
+                             A is x as it stands, and the epilogue applies
+                             out[n] = rstd*(acc[n] - mean*c1[n]) + bias[n] with the
+                             row statistics (one-pass) summed from the A fragments
+                             the workgroup already holds (K = the LN width).  No LN
+                             prologue and no statistics loads; ln_stats, ln_w and
+                             ln_b are not read. */
 } HpaFusedGemm;
+/* LayerNorm folding for hpa_gemm_fused (layernorm_forward :49-89 followed by
+ * matmul_forward :92-114, restated): for W [N][K] row-major (device), writes
+ * dst_frag = frag-packed W[n][k]*ln_w[k], c1[n] = sum_k of those products and
+ * c2[n] = sum_k ln_b[k]*W[n][k] + bias[n] (bias may be NULL); sums in double,
+ * rounded once.  Then sum_k LN(x)_k W[n][k] + bias[n] =
+ * rstd*(sum_k x_k W'[n][k] - mean*c1[n]) + c2[n]. */
+int hpa_ln_fold_pack(const float* W, int N, int K, const float* ln_w, const float* ln_b, const float* bias,
+                     float* dst_frag, float* c1, float* c2);
 int hpa_gemm_fused(const HpaFusedGemm* g);
 /* argmax partials per row a LOGITS launch of g writes into part_out (the
  * `ntiles` of hpa_argmax_final): N/16 tiles, or one per workgroup of the

@@ -51,6 +51,32 @@ __global__ void pack_frag_kernel(const float* __restrict__ src, int rows, int K,
     dst[o] = v;
 }
 
+// LayerNorm folding (hpa_ln_fold_pack): one wave per output column n
+__global__ __launch_bounds__(64) void ln_fold_kernel(const float* __restrict__ W, int K,
+                                                     const float* __restrict__ g, const float* __restrict__ b,
+                                                     const float* __restrict__ bias, float* __restrict__ Wg,
+                                                     float* __restrict__ c1, float* __restrict__ c2) {
+    const int n = blockIdx.x, lane = threadIdx.x;
+    const float* wr = W + (size_t)n * K;
+    float* wgr = Wg + (size_t)n * K;
+    double s1 = 0.0, s2 = 0.0;
+    for (int k = lane; k < K; k += 64) {
+        const float wg = wr[k] * g[k];  // the packed weight, rounded once
+        wgr[k] = wg;
+        s1 += (double)wg;
+        s2 += (double)b[k] * (double)wr[k];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+    }
+    if (lane == 0) {
+        c1[n] = (float)s1;
+        c2[n] = (float)(s2 + (bias ? (double)bias[n] : 0.0));
+    }
+}
+
 __global__ void unpack_frag_kernel(const float4* __restrict__ src, int rows, int K,
                                    float* __restrict__ dst, int ld, size_t n4) {
     const size_t o = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -390,6 +416,21 @@ int hpa_pack_frag(const float* src, int rows, int K, int ld, float* dst) {
         src, rows, K, ld, reinterpret_cast<float4*>(dst), n4);
     HPA_LAUNCH_CHECK();
     return 0;
+}
+
+int hpa_ln_fold_pack(const float* W, int N, int K, const float* ln_w, const float* ln_b, const float* bias,
+                     float* dst_frag, float* c1, float* c2) {
+    HPA_REQUIRE(W && ln_w && ln_b && dst_frag && c1 && c2 && N > 0 && K > 0 && K % 16 == 0,
+                "ln_fold_pack: bad arguments (K % 16)");
+    float* tmp = nullptr;
+    HPA_CHECK(hipMalloc(&tmp, (size_t)N * K * sizeof(float)));
+    ln_fold_kernel<<<N, 64, 0, hpa_stream()>>>(W, K, ln_w, ln_b, bias, tmp, c1, c2);
+    int rc = hipGetLastError() != hipSuccess ? hpa_fail(__FILE__, __LINE__, "ln_fold_kernel launch") : 0;
+    if (!rc) rc = hpa_pack_frag(tmp, N, K, K, dst_frag);
+    const hipError_t e = hipStreamSynchronize(hpa_stream());
+    (void)hipFree(tmp);
+    if (!rc && e != hipSuccess) rc = hpa_fail(__FILE__, __LINE__, hipGetErrorString(e));
+    return rc;
 }
 
 int hpa_unpack_frag(const float* src, int rows, int K, float* dst, int ld) {

@@ -48,6 +48,7 @@ struct FG {
     int bt_stride;
     const int* pos;
     const int* row_seq;  // QKV: block-table row per GEMM row (NULL: the row)
+    const float* fold_c1;  // LN folded into w: out = rstd*(acc - mean*c1) + bias (bias = c2)
     int gx, gy;  // column-tile groups x row groups of the launch
 };
 
@@ -84,6 +85,29 @@ __device__ __forceinline__ float4 ln4(float4 a, float mu, float rs, float4 g, fl
     return a;
 }
 
+// ---- folded LayerNorm: row statistics from the A fragments themselves ----
+// (no statistics loads: measured, they cost more than the operand loads they
+// precede).  A lane holds 4 consecutive k of row (lane & 15) per k-step; the
+// per-lane sums run over the wave's k-steps in order, then the 4 lanes of a
+// row combine (xor 16, xor 32: the same value on all four), then the waves in
+// wave order in the epilogue -- the same order in every body and launch shape.
+__device__ __forceinline__ void row_sums_add(float4 x, float& s1, float& s2) {
+    s1 = (((s1 + x.x) + x.y) + x.z) + x.w;
+    s2 = __fmaf_rn(x.w, x.w, __fmaf_rn(x.z, x.z, __fmaf_rn(x.y, x.y, __fmaf_rn(x.x, x.x, s2))));
+}
+// lanes 0..15 store the wave's (sum, sum of squares) of rows row_base + lane
+__device__ __forceinline__ void row_sums_publish(float s1, float s2, float* wsum_wave_rows) {
+    const int lane = threadIdx.x & 63;
+    s1 += __shfl_xor(s1, 16, 64);
+    s2 += __shfl_xor(s2, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    if (lane < 16) {
+        wsum_wave_rows[2 * lane] = s1;
+        wsum_wave_rows[2 * lane + 1] = s2;
+    }
+}
+
 // ---- shared epilogue ---------------------------------------------------
 // A workgroup's output is NTW 16-column tiles x MT 16-row blocks.  Element e
 // (0 .. NTW*MT*256-1): column tile j = e / (MT*256); within it e' = e % (MT*256):
@@ -96,7 +120,7 @@ struct Epi {
     static constexpr int R = MT * 16;
     static constexpr int TE = MT * 256;                    // elements per column tile
     static constexpr int EPT = (NTW * TE + NT - 1) / NT;   // elements per thread
-    float pre_bias[EPT], pre_res[EPT];
+    float pre_bias[EPT], pre_res[EPT], pre_c1[EPT];
 
     __device__ __forceinline__ static void where(int e, int nt0, int row0, int& j, int& lrow, int& lcol,
                                                  int& row, int& col) {
@@ -120,14 +144,17 @@ struct Epi {
             const bool in = e < NTW * TE;
             pre_bias[i] = (EPI != HPA_FEPI_LOGITS && in && p.bias && col < p.N) ? p.bias[col] : 0.f;
             pre_res[i] = 0.f;
+            pre_c1[i] = (EPI != HPA_FEPI_LOGITS && in && p.fold_c1 && col < p.N) ? p.fold_c1[col] : 0.f;
             if (EPI == HPA_FEPI_RESID && in && row < p.M && col < p.N)
                 pre_res[i] = p.res_in[hpa::frag_index(row, col, p.N)];
         }
     }
 
-    // fold the waves' accumulators through LDS (fixed order) and apply the epilogue
+    // fold the waves' accumulators through LDS (fixed order) and apply the
+    // epilogue; wsum = the waves' row partial statistics [NW][R][2] in LDS,
+    // read when p.fold_c1 (LN folded into w; written before the fold's barrier)
     __device__ __forceinline__ void finish(const FG& p, const f32x4* acc, float* red, float* tile, int nt0,
-                                           int row0) {
+                                           int row0, const float* wsum) {
         const int lane = threadIdx.x & 63;
         const int w = threadIdx.x >> 6;
 #pragma unroll
@@ -139,7 +166,7 @@ struct Epi {
                     red[w * NTW * TE + j * TE + (r * 4 + g) * 64 + lane] = acc[j * MT + r][g];
         __syncthreads();
 
-        constexpr bool rowstat = EPI == HPA_FEPI_RESID || EPI == HPA_FEPI_LOGITS;
+        const bool rowstat = EPI == HPA_FEPI_LOGITS || (EPI == HPA_FEPI_RESID && p.stats_out);  // uniform
 #pragma unroll
         for (int i = 0; i < EPT; ++i) {
             const int e = threadIdx.x + i * NT;
@@ -150,6 +177,17 @@ struct Epi {
                 int j, lrow, lcol, row, col;
                 where(e, nt0, row0, j, lrow, lcol, row, col);
                 const bool live = row < p.M && col < p.N;
+                if (EPI != HPA_FEPI_LOGITS && p.fold_c1) {  // sum_k LN(x)_k W_nk = rstd*(sum_k x_k W'_nk - mean*c1_n)
+                    float S1 = wsum[2 * lrow], S2 = wsum[2 * lrow + 1];
+#pragma unroll
+                    for (int ww = 1; ww < NW; ++ww) {
+                        S1 += wsum[(ww * R + lrow) * 2];
+                        S2 += wsum[(ww * R + lrow) * 2 + 1];
+                    }
+                    const float m = S1 / p.K;  // layernorm_forward statistics, one-pass form
+                    const float rstd = 1.0f / sqrtf(fmaxf(S2 / p.K - m * m, 0.f) + 1e-5f);
+                    val = rstd * (val - m * pre_c1[i]);
+                }
                 val += pre_bias[i];
                 if (EPI == HPA_FEPI_QKV) {
                     if (live) {
@@ -275,7 +313,8 @@ __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
         wf[j] = reinterpret_cast<const float4*>(p.w) + (size_t)min(nt0 + j, p.ntn - 1) * p.K16 * 64 + lane;
     const float4* __restrict__ xf = reinterpret_cast<const float4*>(p.x) + (size_t)rb0 * p.K16 * 64 + lane;
     const size_t rbs = (size_t)p.K16 * 64;  // float4 stride between row blocks
-    const bool use_ln = p.ln_stats != nullptr;
+    const bool ln_apply = p.ln_stats != nullptr && !p.fold_c1;  // folded LN: raw A, statistics in the epilogue
+    const bool use_ln = ln_apply;
     const float4* sg = reinterpret_cast<const float4*>(lngb) + q4;
     const float4* sb = reinterpret_cast<const float4*>(lngb + HPA_FUSED_LN_KMAX) + q4;
 
@@ -301,7 +340,7 @@ __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
 #pragma unroll
     for (int r = 0; r < MT; ++r) mu[r] = rs[r] = 0.f;
     if (use_ln) {
-        for (int i = threadIdx.x; i < p.K / 4; i += NT) {
+        for (int i = threadIdx.x; ln_apply && i < p.K / 4; i += NT) {
             reinterpret_cast<float4*>(lngb)[i] = reinterpret_cast<const float4*>(p.ln_w)[i];
             reinterpret_cast<float4*>(lngb + HPA_FUSED_LN_KMAX)[i] = reinterpret_cast<const float4*>(p.ln_b)[i];
         }
@@ -354,13 +393,17 @@ __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
     f32x4 acc[MT * NTW];
 #pragma unroll
     for (int i = 0; i < MT * NTW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool fold = p.fold_c1 != nullptr;  // row statistics from the A fragments (row_sums_add)
+    float fs1[MT], fs2[MT];
+#pragma unroll
+    for (int r = 0; r < MT; ++r) fs1[r] = fs2[r] = 0.f;
     auto comp = [&](Buf& f, int t) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (t * U + u < nsteps) {
                 float4 xa[MT];
                 float4 g, b;
-                if (use_ln) {
+                if (ln_apply) {
                     const int k = kb0 + t * U + u;
                     g = sg[4 * k];
                     b = sb[4 * k];
@@ -368,7 +411,8 @@ __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
 #pragma unroll
                 for (int r = 0; r < MT; ++r) {
                     xa[r] = f.x[u][r];
-                    if (use_ln) xa[r] = ln4(xa[r], mu[r], rs[r], g, b);
+                    if (fold) row_sums_add(xa[r], fs1[r], fs2[r]);
+                    if (ln_apply) xa[r] = ln4(xa[r], mu[r], rs[r], g, b);
                 }
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
@@ -392,9 +436,12 @@ __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
         comp(Bb, t + 1);
     }
 
+    if (fold)  // [NW][R][2] over the LN weight area (unused when folded)
+#pragma unroll
+        for (int r = 0; r < MT; ++r) row_sums_publish(fs1[r], fs2[r], lngb + (w * R + 16 * r) * 2);
     Epi<NW, EPI, MT, NTW, WT> epi;
     epi.prefetch(p, nt0, row0);
-    epi.finish(p, acc, red, tile, nt0, row0);
+    epi.finish(p, acc, red, tile, nt0, row0, lngb);
 }
 
 template <int NW, int EPI, int MT, int NTW, int UD = 0>
@@ -429,14 +476,15 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
     const int w = threadIdx.x >> 6;
     const int row0 = ry * 16;
     const int q4 = lane >> 4;
-    const bool use_ln = HPA_OS_EXP != 1 && p.ln_stats != nullptr;
+    const bool fold = HPA_OS_EXP != 1 && p.fold_c1 != nullptr;  // LN folded into w: row sums from xv
+    const bool ln_apply = HPA_OS_EXP != 1 && p.ln_stats != nullptr && !fold;
 
     // 1. LN statistics partials of the 16 rows: 4 threads per row, issued first
     constexpr int SPT = 12;  // partial tiles per thread: ln_ntiles <= 48 (C <= 768); else looped
     float s1 = 0.f, s2 = 0.f;
     float sa[SPT], sb[SPT];
     const int srow = row0 + (threadIdx.x >> 2), sq = threadIdx.x & 3;
-    const bool stat_thread = use_ln && threadIdx.x < 64 && srow < p.M;
+    const bool stat_thread = ln_apply && threadIdx.x < 64 && srow < p.M;
     if (stat_thread) {
 #pragma unroll
         for (int j = 0; j < SPT; ++j) {
@@ -448,7 +496,7 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
     // 2. LN weight / bias -> registers (stored to LDS below)
     float4 lw4 = make_float4(0.f, 0.f, 0.f, 0.f), lb4 = lw4;
     const int K4 = p.K / 4;
-    if (use_ln && (int)threadIdx.x < K4) {
+    if (ln_apply && (int)threadIdx.x < K4) {
         lw4 = reinterpret_cast<const float4*>(p.ln_w)[threadIdx.x];
         lb4 = reinterpret_cast<const float4*>(p.ln_b)[threadIdx.x];
     }
@@ -475,9 +523,9 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
     epi.prefetch(p, nt, row0);
     HPA_TS(1, bid);
 
-    // LN: reduce the statistics (waits only for the loads of step 1)
-    float mu = 0.f, rs = 0.f;
-    if (use_ln) {
+    // LN: reduce the statistics (waits only for the loads of step 1) into
+    // lnst; the 4 threads of a row are adjacent lanes of wave 0
+    auto reduce_stats = [&]() {
         if (stat_thread) {
 #pragma unroll
             for (int j = 0; j < SPT; ++j)
@@ -505,6 +553,10 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
                 lnst[2 * (threadIdx.x >> 2) + 1] = 1.0f / sqrtf(v + 1e-5f);
             }
         }
+    };
+    float mu = 0.f, rs = 0.f;
+    if (ln_apply) {
+        reduce_stats();
         if ((int)threadIdx.x < K4) {
             reinterpret_cast<float4*>(lngb)[threadIdx.x] = lw4;
             reinterpret_cast<float4*>(lngb + HPA_FUSED_LN_KMAX)[threadIdx.x] = lb4;
@@ -527,7 +579,7 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
 #pragma unroll
     for (int s = 0; s < S; ++s) {
         float4 xa = xv[s];
-        if (use_ln) xa = ln4(xa, mu, rs, sg[4 * (w * S + s)], sbv[4 * (w * S + s)]);
+        if (ln_apply) xa = ln4(xa, mu, rs, sg[4 * (w * S + s)], sbv[4 * (w * S + s)]);
 #if HPA_OS_EXP == 2
         acc[0][0] += xa.x * wv[s].x + xa.y * wv[s].y;
         acc[0][1] += xa.z * wv[s].z + xa.w * wv[s].w;
@@ -546,7 +598,13 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
     HPA_TS_ACC(acc[0]);
 #endif
     HPA_TS(3, bid);
-    epi.finish(p, acc, red, tile, nt, row0);
+    if (fold) {  // published by the fold's barrier in finish(): [NW][16][2] over the LN weight area
+        float fs1 = 0.f, fs2 = 0.f;
+#pragma unroll
+        for (int s = 0; s < S; ++s) row_sums_add(xv[s], fs1, fs2);
+        row_sums_publish(fs1, fs2, lngb + w * 32);
+    }
+    epi.finish(p, acc, red, tile, nt, row0, lngb);
     HPA_TS(4, bid);
 }
 
@@ -595,6 +653,8 @@ static inline int fused_prepare(const HpaFusedGemm* g, FG* p) {
     p->bt_stride = g->bt_stride;
     p->pos = g->pos;
     p->row_seq = g->row_seq;
+    p->fold_c1 = g->ln_fold_c1;
+    HPA_REQUIRE(!g->ln_fold_c1 || g->epilogue != HPA_FEPI_LOGITS, "gemm_fused: ln_fold_c1 with LOGITS");
     if (g->epilogue == HPA_FEPI_QKV) {
         const HpaKVPool* pool = g->pool;
         HPA_REQUIRE(pool && pool->base && (pool->dtype == HPA_F32 || pool->dtype == HPA_BF16) &&
@@ -609,7 +669,7 @@ static inline int fused_prepare(const HpaFusedGemm* g, FG* p) {
         p->NH = pool->num_heads;
         p->P = pool->page_size;
     }
-    if (g->epilogue == HPA_FEPI_RESID) HPA_REQUIRE(g->res_in && g->stats_out, "gemm_fused RESID");
+    if (g->epilogue == HPA_FEPI_RESID) HPA_REQUIRE(g->res_in, "gemm_fused RESID: res_in");
     if (g->epilogue == HPA_FEPI_LOGITS) HPA_REQUIRE(g->part_out, "gemm_fused LOGITS: part_out");
     p->gx = p->gy = 0;
     return 0;

@@ -612,6 +612,8 @@ struct GPT2Decode {
     int fused;
     float* d_wpack;   /* packed qkvw, attprojw, fcw, fcprojw of every layer, then wte */
     size_t wpack_off[5]; /* per-layer strides (0..3) and wte offset (4) */
+    float* d_fold;    /* LN folded into qkvw / fcw (hpa_ln_fold_pack): per layer c1, c2 of
+                         qkv [3C] [3C] then fc [4C] [4C]; NULL: LN applied on the operand path */
     int fwaves[5];    /* waves per workgroup: qkv, attproj, fc, fcproj, logits */
     int frb[5];       /* 16-row blocks per workgroup, same order */
     int fct[5];       /* 16-column tiles per workgroup, same order */
@@ -774,6 +776,7 @@ static void dec_free(GPT2Decode* d) {
     hpa_free(d->d_res); hpa_free(d->d_res2); hpa_free(d->d_ln); hpa_free(d->d_q);
     hpa_free(d->d_att); hpa_free(d->d_fch); hpa_free(d->d_part); hpa_free(d->d_logits);
     hpa_free(d->d_wpack);
+    hpa_free(d->d_fold);
     hpa_free(d->d_rng);
     dec_lanes_free(d);
     hpa_event_destroy(d->ev_fork);
@@ -812,12 +815,27 @@ static int dec_init_fused(GPT2* model, GPT2Decode* d) {
     size_t total = d->wpack_off[4] + hpa_frag_elems(V, C);
     d->d_wpack = (float*)hpa_malloc(total * 4);
     if (!d->d_wpack) return 1;
+    /* LN1 / LN2 folded into the qkv / fc weights (default; HPA_LN_FOLD=0 keeps
+     * the LN on the operand path): the GEMM then starts on x as it stands and
+     * the row statistics are needed only in its epilogue */
+    const char* fe = getenv("HPA_LN_FOLD");
+    const int fold = !(fe && fe[0] == '0');
+    d->d_fold = NULL;
+    if (fold) {
+        d->d_fold = (float*)hpa_malloc((size_t)L * 14 * C * 4);
+        if (!d->d_fold) return 1;
+    }
     for (int l = 0; l < L; l++) {
         float* base = d->d_wpack + e_layer * l;
         const size_t lc = (size_t)l * C;
-        if (hpa_pack_frag(w->qkvw + lc * 3 * C, 3 * C, C, C, base + d->wpack_off[0]) ||
+        float* fl = fold ? d->d_fold + (size_t)l * 14 * C : NULL;
+        if ((fold ? hpa_ln_fold_pack(w->qkvw + lc * 3 * C, 3 * C, C, w->ln1w + lc, w->ln1b + lc,
+                                     w->qkvb + 3 * lc, base + d->wpack_off[0], fl, fl + 3 * C)
+                  : hpa_pack_frag(w->qkvw + lc * 3 * C, 3 * C, C, C, base + d->wpack_off[0])) ||
             hpa_pack_frag(w->attprojw + lc * C, C, C, C, base + d->wpack_off[1]) ||
-            hpa_pack_frag(w->fcw + lc * 4 * C, 4 * C, C, C, base + d->wpack_off[2]) ||
+            (fold ? hpa_ln_fold_pack(w->fcw + lc * 4 * C, 4 * C, C, w->ln2w + lc, w->ln2b + lc,
+                                     w->fcb + 4 * lc, base + d->wpack_off[2], fl + 6 * C, fl + 10 * C)
+                  : hpa_pack_frag(w->fcw + lc * 4 * C, 4 * C, C, C, base + d->wpack_off[2])) ||
             hpa_pack_frag(w->fcprojw + lc * 4 * C, C, 4 * C, 4 * C, base + d->wpack_off[3]))
             return 1;
     }
@@ -1101,19 +1119,22 @@ static void lane_gemm(GPT2* model, int li, int l, int which, HpaFusedGemm* g) {
             g->x = ln->res; g->K = C; g->ln_stats = ln->st1; g->ln_ntiles = l == 0 ? 1 : ct;
             g->ln_w = w->ln1w + lc; g->ln_b = w->ln1b + lc; g->w = wl + d->wpack_off[0]; g->N = 3 * C;
             g->bias = w->qkvb + 3 * lc; g->out = d->d_q + (size_t)ln->r0 * C;
+            if (d->d_fold) { g->ln_fold_c1 = d->d_fold + 14 * lc; g->bias = g->ln_fold_c1 + 3 * C; }
             break;
         case G_ATTPROJ: /* res2 = res + att . Wap^T + b, LN2 statistics */
             g->x = ln->att; g->K = C; g->w = wl + d->wpack_off[1]; g->N = C; g->bias = w->attprojb + lc;
-            g->out = ln->res2; g->res_in = ln->res; g->stats_out = ln->st2;
+            g->out = ln->res2; g->res_in = ln->res; g->stats_out = d->d_fold ? NULL : ln->st2; /* fc sums its own */
             break;
         case G_FC: /* gelu(LN2(res2) . Wfc^T + b) */
             g->x = ln->res2; g->K = C; g->ln_stats = ln->st2; g->ln_ntiles = ct; g->ln_w = w->ln2w + lc;
             g->ln_b = w->ln2b + lc; g->w = wl + d->wpack_off[2]; g->N = 4 * C; g->bias = w->fcb + 4 * lc;
             g->out = ln->fch;
+            if (d->d_fold) { g->ln_fold_c1 = d->d_fold + 14 * lc + 6 * C; g->bias = g->ln_fold_c1 + 4 * C; }
             break;
         case G_FCPROJ: /* res = res2 + fch . Wfp^T + b, next-LN statistics */
             g->x = ln->fch; g->K = 4 * C; g->w = wl + d->wpack_off[3]; g->N = C; g->bias = w->fcprojb + lc;
-            g->out = ln->res; g->res_in = ln->res2; g->stats_out = ln->st1;
+            g->out = ln->res; g->res_in = ln->res2;
+            g->stats_out = d->d_fold && l + 1 < c.num_layers ? NULL : ln->st1; /* LNf of logits: last layer */
             break;
         default: /* logits = LNf(res) . wte^T, argmax partials */
             g->x = ln->res; g->K = C; g->ln_stats = ln->st1; g->ln_ntiles = c.num_layers == 0 ? 1 : ct;
@@ -1657,19 +1678,23 @@ static int prefill_gemm(GPT2* model, int l, int which, int R) {
             g.epilogue = HPA_FEPI_QKV; g.x = d->pf_res; g.K = C; g.ln_stats = d->pf_st1;
             g.ln_ntiles = l == 0 ? 1 : ct; g.ln_w = w->ln1w + lc; g.ln_b = w->ln1b + lc;
             g.w = wl + d->wpack_off[0]; g.N = 3 * C; g.bias = w->qkvb + 3 * lc; g.out = d->pf_q;
+            if (d->d_fold) { g.ln_fold_c1 = d->d_fold + 14 * lc; g.bias = g.ln_fold_c1 + 3 * C; }
             break;
         case G_ATTPROJ:
             g.epilogue = HPA_FEPI_RESID; g.x = d->pf_att; g.K = C; g.w = wl + d->wpack_off[1]; g.N = C;
-            g.bias = w->attprojb + lc; g.out = d->pf_res2; g.res_in = d->pf_res; g.stats_out = d->pf_st2;
+            g.bias = w->attprojb + lc; g.out = d->pf_res2; g.res_in = d->pf_res;
+            g.stats_out = d->d_fold ? NULL : d->pf_st2;
             break;
         case G_FC:
             g.epilogue = HPA_FEPI_GELU; g.x = d->pf_res2; g.K = C; g.ln_stats = d->pf_st2; g.ln_ntiles = ct;
             g.ln_w = w->ln2w + lc; g.ln_b = w->ln2b + lc; g.w = wl + d->wpack_off[2]; g.N = 4 * C;
             g.bias = w->fcb + 4 * lc; g.out = d->pf_fch;
+            if (d->d_fold) { g.ln_fold_c1 = d->d_fold + 14 * lc + 6 * C; g.bias = g.ln_fold_c1 + 4 * C; }
             break;
         default: /* G_FCPROJ */
             g.epilogue = HPA_FEPI_RESID; g.x = d->pf_fch; g.K = 4 * C; g.w = wl + d->wpack_off[3]; g.N = C;
-            g.bias = w->fcprojb + lc; g.out = d->pf_res; g.res_in = d->pf_res2; g.stats_out = d->pf_st1;
+            g.bias = w->fcprojb + lc; g.out = d->pf_res; g.res_in = d->pf_res2;
+            g.stats_out = d->d_fold && l + 1 < c.num_layers ? NULL : d->pf_st1;
             break;
     }
     return hpa_gemm_fused(&g);

@@ -48,7 +48,8 @@ def test_pack_unpack_roundtrip(hip):
     assert np.array_equal(d_b.download(a.shape), a)
 
 
-def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixed=None, variant=0, ct=0):
+def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixed=None, variant=0, ct=0,
+         fold=False):
     L = hip.lib()
     x = rng.uniform(-1, 1, (M, K)).astype(np.float32)
     W = rng.uniform(-0.05, 0.05, (N, K)).astype(np.float32)
@@ -79,6 +80,20 @@ def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixe
         a = x.astype(np.float64)
     g.w = dev(hip.to_frag(W))
     g.bias = dev(bias) if epi != hip.HPA_FEPI_LOGITS else None
+    if fold:  # LN folded into the packed weights (hpa_ln_fold_pack)
+        assert ln
+        wf = hip.DeviceBuffer(L.hpa_frag_elems(N, K) * 4)
+        c1, c2 = hip.DeviceBuffer(N * 4), hip.DeviceBuffer(N * 4)
+        keep.extend([wf, c1, c2])
+        hip.check(L.hpa_ln_fold_pack(dev(W), N, K, g.ln_w, g.ln_b, g.bias, wf.ptr, c1.ptr, c2.ptr), "fold")
+        hip.check(L.hpa_synchronize())
+        g.w, g.bias, g.ln_fold_c1 = wf.ptr, c2.ptr, c1.ptr
+        Wg = (W * lw).astype(np.float64)  # the packed products (fp32-rounded: within the bound's slack)
+        x64 = x.astype(np.float64)
+        mu = x64.mean(-1)
+        rs = 1 / np.sqrt(((x64 - mu[:, None]) ** 2).mean(-1) + 1e-5)
+        c1h = Wg.sum(1)
+        fold_bound = 4e-6 * rs[:, None] * (np.abs(x64) @ np.abs(Wg).T + np.abs(mu)[:, None] * np.abs(c1h)) + 2e-6
     g.waves = waves
     g.row_blocks = rb
     g.variant = variant
@@ -86,6 +101,8 @@ def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixe
     g.epilogue = epi
     acc = a @ W.astype(np.float64).T
     bound = 4e-6 * (np.abs(a) @ np.abs(W.astype(np.float64)).T) + 2e-6
+    if fold:
+        bound = np.maximum(bound, fold_bound)
     if epi != hip.HPA_FEPI_LOGITS:
         acc = acc + bias
     if epi == hip.HPA_FEPI_RESID:
@@ -328,3 +345,48 @@ def test_fused_oneshot_bit_identical_to_looped(hip, epi, K, N, waves, M):
 def test_fused_oneshot_rejects_unsupported_shape(hip):
     with pytest.raises(RuntimeError):
         _run(hip, hip.HPA_FEPI_GELU, 16, 512, 64, 4, ln=False, rng=np.random.default_rng(1), variant=2)
+
+
+@pytest.mark.parametrize("epi,N,waves,variant,rb,ct", [("GELU", 3072, 4, 2, 1, 1), ("GELU", 3072, 4, 1, 1, 1),
+                                                       ("QKV", 2304, 4, 2, 1, 1), ("QKV", 2304, 8, 1, 4, 2),
+                                                       ("GELU", 3072, 8, 1, 4, 2)])
+@pytest.mark.parametrize("M", [64, 37])
+def test_fused_ln_fold(hip, epi, N, waves, variant, rb, ct, M):
+    """LayerNorm folded into the packed weights (hpa_ln_fold_pack, the
+    engine's qkv / fc): within the f64 bound of LN(x) . W^T + b, for the
+    one-shot (decode) and looped multi-tile (prefill) kernels; the two
+    kernels agree bit for bit"""
+    e = getattr(hip, "HPA_FEPI_" + epi)
+    K = 768
+    r = np.random.default_rng(13)
+    fixed = dict(x=(r.uniform(-1, 1, (M, K)) + r.uniform(-0.5, 0.5, (M, 1))).astype(np.float32),  # mean != 0
+                 W=r.uniform(-0.05, 0.05, (N, K)).astype(np.float32),
+                 bias=r.uniform(-0.1, 0.1, N).astype(np.float32),
+                 lw=r.uniform(0.8, 1.2, K).astype(np.float32), lb=r.uniform(-0.1, 0.1, K).astype(np.float32))
+    pool_args = None
+    if epi == "QKV":
+        pool = hip.Pool(1, N // 3 // 64, 16, 4 * M)
+        bt = np.arange(4 * M, dtype=np.int32).reshape(M, 4)
+        pos = (np.arange(M, dtype=np.int32) * 7) % 64
+        pool_args = (pool, bt, pos)
+    out, acc, bound, keep = _run(hip, e, M, K, N, waves, ln=True, rng=np.random.default_rng(0), rb=rb,
+                                 fixed=fixed, variant=variant, ct=ct, pool_args=pool_args, fold=True)
+    if epi == "QKV":
+        C = N // 3
+        q = out.download((M, C))
+        assert np.all(np.abs(q - acc[:, :C]) <= bound[:, :C])
+        for b in (0, M - 1):
+            k, v = pool.read_tokens(0, bt[b], pos[b] + 1)
+            assert np.all(np.abs(k[pos[b]] - acc[b, C:2 * C]) <= bound[b, C:2 * C])
+            assert np.all(np.abs(v[pos[b]] - acc[b, 2 * C:]) <= bound[b, 2 * C:])
+        got = q
+    else:
+        Mp = (M + 15) // 16 * 16
+        got = hip.from_frag(out.download(Mp * N), M, N)
+        ref = 0.5 * acc * (1 + np.tanh(np.sqrt(2 / np.pi) * (acc + 0.044715 * acc ** 3)))
+        assert np.all(np.abs(got - ref) <= bound + 1e-6)
+    if variant == 2:  # the looped kernel with the same waves: same bits
+        out1, _, _, keep1 = _run(hip, e, M, K, N, waves, ln=True, rng=np.random.default_rng(0), rb=1,
+                                 fixed=fixed, variant=1, ct=1, pool_args=pool_args, fold=True)
+        got1 = out1.download((M, N // 3)) if epi == "QKV" else hip.from_frag(out1.download(Mp * N), M, N)
+        assert np.array_equal(got, got1)
