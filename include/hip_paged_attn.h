@@ -213,7 +213,7 @@ typedef struct {
     int row_blocks;       /* 16-row blocks per workgroup: 1, 2 or 4; 0 = by shape */
     int variant;          /* 0 = by shape; 1 = looped (two trips in flight);
                              2 = one-shot (every operand load issued up front; one
-                             row block; (waves, K/16) in {(4,48),(8,48),(16,48),(8,192)});
+                             row block; (waves, K/16) in {(4,48),(8,48),(16,48),(8,192),(16,192)});
                              3 = looped with larger trips (same results as 1);
                              4 = LOGITS only: activation-resident persistent kernel
                              (K = 768, rows <= 64; 16 waves; else as 1) */

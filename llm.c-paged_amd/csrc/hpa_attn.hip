@@ -62,8 +62,8 @@ __global__ __launch_bounds__(NW * 64, 3) void paged_attn_decode_f32(
     if constexpr (BF16) {
         const unsigned short* base = reinterpret_cast<const unsigned short*>(layer_base);
         float4 acc[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
-        attn_tiles_bf16<P, NW>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, page_elems, bt, ctx, 0,
-                               n_it, qscale, m, l, acc);
+        attn_tiles_bf16<P, NW>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, page_elems, bt, bt_stride, ctx,
+                               0, n_it, qscale, m, l, acc);
         if (!attn_fold_bf16<NW>(m, l, acc, s_m, s_l, s_acc)) return;
         const float inv = l == 0.f ? 0.f : 1.f / l;
 #pragma unroll
@@ -76,8 +76,8 @@ __global__ __launch_bounds__(NW * 64, 3) void paged_attn_decode_f32(
     } else {
         const float* base = reinterpret_cast<const float*>(layer_base);
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        attn_tiles<P, NW>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, page_elems, bt, ctx, 0,
-                          n_it, qscale, m, l, acc);
+        attn_tiles<P, NW>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, page_elems, bt, bt_stride, ctx,
+                          0, n_it, qscale, m, l, acc);
         if (!attn_fold<NW>(m, l, acc, s_m, s_l, s_acc)) return;
         // out[b][h*64 + 4*lane .. +3]: row-major, or the frag layout the next
         // GEMM reads (4 consecutive columns stay one contiguous float4 there)

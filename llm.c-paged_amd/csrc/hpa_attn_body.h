@@ -19,6 +19,20 @@ __device__ __forceinline__ float4 load_stream(const float* ptr) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
+// Page ids of a wave's first tile.  The table load is issued without waiting
+// for ctx (pos[b] is itself a load at kernel start: one dependent round trip
+// fewer before the K/V stream); lanes past ctx then take lane 0's id (token
+// t0 < ctx for every tile below it_end), so garbage entries past the
+// sequence's pages are never used as addresses.
+template <int P>
+__device__ __forceinline__ int first_tile_pid(const int* __restrict__ bt, int bt_len, int ctx, int it,
+                                              int it_end) {
+    const unsigned tok = ((unsigned)it << 6) + (threadIdx.x & 63);
+    const int raw = bt[min(tok / P, (unsigned)bt_len - 1u)];  // inside the table row
+    const int lane0 = __builtin_amdgcn_readfirstlane(raw);
+    return it < it_end && tok < (unsigned)ctx ? raw : lane0;
+}
+
 // The 64-token tiles it = it_begin + w, it_begin + w + NW, ... < it_end of
 // one (sequence, head), folded into this wave's online-softmax state
 // (m, l: log2 domain; acc: lane (g = lane>>4, d4 = lane&15) holds dims
@@ -28,8 +42,8 @@ __device__ __forceinline__ float4 load_stream(const float* ptr) {
 template <int P, int NW>
 __device__ __forceinline__ void attn_tiles(const float* __restrict__ qh, const float* __restrict__ kbase,
                                            const float* __restrict__ vbase, size_t page_elems,
-                                           const int* __restrict__ bt, int ctx, int it_begin, int it_end,
-                                           float qscale, float& m, float& l, float4& acc) {
+                                           const int* __restrict__ bt, int bt_len, int ctx, int it_begin,
+                                           int it_end, float qscale, float& m, float& l, float4& acc) {
     static_assert(P % 4 == 0 && 64 % P == 0, "page size must divide 64 and be a multiple of 4");
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
@@ -37,11 +51,7 @@ __device__ __forceinline__ void attn_tiles(const float* __restrict__ qh, const f
     const int d4 = lane & 15;
     const int v_lane_off = g * HS + d4 * 4;
     int it = it_begin + w;
-    int pid = 0;
-    if (it < it_end) {
-        const unsigned t0 = (unsigned)it << 6, tok = t0 + lane;
-        pid = bt[(tok < (unsigned)ctx ? tok : t0) / P];
-    }
+    int pid = first_tile_pid<P>(bt, bt_len, ctx, it, it_end);
     for (; it < it_end; it += NW) {
         const unsigned t0 = (unsigned)it << 6;
         const unsigned tok = t0 + lane;
@@ -116,8 +126,8 @@ template <int P, int NW>
 __device__ __forceinline__ void attn_tiles_bf16(const float* __restrict__ qh,
                                                 const unsigned short* __restrict__ kbase,
                                                 const unsigned short* __restrict__ vbase, size_t page_elems,
-                                                const int* __restrict__ bt, int ctx, int it_begin, int it_end,
-                                                float qscale, float& m, float& l, float4* acc) {
+                                                const int* __restrict__ bt, int bt_len, int ctx, int it_begin,
+                                                int it_end, float qscale, float& m, float& l, float4* acc) {
     static_assert(P % 8 == 0 && 64 % P == 0, "bf16 pages: page size 8, 16, 32 or 64");
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
@@ -125,11 +135,7 @@ __device__ __forceinline__ void attn_tiles_bf16(const float* __restrict__ qh,
     const int d8 = lane & 7;
     const int v_lane_off = g * HS + d8 * 8;
     int it = it_begin + w;
-    int pid = 0;
-    if (it < it_end) {
-        const unsigned t0 = (unsigned)it << 6, tok = t0 + lane;
-        pid = bt[(tok < (unsigned)ctx ? tok : t0) / P];
-    }
+    int pid = first_tile_pid<P>(bt, bt_len, ctx, it, it_end);
     for (; it < it_end; it += NW) {
         const unsigned t0 = (unsigned)it << 6;
         const unsigned tok = t0 + lane;
@@ -348,7 +354,8 @@ __device__ __forceinline__ void attn_chunk_body(const AttnChunk& a, int bid, flo
     float m = a.m_init, l = 0.f;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     attn_tiles<P, NW>(qh, a.layer_base + (size_t)h * TILE, a.layer_base + (size_t)(a.NH + h) * TILE,
-                      a.page_elems, a.bt + (size_t)b * a.bt_stride, ctx, it0, it1, a.qscale, m, l, acc);
+                      a.page_elems, a.bt + (size_t)b * a.bt_stride, a.bt_stride, ctx, it0, it1, a.qscale, m, l,
+                      acc);
     float* s_m = smem;
     float* s_l = smem + NW;
     float4* s_acc = reinterpret_cast<float4*>(smem + 2 * NW + (4 - (2 * NW) % 4) % 4);

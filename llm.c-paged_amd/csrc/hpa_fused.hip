@@ -375,6 +375,7 @@ int launch_os(const FG& p, int epi, int nw) {
         case 8 * 100 + 6: return launch16_os<8, 6>(p, epi);
         case 16 * 100 + 3: return launch16_os<16, 3>(p, epi);
         case 8 * 100 + 24: return launch16_os<8, 24>(p, epi);
+        case 16 * 100 + 12: return launch16_os<16, 12>(p, epi);
         default: return -1;
     }
 }
@@ -492,7 +493,7 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
     if (g->variant == 2 || (g->variant == 0 && mt == 1 && p.ntn < 1024 && g->col_tiles <= 1)) {
         const int rc = launch_os(p, g->epilogue, nw);
         if (rc >= 0) return rc;
-        HPA_REQUIRE(g->variant == 0, "gemm_fused: one-shot needs (waves, K/16) in {(4,48), (8,48), (16,48), (8,192)}");
+        HPA_REQUIRE(g->variant == 0, "gemm_fused: one-shot needs (waves, K/16) in {(4,48), (8,48), (16,48), (8,192), (16,192)}");
     }
     int ntw = g->col_tiles ? g->col_tiles : pick[2];
     // a launch-shape hint: where this M's row blocks (or the waves) cannot

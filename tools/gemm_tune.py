@@ -78,7 +78,7 @@ SHAPES = [("qkv", B, C, 3 * C, pa.HPA_FEPI_GELU, True), ("attproj", B, C, C, pa.
           ("logits", B, C, V, pa.HPA_FEPI_LOGITS, True)]
 
 
-ONESHOT = {(4, 48), (8, 48), (16, 48), (8, 192)}  # hpa_fused.hip launch_os instances
+ONESHOT = {(4, 48), (8, 48), (16, 48), (8, 192), (16, 192)}  # hpa_fused.hip launch_os instances
 
 
 def main():
