@@ -230,7 +230,21 @@ typedef struct {
                              the workgroup already holds (K = the LN width).  No LN
                              prologue and no statistics loads; ln_stats, ln_w and
                              ln_b are not read. */
+    int k_slices;         /* K split over this many workgroups per output tile (looped
+                             kernel only; 0/1 = none): each slice folds its waves,
+                             publishes the tile as a write-through slab, and the last
+                             arriver sums the slabs in slice order and runs the
+                             epilogue (cdna_hip_programming.md "In-launch split-K
+                             reduction").  A row's summation order depends on
+                             (waves, k_slices), never on M or the arrival order. */
+    float* ks_slab;       /* k_slices > 1: workspace, hpa_fused_ks_workspace floats */
+    int* ks_count;        /* k_slices > 1: per-tile counters, zero before the first launch
+                             (every launch leaves them zero) */
 } HpaFusedGemm;
+/* the K slices the engine uses for a shape (1 = none; by shape, never by M) */
+int hpa_fused_pick_slices(int M, int N, int K);
+/* workspace of g's k_slices launch: slab floats and counters (0 when no split) */
+int hpa_fused_ks_workspace(const HpaFusedGemm* g, size_t* slab_floats, size_t* counters);
 /* LayerNorm folding for hpa_gemm_fused (layernorm_forward :49-89 followed by
  * matmul_forward :92-114, restated): for W [N][K] row-major (device), writes
  * dst_frag = frag-packed W[n][k]*ln_w[k], c1[n] = sum_k of those products and

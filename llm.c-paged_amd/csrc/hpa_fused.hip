@@ -335,7 +335,7 @@ __global__ __launch_bounds__(128) void sample_final_kernel(const float* __restri
 inline dim3 xcd_grid(FG& p, int gx, int gy) {
     p.gx = gx;
     p.gy = gy;
-    return dim3((unsigned)(((gx + 7) / 8) * 8 * gy));
+    return dim3((unsigned)(((gx + 7) / 8) * 8 * gy * p.ks));
 }
 
 template <int NW, int MT, int NTW = 1, int UD = 0>
@@ -376,6 +376,7 @@ int launch_os(const FG& p, int epi, int nw) {
         case 16 * 100 + 3: return launch16_os<16, 3>(p, epi);
         case 8 * 100 + 24: return launch16_os<8, 24>(p, epi);
         case 16 * 100 + 12: return launch16_os<16, 12>(p, epi);
+        case 10 * 100 + 10: return launch16_os<10, 10>(p, epi);  // GPT-2 XL (K = 1600)
         default: return -1;
     }
 }
@@ -477,28 +478,61 @@ int hpa_fused_pick_waves(int M, int N, int K) {
     return p[0];
 }
 
+// the looped kernel's launch shape for g (as hpa_gemm_fused resolves it)
+static void looped_shape(const HpaFusedGemm* g, int Mp, int* nw, int* mt, int* ntw) {
+    int pick[3];
+    hpa_fused_pick(g->M, g->N, g->K, pick);
+    *nw = g->waves ? g->waves : pick[0];
+    *mt = g->row_blocks ? g->row_blocks : pick[1];
+    while (*mt > 1 && (Mp / 16) % *mt) *mt >>= 1;  // row blocks of this M
+    *ntw = g->col_tiles ? g->col_tiles : pick[2];
+    // a launch-shape hint: where this M's row blocks (or the waves) cannot
+    // carry it, fall back to one column tile (results are identical)
+    if ((*ntw == 2 && (*mt == 1 || *nw == 16)) || (*ntw == 4 && (*mt != 4 || *nw != 4))) *ntw = 1;
+}
+
+// K slices by shape (never by M).  Measured on the GPT-2 XL layer GEMMs
+// (profiles/r1/ksplit_xl.txt): 2 or 4 slices were slower than none at every
+// shape (qkv 26 -> 34 / 42 us, fc 26 -> 35 / 48 us): a slice's workgroup
+// keeps the fold, slab exchange and epilogue latency of a whole-K workgroup
+// while its MFMA work shrinks.  So: none; callers may still ask for a split.
+int hpa_fused_pick_slices(int M, int N, int K) {
+    (void)M;
+    (void)N;
+    (void)K;
+    return 1;
+}
+
+int hpa_fused_ks_workspace(const HpaFusedGemm* g, size_t* slab_floats, size_t* counters) {
+    HPA_REQUIRE(g && g->M > 0 && g->N > 0 && g->K > 0 && slab_floats && counters, "ks_workspace: arguments");
+    const int Mp = (g->M + 15) / 16 * 16, ntn = (g->N + 15) / 16;
+    int nw, mt, ntw;
+    looped_shape(g, Mp, &nw, &mt, &ntw);
+    const int ks = g->k_slices > 1 ? g->k_slices : 1;
+    const size_t tiles = (size_t)((ntn + ntw - 1) / ntw) * (size_t)(Mp / 16 / mt);
+    *slab_floats = ks > 1 ? tiles * ks * (size_t)(ntw * mt * 256 + 2 * mt * 16) : 0;
+    *counters = ks > 1 ? tiles : 0;
+    return 0;
+}
+
 int hpa_gemm_fused(const HpaFusedGemm* g) {
     FG p;
     if (fused_prepare(g, &p)) return 1;
-    int pick[3];
-    hpa_fused_pick(g->M, g->N, g->K, pick);
-    const int nw = g->waves ? g->waves : pick[0];
-    int mt = g->row_blocks ? g->row_blocks : pick[1];
-    HPA_REQUIRE(mt == 1 || mt == 2 || mt == 4, "gemm_fused: row_blocks must be 1, 2 or 4");
-    while ((p.Mp / 16) % mt) mt >>= 1;  // row blocks of this M
+    int nw, mt, ntw;
+    HPA_REQUIRE(g->row_blocks == 0 || g->row_blocks == 1 || g->row_blocks == 2 || g->row_blocks == 4,
+                "gemm_fused: row_blocks must be 1, 2 or 4");
+    looped_shape(g, p.Mp, &nw, &mt, &ntw);
     HPA_REQUIRE(g->variant >= 0 && g->variant <= 4, "gemm_fused: variant must be 0 .. 4");
-    if (g->variant == 4 && logits_resident_eligible(p, g->epilogue)) return launch_logits_resident(p);
+    HPA_REQUIRE(p.ks == 1 || g->variant == 0 || g->variant == 1 || g->variant == 3,
+                "gemm_fused: k_slices > 1 runs the looped kernel (variant 0, 1 or 3)");
+    if (p.ks == 1 && g->variant == 4 && logits_resident_eligible(p, g->epilogue)) return launch_logits_resident(p);
     HPA_REQUIRE(g->col_tiles == 0 || g->col_tiles == 1 || g->col_tiles == 2 || g->col_tiles == 4,
                 "gemm_fused: col_tiles must be 1, 2 or 4");
-    if (g->variant == 2 || (g->variant == 0 && mt == 1 && p.ntn < 1024 && g->col_tiles <= 1)) {
+    if (p.ks == 1 && (g->variant == 2 || (g->variant == 0 && mt == 1 && p.ntn < 1024 && g->col_tiles <= 1))) {
         const int rc = launch_os(p, g->epilogue, nw);
         if (rc >= 0) return rc;
-        HPA_REQUIRE(g->variant == 0, "gemm_fused: one-shot needs (waves, K/16) in {(4,48), (8,48), (16,48), (8,192), (16,192)}");
+        HPA_REQUIRE(g->variant == 0, "gemm_fused: one-shot needs (waves, K/16) in {(4,48), (8,48), (16,48), (8,192), (16,192), (10,100)}");
     }
-    int ntw = g->col_tiles ? g->col_tiles : pick[2];
-    // a launch-shape hint: where this M's row blocks (or the waves) cannot
-    // carry it, fall back to one column tile (results are identical)
-    if ((ntw == 2 && (mt == 1 || nw == 16)) || (ntw == 4 && (mt != 4 || nw != 4))) ntw = 1;
     const bool deep = g->variant == 3;  // looped with larger trips (same results as 1)
     switch (nw) {
         case 4: return launch16_mt<4>(p, g->epilogue, mt, ntw, deep);

@@ -50,6 +50,9 @@ struct FG {
     const int* row_seq;  // QKV: block-table row per GEMM row (NULL: the row)
     const float* fold_c1;  // LN folded into w: out = rstd*(acc - mean*c1) + bias (bias = c2)
     int gx, gy;  // column-tile groups x row groups of the launch
+    int ks;      // K slices per output tile (workgroups; looped kernel): 1 = no split
+    float* ks_slab;  // [tile][slice][slab floats] partial tiles (+ folded-LN row sums)
+    int* ks_cnt;     // [tile] arrival counters (zero between launches)
 };
 
 // XCD-aware workgroup order (MI355X_MICROARCH.md "Workgroup dispatch":
@@ -57,12 +60,22 @@ struct FG {
 // of ceil(gx/8)*8*gy blocks is dealt so that the gy row groups of one column
 // group run back to back on ONE XCD: its weight tile is fetched from HBM once
 // and re-read from that XCD's L2.  Returns false for the padding blocks.
-__device__ __forceinline__ bool xcd_tile(const FG& p, int bid, int& cx, int& ry) {
-    const int xg = bid & 7, s = bid >> 3;
+// With K split over p.ks workgroups, the slices of a tile take consecutive
+// s = bid >> 3 (same bid % 8: one XCD under round-robin placement -- a
+// speed choice only, the hand-off is correct for any placement).
+__device__ __forceinline__ bool xcd_tile(const FG& p, int bid, int& cx, int& ry, int& slice) {
+    const int xg = bid & 7;
+    int s = bid >> 3;
+    slice = s % p.ks;
+    s /= p.ks;
     const int q = s / p.gy;
     ry = s - q * p.gy;
     cx = q * 8 + xg;
     return cx < p.gx;
+}
+__device__ __forceinline__ bool xcd_tile(const FG& p, int bid, int& cx, int& ry) {
+    int slice;
+    return xcd_tile(p, bid, cx, ry, slice);
 }
 
 // output store of an epilogue: WT = write-through (sc1), for outputs another
@@ -153,8 +166,70 @@ struct Epi {
     // fold the waves' accumulators through LDS (fixed order) and apply the
     // epilogue; wsum = the waves' row partial statistics [NW][R][2] in LDS,
     // read when p.fold_c1 (LN folded into w; written before the fold's barrier)
+    // K split over p.ks workgroups: every slice publishes its folded tile
+    // (and, LN folded, its rows' partial sums) as a write-through slab and
+    // draws an arrival ticket; the last arriver sums the slabs in slice order
+    // (the result does not depend on arrival order) and runs the epilogue.
+    // cdna_hip_programming.md "In-launch split-K reduction" (sc1 slab stores,
+    // relaxed agent ticket, acquire fence before the plain slab loads).
+    // Returns false in the workgroups that stop here; in the reducer vals
+    // hold the totals and kst[2*lrow..] the rows' total (sum, sum of squares).
+    static constexpr int SLAB = NTW * TE + 2 * R;  // floats per (tile, slice)
+    __device__ __forceinline__ bool ks_exchange(const FG& p, float* vals, float* red, const float* wsum,
+                                                int tile_id, int slice) {
+        float* slabs = p.ks_slab + (size_t)tile_id * p.ks * SLAB;
+        float* mine = slabs + (size_t)slice * SLAB;
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+            const int e = threadIdx.x + i * NT;
+            if (e < NTW * TE) __hip_atomic_store(mine + e, vals[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (p.fold_c1 && threadIdx.x < R) {  // this slice's row sums: its waves in order
+            float S1 = wsum[2 * threadIdx.x], S2 = wsum[2 * threadIdx.x + 1];
+            for (int ww = 1; ww < NW; ++ww) {
+                S1 += wsum[(ww * R + threadIdx.x) * 2];
+                S2 += wsum[(ww * R + threadIdx.x) * 2 + 1];
+            }
+            __hip_atomic_store(mine + NTW * TE + 2 * threadIdx.x, S1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(mine + NTW * TE + 2 * threadIdx.x + 1, S2, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0)
+            red[0] = __int_as_float(
+                __hip_atomic_fetch_add(p.ks_cnt + tile_id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        __syncthreads();
+        if (__float_as_int(red[0]) != p.ks - 1) return false;
+        // every slab load is an sc1 (agent-scope) load: no acquire fence, whose
+        // L2 invalidation would cost the other workgroups of this XCD their
+        // cached operands (measured: 2x slower GEMMs with the fence)
+        if (threadIdx.x == 0) __hip_atomic_store(p.ks_cnt + tile_id, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+            const int e = threadIdx.x + i * NT;
+            if (e < NTW * TE) {
+                float v = ks_load(slabs + e);
+                for (int sl = 1; sl < p.ks; ++sl) v += ks_load(slabs + (size_t)sl * SLAB + e);
+                vals[i] = v;
+            }
+        }
+        if (p.fold_c1) {
+            if (threadIdx.x < 2 * R) {
+                float v = ks_load(slabs + NTW * TE + threadIdx.x);
+                for (int sl = 1; sl < p.ks; ++sl) v += ks_load(slabs + (size_t)sl * SLAB + NTW * TE + threadIdx.x);
+                red[threadIdx.x] = v;
+            }
+            __syncthreads();
+        }
+        return true;
+    }
+    __device__ __forceinline__ static float ks_load(const float* ptr) {
+        return __hip_atomic_load(ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+
     __device__ __forceinline__ void finish(const FG& p, const f32x4* acc, float* red, float* tile, int nt0,
-                                           int row0, const float* wsum) {
+                                           int row0, const float* wsum, int tile_id = 0, int slice = 0) {
         const int lane = threadIdx.x & 63;
         const int w = threadIdx.x >> 6;
 #pragma unroll
@@ -166,23 +241,43 @@ struct Epi {
                     red[w * NTW * TE + j * TE + (r * 4 + g) * 64 + lane] = acc[j * MT + r][g];
         __syncthreads();
 
+        float vals[EPT];
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+            const int e = threadIdx.x + i * NT;
+            float val = 0.f;
+            if (e < NTW * TE) {
+                val = red[e];
+#pragma unroll
+                for (int ww = 1; ww < NW; ++ww) val += red[ww * NTW * TE + e];
+            }
+            vals[i] = val;
+        }
+        const bool split = p.ks > 1;  // uniform
+        if (split && !ks_exchange(p, vals, red, wsum, tile_id, slice)) return;
+
         const bool rowstat = EPI == HPA_FEPI_LOGITS || (EPI == HPA_FEPI_RESID && p.stats_out);  // uniform
 #pragma unroll
         for (int i = 0; i < EPT; ++i) {
             const int e = threadIdx.x + i * NT;
             if (e < NTW * TE) {
-                float val = red[e];
-#pragma unroll
-                for (int ww = 1; ww < NW; ++ww) val += red[ww * NTW * TE + e];
+                float val = vals[i];
                 int j, lrow, lcol, row, col;
                 where(e, nt0, row0, j, lrow, lcol, row, col);
                 const bool live = row < p.M && col < p.N;
                 if (EPI != HPA_FEPI_LOGITS && p.fold_c1) {  // sum_k LN(x)_k W_nk = rstd*(sum_k x_k W'_nk - mean*c1_n)
-                    float S1 = wsum[2 * lrow], S2 = wsum[2 * lrow + 1];
+                    float S1, S2;
+                    if (split) {  // slices in order (ks_exchange)
+                        S1 = red[2 * lrow];
+                        S2 = red[2 * lrow + 1];
+                    } else {
+                        S1 = wsum[2 * lrow];
+                        S2 = wsum[2 * lrow + 1];
 #pragma unroll
-                    for (int ww = 1; ww < NW; ++ww) {
-                        S1 += wsum[(ww * R + lrow) * 2];
-                        S2 += wsum[(ww * R + lrow) * 2 + 1];
+                        for (int ww = 1; ww < NW; ++ww) {
+                            S1 += wsum[(ww * R + lrow) * 2];
+                            S2 += wsum[(ww * R + lrow) * 2 + 1];
+                        }
                     }
                     const float m = S1 / p.K;  // layernorm_forward statistics, one-pass form
                     const float rstd = 1.0f / sqrtf(fmaxf(S2 / p.K - m * m, 0.f) + 1e-5f);
@@ -294,8 +389,8 @@ __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
     float* lnst = tile + NTW * R * 17;               // [R][2] mean, rstd
     float* lnscr = lnst + 2 * R;                     // [4R][2]
 
-    int cx, ry;
-    if (!xcd_tile(p, bid, cx, ry)) return;
+    int cx, ry, slice;
+    if (!xcd_tile(p, bid, cx, ry, slice)) return;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     const int nt0 = cx * NTW;
@@ -303,10 +398,12 @@ __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
     const int row0 = rb0 * 16;
     const int q4 = lane >> 4;  // which 4-k group of the 16-k step
 
-    // ---- this wave's contiguous k-step range
-    const int per = (p.K16 + NW - 1) / NW;
-    const int kb0 = w * per;
-    const int nsteps = max(0, min(p.K16, kb0 + per) - kb0);
+    // ---- this wave's contiguous k-step range (inside this workgroup's K slice)
+    const int kspan = (p.K16 + p.ks - 1) / p.ks;
+    const int ks0 = slice * kspan, ks1 = min(p.K16, ks0 + kspan);
+    const int per = (ks1 - ks0 + NW - 1) / NW;
+    const int kb0 = ks0 + w * per;
+    const int nsteps = max(0, min(ks1, kb0 + per) - kb0);
     const float4* __restrict__ wf[NTW];
 #pragma unroll
     for (int j = 0; j < NTW; ++j)  // tail tiles past ntn re-read the last tile (never stored)
@@ -441,7 +538,7 @@ __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
         for (int r = 0; r < MT; ++r) row_sums_publish(fs1[r], fs2[r], lngb + (w * R + 16 * r) * 2);
     Epi<NW, EPI, MT, NTW, WT> epi;
     epi.prefetch(p, nt0, row0);
-    epi.finish(p, acc, red, tile, nt0, row0, lngb);
+    epi.finish(p, acc, red, tile, nt0, row0, lngb, cx * p.gy + ry, slice);
 }
 
 template <int NW, int EPI, int MT, int NTW, int UD = 0>
@@ -654,6 +751,11 @@ static inline int fused_prepare(const HpaFusedGemm* g, FG* p) {
     p->pos = g->pos;
     p->row_seq = g->row_seq;
     p->fold_c1 = g->ln_fold_c1;
+    p->ks = g->k_slices > 1 ? g->k_slices : 1;
+    p->ks_slab = g->ks_slab;
+    p->ks_cnt = g->ks_count;
+    HPA_REQUIRE(p->ks == 1 || (g->ks_slab && g->ks_count && p->ks <= 16 && p->ks <= p->K16),
+                "gemm_fused: k_slices needs ks_slab / ks_count, <= 16 and <= K/16");
     HPA_REQUIRE(!g->ln_fold_c1 || g->epilogue != HPA_FEPI_LOGITS, "gemm_fused: ln_fold_c1 with LOGITS");
     if (g->epilogue == HPA_FEPI_QKV) {
         const HpaKVPool* pool = g->pool;

@@ -584,6 +584,9 @@ typedef struct {
     int r0, B, Mp;
     float *res, *res2, *att, *fch, *st1, *st2, *part;
     float* astate; /* attention chunk state (pipelined step) */
+    float* ks_slab; /* split-K slabs of the layer GEMMs (hpa_fused_ks_workspace), NULL if none */
+    int* ks_cnt;    /* their per-tile arrival counters (zeroed once; launches leave them zero) */
+    size_t ks_slab_floats, ks_counters;
     void* stream; /* NULL for lane 0 (the launch stream) */
     void* ev_join;
 } DecLane;
@@ -617,6 +620,7 @@ struct GPT2Decode {
     int fwaves[5];    /* waves per workgroup: qkv, attproj, fc, fcproj, logits */
     int frb[5];       /* 16-row blocks per workgroup, same order */
     int fct[5];       /* 16-column tiles per workgroup, same order */
+    int fks[5];       /* K slices (workgroups per output tile), same order */
     DecLane lanes[DEC_MAX_LANES];
     int nlanes;
     int pipeline;     /* 1: two lanes, attention chunks beside the other lane's GEMMs */
@@ -706,11 +710,40 @@ static void dec_lanes_free(GPT2Decode* d) {
         DecLane* ln = &d->lanes[i];
         hpa_free(ln->res); hpa_free(ln->res2); hpa_free(ln->att); hpa_free(ln->fch);
         hpa_free(ln->st1); hpa_free(ln->st2); hpa_free(ln->part); hpa_free(ln->astate);
+        hpa_free(ln->ks_slab); hpa_free(ln->ks_cnt);
         hpa_stream_destroy(ln->stream);
         hpa_event_destroy(ln->ev_join);
         memset(ln, 0, sizeof(*ln));
     }
     d->nlanes = 0;
+}
+
+/* split-K workspace of every lane: the largest of its four layer GEMMs at the
+ * current launch shapes (d->fwaves / frb / fct / fks) */
+static int dec_ks_alloc(GPT2Decode* d, int C) {
+    const int shp[4][2] = {{3 * C, C}, {C, C}, {4 * C, C}, {C, 4 * C}};
+    for (int i = 0; i < d->nlanes; i++) {
+        DecLane* ln = &d->lanes[i];
+        size_t need_f = 0, need_c = 0;
+        for (int k = 0; k < 4; k++) {
+            HpaFusedGemm g;
+            memset(&g, 0, sizeof(g));
+            g.M = ln->B; g.N = shp[k][0]; g.K = shp[k][1];
+            g.waves = d->fwaves[k]; g.row_blocks = d->frb[k]; g.col_tiles = d->fct[k]; g.k_slices = d->fks[k];
+            size_t f, c;
+            if (hpa_fused_ks_workspace(&g, &f, &c)) return 1;
+            if (f > need_f) need_f = f;
+            if (c > need_c) need_c = c;
+        }
+        if (need_f <= ln->ks_slab_floats && need_c <= ln->ks_counters) continue;
+        hpa_free(ln->ks_slab); hpa_free(ln->ks_cnt);
+        ln->ks_slab = (float*)hpa_malloc(need_f * 4);
+        ln->ks_cnt = (int*)hpa_malloc(need_c * 4);
+        if (!ln->ks_slab || !ln->ks_cnt || hpa_memset_async(ln->ks_cnt, 0, need_c * 4)) return 1;
+        ln->ks_slab_floats = need_f;
+        ln->ks_counters = need_c;
+    }
+    return hpa_synchronize();
 }
 
 /* split the batch into up to `n` lanes of whole 16-row blocks */
@@ -751,7 +784,8 @@ static int dec_lanes_alloc(GPT2Decode* d, int n, int C, int V, int NH) {
             hpa_memset_async(ln->st2, 0, (size_t)ct * Mp * 2 * 4))
             return 1;
     }
-    return hpa_synchronize();
+    if (hpa_synchronize()) return 1;
+    return dec_ks_alloc(d, C);
 }
 
 static void dec_prefill_free(GPT2Decode* d) {
@@ -847,6 +881,12 @@ static int dec_init_fused(GPT2* model, GPT2Decode* d) {
         d->fwaves[i] = pk[0];
         d->frb[i] = pk[1];
         d->fct[i] = pk[2];
+        /* K split over workgroups for the MFMA-bound XL layer GEMMs (HPA_KSLICES: unset or 0 =
+         * by shape, 1 = none, n = n slices) */
+        const char* ke = getenv("HPA_KSLICES");
+        const int kn = ke ? atoi(ke) : 0;
+        d->fks[i] = i < 4 ? (kn > 0 ? kn : hpa_fused_pick_slices(B, shp[i][0], shp[i][1])) : 1;
+        if (d->fks[i] < 1) d->fks[i] = 1;
     }
     d->ev_fork = hpa_event_create_nt();
     if (!d->ev_fork) return 1;
@@ -1109,6 +1149,11 @@ static void lane_gemm(GPT2* model, int li, int l, int which, HpaFusedGemm* g) {
     g->waves = d->fwaves[which];
     g->row_blocks = d->frb[which];
     g->col_tiles = d->fct[which];
+    if (which != G_LOGITS && d->fks[which] > 1) {
+        g->k_slices = d->fks[which];
+        g->ks_slab = ln->ks_slab;
+        g->ks_count = ln->ks_cnt;
+    }
     g->pool = &d->pool;
     g->layer = l;
     g->block_table = d->d_bt + (size_t)ln->r0 * d->bt_stride;
@@ -1236,7 +1281,8 @@ static int pipe_launch(GPT2* model, int att_lane, int l, int chunk, int gemm_lan
     if (which < 0) return hpa_attn_chunk_with_gemm(&a, NULL);
     HpaFusedGemm g;
     lane_gemm(model, gemm_lane, gl, which, &g);
-    g.waves = 4;  /* the combo's GEMM role: 4 waves, one row block, one column tile */
+    g.k_slices = 0; /* the combo's GEMM role: no K split, 4 waves, one row block, one column tile */
+    g.waves = 4;
     g.row_blocks = 1;
     g.col_tiles = 1;
     return hpa_attn_chunk_with_gemm(&a, &g);
@@ -1334,7 +1380,8 @@ static int dec_launch_split(GPT2* model) {
  * Two launches per layer instead of ten. */
 static void chain_desc(GPT2* model, int li, int l, int which, HpaFusedGemm* g) {
     lane_gemm(model, li, l, which, g);
-    g->waves = 4; /* the chain's tiles: 4 waves, one row block, one column tile */
+    g->k_slices = 0; /* the chain's tiles: no K split, 4 waves, one row block, one column tile */
+    g->waves = 4;
     g->row_blocks = 1;
     g->col_tiles = 1;
 }
@@ -1902,6 +1949,7 @@ int gpt2_decode_gemm_config(GPT2* model, int* waves5, int* row_blocks5, int* col
         if (row_blocks5 && row_blocks5[i]) d->frb[i] = row_blocks5[i];
         if (col_tiles5 && col_tiles5[i]) d->fct[i] = col_tiles5[i];
     }
+    if (dec_ks_alloc(d, model->config.channels)) return 1; /* split-K slabs of the new shapes */
     if (d->graph) { /* recapture with the new launch shapes */
         hpa_synchronize();
         hpa_graph_destroy(d->graph);

@@ -78,7 +78,7 @@ SHAPES = [("qkv", B, C, 3 * C, pa.HPA_FEPI_GELU, True), ("attproj", B, C, C, pa.
           ("logits", B, C, V, pa.HPA_FEPI_LOGITS, True)]
 
 
-ONESHOT = {(4, 48), (8, 48), (16, 48), (8, 192), (16, 192)}  # hpa_fused.hip launch_os instances
+ONESHOT = {(4, 48), (8, 48), (16, 48), (8, 192), (16, 192), (10, 100)}  # hpa_fused.hip launch_os instances
 
 
 def main():
@@ -97,7 +97,7 @@ def main():
         auto = (pk[0], rb_eff, 2 if oneshot else 1, pk[2])
         res = []
         ref = None
-        for waves in (4, 8, 16):
+        for waves in (4, 8, 10, 16):
             for rb in (1, 2, 4):
                 for variant in (1, 2, 3, 4):
                     for ct in (1, 2, 4):
