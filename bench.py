@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--page-size", type=int, default=16)
     ap.add_argument("--kv-dtype", default="f32", choices=["f32", "bf16"],
                     help="KV pool storage (bf16: BASELINE config 5; arithmetic stays fp32)")
+    ap.add_argument("--w-dtype", default="f32", choices=["f32", "bf16"],
+                    help="GEMM weight storage (bf16: weights and GEMM inputs bf16, fp32 accumulation on "
+                         "bf16 MFMA -- the 'bf16 decode' of BASELINE config 5)")
     ap.add_argument("--model", default="124M", choices=["124M", "XL"])
     ap.add_argument("--prefill", default="synthetic", choices=["synthetic", "real", "decode"])
     ap.add_argument("--prefill-chunk", type=int, default=256, help="tokens per sequence per prefill call")
@@ -98,7 +101,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(cfgd, B, P, ctx, budget_s, kv_bf16=False):
+def cpu_baseline(cfgd, B, P, ctx, budget_s, kv_bf16=False, w_bf16=False):
     """The oracle's OpenMP C restatement of the same paged decode, timed on the
     host cores on a bounded sample (rank 0, N=1).  Test infrastructure only."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -108,7 +111,7 @@ def cpu_baseline(cfgd, B, P, ctx, budget_s, kv_bf16=False):
     os.environ["OMP_NUM_THREADS"] = str(threads)
     params = pagedattn.synthetic_params(cfgd, seed=1337)
     c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
-    dec = oc.PagedDecoder(params, c, B, P, cfgd["maxT"], page_seed=3, fast=True, kv_bf16=kv_bf16)
+    dec = oc.PagedDecoder(params, c, B, P, cfgd["maxT"], page_seed=3, fast=True, kv_bf16=kv_bf16, w_bf16=w_bf16)
     max_steps = min(256, ctx // 2)  # the budget normally ends the sample first (near ctx)
     start_ctx = ctx - max_steps
     dec.fill_random(start_ctx, seed=5)
@@ -133,7 +136,7 @@ def cpu_baseline(cfgd, B, P, ctx, budget_s, kv_bf16=False):
         pass
     return {"value": B * steps / el, "unit": "tokens/s", "cores": threads, "kind": "port",
             "sample": f"oracle/liboracle_fast.so (-O3 -Ofast OpenMP C restatement), GPT-2 124M fp32"
-                      f"{' (bf16 KV)' if kv_bf16 else ''}, B={B}, page {P}, {steps} decode steps at ctx "
+                      f"{' (bf16 KV)' if kv_bf16 else ''}{' (bf16-rounded weights and GEMM inputs)' if w_bf16 else ''}, B={B}, page {P}, {steps} decode steps at ctx "
                       f"{start_ctx}..{start_ctx + steps} after a synthetic K/V fill, {el:.1f} s; cpu: {cpu_model}"}
 
 
@@ -168,6 +171,7 @@ def main():
     if args.ctx > cfgd["maxT"]:  # config 5: ctx 2048 -> 2048 rows of (synthetic) wpe, SURVEY.md 8d
         cfgd["maxT"] = args.ctx
     kv_bf16 = args.kv_dtype == "bf16"
+    w_bf16 = args.w_dtype == "bf16"
     B, lo, hi = shard.batch_layout(args.batch, world, rank, args.scaling)
     B_local = hi - lo
     counts = [shard.batch_layout(args.batch, world, r, args.scaling) for r in range(world)]
@@ -179,7 +183,8 @@ def main():
     start = ctx - window  # positions of the first decoded token
 
     model = pagedattn.Model(cfgd, seed=1337)
-    model.decode_init(B_local, P, ctx, kv_dtype=pagedattn.HPA_BF16 if kv_bf16 else pagedattn.HPA_F32)
+    model.decode_init(B_local, P, ctx, kv_dtype=pagedattn.HPA_BF16 if kv_bf16 else pagedattn.HPA_F32,
+                      w_dtype=pagedattn.HPA_BF16 if w_bf16 else pagedattn.HPA_F32)
     model.set_fused(not args.unfused)
     if not args.unfused:
         model.set_lanes(args.lanes)
@@ -291,7 +296,7 @@ def main():
                 # bounded sample: the oracle keeps an fp32 pool of B*ctx*C*L*2 floats, so
                 # beyond config 2's B*ctx the sample takes a subset of the sequences
                 cpu_B = B_local if B_local * ctx <= 65536 else max(1, 16384 // ctx)
-                cpu = cpu_baseline(cfgd, cpu_B, P, ctx, args.cpu_seconds, kv_bf16)
+                cpu = cpu_baseline(cfgd, cpu_B, P, ctx, args.cpu_seconds, kv_bf16, w_bf16)
                 if cpu_B != B_local:
                     cpu["sample"] += f" (a {cpu_B}-sequence subset of the {B_local}-sequence batch)"
             except Exception as e:  # reported, never fatal for the GPU number
@@ -319,12 +324,14 @@ def main():
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,
-            "dtype": "fp32 (bf16 KV storage)" if kv_bf16 else "fp32",
+            "dtype": ("bf16 weights and GEMM inputs, fp32 accumulate" if w_bf16 else "fp32")
+                     + (" (bf16 KV storage)" if kv_bf16 else ""),
             "data": "synthetic (seeded random GPT-2 124M weights and tokens; KV prefill: "
                     + {"synthetic": "synthetic U(-1,1)", "real": "one-pass prefill of random tokens",
                        "decode": "decode steps"}[args.prefill] + ")",
-            "config": {"workload": f"GPT-2 {args.model} fp32 paged decode, batch={B_local} per GPU x {world} "
-                                   f"(B={B}), ctx {ctx}, page_size={P}{', bf16 KV' if kv_bf16 else ''} (BASELINE.json "
+            "config": {"workload": f"GPT-2 {args.model} {'bf16' if w_bf16 else 'fp32'} paged decode, batch={B_local} per GPU x {world} "
+                                   f"(B={B}), ctx {ctx}, page_size={P}{', bf16 KV' if kv_bf16 else ''}"
+                                   f"{', bf16 weights' if w_bf16 else ''} (BASELINE.json "
                                    + ("configs[4])" if kv_bf16 else "configs[2])" if args.model == "XL" else
                                       "configs[1])" if world == 1 else "configs[3]: per-seq sharded pool)"),
                        "global_batch": B, "batch_per_gpu": B_local, "seq_len": ctx, "page_size": P,

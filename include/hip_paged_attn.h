@@ -175,6 +175,15 @@ int hpa_pool_fill_random(const HpaKVPool* pool, const int* block_table, int bt_s
 size_t hpa_frag_elems(int rows, int K);           /* padded element count */
 int hpa_pack_frag(const float* src, int rows, int K, int ld, float* dst); /* device -> device */
 int hpa_unpack_frag(const float* src, int rows, int K, float* dst, int ld);
+/* bf16 frag layout ([rows][K], rows padded to 16, K % 32 == 0): the
+ * v_mfma_f32_16x16x32_bf16 operand fragment of (16-row block, 32-deep k-step s)
+ * is 1 KiB contiguous; lane l = (m % 16) + 16*g holds k = 32s + 4g + {0..3} then
+ * k = 32s + 16 + 4g + {0..3} (the two float4 the same lane reads from the fp32
+ * frag layout at k16-steps 2s, 2s+1).  Element (m, k) at
+ * ((m/16 * K/32 + k/32) * 64 + m%16 + 16*((k%16)/4)) * 8 + k%4 + 4*((k%32)/16).
+ * Values are fp32 rounded to nearest even (hpa_pack_frag_bf16, device -> device). */
+size_t hpa_frag_bf16_elems(int rows, int K);      /* padded element count (2 bytes each) */
+int hpa_pack_frag_bf16(const float* src, int rows, int K, int ld, void* dst);
 
 /* per-row LayerNorm statistics travel between kernels as partial sums
  * (sum x, sum x^2) over 16-column tiles: stats[tile][Mp][2]; a consumer sums
@@ -240,6 +249,11 @@ typedef struct {
     float* ks_slab;       /* k_slices > 1: workspace, hpa_fused_ks_workspace floats */
     int* ks_count;        /* k_slices > 1: per-tile counters, zero before the first launch
                              (every launch leaves them zero) */
+    int w_dtype;          /* HPA_F32 (0): w is fp32 frag layout.  HPA_BF16: w points at bf16
+                             weights in the bf16 frag layout (hpa_pack_frag_bf16), K % 32 == 0;
+                             A is rounded to bf16 (RNE) after the LayerNorm, products are
+                             summed in fp32 on v_mfma_f32_16x16x32_bf16.  Looped kernel
+                             only (variant, k_slices and ln_fold_c1 must be 0); waves 4/8. */
 } HpaFusedGemm;
 /* the K slices the engine uses for a shape (1 = none; by shape, never by M) */
 int hpa_fused_pick_slices(int M, int N, int K);
@@ -262,6 +276,9 @@ int hpa_logits_partials(const HpaFusedGemm* g);
 /* the launch shape hpa_gemm_fused picks when waves / row_blocks / col_tiles
  * are 0: out3 = {waves, row_blocks, col_tiles} */
 void hpa_fused_pick(int M, int N, int K, int* out3);
+/* the launch shape of a bf16-weight GEMM (w_dtype = HPA_BF16) when waves /
+ * row_blocks / col_tiles are 0 */
+void hpa_fused_pick_bf16(int M, int N, int K, int* out3);
 int hpa_fused_pick_waves(int M, int N, int K);
 /* residual = wte[tok] + wpe[pos] in frag layout [Mp][C], stats (1 tile) */
 int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const float* wpe,

@@ -157,6 +157,12 @@ int  gpt2_decode_init(GPT2* model, int B, int page_size, int max_ctx);
 /* the same with the KV pool's storage type: HPA_F32 (0, default) or HPA_BF16
  * (1: BASELINE config 5; page size a multiple of 8; fused path only) */
 int  gpt2_decode_init_ex(GPT2* model, int B, int page_size, int max_ctx, int kv_dtype);
+/* ... and the weights' storage type: HPA_F32 (0, default) or HPA_BF16 (1:
+ * "bf16 decode" -- the layer and logits weights packed bf16 in HBM, GEMM
+ * inputs rounded to bf16 after their LayerNorm, fp32 accumulation on
+ * v_mfma_f32_16x16x32_bf16; LayerNorm, attention, residuals, GELU, softmax
+ * stay fp32; fused path only, no pipeline / overlap options) */
+int  gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dtype, int w_dtype);
 /* one decode step for every sequence: tokens[b] (host) at position pos[b];
  * tokens == NULL feeds back the previous step's greedy ids (device-resident).
  * next_tokens (host, may be NULL) receives argmax(logits[b]). */

@@ -472,6 +472,18 @@ void hpa_fused_pick(int M, int N, int K, int* out3) {
     }
 }
 
+// bf16 weights: the MFMA is 16x the fp32 rate, so these GEMMs are bound by
+// operand delivery; every activation fragment feeds 2 weight tiles and every
+// weight fragment up to 4 row blocks (first cut)
+void hpa_fused_pick_bf16(int M, int N, int K, int* out3) {
+    (void)M;
+    (void)N;
+    (void)K;
+    out3[0] = 4;
+    out3[1] = 4;
+    out3[2] = 2;
+}
+
 int hpa_fused_pick_waves(int M, int N, int K) {
     int p[3];
     hpa_fused_pick(M, N, K, p);
@@ -519,6 +531,19 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
     FG p;
     if (fused_prepare(g, &p)) return 1;
     int nw, mt, ntw;
+    if (g->w_dtype == HPA_BF16) {  // bf16 weights: hpa_gemm_bf16.hip
+        HPA_REQUIRE(g->K % 32 == 0 && !g->ln_fold_c1 && p.ks == 1 && (g->variant == 0 || g->variant == 4),
+                    "gemm_fused bf16: K % 32, no ln_fold_c1, no k_slices, variant 0");
+        int pk[3];
+        hpa_fused_pick_bf16(g->M, g->N, g->K, pk);
+        nw = g->waves ? g->waves : pk[0];
+        mt = g->row_blocks ? g->row_blocks : pk[1];
+        ntw = g->col_tiles ? g->col_tiles : pk[2];
+        while (mt > 1 && (p.Mp / 16) % mt) mt >>= 1;  // row blocks of this M
+        if (ntw == 2 && mt == 1) ntw = 1;
+        return launch_b16(p, g->epilogue, nw, mt, ntw);
+    }
+    HPA_REQUIRE(g->w_dtype == HPA_F32, "gemm_fused: w_dtype must be HPA_F32 or HPA_BF16");
     HPA_REQUIRE(g->row_blocks == 0 || g->row_blocks == 1 || g->row_blocks == 2 || g->row_blocks == 4,
                 "gemm_fused: row_blocks must be 1, 2 or 4");
     looped_shape(g, p.Mp, &nw, &mt, &ntw);
@@ -547,7 +572,8 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
 int hpa_logits_partials(const HpaFusedGemm* g) {
     FG p;
     if (!g || g->epilogue != HPA_FEPI_LOGITS || fused_prepare(g, &p)) return -1;
-    if (g->variant == 4 && logits_resident_eligible(p, g->epilogue)) return logits_resident_grid(p);
+    if (g->w_dtype == HPA_F32 && g->variant == 4 && logits_resident_eligible(p, g->epilogue))
+        return logits_resident_grid(p);
     return p.ntn;  // one partial per 16-column tile
 }
 

@@ -1,0 +1,243 @@
+// hpa_gemm_bf16.hip -- the fused decode GEMMs on bf16 weights (BASELINE
+// config 5, "GPT-2 124M bf16 decode"; SURVEY.md §8f rank 3: "bf16 weights
+// kept bf16 in HBM").
+//
+// Same launches, epilogues and XCD-aware grid as the fp32 looped kernel
+// (hpa_fused.hip / hpa_gemm_body.h gemm16_body), with two differences:
+//  * weights live in HBM as bf16 (half the bytes of the fp32 pack) in the
+//    "bf16 frag" layout below, and the A operand (LN'ed activations, still
+//    fp32 in HBM) is rounded to bf16 (round to nearest even) in registers;
+//  * the contraction is v_mfma_f32_16x16x32_bf16 (16x the fp32 MFMA rate,
+//    MI355X_MICROARCH.md), fp32 accumulation; bf16 x bf16 products are exact
+//    in fp32, so the only rounding beyond fp32 is the operands' own.
+// The numerics are "bf16 storage of weights and GEMM inputs, fp32 arithmetic"
+// (train_gpt2.cu's bf16 mode); the oracle restates them
+// (oracle_paged_set_w_bf16).
+//
+// bf16 frag layout of a [rows][K] matrix (rows padded to 16, K % 32 == 0): the
+// v_mfma_f32_16x16x32_bf16 operand fragment of (16-row block, 32-deep k-step
+// s) is 1 KiB contiguous, 16 bytes per lane.  Lane l = (row l & 15, group
+// g = l >> 4) holds k = 32s + 4g + {0..3} in elements 0..3 and
+// k = 32s + 16 + 4g + {0..3} in elements 4..7 -- exactly the two float4s the
+// same lane loads from the fp32 frag layout at k16-steps 2s and 2s+1, so the
+// A operand is built from fp32 frag activations with no data movement.  The
+// MFMA sums over the k slots of a lane group in any order as long as A and B
+// agree, which they do by construction (cdna_hip_programming.md "A/B operand
+// lane maps, bf16").
+#include <math.h>
+
+#include "hpa_gemm_body.h"
+
+namespace hpa_gemm {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ bf16x8 pack_bf16(float4 a, float4 b) {
+    u16x8 u;
+    u[0] = hpa::f32_to_bf16(a.x);
+    u[1] = hpa::f32_to_bf16(a.y);
+    u[2] = hpa::f32_to_bf16(a.z);
+    u[3] = hpa::f32_to_bf16(a.w);
+    u[4] = hpa::f32_to_bf16(b.x);
+    u[5] = hpa::f32_to_bf16(b.y);
+    u[6] = hpa::f32_to_bf16(b.z);
+    u[7] = hpa::f32_to_bf16(b.w);
+    return __builtin_bit_cast(bf16x8, u);
+}
+
+// k-steps (32 deep) per trip, two trips in flight: by the registers one step
+// holds (NTW weight fragments + 2*MT activation float4s per lane)
+template <int MT, int NTW>
+constexpr int b16_trip() {
+    return (2 * MT + NTW) <= 3 ? 4 : (2 * MT + NTW) <= 6 ? 2 : 1;
+}
+
+// MT = 16-row blocks, NTW = 16-column tiles per workgroup, NW = waves sharing
+// the K range (contiguous runs of 32-deep steps, folded in wave order in the
+// epilogue): a row's summation order depends on NW only, never on MT, NTW, M.
+template <int NW, int EPI, int MT, int NTW>
+__global__ __launch_bounds__(NW * 64) void gemm_b16_kernel(FG p) {
+    constexpr int U = b16_trip<MT, NTW>();
+    __shared__ __attribute__((aligned(16))) float smem[gemm16_lds_floats<NW, MT, NTW>()];
+    constexpr int R = MT * 16;
+    float* lngb = smem;                         // LN weight [K], bias [K]
+    float* red = smem + 2 * HPA_FUSED_LN_KMAX;  // [NW][NTW][MT x 4][64]
+    float* tile = red + NW * MT * NTW * 256;    // [NTW][R][17]
+    float* lnst = tile + NTW * R * 17;          // [R][2]
+    float* lnscr = lnst + 2 * R;                // [4R][2]
+
+    int cx, ry, slice;
+    if (!xcd_tile(p, blockIdx.x, cx, ry, slice)) return;
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int nt0 = cx * NTW;
+    const int row0 = ry * MT * 16;
+    const int q4 = lane >> 4;
+
+    const int K32 = p.K >> 5;
+    const int per = (K32 + NW - 1) / NW;
+    const int kb0 = w * per;
+    const int nsteps = max(0, min(K32, kb0 + per) - kb0);
+    const uint4* __restrict__ wf[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)  // tail tiles past ntn re-read the last tile (never stored)
+        wf[j] = reinterpret_cast<const uint4*>(p.w) + (size_t)min(nt0 + j, p.ntn - 1) * K32 * 64 + lane;
+    const float4* __restrict__ xf = reinterpret_cast<const float4*>(p.x) + (size_t)ry * MT * p.K16 * 64 + lane;
+    const size_t rbs = (size_t)p.K16 * 64;  // float4 stride between row blocks
+    const bool ln_apply = p.ln_stats != nullptr;
+    const float4* sg = reinterpret_cast<const float4*>(lngb) + q4;
+    const float4* sb = reinterpret_cast<const float4*>(lngb + HPA_FUSED_LN_KMAX) + q4;
+
+    struct Buf {
+        uint4 w[U][NTW];
+        float4 x[U][MT][2];
+    };
+    Buf A, Bb;
+    auto load = [&](Buf& f, int t) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = kb0 + min(t * U + u, max(nsteps - 1, 0));  // clamped, unconditional
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) f.w[u][j] = wf[j][(size_t)k * 64];
+#pragma unroll
+            for (int r = 0; r < MT; ++r) {
+                f.x[u][r][0] = xf[r * rbs + (size_t)(2 * k) * 64];
+                f.x[u][r][1] = xf[r * rbs + (size_t)(2 * k + 1) * 64];
+            }
+        }
+    };
+    const int trips = (nsteps + U - 1) / U;
+    if (trips > 0) load(A, 0);  // first operands in flight during the LN prologue
+
+    float mu[MT], rs[MT];
+#pragma unroll
+    for (int r = 0; r < MT; ++r) mu[r] = rs[r] = 0.f;
+    if (ln_apply) ln_prologue<NW, MT>(p, lngb, lnst, lnscr, row0, true, mu, rs);
+
+    f32x4 acc[MT * NTW];
+#pragma unroll
+    for (int i = 0; i < MT * NTW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto comp = [&](Buf& f, int t) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (t * U + u < nsteps) {
+                const int k = kb0 + t * U + u;
+                float4 g0, b0, g1, b1;
+                if (ln_apply) {
+                    g0 = sg[4 * (2 * k)];
+                    b0 = sb[4 * (2 * k)];
+                    g1 = sg[4 * (2 * k + 1)];
+                    b1 = sb[4 * (2 * k + 1)];
+                }
+                bf16x8 xa[MT];
+#pragma unroll
+                for (int r = 0; r < MT; ++r) {
+                    float4 x0 = f.x[u][r][0], x1 = f.x[u][r][1];
+                    if (ln_apply) {
+                        x0 = ln4(x0, mu[r], rs[r], g0, b0);
+                        x1 = ln4(x1, mu[r], rs[r], g1, b1);
+                    }
+                    xa[r] = pack_bf16(x0, x1);
+                }
+#pragma unroll
+                for (int j = 0; j < NTW; ++j) {
+                    const bf16x8 wb = __builtin_bit_cast(bf16x8, f.w[u][j]);
+#pragma unroll
+                    for (int r = 0; r < MT; ++r)
+                        acc[j * MT + r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[r], wb, acc[j * MT + r], 0, 0, 0);
+                }
+            }
+        }
+    };
+    for (int t = 0; t < trips; t += 2) {
+        if (t + 1 < trips) load(Bb, t + 1);
+        comp(A, t);
+        if (t + 1 >= trips) break;
+        if (t + 2 < trips) load(A, t + 2);
+        comp(Bb, t + 1);
+    }
+
+    Epi<NW, EPI, MT, NTW> epi;
+    epi.prefetch(p, nt0, row0);
+    epi.finish(p, acc, red, tile, nt0, row0, lngb, cx * p.gy + ry, slice);
+}
+
+template <int NW, int MT, int NTW>
+static int launch_b16_t(FG p, int epi) {
+    const int gx = (p.ntn + NTW - 1) / NTW, gy = p.Mp / 16 / MT;
+    p.gx = gx;
+    p.gy = gy;
+    dim3 grid((unsigned)(((gx + 7) / 8) * 8 * gy)), block(NW * 64);
+    switch (epi) {
+        case HPA_FEPI_QKV: gemm_b16_kernel<NW, HPA_FEPI_QKV, MT, NTW><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_RESID: gemm_b16_kernel<NW, HPA_FEPI_RESID, MT, NTW><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_GELU: gemm_b16_kernel<NW, HPA_FEPI_GELU, MT, NTW><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_LOGITS: gemm_b16_kernel<NW, HPA_FEPI_LOGITS, MT, NTW><<<grid, block, 0, hpa_stream()>>>(p); break;
+        default: return hpa_fail(__FILE__, __LINE__, "gemm_fused bf16: unknown epilogue");
+    }
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int NW>
+static int launch_b16_nw(const FG& p, int epi, int mt, int ntw) {
+    switch (mt * 10 + ntw) {
+        case 11: return launch_b16_t<NW, 1, 1>(p, epi);
+        case 21: return launch_b16_t<NW, 2, 1>(p, epi);
+        case 41: return launch_b16_t<NW, 4, 1>(p, epi);
+        case 22: return launch_b16_t<NW, 2, 2>(p, epi);
+        case 42: return launch_b16_t<NW, 4, 2>(p, epi);
+        default:
+            return hpa_fail(__FILE__, __LINE__,
+                            "gemm_fused bf16: (row_blocks, col_tiles) in {(1,1), (2,1), (4,1), (2,2), (4,2)}");
+    }
+}
+
+int launch_b16(const FG& p, int epi, int nw, int mt, int ntw) {
+    switch (nw) {
+        case 4: return launch_b16_nw<4>(p, epi, mt, ntw);
+        case 8: return launch_b16_nw<8>(p, epi, mt, ntw);
+        default: return hpa_fail(__FILE__, __LINE__, "gemm_fused bf16: waves must be 4 or 8");
+    }
+}
+
+}  // namespace hpa_gemm
+
+namespace {
+// one thread per (fragment, lane): 8 bf16 (RNE) from two float4 of row m
+__global__ void pack_frag_bf16_kernel(const float* __restrict__ src, int rows, int K, int ld,
+                                      uint4* __restrict__ dst, size_t n8) {
+    const size_t o = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (o >= n8) return;
+    const int lane = (int)(o & 63);
+    const size_t blk = o >> 6;  // rb * K32 + s
+    const int K32 = K >> 5;
+    const int s = (int)(blk % K32);
+    const int rb = (int)(blk / K32);
+    const int m = rb * 16 + (lane & 15);
+    const int k0 = s * 32 + 4 * (lane >> 4);
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    if (m < rows) {
+        a = *reinterpret_cast<const float4*>(src + (size_t)m * ld + k0);
+        b = *reinterpret_cast<const float4*>(src + (size_t)m * ld + k0 + 16);
+    }
+    dst[o] = __builtin_bit_cast(uint4, hpa_gemm::pack_bf16(a, b));
+}
+}  // namespace
+
+extern "C" {
+
+size_t hpa_frag_bf16_elems(int rows, int K) { return (size_t)((rows + 15) / 16) * 16 * (size_t)K; }
+
+int hpa_pack_frag_bf16(const float* src, int rows, int K, int ld, void* dst) {
+    HPA_REQUIRE(src && dst && rows > 0 && K > 0 && K % 32 == 0 && ld >= K && ld % 4 == 0,
+                "pack_frag_bf16: bad shape (K % 32, ld % 4)");
+    const size_t n8 = hpa_frag_bf16_elems(rows, K) / 8;
+    pack_frag_bf16_kernel<<<(unsigned)((n8 + 255) / 256), 256, 0, hpa_stream()>>>(src, rows, K, ld,
+                                                                                 reinterpret_cast<uint4*>(dst), n8);
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+}  // extern "C"

@@ -359,6 +359,62 @@ struct Epi {
     }
 };
 
+// ---- LayerNorm prologue: the LN weight / bias of K into LDS (lngb) and the
+// mean / rstd of the workgroup's R = 16*MT rows from the producer's 16-column
+// partial sums (4 threads per row, partials summed in tile order); lane l gets
+// the statistics of row (l & 15) of each row block.  Every thread calls it.
+template <int NW, int MT>
+__device__ __forceinline__ void ln_prologue(const FG& p, float* lngb, float* lnst, float* lnscr, int row0,
+                                            bool ln_apply, float* mu, float* rs) {
+    constexpr int NT = NW * 64;
+    constexpr int R = MT * 16;
+    const int lane = threadIdx.x & 63;
+    for (int i = threadIdx.x; ln_apply && i < p.K / 4; i += NT) {
+        reinterpret_cast<float4*>(lngb)[i] = reinterpret_cast<const float4*>(p.ln_w)[i];
+        reinterpret_cast<float4*>(lngb + HPA_FUSED_LN_KMAX)[i] = reinterpret_cast<const float4*>(p.ln_b)[i];
+    }
+    if (threadIdx.x < 4 * R) {
+        const int r = threadIdx.x >> 2, q = threadIdx.x & 3;
+        const int row = row0 + r;
+        float s1 = 0.f, s2 = 0.f;
+        if (row < p.M) {
+            for (int t0 = q; t0 < p.ln_ntiles; t0 += 32) {
+                float a[8], b[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int t = min(t0 + 4 * j, p.ln_ntiles - 1);
+                    a[j] = p.ln_stats[((size_t)t * p.Mp + row) * 2];
+                    b[j] = p.ln_stats[((size_t)t * p.Mp + row) * 2 + 1];
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (t0 + 4 * j < p.ln_ntiles) {
+                        s1 += a[j];
+                        s2 += b[j];
+                    }
+            }
+        }
+        lnscr[2 * threadIdx.x] = s1;
+        lnscr[2 * threadIdx.x + 1] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x < R) {
+        const float* t = lnscr + 8 * threadIdx.x;
+        const float s1 = (t[0] + t[2]) + (t[4] + t[6]);
+        const float s2 = (t[1] + t[3]) + (t[5] + t[7]);
+        const float m = s1 / p.K;
+        const float v = fmaxf(s2 / p.K - m * m, 0.f);
+        lnst[2 * threadIdx.x] = m;
+        lnst[2 * threadIdx.x + 1] = 1.0f / sqrtf(v + 1e-5f);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < MT; ++r) {
+        mu[r] = lnst[2 * (16 * r + (lane & 15))];
+        rs[r] = lnst[2 * (16 * r + (lane & 15)) + 1];
+    }
+}
+
 // MT = 16-row blocks per workgroup (1, 2 or 4), NTW = 16-column tiles per
 // workgroup (every wave computes all of them over its K range), NW = waves
 // sharing the K range.  Grid (ceil(ntn/NTW), Mp/16/MT).  MT = 1 spreads the
@@ -377,7 +433,6 @@ constexpr int gemm16_lds_floats() {
 // (gemm16_kernel, and the GEMM role of the pipelined combo launches)
 template <int NW, int EPI, int MT, int NTW, int UD = 0, bool WT = false>
 __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
-    constexpr int NT = NW * 64;
     constexpr int R = MT * 16;  // rows per workgroup
     // k-steps per trip (two trips in flight; register budget); UD > 0: the
     // "deep" variant's larger trips (more bytes in flight per wave for the
@@ -436,52 +491,7 @@ __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
     float mu[MT], rs[MT];
 #pragma unroll
     for (int r = 0; r < MT; ++r) mu[r] = rs[r] = 0.f;
-    if (use_ln) {
-        for (int i = threadIdx.x; ln_apply && i < p.K / 4; i += NT) {
-            reinterpret_cast<float4*>(lngb)[i] = reinterpret_cast<const float4*>(p.ln_w)[i];
-            reinterpret_cast<float4*>(lngb + HPA_FUSED_LN_KMAX)[i] = reinterpret_cast<const float4*>(p.ln_b)[i];
-        }
-        if (threadIdx.x < 4 * R) {
-            const int r = threadIdx.x >> 2, q = threadIdx.x & 3;
-            const int row = row0 + r;
-            float s1 = 0.f, s2 = 0.f;
-            if (row < p.M) {
-                for (int t0 = q; t0 < p.ln_ntiles; t0 += 32) {
-                    float a[8], b[8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const int t = min(t0 + 4 * j, p.ln_ntiles - 1);
-                        a[j] = p.ln_stats[((size_t)t * p.Mp + row) * 2];
-                        b[j] = p.ln_stats[((size_t)t * p.Mp + row) * 2 + 1];
-                    }
-#pragma unroll
-                    for (int j = 0; j < 8; ++j)
-                        if (t0 + 4 * j < p.ln_ntiles) {
-                            s1 += a[j];
-                            s2 += b[j];
-                        }
-                }
-            }
-            lnscr[2 * threadIdx.x] = s1;
-            lnscr[2 * threadIdx.x + 1] = s2;
-        }
-        __syncthreads();
-        if (threadIdx.x < R) {
-            const float* t = lnscr + 8 * threadIdx.x;
-            const float s1 = (t[0] + t[2]) + (t[4] + t[6]);
-            const float s2 = (t[1] + t[3]) + (t[5] + t[7]);
-            const float m = s1 / p.K;
-            const float v = fmaxf(s2 / p.K - m * m, 0.f);
-            lnst[2 * threadIdx.x] = m;
-            lnst[2 * threadIdx.x + 1] = 1.0f / sqrtf(v + 1e-5f);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < MT; ++r) {
-            mu[r] = lnst[2 * (16 * r + (lane & 15))];
-            rs[r] = lnst[2 * (16 * r + (lane & 15)) + 1];
-        }
-    }
+    if (use_ln) ln_prologue<NW, MT>(p, lngb, lnst, lnscr, row0, ln_apply, mu, rs);
 
     // one accumulator chain per (column tile, row block): a row's summation
     // order depends only on NW (the per-wave K ranges), never on MT, NTW or M
@@ -718,6 +728,10 @@ __global__ __launch_bounds__(NW * 64) void gemm16_os_kernel(FG p) {
 bool logits_resident_eligible(const FG& p, int epi);
 int launch_logits_resident(const FG& p);
 int logits_resident_grid(const FG& p);  // workgroups = argmax partials per row it writes
+
+// bf16-weight GEMM launch (hpa_gemm_bf16.hip): waves 4/8, (row_blocks,
+// col_tiles) in {(1,1), (2,1), (4,1), (2,2), (4,2)}
+int launch_b16(const FG& p, int epi, int nw, int mt, int ntw);
 
 static inline int fused_prepare(const HpaFusedGemm* g, FG* p) {
     HPA_REQUIRE(g && g->x && g->w && g->out, "gemm_fused: null operand");

@@ -614,6 +614,7 @@ struct GPT2Decode {
     /* fused path (hpa_gemm_fused): frag-layout weights and activations */
     int fused;
     float* d_wpack;   /* packed qkvw, attprojw, fcw, fcprojw of every layer, then wte */
+    int w_bf16;       /* weights packed bf16 (hpa_pack_frag_bf16; offsets in elements) */
     size_t wpack_off[5]; /* per-layer strides (0..3) and wte offset (4) */
     float* d_fold;    /* LN folded into qkvw / fcw (hpa_ln_fold_pack): per layer c1, c2 of
                          qkv [3C] [3C] then fc [4C] [4C]; NULL: LN applied on the operand path */
@@ -847,8 +848,33 @@ static int dec_init_fused(GPT2* model, GPT2Decode* d) {
     d->wpack_off[3] = e_qkv + e_ap + e_fc;
     d->wpack_off[4] = e_layer * L; /* wte */
     size_t total = d->wpack_off[4] + hpa_frag_elems(V, C);
-    d->d_wpack = (float*)hpa_malloc(total * 4);
+    d->d_wpack = (float*)hpa_malloc(total * (d->w_bf16 ? 2 : 4));
     if (!d->d_wpack) return 1;
+    if (d->w_bf16) { /* bf16 weights: same element offsets, 2 bytes each; LN on the operand path */
+        unsigned short* b16 = (unsigned short*)d->d_wpack;
+        for (int l = 0; l < L; l++) {
+            unsigned short* base = b16 + e_layer * l;
+            const size_t lc = (size_t)l * C;
+            if (hpa_pack_frag_bf16(w->qkvw + lc * 3 * C, 3 * C, C, C, base + d->wpack_off[0]) ||
+                hpa_pack_frag_bf16(w->attprojw + lc * C, C, C, C, base + d->wpack_off[1]) ||
+                hpa_pack_frag_bf16(w->fcw + lc * 4 * C, 4 * C, C, C, base + d->wpack_off[2]) ||
+                hpa_pack_frag_bf16(w->fcprojw + lc * 4 * C, C, 4 * C, 4 * C, base + d->wpack_off[3]))
+                return 1;
+        }
+        if (hpa_pack_frag_bf16(w->wte, V, C, C, b16 + d->wpack_off[4])) return 1;
+        d->d_fold = NULL;
+        for (int i = 0; i < 5; i++) {
+            int pk[3];
+            hpa_fused_pick_bf16(B, i == 4 ? V : 0, C, pk);
+            d->fwaves[i] = pk[0];
+            d->frb[i] = pk[1];
+            d->fct[i] = pk[2];
+            d->fks[i] = 1;
+        }
+        d->ev_fork = hpa_event_create_nt();
+        if (!d->ev_fork) return 1;
+        return dec_lanes_alloc(d, 1, C, V, c.num_heads);
+    }
     /* LN1 / LN2 folded into the qkv / fc weights (default; HPA_LN_FOLD=0 keeps
      * the LN on the operand path): the GEMM then starts on x as it stands and
      * the row statistics are needed only in its epilogue */
@@ -898,9 +924,17 @@ int gpt2_decode_init(GPT2* model, int B, int page_size, int max_ctx) {
 }
 
 int gpt2_decode_init_ex(GPT2* model, int B, int page_size, int max_ctx, int kv_dtype) {
+    return gpt2_decode_init_w(model, B, page_size, max_ctx, kv_dtype, HPA_F32);
+}
+
+int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dtype, int w_dtype) {
     ensure_device();
     if (kv_dtype != HPA_F32 && kv_dtype != HPA_BF16) {
         fprintf(stderr, "[paged_infer] kv dtype must be HPA_F32 or HPA_BF16\n");
+        return 1;
+    }
+    if (w_dtype != HPA_F32 && w_dtype != HPA_BF16) {
+        fprintf(stderr, "[paged_infer] weight dtype must be HPA_F32 or HPA_BF16\n");
         return 1;
     }
     if (!model->params_memory) { fprintf(stderr, "[paged_infer] model not built\n"); return 1; }
@@ -1002,6 +1036,7 @@ int gpt2_decode_init_ex(GPT2* model, int B, int page_size, int max_ctx, int kv_d
         dec_free(d);
         return 1;
     }
+    d->w_bf16 = w_dtype == HPA_BF16;
     if (dec_init_fused(model, d)) {
         dec_free(d);
         return 1;
@@ -1133,6 +1168,12 @@ static int dec_launch_unfused(GPT2* model) {
 /* the fused GEMMs of one layer of one lane (gemm index = the fwaves/frb/fct
  * slot): descriptor with that lane's rows, buffers and launch shape */
 enum { G_QKV = 0, G_ATTPROJ = 1, G_FC = 2, G_FCPROJ = 3, G_LOGITS = 4 };
+
+/* packed weights at element offset off (fp32 or bf16 pack) */
+static const float* wpack_at(const GPT2Decode* d, size_t off) {
+    return d->w_bf16 ? (const float*)((const unsigned short*)d->d_wpack + off) : d->d_wpack + off;
+}
+
 static void lane_gemm(GPT2* model, int li, int l, int which, HpaFusedGemm* g) {
     GPT2Decode* d = model->decode;
     const DecLane* ln = &d->lanes[li];
@@ -1141,9 +1182,9 @@ static void lane_gemm(GPT2* model, int li, int l, int which, HpaFusedGemm* g) {
     const ParameterTensors* w = &model->params;
     const size_t lc = (size_t)l * C;
     const size_t e_layer = d->wpack_off[3] + hpa_frag_elems(C, 4 * C);
-    const float* wl = d->d_wpack + e_layer * l;
     memset(g, 0, sizeof(*g));
     g->M = ln->B;
+    g->w_dtype = d->w_bf16 ? HPA_BF16 : HPA_F32;
     g->epilogue = which == G_QKV ? HPA_FEPI_QKV : which == G_FC ? HPA_FEPI_GELU
                 : which == G_LOGITS ? HPA_FEPI_LOGITS : HPA_FEPI_RESID;
     g->waves = d->fwaves[which];
@@ -1162,28 +1203,28 @@ static void lane_gemm(GPT2* model, int li, int l, int which, HpaFusedGemm* g) {
     switch (which) {
         case G_QKV: /* LN1 (stats: embedding's 1 tile at layer 0, fcproj's C/16 after) */
             g->x = ln->res; g->K = C; g->ln_stats = ln->st1; g->ln_ntiles = l == 0 ? 1 : ct;
-            g->ln_w = w->ln1w + lc; g->ln_b = w->ln1b + lc; g->w = wl + d->wpack_off[0]; g->N = 3 * C;
+            g->ln_w = w->ln1w + lc; g->ln_b = w->ln1b + lc; g->w = wpack_at(d, e_layer * l + d->wpack_off[0]); g->N = 3 * C;
             g->bias = w->qkvb + 3 * lc; g->out = d->d_q + (size_t)ln->r0 * C;
             if (d->d_fold) { g->ln_fold_c1 = d->d_fold + 14 * lc; g->bias = g->ln_fold_c1 + 3 * C; }
             break;
         case G_ATTPROJ: /* res2 = res + att . Wap^T + b, LN2 statistics */
-            g->x = ln->att; g->K = C; g->w = wl + d->wpack_off[1]; g->N = C; g->bias = w->attprojb + lc;
+            g->x = ln->att; g->K = C; g->w = wpack_at(d, e_layer * l + d->wpack_off[1]); g->N = C; g->bias = w->attprojb + lc;
             g->out = ln->res2; g->res_in = ln->res; g->stats_out = d->d_fold ? NULL : ln->st2; /* fc sums its own */
             break;
         case G_FC: /* gelu(LN2(res2) . Wfc^T + b) */
             g->x = ln->res2; g->K = C; g->ln_stats = ln->st2; g->ln_ntiles = ct; g->ln_w = w->ln2w + lc;
-            g->ln_b = w->ln2b + lc; g->w = wl + d->wpack_off[2]; g->N = 4 * C; g->bias = w->fcb + 4 * lc;
+            g->ln_b = w->ln2b + lc; g->w = wpack_at(d, e_layer * l + d->wpack_off[2]); g->N = 4 * C; g->bias = w->fcb + 4 * lc;
             g->out = ln->fch;
             if (d->d_fold) { g->ln_fold_c1 = d->d_fold + 14 * lc + 6 * C; g->bias = g->ln_fold_c1 + 4 * C; }
             break;
         case G_FCPROJ: /* res = res2 + fch . Wfp^T + b, next-LN statistics */
-            g->x = ln->fch; g->K = 4 * C; g->w = wl + d->wpack_off[3]; g->N = C; g->bias = w->fcprojb + lc;
+            g->x = ln->fch; g->K = 4 * C; g->w = wpack_at(d, e_layer * l + d->wpack_off[3]); g->N = C; g->bias = w->fcprojb + lc;
             g->out = ln->res; g->res_in = ln->res2;
             g->stats_out = d->d_fold && l + 1 < c.num_layers ? NULL : ln->st1; /* LNf of logits: last layer */
             break;
         default: /* logits = LNf(res) . wte^T, argmax partials */
             g->x = ln->res; g->K = C; g->ln_stats = ln->st1; g->ln_ntiles = c.num_layers == 0 ? 1 : ct;
-            g->ln_w = w->lnfw; g->ln_b = w->lnfb; g->w = d->d_wpack + d->wpack_off[4]; g->N = V;
+            g->ln_w = w->lnfw; g->ln_b = w->lnfb; g->w = wpack_at(d, d->wpack_off[4]); g->N = V;
             g->out = d->d_logits + (size_t)ln->r0 * V; g->part_out = ln->part; g->layer = 0;
             g->variant = 4; /* activation-resident kernel where the shape allows (hpa_logits.hip) */
             break;
@@ -1464,8 +1505,8 @@ int gpt2_decode_set_fused(GPT2* model, int enable) {
         hpa_graph_destroy(d->graph);
         d->graph = NULL;
     }
-    if (!enable && d->pool.dtype != HPA_F32) {
-        fprintf(stderr, "[paged_infer] the unfused path needs an fp32 KV pool\n");
+    if (!enable && (d->pool.dtype != HPA_F32 || d->w_bf16)) {
+        fprintf(stderr, "[paged_infer] the unfused path needs an fp32 KV pool and fp32 weights\n");
         return 1;
     }
     d->fused = enable ? 1 : 0;
@@ -1529,8 +1570,8 @@ int gpt2_decode_set_pipeline(GPT2* model, int enable) {
         if (!d->pipeline) return 0;
         return gpt2_decode_set_lanes(model, 1);
     }
-    if (d->B <= 16 || (d->P != 8 && d->P != 16 && d->P != 32) || d->pool.dtype != HPA_F32) {
-        fprintf(stderr, "[paged_infer] pipeline needs B > 16, page size 8/16/32 and an fp32 KV pool\n");
+    if (d->B <= 16 || (d->P != 8 && d->P != 16 && d->P != 32) || d->pool.dtype != HPA_F32 || d->w_bf16) {
+        fprintf(stderr, "[paged_infer] pipeline needs B > 16, page size 8/16/32, an fp32 KV pool and fp32 weights\n");
         return 1;
     }
     if (gpt2_decode_set_lanes(model, 2) || d->nlanes != 2) return 1;
@@ -1583,9 +1624,9 @@ int gpt2_decode_set_overlap(GPT2* model, int chain_blocks) {
         return gpt2_decode_set_lanes(model, 1);
     }
     if (!d->fused || d->B <= 16 || d->B > 128 || (d->P != 8 && d->P != 16 && d->P != 32) ||
-        d->pool.dtype != HPA_F32) {
-        fprintf(stderr, "[paged_infer] overlapped step needs the fused path, 16 < B <= 128, page size 8/16/32 "
-                        "and an fp32 KV pool\n");
+        d->pool.dtype != HPA_F32 || d->w_bf16) {
+        fprintf(stderr, "[paged_infer] overlapped step needs the fused path, 16 < B <= 128, page size 8/16/32, "
+                        "an fp32 KV pool and fp32 weights\n");
         return 1;
     }
     if (gpt2_decode_set_lanes(model, 2) || d->nlanes != 2) return 1;
@@ -1705,10 +1746,10 @@ static int prefill_gemm(GPT2* model, int l, int which, int R) {
     const ParameterTensors* w = &model->params;
     const size_t lc = (size_t)l * C;
     const size_t e_layer = d->wpack_off[3] + hpa_frag_elems(C, 4 * C);
-    const float* wl = d->d_wpack + e_layer * l;
     HpaFusedGemm g;
     memset(&g, 0, sizeof(g));
     g.M = R;
+    g.w_dtype = d->w_bf16 ? HPA_BF16 : HPA_F32;
     /* B*T rows: reuse every activation fragment over 2 weight tiles and every
      * weight fragment over 4 row blocks (MFMA-bound at this M) */
     g.waves = 8;
@@ -1724,22 +1765,22 @@ static int prefill_gemm(GPT2* model, int l, int which, int R) {
         case G_QKV:
             g.epilogue = HPA_FEPI_QKV; g.x = d->pf_res; g.K = C; g.ln_stats = d->pf_st1;
             g.ln_ntiles = l == 0 ? 1 : ct; g.ln_w = w->ln1w + lc; g.ln_b = w->ln1b + lc;
-            g.w = wl + d->wpack_off[0]; g.N = 3 * C; g.bias = w->qkvb + 3 * lc; g.out = d->pf_q;
+            g.w = wpack_at(d, e_layer * l + d->wpack_off[0]); g.N = 3 * C; g.bias = w->qkvb + 3 * lc; g.out = d->pf_q;
             if (d->d_fold) { g.ln_fold_c1 = d->d_fold + 14 * lc; g.bias = g.ln_fold_c1 + 3 * C; }
             break;
         case G_ATTPROJ:
-            g.epilogue = HPA_FEPI_RESID; g.x = d->pf_att; g.K = C; g.w = wl + d->wpack_off[1]; g.N = C;
+            g.epilogue = HPA_FEPI_RESID; g.x = d->pf_att; g.K = C; g.w = wpack_at(d, e_layer * l + d->wpack_off[1]); g.N = C;
             g.bias = w->attprojb + lc; g.out = d->pf_res2; g.res_in = d->pf_res;
             g.stats_out = d->d_fold ? NULL : d->pf_st2;
             break;
         case G_FC:
             g.epilogue = HPA_FEPI_GELU; g.x = d->pf_res2; g.K = C; g.ln_stats = d->pf_st2; g.ln_ntiles = ct;
-            g.ln_w = w->ln2w + lc; g.ln_b = w->ln2b + lc; g.w = wl + d->wpack_off[2]; g.N = 4 * C;
+            g.ln_w = w->ln2w + lc; g.ln_b = w->ln2b + lc; g.w = wpack_at(d, e_layer * l + d->wpack_off[2]); g.N = 4 * C;
             g.bias = w->fcb + 4 * lc; g.out = d->pf_fch;
             if (d->d_fold) { g.ln_fold_c1 = d->d_fold + 14 * lc + 6 * C; g.bias = g.ln_fold_c1 + 4 * C; }
             break;
         default: /* G_FCPROJ */
-            g.epilogue = HPA_FEPI_RESID; g.x = d->pf_fch; g.K = 4 * C; g.w = wl + d->wpack_off[3]; g.N = C;
+            g.epilogue = HPA_FEPI_RESID; g.x = d->pf_fch; g.K = 4 * C; g.w = wpack_at(d, e_layer * l + d->wpack_off[3]); g.N = C;
             g.bias = w->fcprojb + lc; g.out = d->pf_res; g.res_in = d->pf_res2;
             g.stats_out = d->d_fold && l + 1 < c.num_layers ? NULL : d->pf_st1;
             break;
@@ -2010,7 +2051,8 @@ double gpt2_decode_step_bytes(GPT2* model, double* attn_bytes) {
     const GPT2Config c = model->config;
     const double C = c.channels, L = c.num_layers, V = c.vocab_size, w = 4.0;
     const double wkv = (double)d->pool.elem_bytes; /* fp32 or bf16 KV storage */
-    double weights = (L * (12 * C * C + 13 * C) + V * C + 2 * C) * w;
+    const double wm = d->w_bf16 ? 2.0 : 4.0; /* GEMM weight matrices: bf16 or fp32 */
+    double weights = (L * 12 * C * C + V * C) * wm + (L * 13 * C + 2 * C) * w;
     double kv = 0.0;
     for (int b = 0; b < d->B; b++) kv += 2.0 * L * (d->h_pos[b] + 1) * C * wkv;
     double append = 2.0 * L * d->B * C * wkv;

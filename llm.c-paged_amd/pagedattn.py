@@ -66,7 +66,7 @@ class HpaFusedGemm(ctypes.Structure):
                 ("bt_stride", ctypes.c_int), ("pos", _V), ("waves", ctypes.c_int),
                 ("row_blocks", ctypes.c_int), ("variant", ctypes.c_int), ("col_tiles", ctypes.c_int),
                 ("row_seq", _V), ("ln_fold_c1", _V), ("k_slices", ctypes.c_int), ("ks_slab", _V),
-                ("ks_count", _V)]
+                ("ks_count", _V), ("w_dtype", ctypes.c_int)]
 
 
 HPA_FEPI_QKV, HPA_FEPI_RESID, HPA_FEPI_GELU, HPA_FEPI_LOGITS = 0, 1, 2, 3
@@ -211,6 +211,9 @@ def lib():
     _sig(L, "gpt2_forward", None, [v, _I, _I, sz, sz, sz, i])
     _sig(L, "gpt2_decode_init", i, [v, i, i, i])
     _sig(L, "gpt2_decode_init_ex", i, [v, i, i, i, i])
+    _sig(L, "gpt2_decode_init_w", i, [v, i, i, i, i, i])
+    _sig(L, "hpa_pack_frag_bf16", i, [v, i, i, i, v])
+    _sig(L, "hpa_frag_bf16_elems", ctypes.c_size_t, [i, i])
     _sig(L, "gpt2_decode_prefill", i, [v, _I, i, _I])
     _sig(L, "gpt2_decode_prefill_ragged", i, [v, _I, _I, _I])
     _sig(L, "gpt2_decode_release", i, [v, i])
@@ -235,6 +238,7 @@ def lib():
     _sig(L, "hpa_logits_partials", i, [ctypes.POINTER(HpaFusedGemm)])
     _sig(L, "hpa_fused_pick_waves", i, [i, i, i])
     _sig(L, "hpa_fused_pick", None, [i, i, i, _I])
+    _sig(L, "hpa_fused_pick_bf16", None, [i, i, i, _I])
     _sig(L, "hpa_embed_frag", i, [v, v, v, v, v, v, i, i])
     _sig(L, "hpa_argmax_final", i, [v, i, i, i, v, v, v, v])
     _sig(L, "hpa_paged_attention_decode_frag", i, [v, P, i, v, i, v, v, i])
@@ -520,9 +524,10 @@ class Model:
         self._bm = bm
         lib().gpt2_set_manager(self.h, bm.h)
 
-    def decode_init(self, B, page_size=16, max_ctx=None, kv_dtype=HPA_F32):
+    def decode_init(self, B, page_size=16, max_ctx=None, kv_dtype=HPA_F32, w_dtype=HPA_F32):
         max_ctx = max_ctx or self.cfg.max_seq_len
-        check(lib().gpt2_decode_init_ex(self.h, B, page_size, max_ctx, int(kv_dtype)), "gpt2_decode_init")
+        check(lib().gpt2_decode_init_w(self.h, B, page_size, max_ctx, int(kv_dtype), int(w_dtype)),
+              "gpt2_decode_init")
         self.B = B
 
     def set_fused(self, on):

@@ -63,6 +63,7 @@ def lib(fast=False):
     L.oracle_paged_pos.restype = ctypes.c_int
     L.oracle_paged_free.argtypes = [ctypes.c_void_p]
     L.oracle_paged_set_kv_bf16.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.oracle_paged_set_w_bf16.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.oracle_round_bf16.argtypes = [ctypes.c_float]
     L.oracle_round_bf16.restype = ctypes.c_float
     L.oracle_softmax_forward.argtypes = [_F, _F, ctypes.c_int, ctypes.c_int, ctypes.c_int]
@@ -134,7 +135,8 @@ def gpt2_forward(params, c, tokens, fast=False):
 class PagedDecoder:
     """oracle_paged_* : incremental paged decode, absolute positions, all layers."""
 
-    def __init__(self, params, c, B, page_size, max_ctx, page_seed=7, fast=False, kv_bf16=False):
+    def __init__(self, params, c, B, page_size, max_ctx, page_seed=7, fast=False, kv_bf16=False,
+                 w_bf16=False):
         self.L = lib(fast)
         self.params = params  # keep alive
         self.c = c
@@ -144,6 +146,8 @@ class PagedDecoder:
             raise MemoryError("oracle_paged_create failed")
         if kv_bf16:
             self.L.oracle_paged_set_kv_bf16(self.h, 1)
+        if w_bf16 and self.L.oracle_paged_set_w_bf16(self.h, 1) != 0:
+            raise MemoryError("oracle_paged_set_w_bf16")
 
     def step(self, tokens, want_logits=True):
         tokens = np.ascontiguousarray(tokens, np.int32)

@@ -359,6 +359,8 @@ struct OraclePaged {
     int* free_perm;   /* page ids in hand-out order */
     int next_free;
     int kv_bf16;      /* round appended K/V to bf16 (round to nearest even) */
+    float* pw_bf16;   /* bf16 weights mode: params with qkvw/attprojw/fcw/fcprojw rounded */
+    float* wte_bf16;  /* ... and the logits' wte rounded (the embedding keeps fp32 wte) */
     float *x, *ln, *qkv, *atty, *tmp, *res2, *fch, *fchg, *logits;
 };
 
@@ -399,7 +401,7 @@ void oracle_paged_free(OraclePaged* o) {
     if (!o) return;
     free(o->kpool); free(o->vpool); free(o->block_table); free(o->pos); free(o->free_perm);
     free(o->x); free(o->ln); free(o->qkv); free(o->atty); free(o->tmp); free(o->res2);
-    free(o->fch); free(o->fchg); free(o->logits); free(o);
+    free(o->fch); free(o->fchg); free(o->logits); free(o->pw_bf16); free(o->wte_bf16); free(o);
 }
 
 int oracle_paged_pos(const OraclePaged* o, int b) { return o->pos[b]; }
@@ -415,6 +417,38 @@ float oracle_round_bf16(float f) {
     u &= 0xffff0000u;
     memcpy(&f, &u, 4);
     return f;
+}
+
+/* "bf16 decode" (gpt2_decode_init_w with HPA_BF16 weights): every GEMM's
+ * weights and its input rows (after LayerNorm / attention / GELU) are
+ * rounded to bf16 (nearest even), the products summed in fp32; everything
+ * else stays fp32.  Restates hpa_gemm_bf16.hip's numerics for parity tests. */
+int oracle_paged_set_w_bf16(OraclePaged* o, int on) {
+    free(o->pw_bf16); free(o->wte_bf16);
+    o->pw_bf16 = o->wte_bf16 = NULL;
+    if (!on) return 0;
+    size_t n = oracle_num_params(o->cfg);
+    size_t nwte = (size_t)o->cfg.vocab_size * o->cfg.channels;
+    o->pw_bf16 = malloc(n * 4);
+    o->wte_bf16 = malloc(nwte * 4);
+    if (!o->pw_bf16 || !o->wte_bf16) return -1;
+    memcpy(o->pw_bf16, o->params, n * 4);
+    const int mats[4] = {4, 6, 10, 12}; /* qkvw, attprojw, fcw, fcprojw (paged_infer.c:308-326) */
+    size_t sz[16];
+    for (int i = 0; i < 15; i++) sz[i] = o->off[i + 1] - o->off[i];
+    sz[15] = n - o->off[15];
+    for (int m = 0; m < 4; m++)
+        for (size_t i = 0; i < sz[mats[m]]; i++) {
+            float* x = o->pw_bf16 + o->off[mats[m]] + i;
+            *x = oracle_round_bf16(*x);
+        }
+    for (size_t i = 0; i < nwte; i++) o->wte_bf16[i] = oracle_round_bf16(o->params[o->off[0] + i]);
+    return 0;
+}
+
+static void round_bf16_n(OraclePaged* o, float* x, size_t n) {
+    if (!o->pw_bf16) return;
+    for (size_t i = 0; i < n; i++) x[i] = oracle_round_bf16(x[i]);
 }
 
 static float* page_ptr(OraclePaged* o, float* pool, int layer, int page) {
@@ -457,6 +491,7 @@ int oracle_paged_step(OraclePaged* o, const int* tokens, float* logits, int* nex
     int B = o->B, C = cfg.channels, NH = cfg.num_heads, L = cfg.num_layers, V = cfg.vocab_size;
     int hs = C / NH;
     const float* P = o->params;
+    const float* PW = o->pw_bf16 ? o->pw_bf16 : o->params; /* GEMM weights */
     for (int b = 0; b < B; b++) {
         if (o->pos[b] >= cfg.max_seq_len) return -1;
         if (ensure_page(o, b, o->pos[b]) != 0) return -1;
@@ -466,17 +501,18 @@ int oracle_paged_step(OraclePaged* o, const int* tokens, float* logits, int* nex
     for (int l = 0; l < L; l++) {
         const float* ln1w = P + o->off[2] + (size_t)l * C;
         const float* ln1b = P + o->off[3] + (size_t)l * C;
-        const float* qkvw = P + o->off[4] + (size_t)l * 3 * C * C;
+        const float* qkvw = PW + o->off[4] + (size_t)l * 3 * C * C;
         const float* qkvb = P + o->off[5] + (size_t)l * 3 * C;
-        const float* apw = P + o->off[6] + (size_t)l * C * C;
+        const float* apw = PW + o->off[6] + (size_t)l * C * C;
         const float* apb = P + o->off[7] + (size_t)l * C;
         const float* ln2w = P + o->off[8] + (size_t)l * C;
         const float* ln2b = P + o->off[9] + (size_t)l * C;
-        const float* fcw = P + o->off[10] + (size_t)l * 4 * C * C;
+        const float* fcw = PW + o->off[10] + (size_t)l * 4 * C * C;
         const float* fcb = P + o->off[11] + (size_t)l * 4 * C;
-        const float* fpw = P + o->off[12] + (size_t)l * C * 4 * C;
+        const float* fpw = PW + o->off[12] + (size_t)l * C * 4 * C;
         const float* fpb = P + o->off[13] + (size_t)l * C;
         oracle_layernorm_forward(o->ln, NULL, NULL, o->x, ln1w, ln1b, B, 1, C);
+        round_bf16_n(o, o->ln, (size_t)B * C);
         /* decode QKV = matmul_cached's last row (paged_infer.c:117-160) */
         matmul_rows_ocpar(o->qkv, o->ln, qkvw, qkvb, B, C, 3 * C);
         /* add_to_cache (paged_infer.c:548-566): K,V of this token into its page slot */
@@ -513,17 +549,21 @@ int oracle_paged_step(OraclePaged* o, const int* tokens, float* logits, int* nex
                          o->qkv + (size_t)b * 3 * C + h * hs, paged_k, paged_v, &px, 0, n, hs);
                 free(pre); free(att); free(kptr); free(vptr);
             }
+        round_bf16_n(o, o->atty, (size_t)B * C);
         matmul_rows_ocpar(o->tmp, o->atty, apw, apb, B, C, C);
         oracle_residual_forward(o->res2, o->x, o->tmp, B * C);
         oracle_layernorm_forward(o->ln, NULL, NULL, o->res2, ln2w, ln2b, B, 1, C);
+        round_bf16_n(o, o->ln, (size_t)B * C);
         matmul_rows_ocpar(o->fch, o->ln, fcw, fcb, B, C, 4 * C);
         oracle_gelu_forward(o->fchg, o->fch, B * 4 * C);
+        round_bf16_n(o, o->fchg, (size_t)B * 4 * C);
         matmul_rows_ocpar(o->tmp, o->fchg, fpw, fpb, B, 4 * C, C);
         oracle_residual_forward(o->x, o->res2, o->tmp, B * C);
     }
     oracle_layernorm_forward(o->ln, NULL, NULL, o->x, P + o->off[14], P + o->off[15], B, 1, C);
+    round_bf16_n(o, o->ln, (size_t)B * C);
     float* lg = logits ? logits : o->logits;
-    matmul_rows_ocpar(lg, o->ln, P + o->off[0], NULL, B, C, V);
+    matmul_rows_ocpar(lg, o->ln, o->wte_bf16 ? o->wte_bf16 : P + o->off[0], NULL, B, C, V);
     for (int b = 0; b < B; b++) {
         if (next) next[b] = oracle_argmax(lg + (size_t)b * V, V);
         o->pos[b]++;

@@ -100,6 +100,9 @@ int  oracle_paged_pos(const OraclePaged* o, int b);
 /* bf16 KV pool semantics (BASELINE config 5): appended K/V are rounded to
  * bf16 (nearest even) and read back exactly; all arithmetic stays fp32 */
 void oracle_paged_set_kv_bf16(OraclePaged* o, int on);
+/* bf16 weights mode (the engine's HPA_BF16 weights): GEMM weights and GEMM
+ * input rows rounded to bf16 (nearest even), fp32 sums; 0 or -1 (no memory) */
+int oracle_paged_set_w_bf16(OraclePaged* o, int on);
 float oracle_round_bf16(float f);
 void oracle_paged_free(OraclePaged* o);
 

@@ -33,6 +33,93 @@ def _stats_tiles(x, Mp):
     return st
 
 
+def _rbf16(x):
+    """fp32 -> bf16 value (round to nearest even, finite inputs), as fp32"""
+    u = np.ascontiguousarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000
+    return u.astype(np.uint32).view(np.float32)
+
+
+def _bf16_ambiguous(a64):
+    """elements within 1e-5 relative of a bf16 rounding midpoint"""
+    a32 = a64.astype(np.float32)
+    lo = a32.view(np.uint32) & np.uint32(0xFFFF0000)
+    mid = (lo | np.uint32(0x8000)).view(np.float32).astype(np.float64)
+    return np.abs(a64 - mid) <= 1e-5 * np.abs(a64)
+
+
+def test_pack_frag_bf16_layout(hip):
+    """bf16 frag layout (hip_paged_attn.h): element (m, k) at
+    ((m/16 * K/32 + k/32) * 64 + m%16 + 16*((k%16)/4)) * 8 + k%4 + 4*((k%32)/16), RNE values"""
+    L = hip.lib()
+    rng = np.random.default_rng(5)
+    rows, K = 70, 96
+    a = rng.standard_normal((rows, K)).astype(np.float32)
+    d_a = hip.DeviceBuffer.from_array(a)
+    n = L.hpa_frag_bf16_elems(rows, K)
+    assert n == 80 * K
+    d_f = hip.DeviceBuffer(n * 2)
+    hip.check(L.hpa_pack_frag_bf16(d_a.ptr, rows, K, K, d_f.ptr))
+    f = d_f.download(n, np.uint16)
+    m, k = np.meshgrid(np.arange(rows), np.arange(K), indexing="ij")
+    idx = (((m >> 4) * (K >> 5) + (k >> 5)) * 64 + (m & 15) + 16 * ((k >> 2) & 3)) * 8 + (k & 3) + 4 * ((k >> 4) & 1)
+    want = (_rbf16(a).view(np.uint32) >> 16).astype(np.uint16)
+    assert np.array_equal(f[idx], want)
+    mask = np.ones(n, bool)
+    mask[idx.ravel()] = False
+    assert np.all(f[mask] == 0)  # padded rows
+
+
+@pytest.mark.parametrize("epi,M,K,N,waves,rb,ct,ln", [
+    ("RESID", 64, 768, 768, 4, 4, 2, True), ("RESID", 80, 3072, 768, 8, 4, 1, False),
+    ("RESID", 64, 1600, 1600, 8, 2, 2, True), ("RESID", 37, 768, 768, 4, 1, 1, False),
+    ("GELU", 256, 768, 3072, 4, 4, 2, True), ("GELU", 64, 768, 3072, 8, 2, 1, True),
+    ("LOGITS", 64, 768, 50257, 4, 4, 2, True), ("LOGITS", 256, 768, 50257, 0, 0, 0, True)])
+def test_fused_bf16_weights(hip, epi, M, K, N, waves, rb, ct, ln):
+    """w_dtype = HPA_BF16: every epilogue against the f64 product of the
+    bf16-rounded operands (LN applied before the rounding)"""
+    import torch
+    L = hip.lib()
+    e = dict(RESID=hip.HPA_FEPI_RESID, GELU=hip.HPA_FEPI_GELU, LOGITS=hip.HPA_FEPI_LOGITS)[epi]
+    rng = np.random.default_rng(M + K + waves)
+    res = rng.uniform(-1, 1, (M, N)).astype(np.float32)
+    out, acc, bound, keep = _run(hip, e, M, K, N, waves, ln=ln, rng=rng, res=res, rb=rb, ct=ct, w_bf16=True)
+    Mp = (M + 15) // 16 * 16
+    if epi == "RESID":
+        got = hip.from_frag(out.download(Mp * N), M, N)
+        assert np.all(np.abs(got - (res + acc)) <= bound + 1e-6)
+    elif epi == "GELU":
+        got = hip.from_frag(out.download(Mp * N), M, N)
+        ref = torch.nn.functional.gelu(torch.from_numpy(acc), approximate="tanh").numpy()
+        assert np.all(np.abs(got - ref) <= 1.2 * bound + 2e-5)  # |gelu'| <= 1.13
+    else:
+        got = out.download((M, N))
+        assert np.all(np.abs(got - acc) <= bound)
+        part = keep[-3]
+        nxt = hip.DeviceBuffer(M * 4)
+        hip.check(L.hpa_argmax_final(part.ptr, (N + 15) // 16, Mp, M, nxt.ptr, None, None, None))
+        assert np.array_equal(nxt.download(M, np.int32), got.argmax(-1))
+
+
+def test_fused_bf16_rows_independent_of_shape(hip):
+    """a row's bf16 result depends on the waves only, never on row blocks,
+    column tiles or M (bit-identical)"""
+    rng = np.random.default_rng(21)
+    K, N = 768, 768
+    fixed = dict(x=rng.uniform(-1, 1, (64, K)).astype(np.float32),
+                 W=rng.uniform(-0.05, 0.05, (N, K)).astype(np.float32),
+                 bias=rng.uniform(-0.1, 0.1, N).astype(np.float32),
+                 lw=rng.uniform(0.8, 1.2, K).astype(np.float32), lb=rng.uniform(-0.1, 0.1, K).astype(np.float32))
+    res = np.zeros((64, N), np.float32)
+    outs = []
+    for M, rb, ct in [(64, 4, 2), (64, 1, 1), (64, 2, 2), (48, 1, 1)]:
+        out, _, _, keep = _run(hip, hip.HPA_FEPI_RESID, M, K, N, 4, ln=True, rng=rng, res=res[:M], rb=rb, ct=ct,
+                               fixed=fixed, w_bf16=True)
+        outs.append(hip.from_frag(out.download((M + 15) // 16 * 16 * N), M, N))
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0][:o.shape[0]])
+
+
 def test_pack_unpack_roundtrip(hip):
     L = hip.lib()
     rng = np.random.default_rng(0)
@@ -49,7 +136,7 @@ def test_pack_unpack_roundtrip(hip):
 
 
 def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixed=None, variant=0, ct=0,
-         fold=False, ks=0):
+         fold=False, ks=0, w_bf16=False):
     L = hip.lib()
     x = rng.uniform(-1, 1, (M, K)).astype(np.float32)
     W = rng.uniform(-0.05, 0.05, (N, K)).astype(np.float32)
@@ -79,6 +166,20 @@ def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixe
     else:
         a = x.astype(np.float64)
     g.w = dev(hip.to_frag(W))
+    if w_bf16:  # bf16 weights (hpa_gemm_bf16.hip): packed on the device from fp32 W
+        wb = hip.DeviceBuffer(L.hpa_frag_bf16_elems(N, K) * 2)
+        keep.append(wb)
+        hip.check(L.hpa_pack_frag_bf16(dev(W), N, K, K, wb.ptr), "pack bf16")
+        g.w, g.w_dtype = wb.ptr, hip.HPA_BF16
+        # reference: bf16-rounded operands, exact products, f64 sums; an A element
+        # whose f64 value sits within 1e-5 relative of a bf16 rounding midpoint may
+        # round either way on the GPU (fp32 LN): one bf16 ulp (2^-7 |a| bound) there
+        a32 = a.astype(np.float32)
+        amb = _bf16_ambiguous(a)
+        ab = _rbf16(a32).astype(np.float64)
+        Wb = _rbf16(W).astype(np.float64)
+        extra = (amb * np.abs(a) * 2.0 ** -7) @ np.abs(Wb).T
+        a, W = ab, Wb
     g.bias = dev(bias) if epi != hip.HPA_FEPI_LOGITS else None
     if fold:  # LN folded into the packed weights (hpa_ln_fold_pack)
         assert ln
@@ -101,6 +202,8 @@ def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixe
     g.epilogue = epi
     acc = a @ W.astype(np.float64).T
     bound = 4e-6 * (np.abs(a) @ np.abs(W.astype(np.float64)).T) + 2e-6
+    if w_bf16:
+        bound = bound + extra
     if fold:
         bound = np.maximum(bound, fold_bound)
     if epi != hip.HPA_FEPI_LOGITS:
