@@ -225,7 +225,8 @@ typedef struct {
                              row block; (waves, K/16) in {(4,48),(8,48),(16,48),(8,192),(16,192)});
                              3 = looped with larger trips (same results as 1);
                              4 = LOGITS only: activation-resident persistent kernel
-                             (K = 768, rows <= 64; 16 waves; else as 1) */
+                             (K = 768, rows <= 64; 16 waves; else as 1);
+                             5 = bf16 weights only: A-resident kernel (col_tiles = rounds) */
     int col_tiles;        /* 16-column tiles per workgroup: 1; 2 (waves 4/8, row_blocks
                              2/4); 4 (waves 4, row_blocks 4); 0 = by shape.  A hint:
                              where M's row blocks or the waves cannot carry it, 1 */
@@ -279,6 +280,11 @@ void hpa_fused_pick(int M, int N, int K, int* out3);
 /* the launch shape of a bf16-weight GEMM (w_dtype = HPA_BF16) when waves /
  * row_blocks / col_tiles are 0 */
 void hpa_fused_pick_bf16(int M, int N, int K, int* out3);
+/* bf16 weights, A-resident kernel (variant 5: the workgroup's rows of A
+ * LayerNorm'ed and rounded into LDS once, waves walking waves*rounds column
+ * tiles over the whole K; col_tiles = rounds for this variant):
+ * out3 = {waves, row_blocks, rounds}; returns 1 where variant 0 uses it */
+int hpa_fused_pick_bf16_ares(int M, int N, int K, int* out3);
 int hpa_fused_pick_waves(int M, int N, int K);
 /* residual = wte[tok] + wpe[pos] in frag layout [Mp][C], stats (1 tile) */
 int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const float* wpe,

@@ -472,16 +472,35 @@ void hpa_fused_pick(int M, int N, int K, int* out3) {
     }
 }
 
-// bf16 weights: the MFMA is 16x the fp32 rate, so these GEMMs are bound by
-// operand delivery; every activation fragment feeds 2 weight tiles and every
-// weight fragment up to 4 row blocks (first cut)
+// bf16 weights (profiles/r1/gemm_tune_bf16_b256.log, _b64.log; bf16 MFMA is
+// 16x the fp32 rate, so operand delivery bounds these GEMMs):
+//  * A-resident kernel (variant 5) for the logits at every M and for the
+//    K = 768 / N >= 2304 GEMMs (qkv, fc) from M > 112: the looped kernel
+//    re-reads and re-normalises the fp32 A rows per column-tile group
+//    (B = 256 logits 184 -> 56 us, qkv 15.8 -> 10.8, fc 16.1 -> 11.2);
+//  * looped kernel otherwise (8 waves, 2 row blocks x 2 column tiles;
+//    1 x 1 for the N <= 1024 GEMMs at M <= 112).
+// A row's summation order follows the kernel (one k chain per wave in
+// variant 5, 8 wave ranges folded in order in the looped one), so in bf16
+// mode it may depend on M; both are held to the oracle's bf16 bound.
+// A-resident shape: out3 = {waves, row_blocks, rounds}; returns 1 where
+// variant 0 uses it.
+int hpa_fused_pick_bf16_ares(int M, int N, int K, int* out3) {
+    const int ntn = (N + 15) / 16;
+    const int big = (M + 15) / 16 >= 8;
+    out3[0] = 8;
+    out3[1] = K <= 768 ? (big && ntn >= 1024 ? 4 : 2) : K <= 1600 ? 2 : 1;
+    out3[2] = ntn >= 1024 ? (big ? 8 : 4) : 1;
+    if (K > 3200) return 0;
+    return ntn >= 1024 || (big && ntn >= 144);
+}
+
 void hpa_fused_pick_bf16(int M, int N, int K, int* out3) {
-    (void)M;
-    (void)N;
     (void)K;
-    out3[0] = 4;
-    out3[1] = 4;
-    out3[2] = 2;
+    const int small = (M + 15) / 16 < 8 && N <= 1024;
+    out3[0] = 8;
+    out3[1] = small ? 1 : 2;
+    out3[2] = small ? 1 : 2;
 }
 
 int hpa_fused_pick_waves(int M, int N, int K) {
@@ -532,9 +551,17 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
     if (fused_prepare(g, &p)) return 1;
     int nw, mt, ntw;
     if (g->w_dtype == HPA_BF16) {  // bf16 weights: hpa_gemm_bf16.hip
-        HPA_REQUIRE(g->K % 32 == 0 && !g->ln_fold_c1 && p.ks == 1 && (g->variant == 0 || g->variant == 4),
-                    "gemm_fused bf16: K % 32, no ln_fold_c1, no k_slices, variant 0");
+        HPA_REQUIRE(g->K % 32 == 0 && !g->ln_fold_c1 && p.ks == 1 &&
+                        (g->variant == 0 || g->variant == 4 || g->variant == 5 || g->variant == 1),
+                    "gemm_fused bf16: K % 32, no ln_fold_c1, no k_slices, variant 0/1/5");
         int pk[3];
+        if (g->variant == 5 || (g->variant != 1 && hpa_fused_pick_bf16_ares(g->M, g->N, g->K, pk))) {
+            if (g->variant == 5) hpa_fused_pick_bf16_ares(g->M, g->N, g->K, pk);
+            nw = g->waves ? g->waves : pk[0];
+            mt = g->row_blocks ? g->row_blocks : pk[1];
+            while (mt > 1 && ((p.Mp / 16) % mt || mt * g->K > 3200 || (mt == 4 && g->K > 768))) mt >>= 1;
+            return launch_b16_ares(p, g->epilogue, nw, mt, g->col_tiles ? g->col_tiles : pk[2]);
+        }
         hpa_fused_pick_bf16(g->M, g->N, g->K, pk);
         nw = g->waves ? g->waves : pk[0];
         mt = g->row_blocks ? g->row_blocks : pk[1];

@@ -163,6 +163,152 @@ __global__ __launch_bounds__(NW * 64) void gemm_b16_kernel(FG p) {
     epi.finish(p, acc, red, tile, nt0, row0, lngb, cx * p.gy + ry, slice);
 }
 
+// ---- A-resident variant (variant 5): the workgroup's MT*16 rows of A are
+// LayerNorm'ed and rounded to bf16 ONCE into LDS (bf16 frag layout), then its
+// waves walk the workgroup's chunk of column tiles in rounds -- wave w takes
+// tile c0 + round*NW + w over the whole K (no K split, no fold), streaming
+// its weight fragments U steps ahead and reading A fragments from LDS.  The
+// looped kernel instead re-reads (and re-normalises) the fp32 A rows for
+// every column-tile group: at M = 256 that A traffic, not the MFMA, bounds
+// it.  A row's sum is one in-order k chain per wave (differs from the looped
+// kernel's per-wave ranges; equal for every launch shape of this variant).
+// KC = A capacity in 32-deep steps (24: K <= 768, 50: 1600, 100: 3200), MT*KC <= 100
+// (100 KiB of bf16): the LDS, hence the workgroups per CU, follows K
+template <int NW, int MT, int KC>
+constexpr int ares_lds_floats() {
+    return 2 * HPA_FUSED_LN_KMAX + 10 * MT * 16 + MT * KC * 64 * 4 +
+           (NW * MT * 256 > NW * MT * 16 * 17 ? NW * MT * 256 : NW * MT * 16 * 17);
+}
+
+template <int NW, int EPI, int MT, int KC, int U>
+__global__ __launch_bounds__(NW * 64) void gemm_b16_ares_kernel(FG p, int cpw) {
+    constexpr int NT = NW * 64;
+    constexpr int R = MT * 16;
+    constexpr int TE = MT * 256;
+    constexpr int EPT = TE / 64;  // elements per thread of one round (NW tiles x TE over NT)
+    __shared__ __attribute__((aligned(16))) float smem[ares_lds_floats<NW, MT, KC>()];
+    float* lngb = smem;                       // LN weight [K], bias [K]
+    float* lnst = lngb + 2 * HPA_FUSED_LN_KMAX;  // [R][2]
+    float* lnscr = lnst + 2 * R;              // [4R][2]
+    uint4* As = reinterpret_cast<uint4*>(lnscr + 8 * R);  // [MT][K32][64 lanes] bf16x8
+    float* red = reinterpret_cast<float*>(As + MT * KC * 64);  // [NW][TE]; aliased by tile
+
+    int cx, ry, slice;
+    if (!xcd_tile(p, blockIdx.x, cx, ry, slice)) return;
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int row0 = ry * R;
+    const int K32 = p.K >> 5;
+    const int t_begin = cx * cpw, t_end = min(p.ntn, t_begin + cpw);
+
+    // 1. A: LN'ed, rounded, into LDS
+    const bool ln_apply = p.ln_stats != nullptr;
+    float mu[MT], rs[MT];
+    if (ln_apply) ln_prologue<NW, MT>(p, lngb, lnst, lnscr, row0, true, mu, rs);
+    {
+        const float4* xf = reinterpret_cast<const float4*>(p.x) + (size_t)ry * MT * p.K16 * 64 + lane;
+        const float4* sg = reinterpret_cast<const float4*>(lngb) + (lane >> 4);
+        const float4* sb = reinterpret_cast<const float4*>(lngb + HPA_FUSED_LN_KMAX) + (lane >> 4);
+        const int nst = MT * K32;
+        for (int i = w; i < nst; i += NW) {  // (row block, step) pairs, one per wave
+            const int r = i / K32, st = i - r * K32;
+            float4 x0 = xf[(size_t)r * p.K16 * 64 + (size_t)(2 * st) * 64];
+            float4 x1 = xf[(size_t)r * p.K16 * 64 + (size_t)(2 * st + 1) * 64];
+            if (ln_apply) {
+                const float m = lnst[2 * (16 * r + (lane & 15))], q = lnst[2 * (16 * r + (lane & 15)) + 1];
+                x0 = ln4(x0, m, q, sg[4 * (2 * st)], sb[4 * (2 * st)]);
+                x1 = ln4(x1, m, q, sg[4 * (2 * st + 1)], sb[4 * (2 * st + 1)]);
+            }
+            As[(size_t)(r * K32 + st) * 64 + lane] = __builtin_bit_cast(uint4, pack_bf16(x0, x1));
+        }
+    }
+    __syncthreads();
+
+    // 2. rounds of NW column tiles
+    for (int tb = t_begin; tb < t_end; tb += NW) {
+        Epi<NW, EPI, MT, NW> epi;
+        epi.prefetch(p, tb, row0);
+        const int t = min(tb + w, p.ntn - 1);  // past the chunk: computed, never stored (col >= N or next round)
+        const uint4* wp = reinterpret_cast<const uint4*>(p.w) + (size_t)t * K32 * 64 + lane;
+        f32x4 acc[MT];
+#pragma unroll
+        for (int r = 0; r < MT; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+        uint4 wq[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) wq[u] = wp[(size_t)min(u, K32 - 1) * 64];
+        for (int s0 = 0; s0 < K32; s0 += U) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int st = s0 + u;
+                const uint4 wc = wq[u];
+                wq[u] = wp[(size_t)min(st + U, K32 - 1) * 64];  // U steps ahead, clamped (unconditional)
+                if (st < K32) {
+                    const bf16x8 wb = __builtin_bit_cast(bf16x8, wc);
+#pragma unroll
+                    for (int r = 0; r < MT; ++r) {
+                        const bf16x8 a = __builtin_bit_cast(bf16x8, As[(size_t)(r * K32 + st) * 64 + lane]);
+                        acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wb, acc[r], 0, 0, 0);
+                    }
+                }
+            }
+        }
+        // wave w's tile is column tile j = w of the round's Epi<.., NTW = NW>
+#pragma unroll
+        for (int r = 0; r < MT; ++r)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) red[w * TE + (r * 4 + g) * 64 + lane] = acc[r][g];
+        __syncthreads();
+        float vals[EPT];
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) vals[i] = red[threadIdx.x + i * NT];
+        __syncthreads();  // tile (the row statistics' scratch) aliases red
+        epi.apply(p, vals, red, red, tb, row0, nullptr, false);
+        __syncthreads();
+    }
+}
+
+template <int NW, int MT, int KC>
+static int launch_ares_t(FG p, int epi, int rounds) {
+    constexpr int U = 8;
+    const int cpw = NW * rounds;
+    const int gx = (p.ntn + cpw - 1) / cpw, gy = p.Mp / 16 / MT;
+    p.gx = gx;
+    p.gy = gy;
+    dim3 grid((unsigned)(((gx + 7) / 8) * 8 * gy)), block(NW * 64);
+    switch (epi) {
+        case HPA_FEPI_QKV: gemm_b16_ares_kernel<NW, HPA_FEPI_QKV, MT, KC, U><<<grid, block, 0, hpa_stream()>>>(p, cpw); break;
+        case HPA_FEPI_RESID: gemm_b16_ares_kernel<NW, HPA_FEPI_RESID, MT, KC, U><<<grid, block, 0, hpa_stream()>>>(p, cpw); break;
+        case HPA_FEPI_GELU: gemm_b16_ares_kernel<NW, HPA_FEPI_GELU, MT, KC, U><<<grid, block, 0, hpa_stream()>>>(p, cpw); break;
+        case HPA_FEPI_LOGITS: gemm_b16_ares_kernel<NW, HPA_FEPI_LOGITS, MT, KC, U><<<grid, block, 0, hpa_stream()>>>(p, cpw); break;
+        default: return hpa_fail(__FILE__, __LINE__, "gemm_fused bf16: unknown epilogue");
+    }
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+int launch_b16_ares(const FG& p, int epi, int nw, int mt, int rounds) {
+    HPA_REQUIRE(rounds >= 1 && (p.Mp / 16) % mt == 0, "gemm_fused bf16 A-resident: rounds >= 1, row blocks of M");
+    HPA_REQUIRE((mt == 4 && p.K <= 768) || (mt == 2 && p.K <= 1600) || (mt == 1 && p.K <= 3200),
+                "gemm_fused bf16 A-resident: row_blocks * K <= 3200 (4: K <= 768, 2: 1600, 1: 3200)");
+    const int k32 = p.K / 32;
+    const int kc = k32 <= 24 ? 24 : k32 <= 50 ? 50 : 100;
+    switch (nw * 1000 + mt * 100 + kc) {  // kc in {24, 50, 100}: keys unique
+        case 4424: return launch_ares_t<4, 4, 24>(p, epi, rounds);
+        case 4224: return launch_ares_t<4, 2, 24>(p, epi, rounds);
+        case 4250: return launch_ares_t<4, 2, 50>(p, epi, rounds);
+        case 4124: return launch_ares_t<4, 1, 24>(p, epi, rounds);
+        case 4150: return launch_ares_t<4, 1, 50>(p, epi, rounds);
+        case 4200: return launch_ares_t<4, 1, 100>(p, epi, rounds);  // mt 1, kc 100
+        case 8424: return launch_ares_t<8, 4, 24>(p, epi, rounds);
+        case 8224: return launch_ares_t<8, 2, 24>(p, epi, rounds);
+        case 8250: return launch_ares_t<8, 2, 50>(p, epi, rounds);
+        case 8124: return launch_ares_t<8, 1, 24>(p, epi, rounds);
+        case 8150: return launch_ares_t<8, 1, 50>(p, epi, rounds);
+        case 8200: return launch_ares_t<8, 1, 100>(p, epi, rounds);
+        default: return hpa_fail(__FILE__, __LINE__, "gemm_fused bf16 A-resident: waves 4/8, row_blocks 1/2/4");
+    }
+}
+
 template <int NW, int MT, int NTW>
 static int launch_b16_t(FG p, int epi) {
     const int gx = (p.ntn + NTW - 1) / NTW, gy = p.Mp / 16 / MT;

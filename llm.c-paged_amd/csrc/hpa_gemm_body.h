@@ -255,7 +255,14 @@ struct Epi {
         }
         const bool split = p.ks > 1;  // uniform
         if (split && !ks_exchange(p, vals, red, wsum, tile_id, slice)) return;
+        apply(p, vals, red, tile, nt0, row0, wsum, split);
+    }
 
+    // the epilogue proper on the folded values of the owned elements (vals[i]
+    // = element threadIdx.x + i*NT); red is read only for split LN-folded
+    // statistics; tile = LDS scratch for the row statistics
+    __device__ __forceinline__ void apply(const FG& p, const float* vals, const float* red, float* tile, int nt0,
+                                          int row0, const float* wsum, bool split) {
         const bool rowstat = EPI == HPA_FEPI_LOGITS || (EPI == HPA_FEPI_RESID && p.stats_out);  // uniform
 #pragma unroll
         for (int i = 0; i < EPT; ++i) {
@@ -732,6 +739,9 @@ int logits_resident_grid(const FG& p);  // workgroups = argmax partials per row 
 // bf16-weight GEMM launch (hpa_gemm_bf16.hip): waves 4/8, (row_blocks,
 // col_tiles) in {(1,1), (2,1), (4,1), (2,2), (4,2)}
 int launch_b16(const FG& p, int epi, int nw, int mt, int ntw);
+// A-resident bf16 variant (variant 5): waves 4/8, row_blocks (mt) 1/2/4 with
+// mt*K <= 3200; each workgroup takes waves*rounds column tiles
+int launch_b16_ares(const FG& p, int epi, int nw, int mt, int rounds);
 
 static inline int fused_prepare(const HpaFusedGemm* g, FG* p) {
     HPA_REQUIRE(g && g->x && g->w && g->out, "gemm_fused: null operand");

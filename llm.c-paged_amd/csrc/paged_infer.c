@@ -864,11 +864,8 @@ static int dec_init_fused(GPT2* model, GPT2Decode* d) {
         if (hpa_pack_frag_bf16(w->wte, V, C, C, b16 + d->wpack_off[4])) return 1;
         d->d_fold = NULL;
         for (int i = 0; i < 5; i++) {
-            int pk[3];
-            hpa_fused_pick_bf16(B, i == 4 ? V : 0, C, pk);
-            d->fwaves[i] = pk[0];
-            d->frb[i] = pk[1];
-            d->fct[i] = pk[2];
+            /* launch shapes by (M, N, K) in the library (hpa_fused_pick_bf16*) */
+            d->fwaves[i] = d->frb[i] = d->fct[i] = 0;
             d->fks[i] = 1;
         }
         d->ev_fork = hpa_event_create_nt();
@@ -1752,9 +1749,9 @@ static int prefill_gemm(GPT2* model, int l, int which, int R) {
     g.w_dtype = d->w_bf16 ? HPA_BF16 : HPA_F32;
     /* B*T rows: reuse every activation fragment over 2 weight tiles and every
      * weight fragment over 4 row blocks (MFMA-bound at this M) */
-    g.waves = 8;
-    g.row_blocks = 4;
-    g.col_tiles = 2;
+    g.waves = d->w_bf16 ? 0 : 8; /* bf16 weights: the library's shapes by (M, N, K) */
+    g.row_blocks = d->w_bf16 ? 0 : 4;
+    g.col_tiles = d->w_bf16 ? 0 : 2;
     g.pool = &d->pool;
     g.layer = l;
     g.block_table = d->d_bt;

@@ -70,12 +70,17 @@ def test_pack_frag_bf16_layout(hip):
     assert np.all(f[mask] == 0)  # padded rows
 
 
-@pytest.mark.parametrize("epi,M,K,N,waves,rb,ct,ln", [
-    ("RESID", 64, 768, 768, 4, 4, 2, True), ("RESID", 80, 3072, 768, 8, 4, 1, False),
-    ("RESID", 64, 1600, 1600, 8, 2, 2, True), ("RESID", 37, 768, 768, 4, 1, 1, False),
-    ("GELU", 256, 768, 3072, 4, 4, 2, True), ("GELU", 64, 768, 3072, 8, 2, 1, True),
-    ("LOGITS", 64, 768, 50257, 4, 4, 2, True), ("LOGITS", 256, 768, 50257, 0, 0, 0, True)])
-def test_fused_bf16_weights(hip, epi, M, K, N, waves, rb, ct, ln):
+@pytest.mark.parametrize("epi,M,K,N,waves,rb,ct,ln,variant", [
+    ("RESID", 64, 768, 768, 4, 4, 2, True, 1), ("RESID", 80, 3072, 768, 8, 4, 1, False, 1),
+    ("RESID", 64, 1600, 1600, 8, 2, 2, True, 1), ("RESID", 37, 768, 768, 4, 1, 1, False, 1),
+    ("GELU", 256, 768, 3072, 4, 4, 2, True, 1), ("GELU", 64, 768, 3072, 8, 2, 1, True, 1),
+    ("LOGITS", 64, 768, 50257, 4, 4, 2, True, 1), ("LOGITS", 256, 768, 50257, 0, 0, 0, True, 0),
+    # A-resident kernel (variant 5; ct = rounds of `waves` column tiles per workgroup)
+    ("RESID", 64, 768, 768, 8, 4, 1, True, 5), ("RESID", 80, 3072, 768, 4, 1, 2, False, 5),
+    ("RESID", 48, 1600, 1600, 8, 2, 3, True, 5), ("RESID", 37, 768, 784, 4, 1, 1, True, 5),
+    ("GELU", 256, 768, 3072, 8, 4, 2, True, 5), ("GELU", 64, 768, 3072, 4, 2, 1, True, 5),
+    ("LOGITS", 64, 768, 50257, 8, 4, 4, True, 5), ("LOGITS", 256, 768, 50257, 8, 2, 8, True, 5)])
+def test_fused_bf16_weights(hip, epi, M, K, N, waves, rb, ct, ln, variant):
     """w_dtype = HPA_BF16: every epilogue against the f64 product of the
     bf16-rounded operands (LN applied before the rounding)"""
     import torch
@@ -83,7 +88,8 @@ def test_fused_bf16_weights(hip, epi, M, K, N, waves, rb, ct, ln):
     e = dict(RESID=hip.HPA_FEPI_RESID, GELU=hip.HPA_FEPI_GELU, LOGITS=hip.HPA_FEPI_LOGITS)[epi]
     rng = np.random.default_rng(M + K + waves)
     res = rng.uniform(-1, 1, (M, N)).astype(np.float32)
-    out, acc, bound, keep = _run(hip, e, M, K, N, waves, ln=ln, rng=rng, res=res, rb=rb, ct=ct, w_bf16=True)
+    out, acc, bound, keep = _run(hip, e, M, K, N, waves, ln=ln, rng=rng, res=res, rb=rb, ct=ct, w_bf16=True,
+                                 variant=variant)
     Mp = (M + 15) // 16 * 16
     if epi == "RESID":
         got = hip.from_frag(out.download(Mp * N), M, N)
@@ -111,13 +117,15 @@ def test_fused_bf16_rows_independent_of_shape(hip):
                  bias=rng.uniform(-0.1, 0.1, N).astype(np.float32),
                  lw=rng.uniform(0.8, 1.2, K).astype(np.float32), lb=rng.uniform(-0.1, 0.1, K).astype(np.float32))
     res = np.zeros((64, N), np.float32)
-    outs = []
-    for M, rb, ct in [(64, 4, 2), (64, 1, 1), (64, 2, 2), (48, 1, 1)]:
-        out, _, _, keep = _run(hip, hip.HPA_FEPI_RESID, M, K, N, 4, ln=True, rng=rng, res=res[:M], rb=rb, ct=ct,
-                               fixed=fixed, w_bf16=True)
-        outs.append(hip.from_frag(out.download((M + 15) // 16 * 16 * N), M, N))
-    for o in outs[1:]:
-        assert np.array_equal(o, outs[0][:o.shape[0]])
+    for variant, shapes in [(1, [(4, 64, 4, 2), (4, 64, 1, 1), (4, 64, 2, 2), (4, 48, 1, 1)]),
+                            (5, [(8, 64, 4, 1), (4, 64, 1, 3), (8, 64, 2, 2), (4, 48, 1, 1)])]:
+        outs = []
+        for waves, M, rb, ct in shapes:
+            out, _, _, keep = _run(hip, hip.HPA_FEPI_RESID, M, K, N, waves, ln=True, rng=rng, res=res[:M], rb=rb,
+                                   ct=ct, fixed=fixed, w_bf16=True, variant=variant)
+            outs.append(hip.from_frag(out.download((M + 15) // 16 * 16 * N), M, N))
+        for o in outs[1:]:
+            assert np.array_equal(o, outs[0][:o.shape[0]])
 
 
 def test_pack_unpack_roundtrip(hip):

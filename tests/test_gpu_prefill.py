@@ -95,20 +95,22 @@ def _margins(logits):
     return s[:, -1] - s[:, -2]
 
 
-def _run(hip, cfgd, B, P, T, seed, pre_steps=0, post_steps=8, graph=False, kv_bf16=False, tol=LOGIT_TOL):
+def _run(hip, cfgd, B, P, T, seed, pre_steps=0, post_steps=8, graph=False, kv_bf16=False, tol=LOGIT_TOL,
+         w_bf16=False, tie=TIE_MARGIN):
     params = synth.params(cfgd, seed=seed)
     model = hip.Model(cfgd, params=params)
-    model.decode_init(B, P, cfgd["maxT"], kv_dtype=hip.HPA_BF16 if kv_bf16 else hip.HPA_F32)
+    model.decode_init(B, P, cfgd["maxT"], kv_dtype=hip.HPA_BF16 if kv_bf16 else hip.HPA_F32,
+                      w_dtype=hip.HPA_BF16 if w_bf16 else hip.HPA_F32)
     model.set_graph(graph)
     c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
-    orc = oc.PagedDecoder(params, c, B, P, cfgd["maxT"], page_seed=seed + 1, kv_bf16=kv_bf16)
+    orc = oc.PagedDecoder(params, c, B, P, cfgd["maxT"], page_seed=seed + 1, kv_bf16=kv_bf16, w_bf16=w_bf16)
     rng = np.random.default_rng(seed)
     worst = 0.0
 
     def check(g_next, o_next, o_logits):
         nonlocal worst
         worst = max(worst, float(np.abs(model.logits() - o_logits).max()))
-        clear = _margins(o_logits) > TIE_MARGIN
+        clear = _margins(o_logits) > tie
         assert np.array_equal(g_next[clear], o_next[clear])
 
     for _ in range(pre_steps):  # decode steps before the prefill (prefill at a nonzero start)
@@ -166,6 +168,14 @@ def test_prefill_gpt2_124m_shapes(hip):
 
 def test_prefill_bf16_kv(hip):
     _run(hip, SMALL, B=3, P=16, T=50, seed=6, kv_bf16=True, tol=5e-3)
+
+
+@pytest.mark.parametrize("B,T", [(3, 50), (4, 40)])
+def test_prefill_bf16_weights(hip, B, T):
+    """bf16 weights: B*T rows through the bf16 GEMMs (looped and, at B*T > 112
+    rows, the A-resident kernel) against the oracle's bf16-weights decode
+    (tolerance as test_gpu_decode.py BF16W_*)"""
+    _run(hip, SMALL, B=B, P=16, T=T, seed=8 + B, w_bf16=True, kv_bf16=True, tol=2e-2, tie=4e-2)
 
 
 def test_prefill_rejects_overflow(hip):

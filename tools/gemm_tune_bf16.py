@@ -31,29 +31,31 @@ def main():
         W = np.random.default_rng(1).uniform(-0.05, 0.05, (N, K)).astype(np.float32)
         pa.check(L.hpa_pack_frag_bf16(gt.dev(W), N, K, K, wb.ptr), "pack")
         g.w, g.w_dtype = wb.ptr, pa.HPA_BF16
-        pk = (ctypes.c_int * 3)()
-        L.hpa_fused_pick_bf16(M, N, K, ctypes.cast(pk, pa._I))
         res, ref = [], {}
-        for waves in (4, 8):
-            for rb, ct in ((1, 1), (2, 1), (4, 1), (2, 2), (4, 2)):
-                if ((M + 15) // 16) % rb:
-                    continue
-                g.waves, g.row_blocks, g.col_tiles = waves, rb, ct
-                try:
-                    us = gt.time_fused(g)
-                except RuntimeError:
-                    continue
-                o = gt.out_copy(g, M, N, epi)
-                ref.setdefault(waves, o)
-                res.append((us, (waves, rb, ct), float(np.abs(o - ref[waves]).max())))
+        shapes = [(1, w_, rb, ct) for w_ in (4, 8) for rb, ct in ((1, 1), (2, 1), (4, 1), (2, 2), (4, 2))]
+        shapes += [(5, w_, rb, r) for w_ in (4, 8) for rb in (1, 2, 4) for r in (1, 2, 4, 8)
+                   if rb * K <= 3200 and not (rb == 4 and K > 768)]
+        for variant, waves, rb, ct in shapes:
+            if ((M + 15) // 16) % rb:
+                continue
+            g.variant, g.waves, g.row_blocks, g.col_tiles = variant, waves, rb, ct
+            try:
+                us = gt.time_fused(g)
+            except RuntimeError:
+                continue
+            o = gt.out_copy(g, M, N, epi)
+            key = (variant, waves)
+            ref.setdefault(key, o)
+            res.append((us, (variant, waves, rb, ct), float(np.abs(o - ref[key]).max())))
+        g.variant = g.waves = g.row_blocks = g.col_tiles = 0
+        auto_us = gt.time_fused(g)
         best = min(res)
-        auto = [r for r in res if r[1] == tuple(pk)] or [best]
         tot_best += best[0]
-        tot_auto += auto[0][0]
+        tot_auto += auto_us
         tot_f32 += f32
-        print(f"{name:8s} M={M} K={K} N={N}  fp32 default {f32:8.2f} us   bf16 auto {tuple(pk)} {auto[0][0]:8.2f} us")
+        print(f"{name:8s} M={M} K={K} N={N}  fp32 default {f32:8.2f} us   bf16 auto {auto_us:8.2f} us")
         for us, shp, err in sorted(res):
-            print(f"   {us:8.2f} us  (waves, rb, ct)={shp}  {2.0 * M * K * N / us / 1e6:7.1f} TF/s  "
+            print(f"   {us:8.2f} us  (variant, waves, rb, ct|rounds)={shp}  {2.0 * M * K * N / us / 1e6:7.1f} TF/s  "
                   f"{2.0 * N * K / us / 1e3:7.1f} GB/s(W)  maxdiff={err:.2e}")
     print(f"sum: fp32 default {tot_f32:.1f} us  bf16 best {tot_best:.1f} us  bf16 auto {tot_auto:.1f} us")
 
