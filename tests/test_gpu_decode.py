@@ -178,7 +178,7 @@ def test_lanes_match_oracle(hip):
         o_next, o_logits = orc.step(tok)
         g_next = model.step(tok)
         assert np.abs(model.logits() - o_logits).max() <= LOGIT_TOL
-        clear = _margins(o_logits) > tie
+        clear = _margins(o_logits) > TIE_MARGIN
         assert np.array_equal(g_next[clear], o_next[clear])
     model.close()
     orc.close()
@@ -350,7 +350,7 @@ def test_split_step_gpt2_124m_matches_oracle(hip):
         o_next, o_logits = orc.step(tok)
         g_next = model.step(tok)
         assert np.abs(model.logits() - o_logits).max() <= LOGIT_TOL
-        clear = _margins(o_logits) > tie
+        clear = _margins(o_logits) > TIE_MARGIN
         assert np.array_equal(g_next[clear], o_next[clear])
         tok = o_next
     model.close()
@@ -389,7 +389,7 @@ def test_overlap_step_matches_oracle(hip, P, B, chain):
         g_next = model.step(tok)
         assert model.overlap_faults() == 0
         assert np.abs(model.logits() - o_logits).max() <= LOGIT_TOL
-        clear = _margins(o_logits) > tie
+        clear = _margins(o_logits) > TIE_MARGIN
         assert np.array_equal(g_next[clear], o_next[clear])
     model.close()
     orc.close()
@@ -414,7 +414,7 @@ def test_overlap_step_gpt2_124m_matches_oracle(hip):
         g_next = model.step(tok)
         assert model.overlap_faults() == 0
         worst = max(worst, float(np.abs(model.logits() - o_logits).max()))
-        clear = _margins(o_logits) > tie
+        clear = _margins(o_logits) > TIE_MARGIN
         assert np.array_equal(g_next[clear], o_next[clear])
         tok = o_next
     assert worst <= LOGIT_TOL, worst

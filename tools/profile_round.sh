@@ -19,8 +19,11 @@ step prof_c2 400 rocprofv3 --kernel-trace --stats -d "$out/prof_c2" -o run --out
 step pmc_c2 900 bash tools/pmc_traffic.sh "$out/pmc_c2" --steps 8 --warmup 2
 step bench_c5 500 python bench.py --batch 256 --ctx 2048 --page-size 8 --kv-dtype bf16
 step bench_c5w 500 python bench.py --batch 256 --ctx 2048 --page-size 8 --kv-dtype bf16 --w-dtype bf16 --cpu-baseline off
+step prof_c5w 500 rocprofv3 --kernel-trace --stats -d "$out/prof_c5w" -o run --output-format csv -- \
+  python3 bench.py --batch 256 --ctx 2048 --page-size 8 --kv-dtype bf16 --w-dtype bf16 --cpu-baseline off
 step bench_xl 600 python bench.py --model XL --page-size 32 --cpu-baseline off
 step bench_prefill 400 python bench.py --prefill real --cpu-baseline off
 step bench_sample 400 python bench.py --sample --cpu-baseline off
 python3 tools/kstats.py "$out/prof_c2/run_kernel_trace.csv" > "$out/kstats_c2.txt"
+python3 tools/kstats.py "$out/prof_c5w/run_kernel_trace.csv" > "$out/kstats_c5w.txt"
 echo done
