@@ -226,7 +226,8 @@ typedef struct {
                              3 = looped with larger trips (same results as 1);
                              4 = LOGITS only: activation-resident persistent kernel
                              (K = 768, rows <= 64; 16 waves; else as 1);
-                             5 = bf16 weights only: A-resident kernel (col_tiles = rounds) */
+                             5 = A-resident kernel (col_tiles = rounds; fp32: K <= 1600,
+                             bf16: K <= 3200) */
     int col_tiles;        /* 16-column tiles per workgroup: 1; 2 (waves 4/8, row_blocks
                              2/4); 4 (waves 4, row_blocks 4); 0 = by shape.  A hint:
                              where M's row blocks or the waves cannot carry it, 1 */
@@ -285,6 +286,10 @@ void hpa_fused_pick_bf16(int M, int N, int K, int* out3);
  * tiles over the whole K; col_tiles = rounds for this variant):
  * out3 = {waves, row_blocks, rounds}; returns 1 where variant 0 uses it */
 int hpa_fused_pick_bf16_ares(int M, int N, int K, int* out3);
+/* fp32 weights, A-resident kernel (variant 5; row_blocks 2 for K <= 768, 1 for
+ * K <= 1600): out3 = {waves, row_blocks, rounds}; returns 1 where variant 0
+ * uses it (by N, K only) */
+int hpa_fused_pick_f32_ares(int M, int N, int K, int* out3);
 int hpa_fused_pick_waves(int M, int N, int K);
 /* residual = wte[tok] + wpe[pos] in frag layout [Mp][C], stats (1 tile) */
 int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const float* wpe,

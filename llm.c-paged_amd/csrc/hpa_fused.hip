@@ -495,6 +495,23 @@ int hpa_fused_pick_bf16_ares(int M, int N, int K, int* out3) {
     return ntn >= 1024 || (big && ntn >= 144);
 }
 
+// fp32 A-resident kernel (variant 5, hpa_gemm_ares.hip): out3 = {waves,
+// row_blocks, rounds}; returns 1 where variant 0 (or 4 where the resident
+// logits kernel does not apply) uses it -- by N and K only, so a row's
+// summation order never depends on M.  Measured (profiles/r1/
+// gemm_tune_ares_*.log): slower than the one-shot / looped kernels on every
+// GPT-2 layer GEMM (124M qkv 12.7 vs 8.8 us, XL qkv 28.2 vs 27.3) and than the
+// resident logits kernel at 124M (67.4 vs 65.3); faster only for the XL
+// logits in isolation (159.7 vs 171.6 us), but the XL step measured slower
+// with it (10.90 vs 10.71 ms/step), so it is nowhere the default.
+int hpa_fused_pick_f32_ares(int M, int N, int K, int* out3) {
+    const int ntn = (N + 15) / 16;
+    out3[0] = 8;
+    out3[1] = K <= 768 && (M + 15) / 16 % 2 == 0 ? 2 : 1;
+    out3[2] = ntn >= 1024 ? (K > 768 ? 8 : 4) : 1;
+    return 0;
+}
+
 void hpa_fused_pick_bf16(int M, int N, int K, int* out3) {
     (void)K;
     const int small = (M + 15) / 16 < 8 && N <= 1024;
@@ -571,6 +588,18 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
         return launch_b16(p, g->epilogue, nw, mt, ntw);
     }
     HPA_REQUIRE(g->w_dtype == HPA_F32, "gemm_fused: w_dtype must be HPA_F32 or HPA_BF16");
+    {
+        int pk[3];
+        const int dflt = hpa_fused_pick_f32_ares(g->M, g->N, g->K, pk);
+        const bool auto_ok = g->variant == 0 || (g->variant == 4 && !logits_resident_eligible(p, g->epilogue));
+        if (g->variant == 5 || (auto_ok && p.ks == 1 && !g->ln_fold_c1 && dflt)) {
+            HPA_REQUIRE(p.ks == 1 && !g->ln_fold_c1, "gemm_fused A-resident: no k_slices, no ln_fold_c1");
+            nw = g->waves ? g->waves : pk[0];
+            mt = g->row_blocks ? g->row_blocks : pk[1];
+            while (mt > 1 && ((p.Mp / 16) % mt || g->K > 768)) mt >>= 1;
+            return launch_f32_ares(p, g->epilogue, nw, mt, g->col_tiles ? g->col_tiles : pk[2]);
+        }
+    }
     HPA_REQUIRE(g->row_blocks == 0 || g->row_blocks == 1 || g->row_blocks == 2 || g->row_blocks == 4,
                 "gemm_fused: row_blocks must be 1, 2 or 4");
     looped_shape(g, p.Mp, &nw, &mt, &ntw);

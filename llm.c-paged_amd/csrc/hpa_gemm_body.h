@@ -742,6 +742,9 @@ int launch_b16(const FG& p, int epi, int nw, int mt, int ntw);
 // A-resident bf16 variant (variant 5): waves 4/8, row_blocks (mt) 1/2/4 with
 // mt*K <= 3200; each workgroup takes waves*rounds column tiles
 int launch_b16_ares(const FG& p, int epi, int nw, int mt, int rounds);
+// A-resident fp32 kernel (hpa_gemm_ares.hip, variant 5 with fp32 weights):
+// waves 4/8, row_blocks 2 (K <= 768) or 1 (K <= 1600)
+int launch_f32_ares(const FG& p, int epi, int nw, int mt, int rounds);
 
 static inline int fused_prepare(const HpaFusedGemm* g, FG* p) {
     HPA_REQUIRE(g && g->x && g->w && g->out, "gemm_fused: null operand");

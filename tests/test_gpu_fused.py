@@ -563,3 +563,52 @@ def test_fused_k_slices(hip, epi, K, N, waves, rb, ct, ks, fold, M):
         outs.append(got)
     assert np.array_equal(outs[0], outs[1])
     assert np.array_equal(outs[0][:16], outs[2])
+
+
+@pytest.mark.parametrize("epi,M,K,N,waves,rb,rounds,ln", [
+    ("RESID", 64, 768, 768, 8, 2, 1, True), ("RESID", 48, 1600, 1600, 8, 1, 2, True),
+    ("RESID", 37, 768, 784, 4, 1, 1, False), ("GELU", 64, 1600, 6400, 8, 1, 1, True),
+    ("GELU", 64, 768, 3072, 4, 2, 3, True), ("LOGITS", 64, 768, 50257, 8, 2, 4, True),
+    ("LOGITS", 40, 1600, 50257, 8, 1, 8, True)])
+def test_fused_f32_aresident(hip, epi, M, K, N, waves, rb, rounds, ln):
+    """fp32 A-resident kernel (variant 5, hpa_gemm_ares.hip) within the fp32
+    bound of the f64 reference, every epilogue"""
+    import torch
+    L = hip.lib()
+    e = dict(RESID=hip.HPA_FEPI_RESID, GELU=hip.HPA_FEPI_GELU, LOGITS=hip.HPA_FEPI_LOGITS)[epi]
+    rng = np.random.default_rng(M + K + rounds)
+    res = rng.uniform(-1, 1, (M, N)).astype(np.float32)
+    out, acc, bound, keep = _run(hip, e, M, K, N, waves, ln=ln, rng=rng, res=res, rb=rb, ct=rounds, variant=5)
+    Mp = (M + 15) // 16 * 16
+    if epi == "RESID":
+        got = hip.from_frag(out.download(Mp * N), M, N)
+        assert np.all(np.abs(got - (res + acc)) <= bound + 1e-6)
+    elif epi == "GELU":
+        got = hip.from_frag(out.download(Mp * N), M, N)
+        ref = torch.nn.functional.gelu(torch.from_numpy(acc), approximate="tanh").numpy()
+        assert np.all(np.abs(got - ref) <= 1.2 * bound + 2e-5)
+    else:
+        got = out.download((M, N))
+        assert np.all(np.abs(got - acc) <= bound)
+        part = keep[-3]
+        nxt = hip.DeviceBuffer(M * 4)
+        hip.check(L.hpa_argmax_final(part.ptr, (N + 15) // 16, Mp, M, nxt.ptr, None, None, None))
+        assert np.array_equal(nxt.download(M, np.int32), got.argmax(-1))
+
+
+def test_fused_f32_aresident_shape_invariant(hip):
+    """one in-order k chain per output: bit-identical for every (waves, row
+    blocks, rounds) and M"""
+    rng = np.random.default_rng(23)
+    K, N = 768, 2304
+    fixed = dict(x=rng.uniform(-1, 1, (64, K)).astype(np.float32),
+                 W=rng.uniform(-0.05, 0.05, (N, K)).astype(np.float32),
+                 bias=rng.uniform(-0.1, 0.1, N).astype(np.float32),
+                 lw=rng.uniform(0.8, 1.2, K).astype(np.float32), lb=rng.uniform(-0.1, 0.1, K).astype(np.float32))
+    outs = []
+    for waves, M, rb, rounds in [(8, 64, 2, 1), (4, 64, 1, 3), (8, 64, 1, 4), (4, 32, 2, 2)]:
+        out, _, _, keep = _run(hip, hip.HPA_FEPI_GELU, M, K, N, waves, ln=True, rng=rng, rb=rb, ct=rounds,
+                               fixed=fixed, variant=5)
+        outs.append(hip.from_frag(out.download((M + 15) // 16 * 16 * N), M, N))
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0][:o.shape[0]])
