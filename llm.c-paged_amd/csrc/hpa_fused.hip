@@ -28,6 +28,7 @@
 //    operands (bias, residual) are loaded before the LDS fold so their
 //    latency overlaps it.
 #include <math.h>
+#include <stdlib.h>
 
 #include "hpa_gemm_body.h"
 
@@ -572,7 +573,13 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
                         (g->variant == 0 || g->variant == 4 || g->variant == 5 || g->variant == 1),
                     "gemm_fused bf16: K % 32, no ln_fold_c1, no k_slices, variant 0/1/5");
         int pk[3];
-        if (g->variant == 5 || (g->variant != 1 && hpa_fused_pick_bf16_ares(g->M, g->N, g->K, pk))) {
+        // HPA_BF16_ARES=0: no A-resident default (measurement knob; variant 5 still honoured)
+        static const int ares_default = [] {
+            const char* e = getenv("HPA_BF16_ARES");
+            return !(e && e[0] == '0');
+        }();
+        if (g->variant == 5 ||
+            (g->variant != 1 && ares_default && hpa_fused_pick_bf16_ares(g->M, g->N, g->K, pk))) {
             if (g->variant == 5) hpa_fused_pick_bf16_ares(g->M, g->N, g->K, pk);
             nw = g->waves ? g->waves : pk[0];
             mt = g->row_blocks ? g->row_blocks : pk[1];
