@@ -491,7 +491,7 @@ int hpa_fused_pick_bf16_ares(int M, int N, int K, int* out3) {
     const int big = (M + 15) / 16 >= 8;
     out3[0] = 8;
     out3[1] = K <= 768 ? (big && ntn >= 1024 ? 4 : 2) : K <= 1600 ? 2 : 1;
-    out3[2] = ntn >= 1024 ? (big ? 8 : 4) : 1;
+    out3[2] = 0;  // rounds: auto (one pass of workgroups over the CUs, hpa_gemm_bf16.hip)
     if (K > 3200) return 0;
     return ntn >= 1024 || (big && ntn >= 144);
 }

@@ -174,10 +174,17 @@ __global__ __launch_bounds__(NW * 64) void gemm_b16_kernel(FG p) {
 // kernel's per-wave ranges; equal for every launch shape of this variant).
 // KC = A capacity in 32-deep steps (24: K <= 768, 50: 1600, 100: 3200), MT*KC <= 100
 // (100 KiB of bf16): the LDS, hence the workgroups per CU, follows K
+// The LN weights (staging only) and the epilogue's fold / row-statistics
+// scratch (rounds only) share one region, so the K = 768 / MT = 2 instance
+// fits two workgroups per CU.
+template <int NW, int MT>
+constexpr int ares_union_floats() {
+    constexpr int red = NW * MT * 256 > NW * MT * 16 * 17 ? NW * MT * 256 : NW * MT * 16 * 17;
+    return red > 2 * HPA_FUSED_LN_KMAX ? red : 2 * HPA_FUSED_LN_KMAX;
+}
 template <int NW, int MT, int KC>
 constexpr int ares_lds_floats() {
-    return 2 * HPA_FUSED_LN_KMAX + 10 * MT * 16 + MT * KC * 64 * 4 +
-           (NW * MT * 256 > NW * MT * 16 * 17 ? NW * MT * 256 : NW * MT * 16 * 17);
+    return ares_union_floats<NW, MT>() + 10 * MT * 16 + MT * KC * 64 * 4;
 }
 
 template <int NW, int EPI, int MT, int KC, int U>
@@ -187,11 +194,11 @@ __global__ __launch_bounds__(NW * 64) void gemm_b16_ares_kernel(FG p, int cpw) {
     constexpr int TE = MT * 256;
     constexpr int EPT = TE / 64;  // elements per thread of one round (NW tiles x TE over NT)
     __shared__ __attribute__((aligned(16))) float smem[ares_lds_floats<NW, MT, KC>()];
-    float* lngb = smem;                       // LN weight [K], bias [K]
-    float* lnst = lngb + 2 * HPA_FUSED_LN_KMAX;  // [R][2]
+    float* lngb = smem;                       // LN weight [K], bias [K] (staging only)
+    float* red = smem;                        // [NW][TE] fold / tile scratch (rounds only)
+    float* lnst = smem + ares_union_floats<NW, MT>();  // [R][2]
     float* lnscr = lnst + 2 * R;              // [4R][2]
     uint4* As = reinterpret_cast<uint4*>(lnscr + 8 * R);  // [MT][K32][64 lanes] bf16x8
-    float* red = reinterpret_cast<float*>(As + MT * KC * 64);  // [NW][TE]; aliased by tile
 
     int cx, ry, slice;
     if (!xcd_tile(p, blockIdx.x, cx, ry, slice)) return;
@@ -270,8 +277,16 @@ __global__ __launch_bounds__(NW * 64) void gemm_b16_ares_kernel(FG p, int cpw) {
 template <int NW, int MT, int KC>
 static int launch_ares_t(FG p, int epi, int rounds) {
     constexpr int U = 8;
+    const int gy = p.Mp / 16 / MT;
+    if (rounds <= 0) {  // auto: one pass of workgroups over the CUs at this LDS footprint
+        constexpr int lds = ares_lds_floats<NW, MT, KC>() * 4;
+        const int per_cu = (160 * 1024) / lds > 0 ? (160 * 1024) / lds : 1;
+        const int slots = 256 * per_cu;
+        rounds = (p.ntn * gy + NW * slots - 1) / (NW * slots);
+        if (rounds < 1) rounds = 1;
+    }
     const int cpw = NW * rounds;
-    const int gx = (p.ntn + cpw - 1) / cpw, gy = p.Mp / 16 / MT;
+    const int gx = (p.ntn + cpw - 1) / cpw;
     p.gx = gx;
     p.gy = gy;
     dim3 grid((unsigned)(((gx + 7) / 8) * 8 * gy)), block(NW * 64);
@@ -287,7 +302,7 @@ static int launch_ares_t(FG p, int epi, int rounds) {
 }
 
 int launch_b16_ares(const FG& p, int epi, int nw, int mt, int rounds) {
-    HPA_REQUIRE(rounds >= 1 && (p.Mp / 16) % mt == 0, "gemm_fused bf16 A-resident: rounds >= 1, row blocks of M");
+    HPA_REQUIRE(rounds >= 0 && (p.Mp / 16) % mt == 0, "gemm_fused bf16 A-resident: rounds >= 0 (0: auto), row blocks of M");
     HPA_REQUIRE((mt == 4 && p.K <= 768) || (mt == 2 && p.K <= 1600) || (mt == 1 && p.K <= 3200),
                 "gemm_fused bf16 A-resident: row_blocks * K <= 3200 (4: K <= 768, 2: 1600, 1: 3200)");
     const int k32 = p.K / 32;
