@@ -306,6 +306,11 @@ int hpa_argmax_final(const float* part, int ntiles, int Mp, int B, int* next, in
  * active as hpa_argmax_final (an inactive row's state does not advance) */
 int hpa_sample_final(const float* logits, int B, int V, unsigned long long* state, int* next, int* tokens,
                      int* pos, const int* active);
+/* the same draw from the single-lane sequential kernel (the ordered fp32
+ * additions as one dependent chain); kept as the measured baseline and as a
+ * cross-check of hpa_sample_final's integer-scan formulation */
+int hpa_sample_final_serial(const float* logits, int B, int V, unsigned long long* state, int* next, int* tokens,
+                            int* pos, const int* active);
 /* paged decode attention writing its output in frag layout ([B][C]) */
 int hpa_paged_attention_decode_frag(const float* q, const HpaKVPool* pool, int layer,
                                     const int* block_table, int bt_stride, const int* pos,

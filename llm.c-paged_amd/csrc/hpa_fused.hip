@@ -333,6 +333,232 @@ __global__ __launch_bounds__(128) void sample_final_kernel(const float* __restri
     }
 }
 
+// ---------------------------------------------------- order-exact scan sampling
+// The same draw as sample_final_kernel (bit-equal sum, cdf and pick), without
+// the serial chain.  While the running fp32 sum S stays in one binade
+// [2^e, 2^(e+1)) (or below 2^-125, where the grid is the denormal one), every
+// fl(S + a) equals S + RN_u(a), with u = ulp(S) and RN_u rounding a term onto
+// the multiples of u.  The ordered sum is then an integer prefix sum of
+// k_i = RN_u(a_i) / u, which is associative and runs as a block scan.  A term
+// breaks the segment when its rounding is a tie (the result's parity decides
+// it), when it is too large for the grid, or when the sum leaves the binade;
+// that one addition is done in fp32 on the exact S before it, and the scan
+// resumes with the new grid.  Breaks are rare: about one per binade of the sum
+// plus ties, whose odds fall as 1/i.  (softmax_forward :259-286, sample_mult
+// :837-848 order.)
+// 16 waves x 4 terms per 4096-term chunk (measured per launch at B = 64,
+// V = 50257: 16 x 4 251 us with __syncthreads, 4 x 4 295 us, 4 x 16 668 us):
+// a round's latency is set by the per-thread serial work and the barriers,
+// so many threads with few terms each and few rounds per pass win
+constexpr int kSsThreads = 1024, kSsPer = 4, kSsChunk = kSsThreads * kSsPer;
+constexpr unsigned kSsSat = 1u << 30;  // saturation of the integer prefix
+constexpr int kSsNone = 0x7fffffff;
+
+struct SsShared {
+    unsigned tot[kSsThreads / 64];
+    int jmin[kSsThreads / 64];
+    int fmin[kSsThreads / 64];
+    float red[kSsThreads / 64];
+    float S;
+    int found;
+};
+
+// workgroup barrier that orders LDS only: the next chunk's global loads stay
+// in flight across it (__syncthreads would wait for them)
+__device__ __forceinline__ void ss_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ unsigned ss_add(unsigned a, unsigned b) { return min(a + b, kSsSat); }
+
+// x >= 0 as M * 2^E (M with the hidden bit; E of the denormal grid below 2^-126)
+__device__ __forceinline__ void ss_split(float x, unsigned& M, int& E) {
+    const unsigned bits = __float_as_uint(x), e8 = bits >> 23;
+    M = (bits & 0x7fffffu) | (e8 ? 0x800000u : 0u);
+    E = (int)max(e8, 1u) - 150;
+}
+
+// a rounded to the multiples of 2^gexp, in units of 2^gexp; brk on a tie or a
+// term of 2^8 units or more (it leaves the binade anyway)
+__device__ __forceinline__ unsigned ss_quant(float a, int gexp, bool& brk) {
+    unsigned M;
+    int E;
+    ss_split(a, M, E);
+    if (M == 0) return 0;
+    const int s = E - gexp;
+    if (s >= 0) {
+        if (s >= 8) {
+            brk = true;
+            return 0;
+        }
+        return M << s;
+    }
+    const int sh = -s;
+    if (sh >= 25) return 0;  // a < u/2
+    const unsigned half = 1u << (sh - 1), r = M & ((1u << sh) - 1u);
+    unsigned k = M >> sh;
+    if (r > half) k += 1;
+    else if (r == half) brk = true;
+    return k;
+}
+
+// the first lane's value among lanes with v != kSsNone (lanes run in index
+// order, so this is the wave's minimum index): a ballot and a scalar read
+__device__ __forceinline__ int ss_wave_first(int v) {
+    const unsigned long long bal = __ballot(v != kSsNone);
+    return bal ? __builtin_amdgcn_readlane(v, __ffsll((long long)bal) - 1) : kSsNone;
+}
+
+// inclusive saturating wave64 scan on DPP (row_shr 1/2/4/8, row_bcast 15/31):
+// VALU lane moves, no LDS round trips
+template <int CTRL, int ROWS>
+__device__ __forceinline__ unsigned ss_dpp(unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
+}
+__device__ __forceinline__ unsigned ss_wave_scan(unsigned v) {
+    v = ss_add(v, ss_dpp<0x111, 0xf>(v));
+    v = ss_add(v, ss_dpp<0x112, 0xf>(v));
+    v = ss_add(v, ss_dpp<0x114, 0xf>(v));
+    v = ss_add(v, ss_dpp<0x118, 0xf>(v));
+    v = ss_add(v, ss_dpp<0x142, 0xa>(v));
+    v = ss_add(v, ss_dpp<0x143, 0xc>(v));
+    return v;
+}
+
+// One chunk of kSsChunk terms a[] (thread t holds terms 4t..4t+3) added to S
+// in index order.  CDF: also stop at the first term whose running sum exceeds
+// coin (returns true, pick = its index).  Uniform over the block.
+template <bool CDF>
+__device__ bool ss_chunk(const float (&a)[kSsPer], int base, int n, float coin, float& S, int& pick, SsShared& sh) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    int start = 0;
+    while (start < n) {
+        unsigned M;
+        int gexp;
+        ss_split(S, M, gexp);
+        unsigned inc[kSsPer];
+        bool brk[kSsPer];
+        unsigned run = 0;
+#pragma unroll
+        for (int j = 0; j < kSsPer; ++j) {
+            const int l = t * kSsPer + j;
+            brk[j] = false;
+            const unsigned k = l >= start ? ss_quant(a[j], gexp, brk[j]) : 0u;
+            run = ss_add(run, k);
+            inc[j] = run;
+        }
+        const unsigned wsc = ss_wave_scan(run);                  // inclusive over the wave's threads
+        unsigned pre = ss_dpp<0x138, 0xf>(wsc);                    // wave_shr:1 -> exclusive (lane 0: 0)
+        if (lane == 63) sh.tot[w] = wsc;
+        ss_sync();
+        unsigned tv[kSsThreads / 64];
+#pragma unroll
+        for (int v = 0; v < kSsThreads / 64; ++v) tv[v] = sh.tot[v];
+#pragma unroll
+        for (int v = 0; v < kSsThreads / 64; ++v) pre = ss_add(pre, v < w ? tv[v] : 0u);
+        int myj = kSsNone, myf = kSsNone;
+#pragma unroll
+        for (int j = kSsPer - 1; j >= 0; --j) {
+            const int l = t * kSsPer + j;
+            if (l < start) continue;
+            const unsigned P = M + ss_add(pre, inc[j]);  // < 2^31
+            if (brk[j] || P >= (1u << 24)) myj = l;
+            else if (CDF && l < n && coin < ldexpf((float)P, gexp)) myf = l;
+        }
+        myj = ss_wave_first(myj);
+        myf = ss_wave_first(myf);
+        if (lane == 0) {
+            sh.jmin[w] = myj;
+            sh.fmin[w] = myf;
+        }
+        ss_sync();
+        int jb = kSsNone, fb = kSsNone;
+#pragma unroll
+        for (int v = 0; v < kSsThreads / 64; ++v) {
+            jb = min(jb, sh.jmin[v]);
+            fb = min(fb, sh.fmin[v]);
+        }
+        if (CDF && fb < jb) {  // the cdf crossed the coin inside the exact run
+            pick = base + fb;
+            return true;
+        }
+        const int last = jb == kSsNone ? n - 1 : jb;
+        if (t == last / kSsPer) {
+            const int j = last % kSsPer;
+            if (jb == kSsNone) {
+                sh.S = ldexpf((float)(M + ss_add(pre, inc[j])), gexp);
+                sh.found = 0;
+            } else {  // the breaking term: one fp32 addition on the exact sum before it
+                const unsigned Pb = M + (j ? ss_add(pre, inc[j - 1]) : pre);
+                const float Sn = ldexpf((float)Pb, gexp) + a[j];
+                sh.S = Sn;
+                sh.found = CDF && coin < Sn;
+            }
+        }
+        ss_sync();
+        S = sh.S;
+        if (CDF && sh.found) {
+            pick = base + jb;
+            return true;
+        }
+        start = last + 1;
+    }
+    return false;
+}
+
+__device__ __forceinline__ void ss_load(const float* lg, int V, int base, float (&x)[kSsPer]) {
+#pragma unroll
+    for (int j = 0; j < kSsPer; ++j) {
+        const int i = base + threadIdx.x * kSsPer + j;
+        x[j] = i < V ? lg[i] : 0.f;
+    }
+}
+
+__global__ __launch_bounds__(kSsThreads) void sample_scan_kernel(const float* __restrict__ logits, int V,
+                                                                 unsigned long long* __restrict__ state,
+                                                                 int* __restrict__ next, int* __restrict__ tokens,
+                                                                 int* __restrict__ pos, const int* __restrict__ active) {
+    __shared__ SsShared sh;
+    const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (active && active[b] <= 0) return;  // row left as it is (its RNG state too)
+    const float* lg = logits + (size_t)b * V;
+    float mx = -10000.0f;  // maxval as the reference (exact in any order)
+    for (int i = t; i < V; i += kSsThreads) mx = fmaxf(mx, lg[i]);
+    mx = hpa::wave_max(mx);
+    if (lane == 0) sh.red[w] = mx;
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < kSsThreads / 64; ++v) mx = fmaxf(mx, sh.red[v]);
+    float a[kSsPer];
+    int pick = -1;
+    // pass 1: sum += expf(x - maxval)
+    float S = 0.f, x[kSsPer];
+    ss_load(lg, V, 0, x);
+    for (int base = 0; base < V; base += kSsChunk) {
+#pragma unroll
+        for (int j = 0; j < kSsPer; ++j) a[j] = base + t * kSsPer + j < V ? expf(x[j] - mx) : 0.f;
+        ss_load(lg, V, base + kSsChunk, x);  // next chunk in flight during this one's scan
+        ss_chunk<false>(a, base, min(kSsChunk, V - base), 0.f, S, pick, sh);
+    }
+    const float sum = S;
+    // pass 2: cdf += expf(x - maxval) / sum; first i with coin < cdf
+    unsigned long long st = state[b];
+    const float coin = (xorshift_u32(st) >> 8) / 16777216.0f;
+    S = 0.f;
+    ss_load(lg, V, 0, x);
+    for (int base = 0; base < V; base += kSsChunk) {
+#pragma unroll
+        for (int j = 0; j < kSsPer; ++j) a[j] = base + t * kSsPer + j < V ? expf(x[j] - mx) / sum : 0.f;
+        ss_load(lg, V, base + kSsChunk, x);
+        if (ss_chunk<true>(a, base, min(kSsChunk, V - base), coin, S, pick, sh)) break;
+    }
+    if (pick < 0) pick = V - 1;  // sample_mult's "rounding errors" return
+    if (t == 0) {
+        state[b] = st;
+        next[b] = pick;
+        if (tokens) tokens[b] = pick;
+        if (pos) pos[b] += 1;
+    }
+}
+
 inline dim3 xcd_grid(FG& p, int gx, int gy) {
     p.gx = gx;
     p.gy = gy;
@@ -651,6 +877,14 @@ int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const fl
 int hpa_sample_final(const float* logits, int B, int V, unsigned long long* state, int* next, int* tokens,
                      int* pos, const int* active) {
     HPA_REQUIRE(logits && state && next && B > 0 && V > 0, "sample_final: bad arguments");
+    sample_scan_kernel<<<B, kSsThreads, 0, hpa_stream()>>>(logits, V, state, next, tokens, pos, active);
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+int hpa_sample_final_serial(const float* logits, int B, int V, unsigned long long* state, int* next, int* tokens,
+                            int* pos, const int* active) {
+    HPA_REQUIRE(logits && state && next && B > 0 && V > 0, "sample_final_serial: bad arguments");
     sample_final_kernel<<<B, 128, 0, hpa_stream()>>>(logits, V, state, next, tokens, pos, active);
     HPA_LAUNCH_CHECK();
     return 0;

@@ -243,6 +243,8 @@ def lib():
     _sig(L, "hpa_fused_pick_f32_ares", i, [i, i, i, _I])
     _sig(L, "hpa_embed_frag", i, [v, v, v, v, v, v, i, i])
     _sig(L, "hpa_argmax_final", i, [v, i, i, i, v, v, v, v])
+    _sig(L, "hpa_sample_final", i, [v, i, i, v, v, v, v, v])
+    _sig(L, "hpa_sample_final_serial", i, [v, i, i, v, v, v, v, v])
     _sig(L, "hpa_paged_attention_decode_frag", i, [v, P, i, v, i, v, v, i])
     _sig(L, "gpt2_decode_set_positions", i, [v, _I])
     _sig(L, "gpt2_decode_logits", v, [v])
