@@ -343,7 +343,8 @@ __global__ __launch_bounds__(128) void sample_final_kernel(const float* __restri
 // breaks the segment when its rounding is a tie (the result's parity decides
 // it), when it is too large for the grid, or when the sum leaves the binade;
 // that one addition is done in fp32 on the exact S before it, and the scan
-// resumes with the new grid.  Breaks are rare: about one per binade of the sum
+// resumes with the new grid.  Breaks are rare past the first chunk (which one
+// lane sums in order, ss_serial): about one per binade of the sum
 // plus ties, whose odds fall as 1/i.  (softmax_forward :259-286, sample_mult
 // :837-848 order.)
 // 16 waves x 4 terms per 4096-term chunk (measured per launch at B = 64,
@@ -361,6 +362,7 @@ struct SsShared {
     float red[kSsThreads / 64];
     float S;
     int found;
+    __attribute__((aligned(16))) float buf[kSsChunk];  // the first chunk's terms for the serial lane
 };
 
 // workgroup barrier that orders LDS only: the next chunk's global loads stay
@@ -504,6 +506,46 @@ __device__ bool ss_chunk(const float (&a)[kSsPer], int base, int n, float coin, 
     return false;
 }
 
+// The first chunk holds most breaks (tie odds fall as 1/i, the sum crosses
+// binades at i ~ 2^k), so one lane adds it in order, as the serial kernel
+// does (64 adds per cdf test, the crossing batch replayed).
+template <bool CDF>
+__device__ bool ss_serial(const float (&a)[kSsPer], int n, float coin, float& S, int& pick, SsShared& sh) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < kSsPer; ++j) sh.buf[t * kSsPer + j] = a[j];  // +0 beyond n
+    ss_sync();
+    if (t == 0) {
+        float s = S;
+        int f = -1;
+        if (!CDF) s = samp_chain(sh.buf, (n + 63) / 64, s);
+        else
+            for (int q0 = 0; q0 < n; q0 += 64) {
+                const float c0 = s;
+                s = samp_chain(sh.buf + q0, 1, s);
+                if (coin < s) {
+                    float c = c0;
+                    int k = q0;
+                    for (; k < q0 + 63; ++k) {
+                        c += sh.buf[k];
+                        if (coin < c) break;
+                    }
+                    f = k;
+                    break;
+                }
+            }
+        sh.S = s;
+        sh.found = f;
+    }
+    ss_sync();
+    S = sh.S;
+    if (CDF && sh.found >= 0) {
+        pick = sh.found;
+        return true;
+    }
+    return false;
+}
+
 __device__ __forceinline__ void ss_load(const float* lg, int V, int base, float (&x)[kSsPer]) {
 #pragma unroll
     for (int j = 0; j < kSsPer; ++j) {
@@ -536,7 +578,8 @@ __global__ __launch_bounds__(kSsThreads) void sample_scan_kernel(const float* __
 #pragma unroll
         for (int j = 0; j < kSsPer; ++j) a[j] = base + t * kSsPer + j < V ? expf(x[j] - mx) : 0.f;
         ss_load(lg, V, base + kSsChunk, x);  // next chunk in flight during this one's scan
-        ss_chunk<false>(a, base, min(kSsChunk, V - base), 0.f, S, pick, sh);
+        if (base == 0) ss_serial<false>(a, min(kSsChunk, V), 0.f, S, pick, sh);
+        else ss_chunk<false>(a, base, min(kSsChunk, V - base), 0.f, S, pick, sh);
     }
     const float sum = S;
     // pass 2: cdf += expf(x - maxval) / sum; first i with coin < cdf
@@ -548,7 +591,9 @@ __global__ __launch_bounds__(kSsThreads) void sample_scan_kernel(const float* __
 #pragma unroll
         for (int j = 0; j < kSsPer; ++j) a[j] = base + t * kSsPer + j < V ? expf(x[j] - mx) / sum : 0.f;
         ss_load(lg, V, base + kSsChunk, x);
-        if (ss_chunk<true>(a, base, min(kSsChunk, V - base), coin, S, pick, sh)) break;
+        if (base == 0 ? ss_serial<true>(a, min(kSsChunk, V), coin, S, pick, sh)
+                      : ss_chunk<true>(a, base, min(kSsChunk, V - base), coin, S, pick, sh))
+            break;
     }
     if (pick < 0) pick = V - 1;  // sample_mult's "rounding errors" return
     if (t == 0) {
