@@ -3,29 +3,33 @@
 
 Metric (BASELINE.json): decode tokens/sec, GPT-2 124M paged attention,
 B=64, ctx 1024, page 16, fp32, on 1/2/4/8 MI355X (configs[1] at N=1).  For
-N>1 the decode shards by sequence (SURVEY.md 8e, configs[3]): every rank
-decodes its own 64 sequences out of its own page pool with replicated
-weights -> weak scaling; the one collective is the end-of-step RCCL gather
-of the logits to rank 0 (--gather ids: greedy ids only), double-buffered on
-its own stream so that step k's gather overlaps step k+1.  --scaling strong
-splits a fixed global batch instead.
+N>1 the decode shards by sequence: the metric's B = 64 is
+split over the ranks (strong scaling, the default), each rank decoding its
+share from its own page pool with replicated weights; --scaling weak keeps 64
+sequences per GPU (BASELINE configs[3]: B = 512 at 8 GPUs).  The one
+collective is the end-of-step gather of the logits to rank 0 (--gather ids:
+the greedy ids only), run by the C library over RCCL/xGMI
+(gpt2_decode_gather: double-buffered on its own stream, so step k's gather
+overlaps step k+1).  torch.distributed (gloo) is only the launcher's
+rendezvous: the RCCL id exchange, barriers and the max-over-ranks time.
 
 One "step" = one decode step of the whole batch: every sequence gets one new
-token at its absolute position, all 12 layers (LN, QKV + KV append into the
-HBM page pool, paged attention over 0..pos through the block table,
-projections, MLP, residuals), final LN, logits (B x 50257), greedy argmax.
-The KV cache is prefilled to ctx - (warmup + steps) positions with synthetic
-K/V (default; --prefill real runs the one-pass prefill -- B*T-row GEMMs and
-the causal multi-query attention on MFMA -- and reports its throughput too;
---prefill decode runs token-by-token decode steps instead); the timed
-steps then decode at positions up to ctx - 1.  Weights are seeded synthetic
-GPT-2 124M (no checkpoints offline).
+token at its absolute position, all layers (QKV + KV append into the HBM page
+pool, paged attention over 0..pos through the block table, projections, MLP,
+residuals, LayerNorms), final LN, logits (B x 50257), greedy argmax.  The KV
+cache is prefilled to ctx - (warmup + steps + 1) positions with synthetic K/V
+(default; --prefill real runs the one-pass prefill -- B*T-row GEMMs and the
+causal multi-query attention on MFMA -- and reports its throughput too;
+--prefill decode runs token-by-token decode steps instead); the timed steps
+then decode at positions up to ctx - 1.  Weights are seeded synthetic GPT-2
+(no checkpoints offline).
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 Rank 0 prints ONE JSON line.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -42,10 +46,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 def pmc_traffic(kernel_prefix, batch_per_gpu, ctx, page_size, dtype):
     """HBM bytes per launch of the dominant kernel from a committed PMC
-    summary (tools/pmc_traffic.sh -> profiles/r1/pmc_traffic*.json) taken on
-    this workload; (None, None) when there is none"""
+    summary (tools/pmc_traffic.sh -> profiles/rNN/pmc_traffic*.json) taken on
+    this workload, newest round first; (None, None) when there is none"""
     import glob
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r1", "pmc_traffic*.json"))):
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_traffic*.json")), reverse=True)
+    for path in paths:
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
@@ -56,7 +61,8 @@ def pmc_traffic(kernel_prefix, batch_per_gpu, ctx, page_size, dtype):
             continue
         for name, k in d["kernels"].items():
             if name.startswith(kernel_prefix):
-                return k["hbm_bytes"], f"profiles/r1/{os.path.basename(path)}: {name}, {k['launches']} launches"
+                rel = os.path.relpath(path, REPO)
+                return k["hbm_bytes"], f"{rel}: {name}, {k['launches']} launches"
     return None, None
 
 
@@ -66,8 +72,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64,
-                    help="sequences per GPU (weak scaling) or in total (--scaling strong)")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+                    help="sequences in total (--scaling strong, the metric's B=64) or per GPU (weak)")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     ap.add_argument("--ctx", type=int, default=1024)
     ap.add_argument("--page-size", type=int, default=16)
     ap.add_argument("--kv-dtype", default="f32", choices=["f32", "bf16"],
@@ -84,15 +90,9 @@ def parse():
     ap.add_argument("--prof-steps", type=int, default=4,
                     help="attention roofline timing: prof_steps x L back-to-back launches (0 = off)")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="per CPU build (strict and -Ofast)")
     ap.add_argument("--attn-waves", type=int, default=4)
-    ap.add_argument("--unfused", action="store_true", help="row-major GEMMs + separate row kernels")
-    ap.add_argument("--lanes", type=int, default=1, help="micro-batch lanes (concurrent row groups)")
-    ap.add_argument("--pipeline", type=int, default=0, help="1: two lanes, attention chunks beside GEMMs")
-    ap.add_argument("--overlap", type=int, default=0,
-                    help="overlapped step: chain workgroups beside the attention (0 = off)")
-    ap.add_argument("--split", type=int, default=0,
-                    help="split step: GEMM chains on this many CUs beside the attention (0 = off)")
+    ap.add_argument("--attn-splits", type=int, default=0, help="attention context ranges (0 = by shape)")
     ap.add_argument("--sample", action="store_true",
                     help="multinomial sampling as the reference driver (default: greedy argmax)")
     ap.add_argument("--gemm-waves", default="", help="fused GEMM waves qkv,attproj,fc,fcproj,logits (0 = auto)")
@@ -101,30 +101,19 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(cfgd, B, P, ctx, budget_s, kv_bf16=False, w_bf16=False):
-    """The oracle's OpenMP C restatement of the same paged decode, timed on the
-    host cores on a bounded sample (rank 0, N=1).  Test infrastructure only."""
+def cpu_baseline(cfgd, B, P, start_ctx, end_ctx, budget_s, kv_bf16=False, w_bf16=False):
+    """The oracle's OpenMP C restatement of the same paged decode, timed on
+    every host core this process may use, at the GPU's positions: once per
+    build (-O2 -fno-fast-math strict, -O3 -Ofast), each a bounded sample.
+    Rank 0, N=1.  Test infrastructure only (never the measured product)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle_ctypes as oc
     import pagedattn
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    affinity = len(os.sched_getaffinity(0))
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or affinity
     os.environ["OMP_NUM_THREADS"] = str(threads)
     params = pagedattn.synthetic_params(cfgd, seed=1337)
     c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
-    dec = oc.PagedDecoder(params, c, B, P, cfgd["maxT"], page_seed=3, fast=True, kv_bf16=kv_bf16, w_bf16=w_bf16)
-    max_steps = min(256, ctx // 2)  # the budget normally ends the sample first (near ctx)
-    start_ctx = ctx - max_steps
-    dec.fill_random(start_ctx, seed=5)
-    rng = np.random.default_rng(0)
-    tok = rng.integers(0, cfgd["V"], B).astype(np.int32)
-    steps, t0 = 0, time.perf_counter()
-    while True:
-        tok, _ = dec.step(tok, want_logits=False)
-        steps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or steps >= max_steps:
-            break
-    dec.close()
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -134,10 +123,32 @@ def cpu_baseline(cfgd, B, P, ctx, budget_s, kv_bf16=False, w_bf16=False):
                     break
     except OSError:
         pass
-    return {"value": B * steps / el, "unit": "tokens/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/liboracle_fast.so (-O3 -Ofast OpenMP C restatement), GPT-2 124M fp32"
-                      f"{' (bf16 KV)' if kv_bf16 else ''}{' (bf16-rounded weights and GEMM inputs)' if w_bf16 else ''}, B={B}, page {P}, {steps} decode steps at ctx "
-                      f"{start_ctx}..{start_ctx + steps} after a synthetic K/V fill, {el:.1f} s; cpu: {cpu_model}"}
+    runs = []
+    for fast, build in ((False, "-O2 -fno-fast-math -ffp-contract=off (liboracle.so)"),
+                        (True, "-O3 -Ofast -march=x86-64-v3 (liboracle_fast.so)")):
+        dec = oc.PagedDecoder(params, c, B, P, cfgd["maxT"], page_seed=3, fast=fast, kv_bf16=kv_bf16,
+                              w_bf16=w_bf16)
+        dec.fill_random(start_ctx, seed=5)
+        tok = np.random.default_rng(0).integers(0, cfgd["V"], B).astype(np.int32)
+        steps, t0 = 0, time.perf_counter()
+        while start_ctx + steps < end_ctx:
+            tok, _ = dec.step(tok, want_logits=False)
+            steps += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s:
+                break
+        dec.close()
+        runs.append({"build": build, "value": round(B * steps / el, 2), "steps": steps,
+                     "positions": f"{start_ctx}..{start_ctx + steps - 1}", "seconds": round(el, 2)})
+    return {"value": runs[1]["value"], "unit": "tokens/s", "cores": threads, "kind": "port",
+            "nproc": os.cpu_count(), "affinity_cores": affinity,
+            "sample": f"oracle/ C restatement of the same paged decode (OpenMP, {threads} threads = the cores "
+                      f"this process may use; nproc {os.cpu_count()}), GPT-2 124M"
+                      f"{' bf16-rounded weights and GEMM inputs' if w_bf16 else ' fp32'}"
+                      f"{' (bf16 KV)' if kv_bf16 else ''}, B={B}, page {P}, decode steps at the GPU's positions "
+                      f"after a synthetic K/V fill, <= {budget_s:.0f} s per build; value = the -Ofast build; "
+                      f"cpu: {cpu_model}",
+            "builds": runs}
 
 
 def main():
@@ -147,24 +158,23 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and args.gpus != world:
         args.gpus = world
-    import torch
     dist = None
-    if world > 1:
+    if world > 1:  # rendezvous only; the data path's collective is RCCL in the C library
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist.init_process_group("gloo")
     import pagedattn
     import shard
     L = pagedattn.lib()
     pagedattn.init(local_rank)
-    if torch.cuda.is_available():
-        torch.cuda.set_device(local_rank)
-        # one non-default stream shared by the library and torch: the decode
-        # kernels, the id copy and the RCCL gather are ordered on it, and it
-        # can be captured into a hipGraph (the legacy null stream cannot)
-        stream = torch.cuda.Stream()
-        torch.cuda.set_stream(stream)
-        L.hpa_set_stream(stream.cuda_stream)
+    if world > 1 and args.gather != "none":
+        n = L.hpa_comm_id_bytes()
+        uid = ctypes.create_string_buffer(n)
+        if rank == 0:
+            pagedattn.check(L.hpa_comm_unique_id(uid, n), "comm_unique_id")
+        obj = [uid.raw]
+        dist.broadcast_object_list(obj, src=0)
+        uid = ctypes.create_string_buffer(obj[0], n)
+        pagedattn.check(L.hpa_comm_init(world, rank, uid), "comm_init (RCCL)")
     pagedattn.check(L.hpa_set_attention_waves(args.attn_waves), "attention waves")
 
     cfgd = dict(pagedattn.GPT2_124M if args.model == "124M" else pagedattn.GPT2_XL)
@@ -180,18 +190,15 @@ def main():
     ctx = min(args.ctx, cfgd["maxT"])
     need = args.warmup + args.steps + 1
     window = min(need, ctx // 2)
-    start = ctx - window  # positions of the first decoded token
+    start = ctx - window  # position of the first decoded token
 
     model = pagedattn.Model(cfgd, seed=1337)
     model.decode_init(B_local, P, ctx, kv_dtype=pagedattn.HPA_BF16 if kv_bf16 else pagedattn.HPA_F32,
                       w_dtype=pagedattn.HPA_BF16 if w_bf16 else pagedattn.HPA_F32)
-    model.set_fused(not args.unfused)
-    if not args.unfused:
-        model.set_lanes(args.lanes)
-        if args.pipeline:
-            model.set_pipeline(True)
+    if args.attn_splits:
+        model.set_attn_splits(args.attn_splits)
     if args.sample:
-        model.set_sampling(True, seed=1337 + rank * B_local)
+        model.set_sampling(True, seed=1337 + lo)
     if args.gemm_waves or args.gemm_rows or args.gemm_cols:
         ints = lambda a: [int(x) for x in a.split(",")] if a else None  # noqa: E731
         model.gemm_config(ints(args.gemm_waves), ints(args.gemm_rows), ints(args.gemm_cols))
@@ -214,25 +221,15 @@ def main():
                          "tokens_per_s": round(B_local * start / el, 1), "chunk": args.prefill_chunk,
                          "note": "one-pass prefill of positions 0..start-1, rank 0, not part of value"}
     else:
-        for p in range(start):
+        for _ in range(start):
             model.step(rng.integers(0, cfgd["V"], B_local).astype(np.int32), want_next=False)
-    if args.split and not args.unfused:
-        model.set_split(args.split)
-    if args.overlap and not args.unfused:
-        model.set_overlap(args.overlap)
     model.set_graph(not args.no_graph)
+    gather = world > 1 and args.gather != "none"
+    if gather:
+        model.shard(counts, root=0)
+    what = 0 if args.gather == "logits" else 1
     first = rng.integers(0, cfgd["V"], B_local).astype(np.int32)
     pos_now = [start]
-
-    gather = None
-    nstep = [0]
-    if world > 1 and args.gather != "none":
-        # double-buffered: step k's output is copied on the compute stream,
-        # then gathered on a comm stream while step k+1 computes
-        gather = shard.StepGather(dist, world, rank, counts, cfgd["V"], args.gather, "cuda", nbuf=2)
-        comm = torch.cuda.Stream()
-        src, nbytes = ((model.logits_ptr(), B_local * cfgd["V"] * 4) if args.gather == "logits"
-                       else (model.next_ptr(), B_local * 4))
 
     def one_step(tokens=None):
         if pos_now[0] >= ctx:  # slide back: pages kept, positions rewritten
@@ -240,18 +237,11 @@ def main():
             pos_now[0] = start
         model.step_async(tokens)
         pos_now[0] += 1
-        if gather is not None:
-            i = nstep[0] % 2
-            gather.wait(i)  # the compute stream waits for the gather that last used buffer i
-            L.hpa_memcpy_async(gather.buffer(i).data_ptr(), src, nbytes)  # compute stream
-            comm.wait_stream(stream)
-            with torch.cuda.stream(comm):  # RCCL gather to rank 0, overlapped with the next step
-                gather.gather(i, async_op=True)
-        nstep[0] += 1
+        if gather:
+            model.gather(what)  # RCCL gather to rank 0 on the comm stream, overlapped with the next step
 
-    def sync():
-        pagedattn.check(L.hpa_synchronize(), "sync")
-        torch.cuda.synchronize()
+    def sync():  # every stream of the device: the decode stream and the comm stream
+        pagedattn.check(L.hpa_device_synchronize(), "device sync")
 
     one_step(first)
     for _ in range(args.warmup - 1 if args.warmup > 0 else 0):
@@ -268,10 +258,11 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    bytes_after, attn_after = model.step_bytes()
+    bytes_after, _ = model.step_bytes()
     elapsed = t1 - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
@@ -287,7 +278,6 @@ def main():
         attn = dict(avg_ms=avg_ms, launches=iters, per_launch_bytes=per_launch_bytes,
                     achieved=per_launch_bytes / (avg_ms * 1e-3) / 1e9)
 
-    result = None
     if rank == 0:
         cpu = None
         want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
@@ -296,23 +286,27 @@ def main():
                 # bounded sample: the oracle keeps an fp32 pool of B*ctx*C*L*2 floats, so
                 # beyond config 2's B*ctx the sample takes a subset of the sequences
                 cpu_B = B_local if B_local * ctx <= 65536 else max(1, 16384 // ctx)
-                cpu = cpu_baseline(cfgd, cpu_B, P, ctx, args.cpu_seconds, kv_bf16, w_bf16)
+                cpu = cpu_baseline(cfgd, cpu_B, P, start, ctx, args.cpu_seconds, kv_bf16, w_bf16)
                 if cpu_B != B_local:
                     cpu["sample"] += f" (a {cpu_B}-sequence subset of the {B_local}-sequence batch)"
             except Exception as e:  # reported, never fatal for the GPU number
                 cpu = {"value": None, "error": repr(e)}
         name, cus, mem = pagedattn.device_info()
+        splits = model.attn_splits()
         roof = None
         if attn:
-            traffic, tsrc = pmc_traffic("paged_attn_decode_f32", B_local, ctx, P,
-                                        "fp32 (bf16 KV storage)" if kv_bf16 else "fp32")
-            roof = {"bound": "hbm", "kernel": "paged_attn_decode_f32" + ("<bf16 KV>" if kv_bf16 else ""),
+            kname = "paged_attn_decode_f32"
+            traffic, tsrc = pmc_traffic(kname, B_local, ctx, P, "fp32 (bf16 KV storage)" if kv_bf16 else "fp32")
+            roof = {"bound": "hbm", "kernel": kname + ("<bf16 KV>" if kv_bf16 else "")
+                    + (f" ({splits} context ranges per sequence-head)" if splits > 1 else ""),
                     "achieved": round(attn["achieved"], 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(attn["achieved"] / HBM_PEAK_GBS, 4),
                     "traffic": None if traffic is None else int(traffic),
                     "traffic_source": tsrc, "avg_launch_ms": round(attn["avg_ms"], 5),
                     "bytes_per_launch": int(attn["per_launch_bytes"]), "launches_timed": attn["launches"]}
         step_bytes = 0.5 * (bytes_before + bytes_after)
+        which = ("configs[4]" if kv_bf16 else "configs[2]" if args.model == "XL" else
+                 "configs[1]" if world == 1 or args.scaling == "strong" else "configs[3]: per-seq sharded pool")
         result = {
             "metric": METRIC,
             "value": round(tokens_per_s, 1),
@@ -326,23 +320,19 @@ def main():
             "vs_baseline": None,
             "dtype": ("bf16 weights and GEMM inputs, fp32 accumulate" if w_bf16 else "fp32")
                      + (" (bf16 KV storage)" if kv_bf16 else ""),
-            "data": "synthetic (seeded random GPT-2 124M weights and tokens; KV prefill: "
+            "data": f"synthetic (seeded random GPT-2 {args.model} weights and tokens; KV prefill: "
                     + {"synthetic": "synthetic U(-1,1)", "real": "one-pass prefill of random tokens",
                        "decode": "decode steps"}[args.prefill] + ")",
-            "config": {"workload": f"GPT-2 {args.model} {'bf16' if w_bf16 else 'fp32'} paged decode, batch={B_local} per GPU x {world} "
-                                   f"(B={B}), ctx {ctx}, page_size={P}{', bf16 KV' if kv_bf16 else ''}"
-                                   f"{', bf16 weights' if w_bf16 else ''} (BASELINE.json "
-                                   + ("configs[4])" if kv_bf16 else "configs[2])" if args.model == "XL" else
-                                      "configs[1])" if world == 1 else "configs[3]: per-seq sharded pool)"),
+            "config": {"workload": f"GPT-2 {args.model} {'bf16' if w_bf16 else 'fp32'} paged decode, B={B} "
+                                   f"({B_local} on rank 0 of {world}, {args.scaling} scaling), ctx {ctx}, "
+                                   f"page_size={P}{', bf16 KV' if kv_bf16 else ''}{', bf16 weights' if w_bf16 else ''}"
+                                   f" (BASELINE.json {which})",
                        "global_batch": B, "batch_per_gpu": B_local, "seq_len": ctx, "page_size": P,
                        "decode_positions": f"{start}..{start + args.warmup + args.steps - 1}",
-                       "parallelism": f"seq-shard x{world}" + (f" + RCCL gather({args.gather}) to rank 0, overlapped with the next step"
-                                                               if world > 1 and args.gather != "none" else ""),
-                       "hip_graph": not args.no_graph, "gemm_path": "unfused" if args.unfused else "fused",
-                       "lanes": 1 if args.unfused else L.gpt2_decode_lanes(model.h),
-                       "pipeline": bool(L.gpt2_decode_pipeline(model.h)),
-                       "split_gemm_cus": 0 if args.unfused else L.gpt2_decode_split(model.h),
-                       "overlap_chain_blocks": 0 if args.unfused else L.gpt2_decode_overlap(model.h),
+                       "parallelism": f"seq-shard x{world}" + (f" + RCCL gather({args.gather}) to rank 0 in the C "
+                                                               "library, overlapped with the next step"
+                                                               if gather else ""),
+                       "hip_graph": not args.no_graph, "attn_splits": splits,
                        "token_choice": "multinomial (reference sample_mult)" if args.sample else "greedy",
                        "gemm_waves": [int(x) for x in model.gemm_config()[0]],
                        "gemm_row_blocks": [int(x) for x in model.gemm_config()[1]],
@@ -358,6 +348,8 @@ def main():
         print(json.dumps(result), flush=True)
     model.close()
     if world > 1:
+        if gather:
+            L.hpa_comm_destroy()
         dist.barrier()
         dist.destroy_process_group()
 

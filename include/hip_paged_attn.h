@@ -53,20 +53,17 @@ int   hpa_event_record(void* ev);
 float hpa_event_elapsed_ms(void* start, void* stop); /* syncs on stop */
 int   hpa_event_destroy(void* ev);
 void* hpa_event_create_nt(void);          /* no timing: fork/join ordering only */
-/* extra streams for concurrent work (the decode engine's micro-batch lanes);
+int   hpa_event_synchronize(void* ev);     /* host waits until the work before ev is done */
+/* extra streams for concurrent work (e.g. a communication stream);
  * hpa_stream_wait_event: the CURRENT stream waits for `ev` (recorded on any
  * stream).  Inside a capture, fork/join through events pulls the other
  * stream into the same graph as parallel branches. */
 void* hpa_stream_create(void);
-int   hpa_stream_destroy(void* stream); /* CU-masked streams are cached per range: a no-op for them */
-/* a stream restricted to the CUs of mask bits [lo, hi) (hipExtStreamCreateWithCUMask;
- * bits are dealt round-robin over the XCDs): the decode engine's split step
- * runs attention and the GEMM chains on disjoint CU sets */
-void* hpa_stream_create_cumask(int lo, int hi);
+int   hpa_stream_destroy(void* stream);
 int   hpa_stream_wait_event(void* ev);
 const char* hpa_last_error(void);
 /* hipGraph capture of everything enqueued on the current stream between
- * begin and end (the decode step: ~9 launches per layer); replay with
+ * begin and end (the decode step: 5 launches per layer); replay with
  * hpa_graph_launch.  Kernel arguments are frozen at capture, so per-step
  * state (tokens, positions, block tables) must live in device memory. */
 int   hpa_graph_begin(void);
@@ -116,29 +113,6 @@ size_t hpa_pool_v_index(const HpaKVPool* pool, int layer, int page, int head, in
  * already cached for b); the token's K/V go to slot pos[b] and attention
  * covers positions 0..pos[b]. */
 
-/* residual[b] = wte[tok[b]] + wpe[pos[b]];  ln_out[b] = LN(residual[b])
- * (encoder_forward paged_infer.c:24-47 at absolute positions, fused with
- * layernorm_forward :49-89) */
-int hpa_embed_ln(const int* tokens, const int* pos, const float* wte, const float* wpe,
-                 const float* ln_w, const float* ln_b, float* residual, float* ln_out, int B, int C);
-
-/* out = x[M][K] . W[N][K]^T on fp32 MFMA (v_mfma_f32_32x32x2_f32).
- * splitk == 1: out[m][n] = acc + bias[n] (+GELU when epilogue == HPA_EPI_BIAS_GELU)
- * splitk  > 1: out is a partial-slab array [splitk][M][N] (bias not added);
- *              a row epilogue (below) reduces it.
- * Replaces matmul_forward / matmul_cached for decode rows (paged_infer.c:92-160). */
-enum { HPA_EPI_PARTIAL = 0, HPA_EPI_BIAS = 1, HPA_EPI_BIAS_GELU = 2 };
-int hpa_gemm_f32(const float* x, int ldx, const float* W, const float* bias, float* out, int ldo,
-                 int M, int N, int K, int splitk, int epilogue);
-/* the split-K the library would choose for this shape (deterministic) */
-int hpa_gemm_pick_splitk(int M, int N, int K);
-
-/* QKV epilogue + KV append (add_to_cache paged_infer.c:505-573 fused):
- * qkv = sum_s part[s] + bias; q[b] <- qkv[0:C]; K,V -> pool page
- * block_table[b*bt_stride + pos[b]/P], slot pos[b]%P of `layer`. */
-int hpa_qkv_append(const float* part, int splitk, const float* bias, float* q, const HpaKVPool* pool,
-                   int layer, const int* block_table, int bt_stride, const int* pos, int B, int C);
-
 /* paged decode attention (attention_paged paged_infer.c:163-240 for one
  * query row per sequence at absolute position pos[b]): block-table gather of
  * K/V pages -> q.k^T -> online softmax -> PV.  q, out: [B][C]. */
@@ -146,20 +120,23 @@ int hpa_paged_attention_decode(const float* q, const HpaKVPool* pool, int layer,
                                const int* block_table, int bt_stride, const int* pos, float* out,
                                int B);
 
-/* residual_out = residual_in + bias + sum_s part[s];  ln_out = LN(residual_out)
- * (residual_forward :253-257 + layernorm_forward :49-89 fused).  ln_w may be
- * NULL to skip the LN. */
-int hpa_residual_ln(const float* part, int splitk, const float* bias, const float* residual_in,
-                    float* residual_out, const float* ln_w, const float* ln_b, float* ln_out,
-                    int B, int C);
-
-/* out = GELU(bias + sum_s part[s])  (gelu_forward :243-251) */
-int hpa_bias_gelu(const float* part, int splitk, const float* bias, float* out, int M, int N);
-
-/* greedy token choice (generate_tokens_from_logits :937-951 over logits,
- * lowest index wins ties); writes next[b], tokens[b] = next[b] (feeds the
- * next step's embedding) and advances pos[b] += 1.  tokens/pos may be NULL. */
-int hpa_argmax_advance(const float* logits, int B, int V, int* next, int* tokens, int* pos);
+/* split-context (flash-decoding) form: each (sequence, head)'s context is cut
+ * into `splits` (1..HPA_ATTN_MAX_SPLITS) ranges of 64-token tiles, one
+ * workgroup each; the last range to finish merges the ranges' (max, sum,
+ * acc) in range order (so the result does not depend on timing) and writes
+ * out[b] -- row-major [B][C] or, out_frag != 0, the frag layout.  ws:
+ * hpa_attn_ws_bytes(B, NH, splits) bytes of device memory whose counter part
+ * is zero before the first launch (hpa_memset_async the whole buffer once;
+ * every launch leaves it zero).  splits = 1 is the single-pass kernel above
+ * (ws may be NULL).  Within fp32 rounding of the single pass (another
+ * summation grouping), bit-identical across launches for a given splits. */
+#define HPA_ATTN_MAX_SPLITS 16
+size_t hpa_attn_ws_bytes(int B, int num_heads, int splits);
+/* the engine's choice: ~3 workgroups per CU (num_cus <= 0: 256), by shape only */
+int hpa_attn_pick_splits(int B, int num_heads, int max_ctx, int num_cus);
+int hpa_paged_attention_decode_split(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
+                                     int bt_stride, const int* pos, float* out, int B, int splits, void* ws,
+                                     int out_frag);
 
 /* synthetic K/V fill of positions [0, ctx) for every sequence with U(-1,1)
  * from a counter-based hash (attention microbench / bench synthetic prefill) */
@@ -222,12 +199,11 @@ typedef struct {
     int row_blocks;       /* 16-row blocks per workgroup: 1, 2 or 4; 0 = by shape */
     int variant;          /* 0 = by shape; 1 = looped (two trips in flight);
                              2 = one-shot (every operand load issued up front; one
-                             row block; (waves, K/16) in {(4,48),(8,48),(16,48),(8,192),(16,192)});
-                             3 = looped with larger trips (same results as 1);
+                             row block; (waves, K/16) in {(4,48),(8,48),(16,48),(8,192),(16,192),(10,100)});
                              4 = LOGITS only: activation-resident persistent kernel
                              (K = 768, rows <= 64; 16 waves; else as 1);
-                             5 = A-resident kernel (col_tiles = rounds; fp32: K <= 1600,
-                             bf16: K <= 3200) */
+                             5 = bf16 weights only: A-resident kernel (col_tiles = rounds,
+                             K <= 3200) */
     int col_tiles;        /* 16-column tiles per workgroup: 1; 2 (waves 4/8, row_blocks
                              2/4); 4 (waves 4, row_blocks 4); 0 = by shape.  A hint:
                              where M's row blocks or the waves cannot carry it, 1 */
@@ -241,26 +217,12 @@ typedef struct {
                              the workgroup already holds (K = the LN width).  No LN
                              prologue and no statistics loads; ln_stats, ln_w and
                              ln_b are not read. */
-    int k_slices;         /* K split over this many workgroups per output tile (looped
-                             kernel only; 0/1 = none): each slice folds its waves,
-                             publishes the tile as a write-through slab, and the last
-                             arriver sums the slabs in slice order and runs the
-                             epilogue (cdna_hip_programming.md "In-launch split-K
-                             reduction").  A row's summation order depends on
-                             (waves, k_slices), never on M or the arrival order. */
-    float* ks_slab;       /* k_slices > 1: workspace, hpa_fused_ks_workspace floats */
-    int* ks_count;        /* k_slices > 1: per-tile counters, zero before the first launch
-                             (every launch leaves them zero) */
     int w_dtype;          /* HPA_F32 (0): w is fp32 frag layout.  HPA_BF16: w points at bf16
                              weights in the bf16 frag layout (hpa_pack_frag_bf16), K % 32 == 0;
                              A is rounded to bf16 (RNE) after the LayerNorm, products are
-                             summed in fp32 on v_mfma_f32_16x16x32_bf16.  Looped kernel
-                             only (variant, k_slices and ln_fold_c1 must be 0); waves 4/8. */
+                             summed in fp32 on v_mfma_f32_16x16x32_bf16 (variant 0, 1
+                             or 5; ln_fold_c1 must be NULL); waves 4/8. */
 } HpaFusedGemm;
-/* the K slices the engine uses for a shape (1 = none; by shape, never by M) */
-int hpa_fused_pick_slices(int M, int N, int K);
-/* workspace of g's k_slices launch: slab floats and counters (0 when no split) */
-int hpa_fused_ks_workspace(const HpaFusedGemm* g, size_t* slab_floats, size_t* counters);
 /* LayerNorm folding for hpa_gemm_fused (layernorm_forward :49-89 followed by
  * matmul_forward :92-114, restated): for W [N][K] row-major (device), writes
  * dst_frag = frag-packed W[n][k]*ln_w[k], c1[n] = sum_k of those products and
@@ -286,10 +248,6 @@ void hpa_fused_pick_bf16(int M, int N, int K, int* out3);
  * tiles over the whole K; col_tiles = rounds for this variant):
  * out3 = {waves, row_blocks, rounds}; returns 1 where variant 0 uses it */
 int hpa_fused_pick_bf16_ares(int M, int N, int K, int* out3);
-/* fp32 weights, A-resident kernel (variant 5; row_blocks 2 for K <= 768, 1 for
- * K <= 1600): out3 = {waves, row_blocks, rounds}; returns 1 where variant 0
- * uses it (by N, K only) */
-int hpa_fused_pick_f32_ares(int M, int N, int K, int* out3);
 int hpa_fused_pick_waves(int M, int N, int K);
 /* residual = wte[tok] + wpe[pos] in frag layout [Mp][C], stats (1 tile) */
 int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const float* wpe,
@@ -337,37 +295,22 @@ int hpa_paged_attention_prefill_ragged(const float* q, const HpaKVPool* pool, in
 int hpa_gather_rows_frag(const float* src, const float* src_stats, int src_Mp, const int* rows, int n,
                          float* dst, float* dst_stats, int dst_Mp, int C);
 
-/* ---------------- pipelined decode: attention chunk + GEMM in ONE launch ----------------
- * Chunk `chunk` of `nchunks` of the decode attention of B sequences (each
- * sequence's 64-token tiles split evenly; the online-softmax state (m, l, acc)
- * is carried between chunks in `state`, hpa_attn_state_elems floats; the last
- * chunk writes the normalised output in frag layout) runs beside an
- * independent fused GEMM `g` (NULL = none) in one launch: workgroups
- * [0, ceil8(B*NH)) take the attention role, the rest the GEMM role (4 waves,
- * one row block and one column tile per workgroup; one-shot when K = 768).
- * The caller guarantees the two touch disjoint data (different sequences). */
-typedef struct {
-    const float* q;          /* [B][C] row-major */
-    const HpaKVPool* pool;
-    int layer;
-    const int* block_table;  /* [B][bt_stride] */
-    int bt_stride;
-    const int* pos;          /* [B]: context = pos + 1 */
-    float* state;            /* hpa_attn_state_elems(B, NH) floats, 16-byte aligned */
-    float* out_frag;         /* frag layout [Mp][C] */
-    int B, chunk, nchunks;
-} HpaAttnChunk;
-size_t hpa_attn_state_elems(int B, int num_heads);
-int hpa_attn_chunk_with_gemm(const HpaAttnChunk* a, const HpaFusedGemm* g);
-/* one launch of the overlapped decode step (hpa_lane.hip): the whole paged
- * attention of one micro-batch lane (att, nchunks ignored; NULL = none) and
- * the GEMM chain of the OTHER lane -- chain[0..nph-1] = attproj, fc, fcproj
- * and optionally qkv of the next layer, 4-wave tiles -- on disjoint
- * workgroups.  The chain's links are in-launch hand-offs counted in ctl
- * (HPA_LANE_CTL_WORDS words, zeroed before the launch; ctl[1] != 0 after it
- * reports an expired wait); chain_blocks persistent workgroups run it. */
-#define HPA_LANE_CTL_WORDS 32
-int hpa_lane_layer(const HpaAttnChunk* att, const HpaFusedGemm* chain, int nph, unsigned* ctl, int chain_blocks);
+/* ---------------- multi-GPU: RCCL over xGMI (hpa_comm.hip) ----------------
+ * One process per GPU.  Rank 0 makes the id
+ * (hpa_comm_unique_id), the launcher hands it to every rank (any out-of-band
+ * channel: torch.distributed's store, a file, MPI), and each rank binds its
+ * current device with hpa_comm_init.  The decode engine's end-of-step gather
+ * (gpt2_decode_gather) runs on it. */
+size_t hpa_comm_id_bytes(void);                     /* sizeof(ncclUniqueId) = 128 */
+int    hpa_comm_unique_id(void* id, size_t id_bytes);
+int    hpa_comm_init(int nranks, int rank, const void* id);
+int    hpa_comm_destroy(void);
+int    hpa_comm_size(void);                         /* 0 before hpa_comm_init */
+int    hpa_comm_rank(void);                         /* -1 before hpa_comm_init */
+/* root receives every rank's bytes in rank order (ncclSend/ncclRecv group;
+ * uneven sizes allowed) on `stream` (NULL = the library stream), async */
+int    hpa_comm_gatherv(const void* send, size_t send_bytes, void* recv, const size_t* bytes_per_rank, int root,
+                        void* stream);
 
 /* ---------------- reference-layout kernels (drop-in compat) ----------------
  * Pages in the reference layout: token-major [block_size][C] per page

@@ -155,13 +155,13 @@ float* gpt2_acts_probs(GPT2* model);
  * the page size), otherwise creates one sized B x ceil(max_ctx/page_size). */
 int  gpt2_decode_init(GPT2* model, int B, int page_size, int max_ctx);
 /* the same with the KV pool's storage type: HPA_F32 (0, default) or HPA_BF16
- * (1: BASELINE config 5; page size a multiple of 8; fused path only) */
+ * (1: BASELINE config 5; page size a multiple of 8) */
 int  gpt2_decode_init_ex(GPT2* model, int B, int page_size, int max_ctx, int kv_dtype);
 /* ... and the weights' storage type: HPA_F32 (0, default) or HPA_BF16 (1:
  * "bf16 decode" -- the layer and logits weights packed bf16 in HBM, GEMM
  * inputs rounded to bf16 after their LayerNorm, fp32 accumulation on
  * v_mfma_f32_16x16x32_bf16; LayerNorm, attention, residuals, GELU, softmax
- * stay fp32; fused path only, no pipeline / overlap options) */
+ * stay fp32) */
 int  gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dtype, int w_dtype);
 /* one decode step for every sequence: tokens[b] (host) at position pos[b];
  * tokens == NULL feeds back the previous step's greedy ids (device-resident).
@@ -171,7 +171,7 @@ int  gpt2_decode_step(GPT2* model, const int* tokens, int* next_tokens);
  * all T tokens in one pass (B*T-row GEMMs, causal multi-query paged
  * attention on MFMA); afterwards logits / next ids are those of each
  * sequence's last token and pos[b] += T, so decode continues with
- * gpt2_decode_step(model, NULL, ...).  Fused one-lane engine. */
+ * gpt2_decode_step(model, NULL, ...). */
 int  gpt2_decode_prefill(GPT2* model, const int* tokens, int T, int* next_tokens);
 /* continuous batching: one pass over lens[b] >= 0 new tokens per sequence
  * (tokens packed in sequence order, sum(lens) of them): prompts of newly
@@ -192,68 +192,61 @@ int  gpt2_decode_fill_random(GPT2* model, int ctx, unsigned long long seed);
 int  gpt2_decode_reserve(GPT2* model, int ctx);
 /* rewind/advance positions (pages kept) */
 int  gpt2_decode_set_positions(GPT2* model, const int* pos);
-/* 1 (default): fused frag-layout kernels (5 launches per layer);
- * 0: unfused split-K path (9 per layer), kept for A/B and as a cross-check */
-int  gpt2_decode_set_fused(GPT2* model, int enable);
 /* capture the step into a hipGraph and replay it (1) or launch eagerly (0) */
 int  gpt2_decode_set_graph(GPT2* model, int enable);
+/* context ranges per (sequence, head) of the decode attention
+ * (hpa_paged_attention_decode_split): 0 = by shape (~3 workgroups per CU:
+ * 1 at B = 64 with GPT-2 124M, 2 at 32, 4 at 16, 8 at 8), else 1..16 */
+int  gpt2_decode_set_attn_splits(GPT2* model, int splits);
+int  gpt2_decode_attn_splits(GPT2* model);
 /* attention-kernel timing with HIP events around every layer's attention
- * launch (forces eager launches while enabled); collect after each step */
+ * launch (forces eager launches while enabled) */
 int    gpt2_decode_profile(GPT2* model, int enable);
-int    gpt2_decode_profile_collect(GPT2* model);
 double gpt2_decode_profile_read(GPT2* model, long* launches);
-/* device buffers: logits [B][V], next ids [B], positions [B] */
+/* device buffers: logits [B][V], next ids [B]; host positions [B]; batch */
 float* gpt2_decode_logits(GPT2* model);
 int*   gpt2_decode_next(GPT2* model);
 int    gpt2_decode_positions(GPT2* model, int* host_pos);
-/* the per-GEMM split-K chosen for this model/batch (qkv, attproj, fc, fcproj) */
-int    gpt2_decode_splits(GPT2* model, int* splits4);
+int    gpt2_decode_batch(GPT2* model);
+/* sequences the LRU policy paged out since the last call (block_manager.c:
+ * 104-113 evicts a whole sequence when the pool is full; it restarts at
+ * position 0 and must be prefilled again); mask (nullable, [B]) marks them.
+ * Returns how many. */
+int    gpt2_decode_evicted(GPT2* model, int* mask);
+/* K/V of positions [0, n) of sequence b at layer l, token-major [n][C] host
+ * arrays (the reference page layout, block_manager.c:145-146) */
+int    gpt2_decode_read_kv(GPT2* model, int layer, int b, int n, float* k, float* v);
 /* fused GEMM launch shapes [qkv, attproj, fc, fcproj, logits]: waves per
  * workgroup (4/8/16), 16-row blocks (1/2/4) and 16-column tiles (1/2/4) per
  * workgroup.  set = 0 copies them out; set = 1 applies the nonzero entries
  * (NULL = keep).  Invalid combinations fail at the next step's launch. */
 int    gpt2_decode_gemm_config(GPT2* model, int* waves5, int* row_blocks5, int* col_tiles5, int set);
-/* micro-batch lanes (fused path): the batch is cut into `lanes` groups of
- * whole 16-row blocks, each running the step on its own stream so one
- * group's attention overlaps another's GEMMs; results are identical to
- * lanes = 1 row for row.  Returns nonzero for lanes outside 1..8. */
-int    gpt2_decode_set_lanes(GPT2* model, int lanes);
 /* attention kernel timed alone: `iters` back-to-back launches on the engine's
  * pool at the last step's positions; average ms and algorithmic bytes per
  * launch (bench.py roofline) */
 int    gpt2_decode_time_attention(GPT2* model, int iters, double* ms_per_launch,
                                   double* bytes_per_launch);
-int    gpt2_decode_lanes(GPT2* model);
 /* token choice: 0 = greedy argmax (default); 1 = multinomial sampling as the
  * reference driver (softmax_forward + sample_mult with random_f32 coins),
  * sequence b seeded with seed + b; the coins stay on the device */
 int    gpt2_decode_set_sampling(GPT2* model, int enable, unsigned long long seed);
-/* pipelined step (fused path): two lanes on ONE stream; each lane's layer
- * attention runs in 4 context chunks, every chunk in the same launch as one
- * GEMM of the other lane's chain (hpa_attn_chunk_with_gemm).  Logits within
- * the usual fp32 tolerance of the one-lane step (different softmax summation
- * order).  Needs B > 16 and page size 8/16/32; disabling returns to 1 lane. */
-int    gpt2_decode_set_pipeline(GPT2* model, int enable);
-int    gpt2_decode_pipeline(GPT2* model);
-/* split step (fused path): two lanes on two CU-masked streams, the attention
- * of one half of the batch beside the GEMM chains of the other, GEMMs on
- * `gemm_cus` CUs and attention on the rest; launched eagerly (CU masks do not
- * survive graph capture).  Rows bit-identical to one lane.  Needs B > 16;
- * gemm_cus = 0 returns to one lane. */
-int    gpt2_decode_set_split(GPT2* model, int gemm_cus);
-int    gpt2_decode_split(GPT2* model);
-/* overlapped step (fused path, fp32 pool, 16 < B <= 128): two lanes on one
- * stream; each launch runs one lane's attention of a layer beside the other
- * lane's GEMM chain (hpa_lane_layer), 2 launches per layer.  chain_blocks =
- * persistent chain workgroups; 0 returns to one lane.  Logits within the
- * fp32 tolerance of the one-lane step (fcproj folds K over 4 waves here). */
-int    gpt2_decode_set_overlap(GPT2* model, int chain_blocks);
-int    gpt2_decode_overlap(GPT2* model);
-/* nonzero if an in-launch wait of the last overlapped step expired */
-unsigned gpt2_decode_overlap_faults(GPT2* model);
 /* algorithmic HBM bytes one step reads+writes at the current positions
  * (SURVEY.md 8d formula) and the attention kernel's share of them */
 double gpt2_decode_step_bytes(GPT2* model, double* attention_bytes);
+
+/* ---------------- sequence-sharded decode ----------------
+ * One process per GPU: every rank runs its own engine (gpt2_decode_init with
+ * its B_local sequences, private page pool, replicated weights); nothing is
+ * exchanged inside a step.  After hpa_comm_init (hip_paged_attn.h),
+ * gpt2_decode_shard tells the engine every rank's row count (rank order) and
+ * the root; gpt2_decode_gather then enqueues the end-of-step RCCL gather of
+ * the logits (what = 0) or greedy ids (what = 1) on a communication stream
+ * (double-buffered: it overlaps the next step).  gpt2_decode_gathered (root)
+ * returns the device rows of the last gather after gpt2_decode_gather_wait. */
+int    gpt2_decode_shard(GPT2* model, const int* rows_per_rank, int root);
+int    gpt2_decode_gather(GPT2* model, int what);
+int    gpt2_decode_gather_wait(GPT2* model);
+void*  gpt2_decode_gathered(GPT2* model, int what);
 void   gpt2_decode_free(GPT2* model);
 
 #ifdef __cplusplus

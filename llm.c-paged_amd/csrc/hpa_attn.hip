@@ -23,6 +23,15 @@
 //    consecutive 256-B token rows = 1 KiB contiguous.  p values arrive by
 //    ds_bpermute (__shfl); the 4 lane groups are summed once at the end.
 //  * waves combine (m, l, acc) through LDS; wave 0 writes out[b][h*64..+64].
+//  * split context (flash-decoding): when B*NH workgroups
+//    cannot keep every CU streaming (B*NH < ~3 per CU), each (sequence, head)
+//    is cut into S ranges of its 64-token tiles, one workgroup each.  A range
+//    publishes its folded (m, l, acc) record with write-through (sc1) stores,
+//    drains them and draws an arrival ticket (agent-scope atomic add); the
+//    last arriver of the (sequence, head) merges the S records in range order
+//    (sc1 loads: MI355X_MICROARCH.md "Valid forms", row 1) and writes the
+//    output, then rewinds the counter for the next launch.  The merge order is
+//    fixed, so results do not depend on which range finishes last.
 // MFMA is not used: with one query row the QK^T / PV contractions are
 // matrix-vector (M = 1), i.e. HBM-bound at ~0.5 FLOP/B; the MFMA path belongs
 // to multi-query prefill.
@@ -33,17 +42,82 @@
 namespace {
 using namespace hpa_attn;
 
+// split-context records: [B*NH][S][kRec] floats (m, l, -, -, acc[64]), then
+// [B*NH] int arrival counters (zero between launches)
+constexpr int kRec = 68;
+
+__device__ __forceinline__ void st_wt(float* p, float v) {  // write-through (sc1) store
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float* p) {  // L1-bypassing (sc1) load
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Range s of S: publish this workgroup's folded state (K float4 chunks per
+// lane in wave 0: chunk k of lane j holds dims 4*(K*j + k)..+3 -- K = 1 for
+// the fp32 fold, lanes 0..15; K = 2 for the bf16 fold, lanes 0..7); the last
+// arriver merges every range in order and returns true with the merged state.
+template <int K>
+__device__ __forceinline__ bool split_merge(float* __restrict__ rec_bh, int* __restrict__ cnt, int S, int s,
+                                            float& m, float& l, float4* acc) {
+    const int lane = threadIdx.x & 63;
+    float* rec = rec_bh + (size_t)s * kRec;
+    if (lane == 0) {
+        st_wt(rec, m);
+        st_wt(rec + 1, l);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        float* d = rec + 4 + 4 * (K * lane + k);
+        st_wt(d, acc[k].x);
+        st_wt(d + 1, acc[k].y);
+        st_wt(d + 2, acc[k].z);
+        st_wt(d + 3, acc[k].w);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every record store drained before the ticket
+    int ticket = 0;
+    if (lane == 0) ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ticket = __builtin_amdgcn_readfirstlane(ticket);
+    if (ticket != S - 1) return false;
+    if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    float M = -INFINITY;
+    for (int i = 0; i < S; ++i) M = fmaxf(M, ld_wt(rec_bh + (size_t)i * kRec));
+    float L = 0.f;
+    float4 O[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) O[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < S; ++i) {  // ranges in order: independent of arrival order
+        const float* r = rec_bh + (size_t)i * kRec;
+        const float f = exp2f(ld_wt(r) - M);
+        L = fmaf(ld_wt(r + 1), f, L);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const float* d = r + 4 + 4 * (K * lane + k);
+            O[k].x = fmaf(ld_wt(d), f, O[k].x);
+            O[k].y = fmaf(ld_wt(d + 1), f, O[k].y);
+            O[k].z = fmaf(ld_wt(d + 2), f, O[k].z);
+            O[k].w = fmaf(ld_wt(d + 3), f, O[k].w);
+        }
+    }
+    m = M;
+    l = L;
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = O[k];
+    return true;
+}
+
 template <int P, int NW, bool FRAG, bool BF16>
 __global__ __launch_bounds__(NW * 64, 3) void paged_attn_decode_f32(
     const float* __restrict__ q, const void* __restrict__ layer_base, size_t page_elems, int NH,
     const int* __restrict__ block_table, int bt_stride, const int* __restrict__ pos,
-    float* __restrict__ out, float qscale, float m_init) {
+    float* __restrict__ out, float qscale, float m_init, int S, float* __restrict__ ws) {
     constexpr int TILE = P * HS;
     __shared__ float s_m[NW];
     __shared__ float s_l[NW];
     __shared__ float4 s_acc[NW * 16];
 
-    const int bh = blockIdx.x;
+    const int bh = S == 1 ? (int)blockIdx.x : (int)blockIdx.x / S;
+    const int sr = (int)blockIdx.x - bh * S;  // context range of this workgroup
     const int b = bh / NH;
     const int h = bh - b * NH;
     const int lane = threadIdx.x & 63;
@@ -56,15 +130,20 @@ __global__ __launch_bounds__(NW * 64, 3) void paged_attn_decode_f32(
     // reference applies `val *= scale` after the dot, :197).
     const float* __restrict__ qh = q + ((size_t)b * NH + h) * HS;
     const int* bt = block_table + (size_t)b * bt_stride;
-    const int n_it = (ctx + 63) >> 6;
+    const int n_it_all = (ctx + 63) >> 6;
+    const int it0 = S == 1 ? 0 : (int)((long long)sr * n_it_all / S);
+    const int n_it = S == 1 ? n_it_all : (int)((long long)(sr + 1) * n_it_all / S);
+    float* rec_bh = S == 1 ? nullptr : ws + (size_t)bh * S * kRec;
+    int* cnt = S == 1 ? nullptr : reinterpret_cast<int*>(ws + (size_t)gridDim.x * kRec) + bh;
     float m = m_init;
     float l = 0.f;
     if constexpr (BF16) {
         const unsigned short* base = reinterpret_cast<const unsigned short*>(layer_base);
         float4 acc[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
         attn_tiles_bf16<P, NW>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, page_elems, bt, bt_stride, ctx,
-                               0, n_it, qscale, m, l, acc);
+                               it0, n_it, qscale, m, l, acc);
         if (!attn_fold_bf16<NW>(m, l, acc, s_m, s_l, s_acc)) return;
+        if (S > 1 && !split_merge<2>(rec_bh, cnt, S, sr, m, l, acc)) return;
         const float inv = l == 0.f ? 0.f : 1.f / l;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {  // dims 8*lane + 4k .. +3
@@ -77,8 +156,9 @@ __global__ __launch_bounds__(NW * 64, 3) void paged_attn_decode_f32(
         const float* base = reinterpret_cast<const float*>(layer_base);
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         attn_tiles<P, NW>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, page_elems, bt, bt_stride, ctx,
-                          0, n_it, qscale, m, l, acc);
+                          it0, n_it, qscale, m, l, acc);
         if (!attn_fold<NW>(m, l, acc, s_m, s_l, s_acc)) return;
+        if (S > 1 && !split_merge<1>(rec_bh, cnt, S, sr, m, l, &acc)) return;
         // out[b][h*64 + 4*lane .. +3]: row-major, or the frag layout the next
         // GEMM reads (4 consecutive columns stay one contiguous float4 there)
         const size_t oi =
@@ -90,28 +170,28 @@ __global__ __launch_bounds__(NW * 64, 3) void paged_attn_decode_f32(
 
 template <int P, bool FRAG, bool BF16>
 int launch_decode(const float* q, const HpaKVPool* pool, int layer, const int* bt, int bt_stride,
-                  const int* pos, float* out, int B, int nw) {
+                  const int* pos, float* out, int B, int nw, int S, float* ws) {
     const void* base = (const char*)pool->base + (size_t)layer * pool->layer_elems * pool->elem_bytes;
     const float log2e = 1.4426950408889634f;
     const float qscale = (float)(1.0 / sqrt((double)HS)) * log2e;
     const float m_init = -10000.0f * log2e;
-    dim3 grid(B * pool->num_heads);
+    dim3 grid(B * pool->num_heads * S);
     switch (nw) {
         case 1:
             paged_attn_decode_f32<P, 1, FRAG, BF16><<<grid, 64, 0, hpa_stream()>>>(
-                q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init);
+                q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init, S, ws);
             break;
         case 2:
             paged_attn_decode_f32<P, 2, FRAG, BF16><<<grid, 128, 0, hpa_stream()>>>(
-                q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init);
+                q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init, S, ws);
             break;
         case 8:
             paged_attn_decode_f32<P, 8, FRAG, BF16><<<grid, 512, 0, hpa_stream()>>>(
-                q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init);
+                q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init, S, ws);
             break;
         default:
             paged_attn_decode_f32<P, 4, FRAG, BF16><<<grid, 256, 0, hpa_stream()>>>(
-                q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init);
+                q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init, S, ws);
             break;
     }
     HPA_LAUNCH_CHECK();
@@ -132,25 +212,24 @@ int hpa_set_attention_waves(int nw) {
 }
 
 static int attn_dispatch(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
-                         int bt_stride, const int* pos, float* out, int B, bool frag) {
+                         int bt_stride, const int* pos, float* out, int B, bool frag, int S, void* ws) {
     HPA_REQUIRE(pool && pool->base, "pool not created");
     HPA_REQUIRE(pool->dtype == HPA_F32 || pool->dtype == HPA_BF16, "decode attention: fp32 or bf16 pool");
     HPA_REQUIRE(pool->head_size == HS, "decode attention requires head_size 64");
     HPA_REQUIRE(layer >= 0 && layer < pool->num_layers, "layer out of range");
     HPA_REQUIRE(B > 0 && q && out && block_table && pos, "bad arguments");
     HPA_REQUIRE(((uintptr_t)q & 15) == 0 && ((uintptr_t)out & 15) == 0, "q/out must be 16-byte aligned");
+    HPA_REQUIRE(S >= 1 && S <= HPA_ATTN_MAX_SPLITS && (S == 1 || ws), "decode attention: splits 1..16, workspace");
     const bool bf = pool->dtype == HPA_BF16;
-#define HPA_ATTN_CASE(PS)                                                                              \
-    case PS:                                                                                            \
-        if (bf)                                                                                         \
-            return frag ? launch_decode<PS, true, true>(q, pool, layer, block_table, bt_stride, pos, out, B, \
-                                                        g_attn_waves)                                   \
-                        : launch_decode<PS, false, true>(q, pool, layer, block_table, bt_stride, pos, out, \
-                                                         B, g_attn_waves);                              \
-        return frag ? launch_decode<PS, true, false>(q, pool, layer, block_table, bt_stride, pos, out, B, \
-                                                     g_attn_waves)                                      \
-                    : launch_decode<PS, false, false>(q, pool, layer, block_table, bt_stride, pos, out, B, \
-                                                      g_attn_waves);
+    float* w = (float*)ws;
+    const int nw = g_attn_waves;
+#define HPA_ATTN_CASE(PS)                                                                                      \
+    case PS:                                                                                                    \
+        if (bf)                                                                                                 \
+            return frag ? launch_decode<PS, true, true>(q, pool, layer, block_table, bt_stride, pos, out, B, nw, S, w) \
+                        : launch_decode<PS, false, true>(q, pool, layer, block_table, bt_stride, pos, out, B, nw, S, w); \
+        return frag ? launch_decode<PS, true, false>(q, pool, layer, block_table, bt_stride, pos, out, B, nw, S, w)     \
+                    : launch_decode<PS, false, false>(q, pool, layer, block_table, bt_stride, pos, out, B, nw, S, w);
     switch (pool->page_size) {
         HPA_ATTN_CASE(8)
         HPA_ATTN_CASE(16)
@@ -164,13 +243,39 @@ static int attn_dispatch(const float* q, const HpaKVPool* pool, int layer, const
 int hpa_paged_attention_decode(const float* q, const HpaKVPool* pool, int layer,
                                const int* block_table, int bt_stride, const int* pos, float* out,
                                int B) {
-    return attn_dispatch(q, pool, layer, block_table, bt_stride, pos, out, B, false);
+    return attn_dispatch(q, pool, layer, block_table, bt_stride, pos, out, B, false, 1, nullptr);
 }
 
 int hpa_paged_attention_decode_frag(const float* q, const HpaKVPool* pool, int layer,
                                     const int* block_table, int bt_stride, const int* pos,
                                     float* out_frag, int B) {
-    return attn_dispatch(q, pool, layer, block_table, bt_stride, pos, out_frag, B, true);
+    return attn_dispatch(q, pool, layer, block_table, bt_stride, pos, out_frag, B, true, 1, nullptr);
+}
+
+size_t hpa_attn_ws_bytes(int B, int num_heads, int splits) {
+    if (B <= 0 || num_heads <= 0 || splits <= 1) return 0;
+    const size_t recs = (size_t)B * num_heads * splits * kRec * sizeof(float);
+    return recs + (size_t)B * num_heads * splits * sizeof(int);  // counters ([B*NH], padded by the grid size)
+}
+
+// Splits by shape (never by context, which varies per sequence and step):
+// enough (sequence, head, range) workgroups of 4 waves for ~3 per CU, the
+// number that keeps the B = 64 single-pass kernel at 6.5 TB/s (768
+// workgroups); at most one range per 2 tiles of 64 tokens of max_ctx.
+int hpa_attn_pick_splits(int B, int num_heads, int max_ctx, int num_cus) {
+    if (B <= 0 || num_heads <= 0) return 1;
+    if (num_cus <= 0) num_cus = 256;
+    const long bh = (long)B * num_heads;
+    const long want = 3L * num_cus;
+    int s = 1;
+    while (s < HPA_ATTN_MAX_SPLITS && bh * s * 2 <= want && (long)(s * 2) * 128 <= (long)max_ctx) s *= 2;
+    return s;
+}
+
+int hpa_paged_attention_decode_split(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
+                                     int bt_stride, const int* pos, float* out, int B, int splits, void* ws,
+                                     int out_frag) {
+    return attn_dispatch(q, pool, layer, block_table, bt_stride, pos, out, B, out_frag != 0, splits, ws);
 }
 
 }  // extern "C"

@@ -1,6 +1,6 @@
 // hpa_attn_body.h -- device pieces of the paged decode attention (design
-// notes in hpa_attn.hip), shared by the single-pass kernel and the
-// context-chunk body of the pipelined launches (hpa_combo.hip).
+// notes in hpa_attn.hip): the per-wave tile loops (fp32 and bf16 pools) and
+// the in-workgroup folds of the online-softmax state.
 #pragma once
 #include <math.h>
 
@@ -298,88 +298,6 @@ __device__ __forceinline__ bool attn_fold(float& m, float& l, float4& acc, float
         l = L;
         acc = O;
         return true;
-    }
-}
-
-// ---- context-chunk attention (the pipelined decode, hpa_combo.hip) ----
-// Chunk c of n covers the 64-token tiles [c*T/n, (c+1)*T/n) of each
-// (sequence, head), T = ceil(ctx/64).  The running (m, l, acc) is carried
-// between launches in `state` ([B][NH][68] floats: m, l, -, -, acc[64]);
-// chunk 0 starts from (m_init, 0, 0), later chunks merge into the carried
-// state in a fixed order, the last chunk normalises and writes the output
-// (frag layout [Mp][C]).
-struct AttnChunk {
-    const float* q;
-    const float* layer_base;
-    size_t page_elems;
-    int NH;
-    const int* bt;
-    int bt_stride;
-    const int* pos;
-    float* state;
-    float* out;
-    int B, chunk, nchunks;
-    float qscale, m_init;
-    int nblocks;  // B*NH rounded up to a multiple of 8 (keeps the GEMM role's b % 8 XCD order)
-};
-constexpr int kStateStride = 68;
-
-template <int NW>
-constexpr int attn_lds_floats() {
-    return 2 * NW + 4 * 16 * NW;
-}
-
-template <int P, int NW>
-__device__ __forceinline__ void attn_chunk_body(const AttnChunk& a, int bid, float* smem) {
-    if (bid >= a.B * a.NH) return;
-    constexpr int TILE = P * HS;
-    const int b = bid / a.NH;
-    const int h = bid - b * a.NH;
-    const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
-    const int ctx = a.pos[b] + 1;
-    const int n_it = (ctx + 63) >> 6;
-    const int it0 = (int)((long long)a.chunk * n_it / a.nchunks);
-    const int it1 = (int)((long long)(a.chunk + 1) * n_it / a.nchunks);
-    float* st = a.state + ((size_t)b * a.NH + h) * kStateStride;
-    // carried state, loaded before the stream so its latency hides under it
-    float pm = a.m_init, pl = 0.f;
-    float4 pa = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (a.chunk > 0 && w == 0 && lane < 16) {
-        pm = st[0];
-        pl = st[1];
-        pa = reinterpret_cast<const float4*>(st + 4)[lane];
-    }
-    const float* qh = a.q + ((size_t)b * a.NH + h) * HS;
-    float m = a.m_init, l = 0.f;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    attn_tiles<P, NW>(qh, a.layer_base + (size_t)h * TILE, a.layer_base + (size_t)(a.NH + h) * TILE,
-                      a.page_elems, a.bt + (size_t)b * a.bt_stride, a.bt_stride, ctx, it0, it1, a.qscale, m, l,
-                      acc);
-    float* s_m = smem;
-    float* s_l = smem + NW;
-    float4* s_acc = reinterpret_cast<float4*>(smem + 2 * NW + (4 - (2 * NW) % 4) % 4);
-    if (!attn_fold<NW>(m, l, acc, s_m, s_l, s_acc)) return;
-    // merge: carried state first, then this chunk (fixed order)
-    const float M = fmaxf(pm, m);
-    const float f0 = exp2f(pm - M), f1 = exp2f(m - M);
-    const float L = fmaf(pl, f0, l * f1);
-    float4 O;
-    O.x = fmaf(pa.x, f0, acc.x * f1);
-    O.y = fmaf(pa.y, f0, acc.y * f1);
-    O.z = fmaf(pa.z, f0, acc.z * f1);
-    O.w = fmaf(pa.w, f0, acc.w * f1);
-    if (a.chunk + 1 < a.nchunks) {
-        if (lane == 0) {
-            st[0] = M;
-            st[1] = L;
-        }
-        reinterpret_cast<float4*>(st + 4)[lane] = O;
-    } else {
-        const float inv = L == 0.f ? 0.f : 1.f / L;
-        const int C = a.NH * HS;
-        *reinterpret_cast<float4*>(a.out + hpa::frag_index(b, h * HS + 4 * lane, C)) =
-            make_float4(O.x * inv, O.y * inv, O.z * inv, O.w * inv);
     }
 }
 

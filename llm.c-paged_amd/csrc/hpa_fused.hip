@@ -607,17 +607,17 @@ __global__ __launch_bounds__(kSsThreads) void sample_scan_kernel(const float* __
 inline dim3 xcd_grid(FG& p, int gx, int gy) {
     p.gx = gx;
     p.gy = gy;
-    return dim3((unsigned)(((gx + 7) / 8) * 8 * gy * p.ks));
+    return dim3((unsigned)(((gx + 7) / 8) * 8 * gy));
 }
 
-template <int NW, int MT, int NTW = 1, int UD = 0>
+template <int NW, int MT, int NTW = 1>
 int launch16(FG p, int epi) {
     dim3 grid = xcd_grid(p, (p.ntn + NTW - 1) / NTW, p.Mp / 16 / MT), block(NW * 64);
     switch (epi) {
-        case HPA_FEPI_QKV: gemm16_kernel<NW, HPA_FEPI_QKV, MT, NTW, UD><<<grid, block, 0, hpa_stream()>>>(p); break;
-        case HPA_FEPI_RESID: gemm16_kernel<NW, HPA_FEPI_RESID, MT, NTW, UD><<<grid, block, 0, hpa_stream()>>>(p); break;
-        case HPA_FEPI_GELU: gemm16_kernel<NW, HPA_FEPI_GELU, MT, NTW, UD><<<grid, block, 0, hpa_stream()>>>(p); break;
-        case HPA_FEPI_LOGITS: gemm16_kernel<NW, HPA_FEPI_LOGITS, MT, NTW, UD><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_QKV: gemm16_kernel<NW, HPA_FEPI_QKV, MT, NTW><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_RESID: gemm16_kernel<NW, HPA_FEPI_RESID, MT, NTW><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_GELU: gemm16_kernel<NW, HPA_FEPI_GELU, MT, NTW><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_LOGITS: gemm16_kernel<NW, HPA_FEPI_LOGITS, MT, NTW><<<grid, block, 0, hpa_stream()>>>(p); break;
         default: return hpa_fail(__FILE__, __LINE__, "gemm_fused: unknown epilogue");
     }
     HPA_LAUNCH_CHECK();
@@ -656,11 +656,10 @@ int launch_os(const FG& p, int epi, int nw) {
 // multi-column-tile instances: (waves, row_blocks, col_tiles) in
 // {(4|8, 4, 2), (4|8, 2, 2), (4, 4, 4)} -- the rest exceed LDS or registers
 template <int NW>
-int launch16_mt(const FG& p, int epi, int mt, int ntw, bool deep) {
-    if constexpr (NW > 8) deep = false;  // 1024-thread groups: no registers for larger trips
+int launch16_mt(const FG& p, int epi, int mt, int ntw) {
     if constexpr (NW <= 8) {
-        if (ntw == 2 && mt == 4) return deep ? launch16<NW, 4, 2, 2>(p, epi) : launch16<NW, 4, 2>(p, epi);
-        if (ntw == 2 && mt == 2) return deep ? launch16<NW, 2, 2, 4>(p, epi) : launch16<NW, 2, 2>(p, epi);
+        if (ntw == 2 && mt == 4) return launch16<NW, 4, 2>(p, epi);
+        if (ntw == 2 && mt == 2) return launch16<NW, 2, 2>(p, epi);
     }
     if constexpr (NW == 4) {
         if (ntw == 4 && mt == 4) return launch16<NW, 4, 4>(p, epi);
@@ -669,9 +668,9 @@ int launch16_mt(const FG& p, int epi, int mt, int ntw, bool deep) {
         return hpa_fail(__FILE__, __LINE__,
                         "gemm_fused: col_tiles 2 needs waves 4/8 and row_blocks 2/4; 4 needs waves 4, row_blocks 4");
     switch (mt) {
-        case 1: return deep ? launch16<NW, 1, 1, 8>(p, epi) : launch16<NW, 1>(p, epi);
-        case 2: return deep ? launch16<NW, 2, 1, 8>(p, epi) : launch16<NW, 2>(p, epi);
-        case 4: return deep ? launch16<NW, 4, 1, 4>(p, epi) : launch16<NW, 4>(p, epi);
+        case 1: return launch16<NW, 1>(p, epi);
+        case 2: return launch16<NW, 2>(p, epi);
+        case 4: return launch16<NW, 4>(p, epi);
         default: return hpa_fail(__FILE__, __LINE__, "gemm_fused: row_blocks must be 1, 2 or 4");
     }
 }
@@ -767,23 +766,6 @@ int hpa_fused_pick_bf16_ares(int M, int N, int K, int* out3) {
     return ntn >= 1024 || (big && ntn >= 144);
 }
 
-// fp32 A-resident kernel (variant 5, hpa_gemm_ares.hip): out3 = {waves,
-// row_blocks, rounds}; returns 1 where variant 0 (or 4 where the resident
-// logits kernel does not apply) uses it -- by N and K only, so a row's
-// summation order never depends on M.  Measured (profiles/r1/
-// gemm_tune_ares_*.log): slower than the one-shot / looped kernels on every
-// GPT-2 layer GEMM (124M qkv 12.7 vs 8.8 us, XL qkv 28.2 vs 27.3) and than the
-// resident logits kernel at 124M (67.4 vs 65.3); faster only for the XL
-// logits in isolation (159.7 vs 171.6 us), but the XL step measured slower
-// with it (10.90 vs 10.71 ms/step), so it is nowhere the default.
-int hpa_fused_pick_f32_ares(int M, int N, int K, int* out3) {
-    const int ntn = (N + 15) / 16;
-    out3[0] = 8;
-    out3[1] = K <= 768 && (M + 15) / 16 % 2 == 0 ? 2 : 1;
-    out3[2] = ntn >= 1024 ? (K > 768 ? 8 : 4) : 1;
-    return 0;
-}
-
 void hpa_fused_pick_bf16(int M, int N, int K, int* out3) {
     (void)K;
     const int small = (M + 15) / 16 < 8 && N <= 1024;
@@ -811,38 +793,14 @@ static void looped_shape(const HpaFusedGemm* g, int Mp, int* nw, int* mt, int* n
     if ((*ntw == 2 && (*mt == 1 || *nw == 16)) || (*ntw == 4 && (*mt != 4 || *nw != 4))) *ntw = 1;
 }
 
-// K slices by shape (never by M).  Measured on the GPT-2 XL layer GEMMs
-// (profiles/r1/ksplit_xl.txt): 2 or 4 slices were slower than none at every
-// shape (qkv 26 -> 34 / 42 us, fc 26 -> 35 / 48 us): a slice's workgroup
-// keeps the fold, slab exchange and epilogue latency of a whole-K workgroup
-// while its MFMA work shrinks.  So: none; callers may still ask for a split.
-int hpa_fused_pick_slices(int M, int N, int K) {
-    (void)M;
-    (void)N;
-    (void)K;
-    return 1;
-}
-
-int hpa_fused_ks_workspace(const HpaFusedGemm* g, size_t* slab_floats, size_t* counters) {
-    HPA_REQUIRE(g && g->M > 0 && g->N > 0 && g->K > 0 && slab_floats && counters, "ks_workspace: arguments");
-    const int Mp = (g->M + 15) / 16 * 16, ntn = (g->N + 15) / 16;
-    int nw, mt, ntw;
-    looped_shape(g, Mp, &nw, &mt, &ntw);
-    const int ks = g->k_slices > 1 ? g->k_slices : 1;
-    const size_t tiles = (size_t)((ntn + ntw - 1) / ntw) * (size_t)(Mp / 16 / mt);
-    *slab_floats = ks > 1 ? tiles * ks * (size_t)(ntw * mt * 256 + 2 * mt * 16) : 0;
-    *counters = ks > 1 ? tiles : 0;
-    return 0;
-}
-
 int hpa_gemm_fused(const HpaFusedGemm* g) {
     FG p;
     if (fused_prepare(g, &p)) return 1;
     int nw, mt, ntw;
     if (g->w_dtype == HPA_BF16) {  // bf16 weights: hpa_gemm_bf16.hip
-        HPA_REQUIRE(g->K % 32 == 0 && !g->ln_fold_c1 && p.ks == 1 &&
+        HPA_REQUIRE(g->K % 32 == 0 && !g->ln_fold_c1 &&
                         (g->variant == 0 || g->variant == 4 || g->variant == 5 || g->variant == 1),
-                    "gemm_fused bf16: K % 32, no ln_fold_c1, no k_slices, variant 0/1/5");
+                    "gemm_fused bf16: K % 32, no ln_fold_c1, variant 0/1/5");
         int pk[3];
         // HPA_BF16_ARES=0: no A-resident default (measurement knob; variant 5 still honoured)
         static const int ares_default = [] {
@@ -866,39 +824,24 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
         return launch_b16(p, g->epilogue, nw, mt, ntw);
     }
     HPA_REQUIRE(g->w_dtype == HPA_F32, "gemm_fused: w_dtype must be HPA_F32 or HPA_BF16");
-    {
-        int pk[3];
-        const int dflt = hpa_fused_pick_f32_ares(g->M, g->N, g->K, pk);
-        const bool auto_ok = g->variant == 0 || (g->variant == 4 && !logits_resident_eligible(p, g->epilogue));
-        if (g->variant == 5 || (auto_ok && p.ks == 1 && !g->ln_fold_c1 && dflt)) {
-            HPA_REQUIRE(p.ks == 1 && !g->ln_fold_c1, "gemm_fused A-resident: no k_slices, no ln_fold_c1");
-            nw = g->waves ? g->waves : pk[0];
-            mt = g->row_blocks ? g->row_blocks : pk[1];
-            while (mt > 1 && ((p.Mp / 16) % mt || g->K > 768)) mt >>= 1;
-            return launch_f32_ares(p, g->epilogue, nw, mt, g->col_tiles ? g->col_tiles : pk[2]);
-        }
-    }
     HPA_REQUIRE(g->row_blocks == 0 || g->row_blocks == 1 || g->row_blocks == 2 || g->row_blocks == 4,
                 "gemm_fused: row_blocks must be 1, 2 or 4");
     looped_shape(g, p.Mp, &nw, &mt, &ntw);
-    HPA_REQUIRE(g->variant >= 0 && g->variant <= 4, "gemm_fused: variant must be 0 .. 4");
-    HPA_REQUIRE(p.ks == 1 || g->variant == 0 || g->variant == 1 || g->variant == 3,
-                "gemm_fused: k_slices > 1 runs the looped kernel (variant 0, 1 or 3)");
-    if (p.ks == 1 && g->variant == 4 && logits_resident_eligible(p, g->epilogue)) return launch_logits_resident(p);
+    HPA_REQUIRE(g->variant >= 0 && g->variant <= 4 && g->variant != 3, "gemm_fused: variant must be 0, 1, 2 or 4");
+    if (g->variant == 4 && logits_resident_eligible(p, g->epilogue)) return launch_logits_resident(p);
     HPA_REQUIRE(g->col_tiles == 0 || g->col_tiles == 1 || g->col_tiles == 2 || g->col_tiles == 4,
                 "gemm_fused: col_tiles must be 1, 2 or 4");
-    if (p.ks == 1 && (g->variant == 2 || (g->variant == 0 && mt == 1 && p.ntn < 1024 && g->col_tiles <= 1))) {
+    if (g->variant == 2 || (g->variant == 0 && mt == 1 && p.ntn < 1024 && g->col_tiles <= 1)) {
         const int rc = launch_os(p, g->epilogue, nw);
         if (rc >= 0) return rc;
         HPA_REQUIRE(g->variant == 0, "gemm_fused: one-shot needs (waves, K/16) in {(4,48), (8,48), (16,48), (8,192), (16,192), (10,100)}");
     }
-    const bool deep = g->variant == 3;  // looped with larger trips (same results as 1)
     switch (nw) {
-        case 4: return launch16_mt<4>(p, g->epilogue, mt, ntw, deep);
-        case 8: return launch16_mt<8>(p, g->epilogue, mt, ntw, deep);
+        case 4: return launch16_mt<4>(p, g->epilogue, mt, ntw);
+        case 8: return launch16_mt<8>(p, g->epilogue, mt, ntw);
         case 16:
             HPA_REQUIRE(ntw == 1, "gemm_fused: col_tiles > 1 needs waves 4 or 8");
-            return launch16_mt<16>(p, g->epilogue, mt, ntw, deep);
+            return launch16_mt<16>(p, g->epilogue, mt, ntw);
         default: return hpa_fail(__FILE__, __LINE__, "gemm_fused: waves must be 4, 8 or 16");
     }
 }

@@ -67,8 +67,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_b16_kernel(FG p) {
     float* lnst = tile + NTW * R * 17;          // [R][2]
     float* lnscr = lnst + 2 * R;                // [4R][2]
 
-    int cx, ry, slice;
-    if (!xcd_tile(p, blockIdx.x, cx, ry, slice)) return;
+    int cx, ry;
+    if (!xcd_tile(p, blockIdx.x, cx, ry)) return;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     const int nt0 = cx * NTW;
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_b16_kernel(FG p) {
 
     Epi<NW, EPI, MT, NTW> epi;
     epi.prefetch(p, nt0, row0);
-    epi.finish(p, acc, red, tile, nt0, row0, lngb, cx * p.gy + ry, slice);
+    epi.finish(p, acc, red, tile, nt0, row0, lngb);
 }
 
 // ---- A-resident variant (variant 5): the workgroup's MT*16 rows of A are
@@ -200,8 +200,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_b16_ares_kernel(FG p, int cpw) {
     float* lnscr = lnst + 2 * R;              // [4R][2]
     uint4* As = reinterpret_cast<uint4*>(lnscr + 8 * R);  // [MT][K32][64 lanes] bf16x8
 
-    int cx, ry, slice;
-    if (!xcd_tile(p, blockIdx.x, cx, ry, slice)) return;
+    int cx, ry;
+    if (!xcd_tile(p, blockIdx.x, cx, ry)) return;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     const int row0 = ry * R;
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_b16_ares_kernel(FG p, int cpw) {
 #pragma unroll
         for (int i = 0; i < EPT; ++i) vals[i] = red[threadIdx.x + i * NT];
         __syncthreads();  // tile (the row statistics' scratch) aliases red
-        epi.apply(p, vals, red, red, tb, row0, nullptr, false);
+        epi.apply(p, vals, red, tb, row0, nullptr);
         __syncthreads();
     }
 }

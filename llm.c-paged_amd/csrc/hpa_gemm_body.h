@@ -1,25 +1,11 @@
 // hpa_gemm_body.h -- the fused decode GEMM workgroup bodies (see
-// hpa_fused.hip for the design notes).  Shared by hpa_fused.hip (stand-alone
-// launches) and hpa_combo.hip (the GEMM role of the pipelined launches).
+// hpa_fused.hip for the design notes), shared by the fp32 launchers
+// (hpa_fused.hip), the bf16-weight kernels (hpa_gemm_bf16.hip) and the
+// resident logits kernel (hpa_logits.hip).
 #pragma once
 #include <math.h>
 
 #include "hpa_internal.h"
-
-// phase timestamps of the one-shot body: empty in the library; the
-// tools/micro/os_trace.hip build defines it to record s_memrealtime per wave
-#ifndef HPA_TS
-#define HPA_TS(i, bid)
-#endif
-#ifndef HPA_OS_ORDER
-#define HPA_OS_ORDER 1
-#endif
-// one-shot body timing experiments (tools/micro/os_trace.hip only; 0 in the
-// library): 1 no LayerNorm, 2 no MFMA (VALU stand-in), 3 every workgroup reads
-// the weight/activation tiles of (0, 0) (L2-resident operands), 4 no epilogue
-#ifndef HPA_OS_EXP
-#define HPA_OS_EXP 0
-#endif
 
 namespace hpa_gemm {
 
@@ -50,9 +36,6 @@ struct FG {
     const int* row_seq;  // QKV: block-table row per GEMM row (NULL: the row)
     const float* fold_c1;  // LN folded into w: out = rstd*(acc - mean*c1) + bias (bias = c2)
     int gx, gy;  // column-tile groups x row groups of the launch
-    int ks;      // K slices per output tile (workgroups; looped kernel): 1 = no split
-    float* ks_slab;  // [tile][slice][slab floats] partial tiles (+ folded-LN row sums)
-    int* ks_cnt;     // [tile] arrival counters (zero between launches)
 };
 
 // XCD-aware workgroup order (MI355X_MICROARCH.md "Workgroup dispatch":
@@ -60,33 +43,13 @@ struct FG {
 // of ceil(gx/8)*8*gy blocks is dealt so that the gy row groups of one column
 // group run back to back on ONE XCD: its weight tile is fetched from HBM once
 // and re-read from that XCD's L2.  Returns false for the padding blocks.
-// With K split over p.ks workgroups, the slices of a tile take consecutive
-// s = bid >> 3 (same bid % 8: one XCD under round-robin placement -- a
-// speed choice only, the hand-off is correct for any placement).
-__device__ __forceinline__ bool xcd_tile(const FG& p, int bid, int& cx, int& ry, int& slice) {
+__device__ __forceinline__ bool xcd_tile(const FG& p, int bid, int& cx, int& ry) {
     const int xg = bid & 7;
-    int s = bid >> 3;
-    slice = s % p.ks;
-    s /= p.ks;
+    const int s = bid >> 3;
     const int q = s / p.gy;
     ry = s - q * p.gy;
     cx = q * 8 + xg;
     return cx < p.gx;
-}
-__device__ __forceinline__ bool xcd_tile(const FG& p, int bid, int& cx, int& ry) {
-    int slice;
-    return xcd_tile(p, bid, cx, ry, slice);
-}
-
-// output store of an epilogue: WT = write-through (sc1), for outputs another
-// workgroup of the same launch consumes (hpa_lane.hip; MI355X_MICROARCH.md
-// "publish-large": sc1 stores + a drained counter instead of a release fence)
-template <bool WT>
-__device__ __forceinline__ void st_out(float* p, float v) {
-    if constexpr (WT)
-        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-        *p = v;
 }
 
 __device__ __forceinline__ float4 ln4(float4 a, float mu, float rs, float4 g, float4 b) {
@@ -127,7 +90,7 @@ __device__ __forceinline__ void row_sums_publish(float s1, float s2, float* wsum
 // rb = e'>>8, reg = (e'>>6)&3, l = e'&63 -> row rb*16 + (l>>4)*4 + reg,
 // col l&15 (16x16 C/D map: col = lane & 15, row = 4*(lane >> 4) + reg).
 // Thread t owns e = t + i*NT.  Accumulator acc[j*MT + r] holds (tile j, block r).
-template <int NW, int EPI, int MT, int NTW = 1, bool WT = false>
+template <int NW, int EPI, int MT, int NTW = 1>
 struct Epi {
     static constexpr int NT = NW * 64;
     static constexpr int R = MT * 16;
@@ -166,70 +129,8 @@ struct Epi {
     // fold the waves' accumulators through LDS (fixed order) and apply the
     // epilogue; wsum = the waves' row partial statistics [NW][R][2] in LDS,
     // read when p.fold_c1 (LN folded into w; written before the fold's barrier)
-    // K split over p.ks workgroups: every slice publishes its folded tile
-    // (and, LN folded, its rows' partial sums) as a write-through slab and
-    // draws an arrival ticket; the last arriver sums the slabs in slice order
-    // (the result does not depend on arrival order) and runs the epilogue.
-    // cdna_hip_programming.md "In-launch split-K reduction" (sc1 slab stores,
-    // relaxed agent ticket, acquire fence before the plain slab loads).
-    // Returns false in the workgroups that stop here; in the reducer vals
-    // hold the totals and kst[2*lrow..] the rows' total (sum, sum of squares).
-    static constexpr int SLAB = NTW * TE + 2 * R;  // floats per (tile, slice)
-    __device__ __forceinline__ bool ks_exchange(const FG& p, float* vals, float* red, const float* wsum,
-                                                int tile_id, int slice) {
-        float* slabs = p.ks_slab + (size_t)tile_id * p.ks * SLAB;
-        float* mine = slabs + (size_t)slice * SLAB;
-#pragma unroll
-        for (int i = 0; i < EPT; ++i) {
-            const int e = threadIdx.x + i * NT;
-            if (e < NTW * TE) __hip_atomic_store(mine + e, vals[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (p.fold_c1 && threadIdx.x < R) {  // this slice's row sums: its waves in order
-            float S1 = wsum[2 * threadIdx.x], S2 = wsum[2 * threadIdx.x + 1];
-            for (int ww = 1; ww < NW; ++ww) {
-                S1 += wsum[(ww * R + threadIdx.x) * 2];
-                S2 += wsum[(ww * R + threadIdx.x) * 2 + 1];
-            }
-            __hip_atomic_store(mine + NTW * TE + 2 * threadIdx.x, S1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(mine + NTW * TE + 2 * threadIdx.x + 1, S2, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0)
-            red[0] = __int_as_float(
-                __hip_atomic_fetch_add(p.ks_cnt + tile_id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        __syncthreads();
-        if (__float_as_int(red[0]) != p.ks - 1) return false;
-        // every slab load is an sc1 (agent-scope) load: no acquire fence, whose
-        // L2 invalidation would cost the other workgroups of this XCD their
-        // cached operands (measured: 2x slower GEMMs with the fence)
-        if (threadIdx.x == 0) __hip_atomic_store(p.ks_cnt + tile_id, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (int i = 0; i < EPT; ++i) {
-            const int e = threadIdx.x + i * NT;
-            if (e < NTW * TE) {
-                float v = ks_load(slabs + e);
-                for (int sl = 1; sl < p.ks; ++sl) v += ks_load(slabs + (size_t)sl * SLAB + e);
-                vals[i] = v;
-            }
-        }
-        if (p.fold_c1) {
-            if (threadIdx.x < 2 * R) {
-                float v = ks_load(slabs + NTW * TE + threadIdx.x);
-                for (int sl = 1; sl < p.ks; ++sl) v += ks_load(slabs + (size_t)sl * SLAB + NTW * TE + threadIdx.x);
-                red[threadIdx.x] = v;
-            }
-            __syncthreads();
-        }
-        return true;
-    }
-    __device__ __forceinline__ static float ks_load(const float* ptr) {
-        return __hip_atomic_load(ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-
     __device__ __forceinline__ void finish(const FG& p, const f32x4* acc, float* red, float* tile, int nt0,
-                                           int row0, const float* wsum, int tile_id = 0, int slice = 0) {
+                                           int row0, const float* wsum) {
         const int lane = threadIdx.x & 63;
         const int w = threadIdx.x >> 6;
 #pragma unroll
@@ -253,16 +154,13 @@ struct Epi {
             }
             vals[i] = val;
         }
-        const bool split = p.ks > 1;  // uniform
-        if (split && !ks_exchange(p, vals, red, wsum, tile_id, slice)) return;
-        apply(p, vals, red, tile, nt0, row0, wsum, split);
+        apply(p, vals, tile, nt0, row0, wsum);
     }
 
     // the epilogue proper on the folded values of the owned elements (vals[i]
-    // = element threadIdx.x + i*NT); red is read only for split LN-folded
-    // statistics; tile = LDS scratch for the row statistics
-    __device__ __forceinline__ void apply(const FG& p, const float* vals, const float* red, float* tile, int nt0,
-                                          int row0, const float* wsum, bool split) {
+    // = element threadIdx.x + i*NT); tile = LDS scratch for the row statistics
+    __device__ __forceinline__ void apply(const FG& p, const float* vals, float* tile, int nt0, int row0,
+                                          const float* wsum) {
         const bool rowstat = EPI == HPA_FEPI_LOGITS || (EPI == HPA_FEPI_RESID && p.stats_out);  // uniform
 #pragma unroll
         for (int i = 0; i < EPT; ++i) {
@@ -273,18 +171,11 @@ struct Epi {
                 where(e, nt0, row0, j, lrow, lcol, row, col);
                 const bool live = row < p.M && col < p.N;
                 if (EPI != HPA_FEPI_LOGITS && p.fold_c1) {  // sum_k LN(x)_k W_nk = rstd*(sum_k x_k W'_nk - mean*c1_n)
-                    float S1, S2;
-                    if (split) {  // slices in order (ks_exchange)
-                        S1 = red[2 * lrow];
-                        S2 = red[2 * lrow + 1];
-                    } else {
-                        S1 = wsum[2 * lrow];
-                        S2 = wsum[2 * lrow + 1];
+                    float S1 = wsum[2 * lrow], S2 = wsum[2 * lrow + 1];
 #pragma unroll
-                        for (int ww = 1; ww < NW; ++ww) {
-                            S1 += wsum[(ww * R + lrow) * 2];
-                            S2 += wsum[(ww * R + lrow) * 2 + 1];
-                        }
+                    for (int ww = 1; ww < NW; ++ww) {
+                        S1 += wsum[(ww * R + lrow) * 2];
+                        S2 += wsum[(ww * R + lrow) * 2 + 1];
                     }
                     const float m = S1 / p.K;  // layernorm_forward statistics, one-pass form
                     const float rstd = 1.0f / sqrtf(fmaxf(S2 / p.K - m * m, 0.f) + 1e-5f);
@@ -321,10 +212,10 @@ struct Epi {
                     }
                 } else if (EPI == HPA_FEPI_GELU) {
                     if (row < p.Mp && col < p.N)
-                        st_out<WT>(p.out + hpa::frag_index(row, col, p.N), live ? hpa::gelu_ref(val) : 0.f);
+                        p.out[hpa::frag_index(row, col, p.N)] = live ? hpa::gelu_ref(val) : 0.f;
                 } else if (EPI == HPA_FEPI_RESID) {
                     val = live ? pre_res[i] + val : 0.f;  // residual_forward(out, res, proj)
-                    if (row < p.Mp && col < p.N) st_out<WT>(p.out + hpa::frag_index(row, col, p.N), val);
+                    if (row < p.Mp && col < p.N) p.out[hpa::frag_index(row, col, p.N)] = val;
                     tile[(j * R + lrow) * 17 + lcol] = val;
                 } else {  // LOGITS
                     if (live) p.out[(size_t)row * p.N + col] = val;
@@ -346,8 +237,8 @@ struct Epi {
                             s1 += tr[c];
                             s2 += tr[c] * tr[c];
                         }
-                        st_out<WT>(p.stats_out + ((size_t)nt * p.Mp + row) * 2, s1);
-                        st_out<WT>(p.stats_out + ((size_t)nt * p.Mp + row) * 2 + 1, s2);
+                        p.stats_out[((size_t)nt * p.Mp + row) * 2] = s1;
+                        p.stats_out[((size_t)nt * p.Mp + row) * 2 + 1] = s2;
                     } else {
                         float bv = tr[0];
                         int bi = 0;
@@ -438,21 +329,19 @@ constexpr int gemm16_lds_floats() {
 
 // body of the looped GEMM workgroup `bid` of the XCD-ordered 1-D grid
 // (gemm16_kernel, and the GEMM role of the pipelined combo launches)
-template <int NW, int EPI, int MT, int NTW, int UD = 0, bool WT = false>
+template <int NW, int EPI, int MT, int NTW>
 __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
     constexpr int R = MT * 16;  // rows per workgroup
-    // k-steps per trip (two trips in flight; register budget); UD > 0: the
-    // "deep" variant's larger trips (more bytes in flight per wave for the
-    // MFMA-bound shapes)
-    constexpr int U = UD > 0 ? UD : (NTW > 1 ? 1 : (NW >= 16 ? (MT == 4 ? 1 : 2) : (MT == 4 ? 2 : 4)));
+    // k-steps per trip (two trips in flight; register budget)
+    constexpr int U = NTW > 1 ? 1 : (NW >= 16 ? (MT == 4 ? 1 : 2) : (MT == 4 ? 2 : 4));
     float* lngb = smem;                              // LN weight [K], bias [K]
     float* red = smem + 2 * HPA_FUSED_LN_KMAX;       // [NW][NTW][MT rb x 4 reg][64 lanes]
     float* tile = red + NW * MT * NTW * 256;         // [NTW][R rows][17]
     float* lnst = tile + NTW * R * 17;               // [R][2] mean, rstd
     float* lnscr = lnst + 2 * R;                     // [4R][2]
 
-    int cx, ry, slice;
-    if (!xcd_tile(p, bid, cx, ry, slice)) return;
+    int cx, ry;
+    if (!xcd_tile(p, bid, cx, ry)) return;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     const int nt0 = cx * NTW;
@@ -460,12 +349,10 @@ __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
     const int row0 = rb0 * 16;
     const int q4 = lane >> 4;  // which 4-k group of the 16-k step
 
-    // ---- this wave's contiguous k-step range (inside this workgroup's K slice)
-    const int kspan = (p.K16 + p.ks - 1) / p.ks;
-    const int ks0 = slice * kspan, ks1 = min(p.K16, ks0 + kspan);
-    const int per = (ks1 - ks0 + NW - 1) / NW;
-    const int kb0 = ks0 + w * per;
-    const int nsteps = max(0, min(ks1, kb0 + per) - kb0);
+    // ---- this wave's contiguous k-step range
+    const int per = (p.K16 + NW - 1) / NW;
+    const int kb0 = w * per;
+    const int nsteps = max(0, min(p.K16, kb0 + per) - kb0);
     const float4* __restrict__ wf[NTW];
 #pragma unroll
     for (int j = 0; j < NTW; ++j)  // tail tiles past ntn re-read the last tile (never stored)
@@ -553,15 +440,15 @@ __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
     if (fold)  // [NW][R][2] over the LN weight area (unused when folded)
 #pragma unroll
         for (int r = 0; r < MT; ++r) row_sums_publish(fs1[r], fs2[r], lngb + (w * R + 16 * r) * 2);
-    Epi<NW, EPI, MT, NTW, WT> epi;
+    Epi<NW, EPI, MT, NTW> epi;
     epi.prefetch(p, nt0, row0);
-    epi.finish(p, acc, red, tile, nt0, row0, lngb, cx * p.gy + ry, slice);
+    epi.finish(p, acc, red, tile, nt0, row0, lngb);
 }
 
-template <int NW, int EPI, int MT, int NTW, int UD = 0>
+template <int NW, int EPI, int MT, int NTW>
 __global__ __launch_bounds__(NW * 64) void gemm16_kernel(FG p) {
     __shared__ __attribute__((aligned(16))) float smem[gemm16_lds_floats<NW, MT, NTW>()];
-    gemm16_body<NW, EPI, MT, NTW, UD>(p, blockIdx.x, smem);
+    gemm16_body<NW, EPI, MT, NTW>(p, blockIdx.x, smem);
 }
 
 // One-shot variant for the layer GEMMs (one 16-row block per workgroup,
@@ -575,7 +462,7 @@ constexpr int gemm16_os_lds_floats() {
     return 2 * HPA_FUSED_LN_KMAX + NW * 256 + 16 * 17 + 2 * 16;
 }
 
-template <int NW, int EPI, int S, bool WT = false>
+template <int NW, int EPI, int S>
 __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem) {
     constexpr int NT = NW * 64;
     float* lngb = smem;                         // LN weight [K], bias [K]
@@ -585,13 +472,12 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
 
     int nt, ry;
     if (!xcd_tile(p, bid, nt, ry)) return;
-    HPA_TS(0, bid);
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     const int row0 = ry * 16;
     const int q4 = lane >> 4;
-    const bool fold = HPA_OS_EXP != 1 && p.fold_c1 != nullptr;  // LN folded into w: row sums from xv
-    const bool ln_apply = HPA_OS_EXP != 1 && p.ln_stats != nullptr && !fold;
+    const bool fold = p.fold_c1 != nullptr;  // LN folded into w: row sums from xv
+    const bool ln_apply = p.ln_stats != nullptr && !fold;
 
     // 1. LN statistics partials of the 16 rows: 4 threads per row, issued first
     constexpr int SPT = 12;  // partial tiles per thread: ln_ntiles <= 48 (C <= 768); else looped
@@ -615,9 +501,8 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
         lb4 = reinterpret_cast<const float4*>(p.ln_b)[threadIdx.x];
     }
     // 3. all operand fragments of this wave's k range [w*S, w*S+S)
-    const int nt_ld = HPA_OS_EXP == 3 ? 0 : nt, ry_ld = HPA_OS_EXP == 3 ? 0 : ry;
-    const float4* __restrict__ wf = reinterpret_cast<const float4*>(p.w) + ((size_t)nt_ld * p.K16 + w * S) * 64 + lane;
-    const float4* __restrict__ xf = reinterpret_cast<const float4*>(p.x) + ((size_t)ry_ld * p.K16 + w * S) * 64 + lane;
+    const float4* __restrict__ wf = reinterpret_cast<const float4*>(p.w) + ((size_t)nt * p.K16 + w * S) * 64 + lane;
+    const float4* __restrict__ xf = reinterpret_cast<const float4*>(p.x) + ((size_t)ry * p.K16 + w * S) * 64 + lane;
     // issued strictly in k-step order (a scheduling barrier per step): the
     // chain below then waits for each step's pair with a descending vmcnt and
     // the MFMAs of early steps overlap the arrival of later ones (left to
@@ -626,16 +511,13 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
     float4 wv[S], xv[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-        wv[s] = wf[s * 64];  // default policy: nt measured no faster here (tools/ab_bench.sh)
+        wv[s] = wf[s * 64];  // default policy: nt measured no faster here
         xv[s] = xf[s * 64];
-#if HPA_OS_ORDER
         __builtin_amdgcn_sched_barrier(0);
-#endif
     }
     // 4. epilogue operands
-    Epi<NW, EPI, 1, 1, WT> epi;
+    Epi<NW, EPI, 1, 1> epi;
     epi.prefetch(p, nt, row0);
-    HPA_TS(1, bid);
 
     // LN: reduce the statistics (waits only for the loads of step 1) into
     // lnst; the 4 threads of a row are adjacent lanes of wave 0
@@ -684,7 +566,6 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
         rs = lnst[2 * (lane & 15) + 1];
     }
 
-    HPA_TS(2, bid);
     // one accumulator chain: the same k order as gemm16_kernel with NW waves
     f32x4 acc[1];
     acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -694,24 +575,11 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
     for (int s = 0; s < S; ++s) {
         float4 xa = xv[s];
         if (ln_apply) xa = ln4(xa, mu, rs, sg[4 * (w * S + s)], sbv[4 * (w * S + s)]);
-#if HPA_OS_EXP == 2
-        acc[0][0] += xa.x * wv[s].x + xa.y * wv[s].y;
-        acc[0][1] += xa.z * wv[s].z + xa.w * wv[s].w;
-#else
         acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.x, wv[s].x, acc[0], 0, 0, 0);
         acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.y, wv[s].y, acc[0], 0, 0, 0);
         acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.z, wv[s].z, acc[0], 0, 0, 0);
         acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.w, wv[s].w, acc[0], 0, 0, 0);
-#endif
     }
-#if HPA_OS_EXP == 4
-    if (acc[0][0] == 1.2345f && acc[0][1] == 5.4321f) asm volatile("" ::"v"(acc[0][2]));  // no epilogue
-    return;
-#endif
-#ifdef HPA_TS_ACC
-    HPA_TS_ACC(acc[0]);
-#endif
-    HPA_TS(3, bid);
     if (fold) {  // published by the fold's barrier in finish(): [NW][16][2] over the LN weight area
         float fs1 = 0.f, fs2 = 0.f;
 #pragma unroll
@@ -719,7 +587,6 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
         row_sums_publish(fs1, fs2, lngb + w * 32);
     }
     epi.finish(p, acc, red, tile, nt, row0, lngb);
-    HPA_TS(4, bid);
 }
 
 template <int NW, int EPI, int S>
@@ -742,9 +609,6 @@ int launch_b16(const FG& p, int epi, int nw, int mt, int ntw);
 // A-resident bf16 variant (variant 5): waves 4/8, row_blocks (mt) 1/2/4 with
 // mt*K <= 3200; each workgroup takes waves*rounds column tiles
 int launch_b16_ares(const FG& p, int epi, int nw, int mt, int rounds);
-// A-resident fp32 kernel (hpa_gemm_ares.hip, variant 5 with fp32 weights):
-// waves 4/8, row_blocks 2 (K <= 768) or 1 (K <= 1600)
-int launch_f32_ares(const FG& p, int epi, int nw, int mt, int rounds);
 
 static inline int fused_prepare(const HpaFusedGemm* g, FG* p) {
     HPA_REQUIRE(g && g->x && g->w && g->out, "gemm_fused: null operand");
@@ -778,11 +642,6 @@ static inline int fused_prepare(const HpaFusedGemm* g, FG* p) {
     p->pos = g->pos;
     p->row_seq = g->row_seq;
     p->fold_c1 = g->ln_fold_c1;
-    p->ks = g->k_slices > 1 ? g->k_slices : 1;
-    p->ks_slab = g->ks_slab;
-    p->ks_cnt = g->ks_count;
-    HPA_REQUIRE(p->ks == 1 || (g->ks_slab && g->ks_count && p->ks <= 16 && p->ks <= p->K16),
-                "gemm_fused: k_slices needs ks_slab / ks_count, <= 16 and <= K/16");
     HPA_REQUIRE(!g->ln_fold_c1 || g->epilogue != HPA_FEPI_LOGITS, "gemm_fused: ln_fold_c1 with LOGITS");
     if (g->epilogue == HPA_FEPI_QKV) {
         const HpaKVPool* pool = g->pool;

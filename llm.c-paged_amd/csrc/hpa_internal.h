@@ -11,7 +11,6 @@
 // (cudaCheck convention, reference train_gpt2.cu:27-34).
 int hpa_fail(const char* file, int line, const char* what);
 hipStream_t hpa_stream();
-int hpa_stream_cus();  // CU budget of the current stream (0 = whole device)
 
 #define HPA_CHECK(call)                                                          \
     do {                                                                         \

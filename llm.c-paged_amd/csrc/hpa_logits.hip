@@ -270,7 +270,7 @@ int logits_resident_grid(const FG& p) {
             g_num_cus <= 0)
             return hpa_fail(__FILE__, __LINE__, "logits: CU count"), 1;
     }
-    const int cus = hpa_stream_cus() > 0 ? hpa_stream_cus() : g_num_cus;
+    const int cus = g_num_cus;
     return min(p.ntn, cus);
 }
 

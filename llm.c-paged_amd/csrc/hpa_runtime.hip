@@ -19,22 +19,6 @@ int hpa_fail(const char* file, int line, const char* what) {
 
 hipStream_t hpa_stream() { return g_stream; }
 
-// CU-masked streams (hpa_stream_create_cumask), one per CU range, kept for
-// the life of the process: destroying a CU-masked stream was seen to block in
-// hipStreamDestroy after a few create/destroy cycles, so they are cached and
-// reused instead.  ncu = the CU budget persistent kernels size their grids by.
-static struct { hipStream_t s; int lo, hi, ncu; } g_masked[16];
-int hpa_stream_cus() {
-    for (auto& m : g_masked)
-        if (m.s && m.s == g_stream) return m.ncu;
-    return 0;
-}
-static bool is_masked(hipStream_t s) {
-    for (auto& m : g_masked)
-        if (m.s && m.s == s) return true;
-    return false;
-}
-
 extern "C" {
 
 const char* hpa_last_error(void) { return g_last_error; }
@@ -180,49 +164,7 @@ void* hpa_stream_create(void) {
     return (void*)s;
 }
 
-/* a stream whose kernels run only on the CUs of mask bits [lo, hi).  The
- * driver deals mask bits round-robin over the XCDs (bit i -> XCD i % 8 on
- * MI355X), so a contiguous bit range is an equal share of every XCD. */
-void* hpa_stream_create_cumask(int lo, int hi) {
-    int dev = g_device >= 0 ? g_device : 0, ncu = 0;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0 ||
-        lo < 0 || hi > ncu || lo >= hi) {
-        hpa_fail(__FILE__, __LINE__, "hpa_stream_create_cumask: bad CU range");
-        return nullptr;
-    }
-    for (auto& m : g_masked)
-        if (m.s && m.lo == lo && m.hi == hi) return (void*)m.s;
-    uint32_t mask[32] = {0};
-    const int words = (ncu + 31) / 32;
-    if (words > 32) {
-        hpa_fail(__FILE__, __LINE__, "hpa_stream_create_cumask: too many CUs");
-        return nullptr;
-    }
-    for (int i = lo; i < hi; i++) mask[i / 32] |= 1u << (i % 32);
-    int slot = -1;
-    for (int i = 0; i < 16; i++)
-        if (!g_masked[i].s) {
-            slot = i;
-            break;
-        }
-    if (slot < 0) {
-        hpa_fail(__FILE__, __LINE__, "hpa_stream_create_cumask: too many CU ranges");
-        return nullptr;
-    }
-    hipStream_t s = nullptr;
-    if (hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask) != hipSuccess) {
-        hpa_fail(__FILE__, __LINE__, "hipExtStreamCreateWithCUMask failed");
-        return nullptr;
-    }
-    g_masked[slot].s = s;
-    g_masked[slot].lo = lo;
-    g_masked[slot].hi = hi;
-    g_masked[slot].ncu = hi - lo;
-    return (void*)s;
-}
-
 int hpa_stream_destroy(void* s) {
-    if (s && is_masked((hipStream_t)s)) return 0;  // cached for reuse (see g_masked)
     if (s) HPA_CHECK(hipStreamDestroy((hipStream_t)s));
     return 0;
 }
@@ -241,6 +183,11 @@ float hpa_event_elapsed_ms(void* start, void* stop) {
     if (hipEventSynchronize((hipEvent_t)stop) != hipSuccess) return -1.f;
     if (hipEventElapsedTime(&ms, (hipEvent_t)start, (hipEvent_t)stop) != hipSuccess) return -1.f;
     return ms;
+}
+
+int hpa_event_synchronize(void* ev) {
+    if (ev) HPA_CHECK(hipEventSynchronize((hipEvent_t)ev));
+    return 0;
 }
 
 int hpa_event_destroy(void* ev) {

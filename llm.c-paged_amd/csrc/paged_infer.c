@@ -565,87 +565,93 @@ void print_generated_sequence(int* tokens, int B, int T) {
     }
 }
 
+
 /* ------------------------------------------------------------------------ */
 /* decode engine                                                            */
 /* ------------------------------------------------------------------------ */
-/* a micro-batch lane: a contiguous group of the batch's sequences (rows
- * r0..r0+B-1) that runs the whole fused step on its own stream with its own
- * activations, so one lane's HBM-bound attention overlaps another lane's
- * latency-bound GEMMs.  Lane 0 runs on the launch stream; the others fork from
- * it and join back (captured into the same graph as parallel branches). */
+/* One batched decode step = embed, then per layer QKV(+LN1, +KV append) ->
+ * paged attention -> attproj(+residual) -> fc(+LN2, +GELU) ->
+ * fcproj(+residual), then logits(+LNf) and the token choice: 5 launches per
+ * layer + 3, replayed as one hipGraph (reference gpt2_forward,
+ * paged_infer.c:575-729, for one new token per sequence). */
+
 /* manager page index -> pool slot (page_map_create) */
 typedef struct {
     HpaKVPool* pool;
     int* map;
 } PageView;
 
-#define DEC_MAX_LANES 8
+/* the end-of-step gather of a sequence-sharded decode (gpt2_decode_shard) */
 typedef struct {
-    int r0, B, Mp;
-    float *res, *res2, *att, *fch, *st1, *st2, *part;
-    float* astate; /* attention chunk state (pipelined step) */
-    float* ks_slab; /* split-K slabs of the layer GEMMs (hpa_fused_ks_workspace), NULL if none */
-    int* ks_cnt;    /* their per-tile arrival counters (zeroed once; launches leave them zero) */
-    size_t ks_slab_floats, ks_counters;
-    void* stream; /* NULL for lane 0 (the launch stream) */
-    void* ev_join;
-} DecLane;
-
-struct GPT2Decode;
-/* attention profiling events of (layer, lane): k = 0 start, 1 stop */
-#define PROF_EV(d, l, lane, k) ((d)->prof_ev[(((size_t)(l) * DEC_MAX_LANES + (lane)) << 1) + (k)])
+    int nranks, rank, root;
+    int* rows;        /* [nranks] sequences per rank, rank order */
+    size_t* bytes;    /* [nranks] bytes per rank of the current gather */
+    void* stream;     /* communication stream */
+    float* send[2];   /* double-buffered copies of this rank's logits [B][V] */
+    float* recv[2];   /* root: [sum rows][V] */
+    int* send_ids[2];
+    int* recv_ids[2];
+    void* ev_ready[2]; /* send buffer k filled (compute stream) */
+    void* ev_done[2];  /* gather from buffer k done (comm stream) */
+    int k, last, pending[2];
+} DecShard;
 
 struct GPT2Decode {
-    int B, P, max_ctx, max_pages;
+    int B, P, max_ctx, max_pages, Mp;
     HpaKVPool pool;
     BlockManager* bm;
     int own_bm;
     int bt_stride;
-    int* d_bt;        /* [max_prompts][bt_stride] device mirror of bm->block_table */
+    int* d_bt;        /* [max_prompts][bt_stride] device mirror of bm->block_table (pool slots) */
     int* d_pos;       /* [B] */
     int* d_tokens;    /* [B] */
     int* d_next;      /* [B] */
     int* h_pos;       /* host mirror of d_pos */
-    int* h_stage;     /* pinned staging: tokens / next */
-    int* h_bt_stage;  /* pinned staging for block-table rows */
-    PageView pv;      /* manager page index -> pool slot (page_map_create) */
-    float *d_res, *d_res2, *d_ln, *d_q, *d_att, *d_fch, *d_part, *d_logits;
-    int split[4];     /* qkv, attproj, fc, fcproj */
-    /* fused path (hpa_gemm_fused): frag-layout weights and activations */
-    int fused;
+    char* h_evicted;  /* [B] sequences paged out by the LRU policy since the last query */
+    /* pinned staging, double-buffered: a buffer is rewritten only after the
+     * event recorded behind its previous upload has completed (no stream sync) */
+    int* h_tok[2];
+    void* ev_tok[2];
+    int tok_k;
+    int* h_bt[2];
+    void* ev_bt[2];
+    int bt_k;
+    int* h_next;      /* pinned readback of the next ids */
+    PageView pv;
+    float* d_q;       /* [B][C] row-major */
+    float* d_logits;  /* [B][V] */
+    /* frag-layout activations [Mp][*] (padded rows stay zero) and LN statistics */
+    float *res, *res2, *att, *fch, *st1, *st2, *part;
     float* d_wpack;   /* packed qkvw, attprojw, fcw, fcprojw of every layer, then wte */
     int w_bf16;       /* weights packed bf16 (hpa_pack_frag_bf16; offsets in elements) */
-    size_t wpack_off[5]; /* per-layer strides (0..3) and wte offset (4) */
+    size_t wpack_off[5]; /* per-layer offsets (0..3) and wte offset (4) */
     float* d_fold;    /* LN folded into qkvw / fcw (hpa_ln_fold_pack): per layer c1, c2 of
                          qkv [3C] [3C] then fc [4C] [4C]; NULL: LN applied on the operand path */
     int fwaves[5];    /* waves per workgroup: qkv, attproj, fc, fcproj, logits */
     int frb[5];       /* 16-row blocks per workgroup, same order */
     int fct[5];       /* 16-column tiles per workgroup, same order */
-    int fks[5];       /* K slices (workgroups per output tile), same order */
-    DecLane lanes[DEC_MAX_LANES];
-    int nlanes;
-    int pipeline;     /* 1: two lanes, attention chunks beside the other lane's GEMMs */
-    int split_cus;    /* > 0: split step, the GEMM chains on this many CUs (dec_launch_split) */
-    void *s_att, *s_gemm; /* CU-masked streams of the split step */
-    void** sp_ev;     /* [2][L+1][2] split-step events: kind (Q ready, attention done), layer, lane */
-    int overlap;      /* > 0: overlapped step (dec_launch_overlap) with this many chain workgroups */
-    unsigned* d_ctl;  /* [2L+2][HPA_LANE_CTL_WORDS] in-launch hand-off counters, zeroed per step */
+    int attn_splits;  /* context ranges per (sequence, head) of the decode attention */
+    void* d_attn_ws;  /* split records + counters (hpa_attn_ws_bytes at HPA_ATTN_MAX_SPLITS) */
+    size_t attn_ws_bytes;
     int sample;       /* 0: greedy argmax; 1: multinomial with per-sequence xorshift */
     unsigned long long* d_rng; /* [B] sampler states */
-    /* prefill workspace (gpt2_decode_prefill), rows R = B*T, grown on demand */
-    int pf_cap;       /* row capacity */
+    /* prefill workspace (gpt2_decode_prefill), rows R = sum of lengths, grown on demand */
+    int pf_cap;
     float *pf_res, *pf_res2, *pf_att, *pf_fch, *pf_st1, *pf_st2, *pf_q;
     int *pf_tok, *pf_pos, *pf_seq, *pf_start, *pf_last, *h_pf;
-    void* ev_fork;
     int use_graph;
     void* graph;
-    /* per-layer HIP events around the attention launch (eager profiling) */
-    void** prof_ev;   /* [L][2] or NULL */
-    double prof_ms;   /* accumulated attention kernel time */
+    void* prof_ev[2];  /* eager profiling: events around every attention launch */
+    int profiling;
+    double prof_ms;
     long prof_launches;
+    DecShard* shard;
+    /* gpt2_forward: token at every cached position [B][max_ctx] and, when it
+     * fits, the logits of every position [B][max_ctx][V] (managed) */
+    int* h_hist;
+    float* pos_logits;
 };
 
-/* the pool view backend: page payload pointers are layer-0 tiles in HBM */
 /* the manager's page index -> pool slot: a fixed pseudo-random permutation,
  * so that whatever order pages are allocated in (first-fit hands each
  * sequence a contiguous run) the K/V streams of concurrent workgroups spread
@@ -672,6 +678,7 @@ static int* page_map_create(int n, int G) {
     return map;
 }
 
+/* the pool view backend: page payload pointers are layer-0 tiles in HBM */
 static void* pool_view_alloc(void* ctx, int page, int kv, size_t bytes) {
     (void)bytes;
     PageView* v = (PageView*)ctx;
@@ -680,113 +687,6 @@ static void* pool_view_alloc(void* ctx, int page, int kv, size_t bytes) {
 }
 static void pool_view_release(void* ctx, int page, int kv, void* p) {
     (void)ctx; (void)page; (void)kv; (void)p;
-}
-
-static void dec_prof_free(GPT2Decode* d, int L) {
-    if (!d->prof_ev) return;
-    for (size_t i = 0; i < 2 * (size_t)L * DEC_MAX_LANES; i++) hpa_event_destroy(d->prof_ev[i]);
-    free(d->prof_ev);
-    d->prof_ev = NULL;
-}
-
-static void dec_split_free(GPT2Decode* d, int L) {
-    if (d->sp_ev)
-        for (int i = 0; i < 4 * (L + 1); i++) hpa_event_destroy(d->sp_ev[i]);
-    free(d->sp_ev);
-    d->sp_ev = NULL;
-    hpa_stream_destroy(d->s_att);
-    hpa_stream_destroy(d->s_gemm);
-    d->s_att = d->s_gemm = NULL;
-    d->split_cus = 0;
-}
-
-static void dec_overlap_free(GPT2Decode* d) {
-    hpa_free(d->d_ctl);
-    d->d_ctl = NULL;
-    d->overlap = 0;
-}
-
-static void dec_lanes_free(GPT2Decode* d) {
-    for (int i = 0; i < d->nlanes; i++) {
-        DecLane* ln = &d->lanes[i];
-        hpa_free(ln->res); hpa_free(ln->res2); hpa_free(ln->att); hpa_free(ln->fch);
-        hpa_free(ln->st1); hpa_free(ln->st2); hpa_free(ln->part); hpa_free(ln->astate);
-        hpa_free(ln->ks_slab); hpa_free(ln->ks_cnt);
-        hpa_stream_destroy(ln->stream);
-        hpa_event_destroy(ln->ev_join);
-        memset(ln, 0, sizeof(*ln));
-    }
-    d->nlanes = 0;
-}
-
-/* split-K workspace of every lane: the largest of its four layer GEMMs at the
- * current launch shapes (d->fwaves / frb / fct / fks) */
-static int dec_ks_alloc(GPT2Decode* d, int C) {
-    const int shp[4][2] = {{3 * C, C}, {C, C}, {4 * C, C}, {C, 4 * C}};
-    for (int i = 0; i < d->nlanes; i++) {
-        DecLane* ln = &d->lanes[i];
-        size_t need_f = 0, need_c = 0;
-        for (int k = 0; k < 4; k++) {
-            HpaFusedGemm g;
-            memset(&g, 0, sizeof(g));
-            g.M = ln->B; g.N = shp[k][0]; g.K = shp[k][1];
-            g.waves = d->fwaves[k]; g.row_blocks = d->frb[k]; g.col_tiles = d->fct[k]; g.k_slices = d->fks[k];
-            size_t f, c;
-            if (hpa_fused_ks_workspace(&g, &f, &c)) return 1;
-            if (f > need_f) need_f = f;
-            if (c > need_c) need_c = c;
-        }
-        if (need_f <= ln->ks_slab_floats && need_c <= ln->ks_counters) continue;
-        hpa_free(ln->ks_slab); hpa_free(ln->ks_cnt);
-        ln->ks_slab = (float*)hpa_malloc(need_f * 4);
-        ln->ks_cnt = (int*)hpa_malloc(need_c * 4);
-        if (!ln->ks_slab || !ln->ks_cnt || hpa_memset_async(ln->ks_cnt, 0, need_c * 4)) return 1;
-        ln->ks_slab_floats = need_f;
-        ln->ks_counters = need_c;
-    }
-    return hpa_synchronize();
-}
-
-/* split the batch into up to `n` lanes of whole 16-row blocks */
-static int dec_lanes_alloc(GPT2Decode* d, int n, int C, int V, int NH) {
-    dec_lanes_free(d);
-    int blocks = (d->B + 15) / 16;
-    if (n < 1) n = 1;
-    if (n > DEC_MAX_LANES) n = DEC_MAX_LANES;
-    if (n > blocks) n = blocks;
-    const int per = (blocks + n - 1) / n; /* 16-row blocks per lane */
-    const int ct = C / 16;
-    int r0 = 0;
-    for (int i = 0; i < n && r0 < d->B; i++) {
-        DecLane* ln = &d->lanes[i];
-        ln->r0 = r0;
-        ln->B = d->B - r0 < per * 16 ? d->B - r0 : per * 16;
-        ln->Mp = (ln->B + 15) / 16 * 16;
-        r0 += ln->B;
-        d->nlanes = i + 1;
-        const size_t Mp = ln->Mp;
-        ln->res = (float*)hpa_malloc(Mp * C * 4);
-        ln->res2 = (float*)hpa_malloc(Mp * C * 4);
-        ln->att = (float*)hpa_malloc(Mp * C * 4);
-        ln->fch = (float*)hpa_malloc(Mp * 4 * C * 4);
-        ln->st1 = (float*)hpa_malloc((size_t)ct * Mp * 2 * 4);
-        ln->st2 = (float*)hpa_malloc((size_t)ct * Mp * 2 * 4);
-        ln->part = (float*)hpa_malloc((size_t)((V + 15) / 16) * Mp * 2 * 4);
-        ln->astate = (float*)hpa_malloc(hpa_attn_state_elems(ln->B, NH) * 4);
-        ln->ev_join = hpa_event_create_nt();
-        if (i > 0) ln->stream = hpa_stream_create();
-        if (!ln->res || !ln->res2 || !ln->att || !ln->fch || !ln->st1 || !ln->st2 || !ln->part || !ln->astate ||
-            !ln->ev_join || (i > 0 && !ln->stream))
-            return 1;
-        /* padded rows stay zero forever */
-        if (hpa_memset_async(ln->res, 0, Mp * C * 4) || hpa_memset_async(ln->res2, 0, Mp * C * 4) ||
-            hpa_memset_async(ln->att, 0, Mp * C * 4) || hpa_memset_async(ln->fch, 0, Mp * 4 * C * 4) ||
-            hpa_memset_async(ln->st1, 0, (size_t)ct * Mp * 2 * 4) ||
-            hpa_memset_async(ln->st2, 0, (size_t)ct * Mp * 2 * 4))
-            return 1;
-    }
-    if (hpa_synchronize()) return 1;
-    return dec_ks_alloc(d, C);
 }
 
 static void dec_prefill_free(GPT2Decode* d) {
@@ -799,55 +699,89 @@ static void dec_prefill_free(GPT2Decode* d) {
     d->pf_cap = 0;
 }
 
+static void dec_shard_free(GPT2Decode* d) {
+    DecShard* s = d->shard;
+    if (!s) return;
+    if (s->stream) {
+        void* prev = hpa_get_stream();
+        hpa_set_stream(s->stream);
+        hpa_synchronize();
+        hpa_set_stream(prev);
+    }
+    for (int k = 0; k < 2; k++) {
+        hpa_free(s->send[k]); hpa_free(s->recv[k]); hpa_free(s->send_ids[k]); hpa_free(s->recv_ids[k]);
+        hpa_event_destroy(s->ev_ready[k]);
+        hpa_event_destroy(s->ev_done[k]);
+    }
+    hpa_stream_destroy(s->stream);
+    free(s->rows);
+    free(s->bytes);
+    free(s);
+    d->shard = NULL;
+}
+
+/* every teardown and error path: a caller-owned manager gets its pages back
+ * and its default backend, so it never keeps pointers into the freed pool */
 static void dec_free(GPT2Decode* d) {
     if (!d) return;
+    hpa_synchronize();
+    if (!d->own_bm && d->bm && d->pv.map) {
+        for (int p = 0; p < d->bm->max_prompts; p++)
+            if (d->bm->prompt_block_count[p]) free_blocks_for_prompt(d->bm, p);
+        bm_set_backend(d->bm, NULL);
+    }
+    dec_shard_free(d);
     dec_prefill_free(d);
-    dec_prof_free(d, d->pool.num_layers);
-    dec_split_free(d, d->pool.num_layers);
-    dec_overlap_free(d);
+    for (int k = 0; k < 2; k++) {
+        hpa_event_destroy(d->prof_ev[k]);
+        hpa_event_destroy(d->ev_tok[k]);
+        hpa_event_destroy(d->ev_bt[k]);
+        hpa_host_free(d->h_tok[k]);
+        hpa_host_free(d->h_bt[k]);
+    }
     if (d->graph) hpa_graph_destroy(d->graph);
     hpa_pool_destroy(&d->pool);
     hpa_free(d->d_bt); hpa_free(d->d_pos); hpa_free(d->d_tokens); hpa_free(d->d_next);
-    hpa_free(d->d_res); hpa_free(d->d_res2); hpa_free(d->d_ln); hpa_free(d->d_q);
-    hpa_free(d->d_att); hpa_free(d->d_fch); hpa_free(d->d_part); hpa_free(d->d_logits);
+    hpa_free(d->d_q); hpa_free(d->d_logits);
+    hpa_free(d->res); hpa_free(d->res2); hpa_free(d->att); hpa_free(d->fch);
+    hpa_free(d->st1); hpa_free(d->st2); hpa_free(d->part);
     hpa_free(d->d_wpack);
     hpa_free(d->d_fold);
+    hpa_free(d->d_attn_ws);
     hpa_free(d->d_rng);
-    dec_lanes_free(d);
-    hpa_event_destroy(d->ev_fork);
-    hpa_host_free(d->h_stage);
-    hpa_host_free(d->h_bt_stage);
+    hpa_free(d->pos_logits);
+    hpa_host_free(d->h_next);
     free(d->pv.map);
     free(d->h_pos);
+    free(d->h_evicted);
+    free(d->h_hist);
     if (d->own_bm) destroy_block_manager(d->bm);
     free(d);
 }
 
 void gpt2_decode_free(GPT2* model) {
     if (model && model->decode) {
-        hpa_synchronize();
         dec_free(model->decode);
         model->decode = NULL;
     }
 }
 
-/* fused path state: frag-packed weights (packed once; the weights stay also
- * in checkpoint layout for the embedding gather and the reference API),
- * frag-layout activations and LN statistics */
-static int dec_init_fused(GPT2* model, GPT2Decode* d) {
+/* frag-packed weights (packed once; the weights stay also in checkpoint
+ * layout for the embedding gather and the reference API), frag-layout
+ * activations, LN statistics, launch shapes */
+static int dec_init_weights(GPT2* model, GPT2Decode* d) {
     const GPT2Config c = model->config;
     const int B = d->B, C = c.channels, L = c.num_layers, V = c.vocab_size;
     const ParameterTensors* w = &model->params;
-    d->fused = 1;
-    size_t e_qkv = hpa_frag_elems(3 * C, C), e_ap = hpa_frag_elems(C, C);
-    size_t e_fc = hpa_frag_elems(4 * C, C), e_fp = hpa_frag_elems(C, 4 * C);
-    size_t e_layer = e_qkv + e_ap + e_fc + e_fp;
+    const size_t e_qkv = hpa_frag_elems(3 * C, C), e_ap = hpa_frag_elems(C, C);
+    const size_t e_fc = hpa_frag_elems(4 * C, C), e_fp = hpa_frag_elems(C, 4 * C);
+    const size_t e_layer = e_qkv + e_ap + e_fc + e_fp;
     d->wpack_off[0] = 0;
     d->wpack_off[1] = e_qkv;
     d->wpack_off[2] = e_qkv + e_ap;
     d->wpack_off[3] = e_qkv + e_ap + e_fc;
     d->wpack_off[4] = e_layer * L; /* wte */
-    size_t total = d->wpack_off[4] + hpa_frag_elems(V, C);
+    const size_t total = d->wpack_off[4] + hpa_frag_elems(V, C);
     d->d_wpack = (float*)hpa_malloc(total * (d->w_bf16 ? 2 : 4));
     if (!d->d_wpack) return 1;
     if (d->w_bf16) { /* bf16 weights: same element offsets, 2 bytes each; LN on the operand path */
@@ -862,37 +796,22 @@ static int dec_init_fused(GPT2* model, GPT2Decode* d) {
                 return 1;
         }
         if (hpa_pack_frag_bf16(w->wte, V, C, C, b16 + d->wpack_off[4])) return 1;
-        d->d_fold = NULL;
-        for (int i = 0; i < 5; i++) {
-            /* launch shapes by (M, N, K) in the library (hpa_fused_pick_bf16*) */
-            d->fwaves[i] = d->frb[i] = d->fct[i] = 0;
-            d->fks[i] = 1;
-        }
-        d->ev_fork = hpa_event_create_nt();
-        if (!d->ev_fork) return 1;
-        return dec_lanes_alloc(d, 1, C, V, c.num_heads);
+        for (int i = 0; i < 5; i++) d->fwaves[i] = d->frb[i] = d->fct[i] = 0; /* by (M, N, K) in the library */
+        return 0;
     }
-    /* LN1 / LN2 folded into the qkv / fc weights (default; HPA_LN_FOLD=0 keeps
-     * the LN on the operand path): the GEMM then starts on x as it stands and
-     * the row statistics are needed only in its epilogue */
-    const char* fe = getenv("HPA_LN_FOLD");
-    const int fold = !(fe && fe[0] == '0');
-    d->d_fold = NULL;
-    if (fold) {
-        d->d_fold = (float*)hpa_malloc((size_t)L * 14 * C * 4);
-        if (!d->d_fold) return 1;
-    }
+    /* LN1 / LN2 folded into the qkv / fc weights: the GEMM then starts on x
+     * as it stands and the row statistics are needed only in its epilogue */
+    d->d_fold = (float*)hpa_malloc((size_t)L * 14 * C * 4);
+    if (!d->d_fold) return 1;
     for (int l = 0; l < L; l++) {
         float* base = d->d_wpack + e_layer * l;
         const size_t lc = (size_t)l * C;
-        float* fl = fold ? d->d_fold + (size_t)l * 14 * C : NULL;
-        if ((fold ? hpa_ln_fold_pack(w->qkvw + lc * 3 * C, 3 * C, C, w->ln1w + lc, w->ln1b + lc,
-                                     w->qkvb + 3 * lc, base + d->wpack_off[0], fl, fl + 3 * C)
-                  : hpa_pack_frag(w->qkvw + lc * 3 * C, 3 * C, C, C, base + d->wpack_off[0])) ||
+        float* fl = d->d_fold + (size_t)l * 14 * C;
+        if (hpa_ln_fold_pack(w->qkvw + lc * 3 * C, 3 * C, C, w->ln1w + lc, w->ln1b + lc, w->qkvb + 3 * lc,
+                             base + d->wpack_off[0], fl, fl + 3 * C) ||
             hpa_pack_frag(w->attprojw + lc * C, C, C, C, base + d->wpack_off[1]) ||
-            (fold ? hpa_ln_fold_pack(w->fcw + lc * 4 * C, 4 * C, C, w->ln2w + lc, w->ln2b + lc,
-                                     w->fcb + 4 * lc, base + d->wpack_off[2], fl + 6 * C, fl + 10 * C)
-                  : hpa_pack_frag(w->fcw + lc * 4 * C, 4 * C, C, C, base + d->wpack_off[2])) ||
+            hpa_ln_fold_pack(w->fcw + lc * 4 * C, 4 * C, C, w->ln2w + lc, w->ln2b + lc, w->fcb + 4 * lc,
+                             base + d->wpack_off[2], fl + 6 * C, fl + 10 * C) ||
             hpa_pack_frag(w->fcprojw + lc * 4 * C, C, 4 * C, 4 * C, base + d->wpack_off[3]))
             return 1;
     }
@@ -904,16 +823,27 @@ static int dec_init_fused(GPT2* model, GPT2Decode* d) {
         d->fwaves[i] = pk[0];
         d->frb[i] = pk[1];
         d->fct[i] = pk[2];
-        /* K split over workgroups for the MFMA-bound XL layer GEMMs (HPA_KSLICES: unset or 0 =
-         * by shape, 1 = none, n = n slices) */
-        const char* ke = getenv("HPA_KSLICES");
-        const int kn = ke ? atoi(ke) : 0;
-        d->fks[i] = i < 4 ? (kn > 0 ? kn : hpa_fused_pick_slices(B, shp[i][0], shp[i][1])) : 1;
-        if (d->fks[i] < 1) d->fks[i] = 1;
     }
-    d->ev_fork = hpa_event_create_nt();
-    if (!d->ev_fork) return 1;
-    return dec_lanes_alloc(d, 1, C, V, c.num_heads);
+    return 0;
+}
+
+/* the attention's context ranges and their workspace (zeroed whenever the
+ * split count changes: the counters sit after the records of that count) */
+static int dec_set_splits(GPT2Decode* d, int splits) {
+    if (splits < 1 || splits > HPA_ATTN_MAX_SPLITS) return 1;
+    if (splits > 1 && !d->d_attn_ws) {
+        d->attn_ws_bytes = hpa_attn_ws_bytes(d->B, d->pool.num_heads, HPA_ATTN_MAX_SPLITS);
+        d->d_attn_ws = hpa_malloc(d->attn_ws_bytes);
+        if (!d->d_attn_ws) return 1;
+    }
+    if (d->d_attn_ws && hpa_memset_async(d->d_attn_ws, 0, d->attn_ws_bytes)) return 1;
+    d->attn_splits = splits;
+    if (d->graph) { /* recapture with the new grid */
+        hpa_synchronize();
+        hpa_graph_destroy(d->graph);
+        d->graph = NULL;
+    }
+    return 0;
 }
 
 int gpt2_decode_init(GPT2* model, int B, int page_size, int max_ctx) {
@@ -935,7 +865,7 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
         return 1;
     }
     if (!model->params_memory) { fprintf(stderr, "[paged_infer] model not built\n"); return 1; }
-    GPT2Config c = model->config;
+    const GPT2Config c = model->config;
     if (c.channels != c.num_heads * 64) {
         fprintf(stderr, "[paged_infer] decode engine needs head_size 64 (C = 64*NH)\n");
         return 1;
@@ -946,6 +876,7 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
     }
     gpt2_decode_free(model);
     GPT2Decode* d = (GPT2Decode*)calloc(1, sizeof(GPT2Decode));
+    if (!d) return 1;
     if (model->manager) {
         d->bm = model->manager;
         page_size = d->bm->block_size;
@@ -964,6 +895,7 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
     d->P = page_size;
     d->max_ctx = max_ctx;
     d->max_pages = (max_ctx + page_size - 1) / page_size;
+    d->Mp = (B + 15) / 16 * 16;
     int num_pages;
     if (model->manager) {
         num_pages = d->bm->max_blocks;
@@ -975,13 +907,11 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
     }
     if (d->bm->max_blocks_per_prompt < d->max_pages) {
         fprintf(stderr, "[paged_infer] manager's per-prompt page list shorter than max_ctx\n");
-        if (d->own_bm) destroy_block_manager(d->bm);
-        free(d);
+        dec_free(d);
         return 1;
     }
     if (hpa_pool_create(&d->pool, c.num_layers, c.num_heads, 64, page_size, num_pages, kv_dtype, 0)) {
-        if (d->own_bm) destroy_block_manager(d->bm);
-        free(d);
+        dec_free(d);
         return 1;
     }
     /* pages of this manager are views into the pool from now on */
@@ -993,54 +923,56 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
         d->pv.map = page_map_create(num_pages, tile_bytes >= 4096 ? 1 : 16);
     }
     if (!d->pv.map) {
-        hpa_pool_destroy(&d->pool);
-        if (d->own_bm) destroy_block_manager(d->bm);
-        free(d);
+        dec_free(d);
         return 1;
     }
     BMPageBackend be = {pool_view_alloc, pool_view_release, &d->pv};
     bm_set_backend(d->bm, &be);
     d->bt_stride = d->bm->max_blocks_per_prompt;
-    int C = c.channels, V = c.vocab_size;
-    size_t btn = (size_t)d->bm->max_prompts * d->bt_stride;
+    const int C = c.channels, V = c.vocab_size, ct = C / 16;
+    const size_t btn = (size_t)d->bm->max_prompts * d->bt_stride, Mp = d->Mp;
     d->d_bt = (int*)hpa_malloc(btn * sizeof(int));
     d->d_pos = (int*)hpa_malloc(B * sizeof(int));
     d->d_tokens = (int*)hpa_malloc(B * sizeof(int));
     d->d_next = (int*)hpa_malloc(B * sizeof(int));
     d->h_pos = (int*)calloc(B, sizeof(int));
-    d->h_stage = (int*)hpa_host_alloc(2 * (size_t)B * sizeof(int));
-    d->h_bt_stage = (int*)hpa_host_alloc(btn * sizeof(int));
-    d->split[0] = hpa_gemm_pick_splitk(B, 3 * C, C);
-    d->split[1] = hpa_gemm_pick_splitk(B, C, C);
-    d->split[2] = hpa_gemm_pick_splitk(B, 4 * C, C);
-    d->split[3] = hpa_gemm_pick_splitk(B, C, 4 * C);
-    size_t part = 0, t;
-    t = (size_t)d->split[0] * B * 3 * C; part = t > part ? t : part;
-    t = (size_t)d->split[1] * B * C; part = t > part ? t : part;
-    t = (size_t)d->split[2] * B * 4 * C; part = t > part ? t : part;
-    t = (size_t)d->split[3] * B * C; part = t > part ? t : part;
-    d->d_res = (float*)hpa_malloc((size_t)B * C * 4);
-    d->d_res2 = (float*)hpa_malloc((size_t)B * C * 4);
-    d->d_ln = (float*)hpa_malloc((size_t)B * C * 4);
+    d->h_evicted = (char*)calloc(B, 1);
+    d->h_next = (int*)hpa_host_alloc(B * sizeof(int));
     d->d_q = (float*)hpa_malloc((size_t)B * C * 4);
-    d->d_att = (float*)hpa_malloc((size_t)B * C * 4);
-    d->d_fch = (float*)hpa_malloc((size_t)B * 4 * C * 4);
-    d->d_part = (float*)hpa_malloc(part * 4);
     d->d_logits = (float*)hpa_malloc((size_t)B * V * 4);
-    if (!d->d_bt || !d->d_pos || !d->d_tokens || !d->d_next || !d->h_pos || !d->h_stage ||
-        !d->h_bt_stage || !d->d_res || !d->d_res2 || !d->d_ln || !d->d_q || !d->d_att ||
-        !d->d_fch || !d->d_part || !d->d_logits) {
+    d->res = (float*)hpa_malloc(Mp * C * 4);
+    d->res2 = (float*)hpa_malloc(Mp * C * 4);
+    d->att = (float*)hpa_malloc(Mp * C * 4);
+    d->fch = (float*)hpa_malloc(Mp * 4 * C * 4);
+    d->st1 = (float*)hpa_malloc((size_t)ct * Mp * 2 * 4);
+    d->st2 = (float*)hpa_malloc((size_t)ct * Mp * 2 * 4);
+    d->part = (float*)hpa_malloc((size_t)((V + 15) / 16) * Mp * 2 * 4);
+    int ok = d->d_bt && d->d_pos && d->d_tokens && d->d_next && d->h_pos && d->h_evicted && d->h_next && d->d_q &&
+             d->d_logits && d->res && d->res2 && d->att && d->fch && d->st1 && d->st2 && d->part;
+    for (int k = 0; k < 2 && ok; k++) {
+        d->h_tok[k] = (int*)hpa_host_alloc(B * sizeof(int));
+        d->h_bt[k] = (int*)hpa_host_alloc(btn * sizeof(int));
+        d->ev_tok[k] = hpa_event_create_nt();
+        d->ev_bt[k] = hpa_event_create_nt();
+        d->prof_ev[k] = hpa_event_create();
+        ok = d->h_tok[k] && d->h_bt[k] && d->ev_tok[k] && d->ev_bt[k] && d->prof_ev[k];
+    }
+    /* padded rows stay zero forever */
+    if (!ok || hpa_memset_async(d->res, 0, Mp * C * 4) || hpa_memset_async(d->res2, 0, Mp * C * 4) ||
+        hpa_memset_async(d->att, 0, Mp * C * 4) || hpa_memset_async(d->fch, 0, Mp * 4 * C * 4) ||
+        hpa_memset_async(d->st1, 0, (size_t)ct * Mp * 2 * 4) || hpa_memset_async(d->st2, 0, (size_t)ct * Mp * 2 * 4)) {
         dec_free(d);
         return 1;
     }
     d->w_bf16 = w_dtype == HPA_BF16;
-    if (dec_init_fused(model, d)) {
+    int ncu = 0;
+    hpa_device_info(NULL, 0, &ncu, NULL);
+    if (dec_init_weights(model, d) || dec_set_splits(d, hpa_attn_pick_splits(B, c.num_heads, max_ctx, ncu))) {
         dec_free(d);
         return 1;
     }
-    for (size_t i = 0; i < btn; i++) d->h_bt_stage[i] = -1;
-    if (hpa_memcpy(d->d_bt, d->h_bt_stage, btn * sizeof(int)) ||
-        hpa_memset_async(d->d_pos, 0, B * sizeof(int)) ||
+    for (size_t i = 0; i < btn; i++) d->h_bt[0][i] = -1;
+    if (hpa_memcpy(d->d_bt, d->h_bt[0], btn * sizeof(int)) || hpa_memset_async(d->d_pos, 0, B * sizeof(int)) ||
         hpa_memset_async(d->d_tokens, 0, B * sizeof(int)) || hpa_synchronize()) {
         dec_free(d);
         return 1;
@@ -1050,28 +982,41 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
     return 0;
 }
 
-/* upload the block-table rows the manager changed since the last upload */
+/* upload the block-table rows the manager changed since the last upload,
+ * through the staging buffer whose previous upload is known to be done */
 static int dec_sync_block_table(GPT2Decode* d) {
     BlockManager* m = d->bm;
     if (m->dirty_hi < m->dirty_lo) return 0;
-    size_t lo = (size_t)m->dirty_lo * d->bt_stride;
-    size_t n = (size_t)(m->dirty_hi - m->dirty_lo + 1) * d->bt_stride;
-    /* the staging copy must not be overwritten while a previous async copy
-     * may still read it: wait for the stream's earlier work first */
-    if (hpa_synchronize()) return 1;
+    const size_t lo = (size_t)m->dirty_lo * d->bt_stride;
+    const size_t n = (size_t)(m->dirty_hi - m->dirty_lo + 1) * d->bt_stride;
+    const int k = d->bt_k;
+    if (hpa_event_synchronize(d->ev_bt[k])) return 1;
+    int* st = d->h_bt[k];
     for (size_t i = 0; i < n; i++) {
         const int v = m->block_table[lo + i];
-        d->h_bt_stage[lo + i] = v >= 0 ? d->pv.map[v] : -1;
+        st[lo + i] = v >= 0 ? d->pv.map[v] : -1;
     }
-    if (hpa_memcpy_async(d->d_bt + lo, d->h_bt_stage + lo, n * sizeof(int))) return 1;
+    if (hpa_memcpy_async(d->d_bt + lo, st + lo, n * sizeof(int)) || hpa_event_record(d->ev_bt[k])) return 1;
+    d->bt_k ^= 1;
     bm_clear_dirty(m);
+    return 0;
+}
+
+/* host tokens -> d_tokens through the double-buffered pinned staging */
+static int dec_upload_tokens(GPT2Decode* d, const int* tokens) {
+    const int k = d->tok_k;
+    if (hpa_event_synchronize(d->ev_tok[k])) return 1;
+    memcpy(d->h_tok[k], tokens, d->B * sizeof(int));
+    if (hpa_memcpy_async(d->d_tokens, d->h_tok[k], d->B * sizeof(int)) || hpa_event_record(d->ev_tok[k])) return 1;
+    d->tok_k ^= 1;
     return 0;
 }
 
 /* pages for positions pos[b] .. pos[b]+n-1 of sequence b.  The reference
  * policy may evict a whole LRU sequence to make room (block_manager.c:104-162);
- * the evicted sequence restarts at position 0.  `busy` (nullable) marks the
- * sequences of the current batch: evicting one of those fails the call. */
+ * the evicted sequence restarts at position 0 and is reported by
+ * gpt2_decode_evicted.  `busy` (nullable) marks the sequences of the current
+ * call: evicting one of those fails the call. */
 static int dec_grow(GPT2Decode* d, int b, int n, const int* busy, int* evicted) {
     for (;;) {
         const int need = (d->h_pos[b] + n - 1) / d->P + 1;
@@ -1079,8 +1024,8 @@ static int dec_grow(GPT2Decode* d, int b, int n, const int* busy, int* evicted) 
         if (!request_block(d->bm, b)) return 1;
         const int ev = d->bm->last_evicted_prompt; /* may be b itself */
         if (ev < 0 || ev >= d->B) continue;
-        fprintf(stderr, "[paged_infer] page pool full: sequence %d evicted (LRU)\n", ev);
         if (evicted) ++*evicted;
+        d->h_evicted[ev] = 1;
         d->h_pos[ev] = 0;
         if (hpa_memcpy(d->d_pos + ev, &d->h_pos[ev], sizeof(int))) return 1;
         if (busy && busy[ev]) {
@@ -1111,59 +1056,6 @@ static int dec_ensure_pages(GPT2Decode* d) {
     return 1;
 }
 
-static int dec_launch_unfused(GPT2* model) {
-    GPT2Decode* d = model->decode;
-    const GPT2Config c = model->config;
-    const int B = d->B, C = c.channels, L = c.num_layers, V = c.vocab_size;
-    const ParameterTensors* w = &model->params;
-    int rc = 0;
-    rc |= hpa_embed_ln(d->d_tokens, d->d_pos, w->wte, w->wpe, w->ln1w, w->ln1b, d->d_res, d->d_ln, B, C);
-    for (int l = 0; l < L && !rc; l++) {
-        const size_t lc = (size_t)l * C;
-        /* QKV + KV append into the page of pos[b] (add_to_cache fused) */
-        int s = d->split[0];
-        rc |= hpa_gemm_f32(d->d_ln, C, w->qkvw + lc * 3 * C, w->qkvb + 3 * lc, d->d_part, 3 * C, B,
-                           3 * C, C, s, s > 1 ? HPA_EPI_PARTIAL : HPA_EPI_BIAS);
-        rc |= hpa_qkv_append(d->d_part, s, s > 1 ? w->qkvb + 3 * lc : NULL, d->d_q, &d->pool, l,
-                             d->d_bt, d->bt_stride, d->d_pos, B, C);
-        /* paged attention over 0..pos[b] */
-        if (d->prof_ev) rc |= hpa_event_record(PROF_EV(d, l, 0, 0));
-        rc |= hpa_paged_attention_decode(d->d_q, &d->pool, l, d->d_bt, d->bt_stride, d->d_pos,
-                                         d->d_att, B);
-        if (d->prof_ev) rc |= hpa_event_record(PROF_EV(d, l, 0, 1));
-        /* attn proj + residual + LN2 */
-        s = d->split[1];
-        rc |= hpa_gemm_f32(d->d_att, C, w->attprojw + lc * C, w->attprojb + lc, d->d_part, C, B, C, C,
-                           s, s > 1 ? HPA_EPI_PARTIAL : HPA_EPI_BIAS);
-        rc |= hpa_residual_ln(d->d_part, s, s > 1 ? w->attprojb + lc : NULL, d->d_res, d->d_res2,
-                              w->ln2w + lc, w->ln2b + lc, d->d_ln, B, C);
-        /* fc + GELU */
-        s = d->split[2];
-        if (s > 1) {
-            rc |= hpa_gemm_f32(d->d_ln, C, w->fcw + lc * 4 * C, NULL, d->d_part, 4 * C, B, 4 * C, C,
-                               s, HPA_EPI_PARTIAL);
-            rc |= hpa_bias_gelu(d->d_part, s, w->fcb + 4 * lc, d->d_fch, B, 4 * C);
-        } else {
-            rc |= hpa_gemm_f32(d->d_ln, C, w->fcw + lc * 4 * C, w->fcb + 4 * lc, d->d_fch, 4 * C, B,
-                               4 * C, C, 1, HPA_EPI_BIAS_GELU);
-        }
-        /* fc proj + residual + next LN (LN1 of l+1, or the final LN) */
-        s = d->split[3];
-        rc |= hpa_gemm_f32(d->d_fch, 4 * C, w->fcprojw + lc * 4 * C, w->fcprojb + lc, d->d_part, C, B,
-                           C, 4 * C, s, s > 1 ? HPA_EPI_PARTIAL : HPA_EPI_BIAS);
-        const float* nw = l + 1 < L ? w->ln1w + lc + C : w->lnfw;
-        const float* nb = l + 1 < L ? w->ln1b + lc + C : w->lnfb;
-        rc |= hpa_residual_ln(d->d_part, s, s > 1 ? w->fcprojb + lc : NULL, d->d_res2, d->d_res, nw,
-                              nb, d->d_ln, B, C);
-    }
-    /* logits = lnf . wte^T (paged_infer.c:727), greedy id, advance positions */
-    rc |= hpa_gemm_f32(d->d_ln, C, w->wte, NULL, d->d_logits, V, B, V, C, 1, HPA_EPI_BIAS);
-    rc |= hpa_argmax_advance(d->d_logits, B, V, d->d_next, d->d_tokens, d->d_pos);
-    return rc;
-}
-
-/* the fused GEMMs of one layer of one lane (gemm index = the fwaves/frb/fct
- * slot): descriptor with that lane's rows, buffers and launch shape */
 enum { G_QKV = 0, G_ATTPROJ = 1, G_FC = 2, G_FCPROJ = 3, G_LOGITS = 4 };
 
 /* packed weights at element offset off (fp32 or bf16 pack) */
@@ -1171,361 +1063,111 @@ static const float* wpack_at(const GPT2Decode* d, size_t off) {
     return d->w_bf16 ? (const float*)((const unsigned short*)d->d_wpack + off) : d->d_wpack + off;
 }
 
-static void lane_gemm(GPT2* model, int li, int l, int which, HpaFusedGemm* g) {
+/* descriptor of fused GEMM `which` of layer l over the decode rows */
+static void dec_gemm_desc(GPT2* model, int l, int which, HpaFusedGemm* g) {
     GPT2Decode* d = model->decode;
-    const DecLane* ln = &d->lanes[li];
     const GPT2Config c = model->config;
     const int C = c.channels, V = c.vocab_size, ct = C / 16;
     const ParameterTensors* w = &model->params;
     const size_t lc = (size_t)l * C;
     const size_t e_layer = d->wpack_off[3] + hpa_frag_elems(C, 4 * C);
     memset(g, 0, sizeof(*g));
-    g->M = ln->B;
+    g->M = d->B;
     g->w_dtype = d->w_bf16 ? HPA_BF16 : HPA_F32;
     g->epilogue = which == G_QKV ? HPA_FEPI_QKV : which == G_FC ? HPA_FEPI_GELU
                 : which == G_LOGITS ? HPA_FEPI_LOGITS : HPA_FEPI_RESID;
     g->waves = d->fwaves[which];
     g->row_blocks = d->frb[which];
     g->col_tiles = d->fct[which];
-    if (which != G_LOGITS && d->fks[which] > 1) {
-        g->k_slices = d->fks[which];
-        g->ks_slab = ln->ks_slab;
-        g->ks_count = ln->ks_cnt;
-    }
     g->pool = &d->pool;
     g->layer = l;
-    g->block_table = d->d_bt + (size_t)ln->r0 * d->bt_stride;
+    g->block_table = d->d_bt;
     g->bt_stride = d->bt_stride;
-    g->pos = d->d_pos + ln->r0;
+    g->pos = d->d_pos;
     switch (which) {
         case G_QKV: /* LN1 (stats: embedding's 1 tile at layer 0, fcproj's C/16 after) */
-            g->x = ln->res; g->K = C; g->ln_stats = ln->st1; g->ln_ntiles = l == 0 ? 1 : ct;
-            g->ln_w = w->ln1w + lc; g->ln_b = w->ln1b + lc; g->w = wpack_at(d, e_layer * l + d->wpack_off[0]); g->N = 3 * C;
-            g->bias = w->qkvb + 3 * lc; g->out = d->d_q + (size_t)ln->r0 * C;
+            g->x = d->res; g->K = C; g->ln_stats = d->st1; g->ln_ntiles = l == 0 ? 1 : ct;
+            g->ln_w = w->ln1w + lc; g->ln_b = w->ln1b + lc; g->w = wpack_at(d, e_layer * l + d->wpack_off[0]);
+            g->N = 3 * C; g->bias = w->qkvb + 3 * lc; g->out = d->d_q;
             if (d->d_fold) { g->ln_fold_c1 = d->d_fold + 14 * lc; g->bias = g->ln_fold_c1 + 3 * C; }
             break;
-        case G_ATTPROJ: /* res2 = res + att . Wap^T + b, LN2 statistics */
-            g->x = ln->att; g->K = C; g->w = wpack_at(d, e_layer * l + d->wpack_off[1]); g->N = C; g->bias = w->attprojb + lc;
-            g->out = ln->res2; g->res_in = ln->res; g->stats_out = d->d_fold ? NULL : ln->st2; /* fc sums its own */
+        case G_ATTPROJ: /* res2 = res + att . Wap^T + b (LN2 statistics only when fc needs them) */
+            g->x = d->att; g->K = C; g->w = wpack_at(d, e_layer * l + d->wpack_off[1]); g->N = C;
+            g->bias = w->attprojb + lc; g->out = d->res2; g->res_in = d->res; g->stats_out = d->d_fold ? NULL : d->st2;
             break;
         case G_FC: /* gelu(LN2(res2) . Wfc^T + b) */
-            g->x = ln->res2; g->K = C; g->ln_stats = ln->st2; g->ln_ntiles = ct; g->ln_w = w->ln2w + lc;
-            g->ln_b = w->ln2b + lc; g->w = wpack_at(d, e_layer * l + d->wpack_off[2]); g->N = 4 * C; g->bias = w->fcb + 4 * lc;
-            g->out = ln->fch;
+            g->x = d->res2; g->K = C; g->ln_stats = d->st2; g->ln_ntiles = ct; g->ln_w = w->ln2w + lc;
+            g->ln_b = w->ln2b + lc; g->w = wpack_at(d, e_layer * l + d->wpack_off[2]); g->N = 4 * C;
+            g->bias = w->fcb + 4 * lc; g->out = d->fch;
             if (d->d_fold) { g->ln_fold_c1 = d->d_fold + 14 * lc + 6 * C; g->bias = g->ln_fold_c1 + 4 * C; }
             break;
         case G_FCPROJ: /* res = res2 + fch . Wfp^T + b, next-LN statistics */
-            g->x = ln->fch; g->K = 4 * C; g->w = wpack_at(d, e_layer * l + d->wpack_off[3]); g->N = C; g->bias = w->fcprojb + lc;
-            g->out = ln->res; g->res_in = ln->res2;
-            g->stats_out = d->d_fold && l + 1 < c.num_layers ? NULL : ln->st1; /* LNf of logits: last layer */
+            g->x = d->fch; g->K = 4 * C; g->w = wpack_at(d, e_layer * l + d->wpack_off[3]); g->N = C;
+            g->bias = w->fcprojb + lc; g->out = d->res; g->res_in = d->res2;
+            g->stats_out = d->d_fold && l + 1 < c.num_layers ? NULL : d->st1; /* LNf of logits: last layer */
             break;
         default: /* logits = LNf(res) . wte^T, argmax partials */
-            g->x = ln->res; g->K = C; g->ln_stats = ln->st1; g->ln_ntiles = c.num_layers == 0 ? 1 : ct;
+            g->x = d->res; g->K = C; g->ln_stats = d->st1; g->ln_ntiles = ct;
             g->ln_w = w->lnfw; g->ln_b = w->lnfb; g->w = wpack_at(d, d->wpack_off[4]); g->N = V;
-            g->out = d->d_logits + (size_t)ln->r0 * V; g->part_out = ln->part; g->layer = 0;
+            g->out = d->d_logits; g->part_out = d->part; g->layer = 0;
             g->variant = 4; /* activation-resident kernel where the shape allows (hpa_logits.hip) */
             break;
     }
 }
 
-static int lane_gemm_run(GPT2* model, int li, int l, int which) {
+static int dec_gemm(GPT2* model, int l, int which) {
     HpaFusedGemm g;
-    lane_gemm(model, li, l, which, &g);
+    dec_gemm_desc(model, l, which, &g);
     return hpa_gemm_fused(&g);
 }
 
-static int lane_embed(GPT2* model, int li) {
+/* greedy or sampled next token; active (nullable): rows with active[b] <= 0
+ * are left untouched */
+static int dec_pick(GPT2* model, const int* active) {
     GPT2Decode* d = model->decode;
-    const DecLane* ln = &d->lanes[li];
-    const ParameterTensors* w = &model->params;
-    return hpa_embed_frag(d->d_tokens + ln->r0, d->d_pos + ln->r0, w->wte, w->wpe, ln->res, ln->st1, ln->B,
-                          model->config.channels);
-}
-
-/* greedy or sampled next token of the lane's rows; active (nullable):
- * rows with active[b] <= 0 are left untouched */
-static int lane_pick(GPT2* model, int li, const int* active) {
-    GPT2Decode* d = model->decode;
-    const DecLane* ln = &d->lanes[li];
     const int V = model->config.vocab_size;
     if (d->sample)
-        return hpa_sample_final(d->d_logits + (size_t)ln->r0 * V, ln->B, V, d->d_rng + ln->r0, d->d_next + ln->r0,
-                                d->d_tokens + ln->r0, d->d_pos + ln->r0, active);
+        return hpa_sample_final(d->d_logits, d->B, V, d->d_rng, d->d_next, d->d_tokens, d->d_pos, active);
     HpaFusedGemm g;
-    lane_gemm(model, li, 0, G_LOGITS, &g);
+    dec_gemm_desc(model, 0, G_LOGITS, &g);
     const int npart = hpa_logits_partials(&g); /* per-tile or per-workgroup partials */
     if (npart <= 0) return 1;
-    return hpa_argmax_final(ln->part, npart, ln->Mp, ln->B, d->d_next + ln->r0, d->d_tokens + ln->r0,
-                            d->d_pos + ln->r0, active);
+    return hpa_argmax_final(d->part, npart, d->Mp, d->B, d->d_next, d->d_tokens, d->d_pos, active);
 }
 
-/* one lane's fused step on the current stream: embed, then per layer
- * QKV(+LN1, +KV append) -> attention -> attproj(+residual, LN2 stats) ->
- * fc(+LN2, +GELU) -> fcproj(+residual, next LN stats), then logits(+LNf,
- * argmax partials) and the greedy pick: 5 launches per layer + 3 */
-static int dec_launch_lane(GPT2* model, int li) {
+static int dec_attention(GPT2* model, int l) {
     GPT2Decode* d = model->decode;
-    const DecLane* ln = &d->lanes[li];
-    const int C = model->config.channels, L = model->config.num_layers;
-    int rc = lane_embed(model, li);
-    for (int l = 0; l < L && !rc; l++) {
-        rc |= lane_gemm_run(model, li, l, G_QKV);
-        if (d->prof_ev) rc |= hpa_event_record(PROF_EV(d, l, li, 0));
-        rc |= hpa_paged_attention_decode_frag(d->d_q + (size_t)ln->r0 * C, &d->pool, l,
-                                              d->d_bt + (size_t)ln->r0 * d->bt_stride, d->bt_stride,
-                                              d->d_pos + ln->r0, ln->att, ln->B);
-        if (d->prof_ev) rc |= hpa_event_record(PROF_EV(d, l, li, 1));
-        rc |= lane_gemm_run(model, li, l, G_ATTPROJ);
-        rc |= lane_gemm_run(model, li, l, G_FC);
-        rc |= lane_gemm_run(model, li, l, G_FCPROJ);
-    }
-    rc |= lane_gemm_run(model, li, 0, G_LOGITS);
-    rc |= lane_pick(model, li, NULL);
-    return rc;
-}
-
-/* ---- pipelined step (two lanes, one stream) ----
- * Each lane's layer attention is cut into PIPE_CHUNKS context chunks; every
- * chunk of lane X's attention shares its launch with one GEMM of lane Y's
- * chain (hpa_attn_chunk_with_gemm), so the HBM-bound stream and the
- * latency-bound GEMMs run side by side:
- *   A: qkv(0)                                     (alone)
- *   layer l: attn_A(l) chunks 0..3  |  B: attproj(l-1) fc(l-1) fcproj(l-1) qkv(l)
- *            attn_B(l) chunks 0..3  |  A: attproj(l)   fc(l)   fcproj(l)   qkv(l+1)
- *   B: attproj(L-1) fc(L-1) fcproj(L-1); logits A, B; greedy A, B  (alone)
- * Every dependency is a launch boundary on the one stream. */
-#define PIPE_CHUNKS 4
-
-static void lane_attn(GPT2* model, int li, int l, int chunk, HpaAttnChunk* a) {
-    GPT2Decode* d = model->decode;
-    const DecLane* ln = &d->lanes[li];
-    const int C = model->config.channels;
-    a->q = d->d_q + (size_t)ln->r0 * C;
-    a->pool = &d->pool;
-    a->layer = l;
-    a->block_table = d->d_bt + (size_t)ln->r0 * d->bt_stride;
-    a->bt_stride = d->bt_stride;
-    a->pos = d->d_pos + ln->r0;
-    a->state = ln->astate;
-    a->out_frag = ln->att;
-    a->B = ln->B;
-    a->chunk = chunk;
-    a->nchunks = PIPE_CHUNKS;
-}
-
-static int pipe_launch(GPT2* model, int att_lane, int l, int chunk, int gemm_lane, int gl, int which) {
-    HpaAttnChunk a;
-    lane_attn(model, att_lane, l, chunk, &a);
-    if (which < 0) return hpa_attn_chunk_with_gemm(&a, NULL);
-    HpaFusedGemm g;
-    lane_gemm(model, gemm_lane, gl, which, &g);
-    g.k_slices = 0; /* the combo's GEMM role: no K split, 4 waves, one row block, one column tile */
-    g.waves = 4;
-    g.row_blocks = 1;
-    g.col_tiles = 1;
-    return hpa_attn_chunk_with_gemm(&a, &g);
-}
-
-static int dec_launch_pipelined(GPT2* model) {
-    const int L = model->config.num_layers;
-    const int A = 0, B = 1;
-    int rc = lane_embed(model, A);
-    rc |= lane_embed(model, B);
-    rc |= lane_gemm_run(model, A, 0, G_QKV);
-    for (int l = 0; l < L && !rc; l++) {
-        /* lane B's chain: the rest of layer l-1, then qkv(l) */
-        const int segB[PIPE_CHUNKS][2] = {{l - 1, l > 0 ? G_ATTPROJ : -1}, {l - 1, l > 0 ? G_FC : -1},
-                                          {l - 1, l > 0 ? G_FCPROJ : -1}, {l, G_QKV}};
-        for (int c = 0; c < PIPE_CHUNKS; c++) rc |= pipe_launch(model, A, l, c, B, segB[c][0], segB[c][1]);
-        /* lane A's chain: the rest of layer l, then qkv(l+1) */
-        const int segA[PIPE_CHUNKS][2] = {{l, G_ATTPROJ}, {l, G_FC}, {l, G_FCPROJ},
-                                          {l + 1, l + 1 < L ? G_QKV : -1}};
-        for (int c = 0; c < PIPE_CHUNKS; c++) rc |= pipe_launch(model, B, l, c, A, segA[c][0], segA[c][1]);
-    }
-    rc |= lane_gemm_run(model, B, L - 1, G_ATTPROJ);
-    rc |= lane_gemm_run(model, B, L - 1, G_FC);
-    rc |= lane_gemm_run(model, B, L - 1, G_FCPROJ);
-    rc |= lane_gemm_run(model, A, 0, G_LOGITS);
-    rc |= lane_gemm_run(model, B, 0, G_LOGITS);
-    rc |= lane_pick(model, A, NULL);
-    rc |= lane_pick(model, B, NULL);
-    return rc;
-}
-
-/* ---- split step (two lanes, two CU-masked streams) ----
- * The attention stream owns most CUs, the GEMM stream the remaining
- * split_cus; the two lanes alternate between them as a two-stage pipeline:
- *   att  stream:  attn_A(l)            attn_B(l)            attn_A(l+1) ...
- *   gemm stream:  chain_B(l-1)         chain_A(l)           chain_B(l)  ...
- * where chain_X(l) = attproj, fc, fcproj of layer l and qkv of layer l+1.
- * The HBM-bound attention of one half of the batch thus runs beside the
- * latency-bound GEMMs of the other half on CUs of its own (a plain
- * second stream gets no CUs while the attention grid fills them).  Events
- * carry the dependencies; logits and the token choice run on the launch
- * stream (all CUs).  Kernel node CU masks do not survive graph capture, so
- * this step is launched eagerly.  Rows are bit-identical to one lane. */
-#define SP_EV(d, kind, l, lane) ((d)->sp_ev[((kind) * (model->config.num_layers + 1) + (l)) * 2 + (lane)])
-static int dec_launch_split(GPT2* model) {
-    GPT2Decode* d = model->decode;
-    const int C = model->config.channels, L = model->config.num_layers;
-    void* main_stream = hpa_get_stream();
-    int rc = hpa_event_record(d->ev_fork);
-    hpa_set_stream(d->s_att);
-    rc |= hpa_stream_wait_event(d->ev_fork);
-    hpa_set_stream(d->s_gemm);
-    rc |= hpa_stream_wait_event(d->ev_fork);
-    for (int li = 0; li < 2; li++) {
-        rc |= lane_embed(model, li);
-        rc |= lane_gemm_run(model, li, 0, G_QKV);
-        rc |= hpa_event_record(SP_EV(d, 0, 0, li));
-    }
-    for (int l = 0; l < L && !rc; l++) {
-        for (int li = 0; li < 2; li++) {
-            const DecLane* ln = &d->lanes[li];
-            hpa_set_stream(d->s_att);
-            rc |= hpa_stream_wait_event(SP_EV(d, 0, l, li));
-            rc |= hpa_paged_attention_decode_frag(d->d_q + (size_t)ln->r0 * C, &d->pool, l,
-                                                  d->d_bt + (size_t)ln->r0 * d->bt_stride, d->bt_stride,
-                                                  d->d_pos + ln->r0, ln->att, ln->B);
-            rc |= hpa_event_record(SP_EV(d, 1, l, li));
-            hpa_set_stream(d->s_gemm);
-            rc |= hpa_stream_wait_event(SP_EV(d, 1, l, li));
-            rc |= lane_gemm_run(model, li, l, G_ATTPROJ);
-            rc |= lane_gemm_run(model, li, l, G_FC);
-            rc |= lane_gemm_run(model, li, l, G_FCPROJ);
-            if (l + 1 < L) rc |= lane_gemm_run(model, li, l + 1, G_QKV);
-            rc |= hpa_event_record(SP_EV(d, 0, l + 1, li));
-        }
-    }
-    hpa_set_stream(main_stream);
-    for (int li = 0; li < 2; li++) {
-        rc |= hpa_stream_wait_event(SP_EV(d, 0, L, li));
-        rc |= lane_gemm_run(model, li, 0, G_LOGITS);
-        rc |= lane_pick(model, li, NULL);
+    int rc = 0;
+    if (d->profiling) rc |= hpa_event_record(d->prof_ev[0]);
+    rc |= hpa_paged_attention_decode_split(d->d_q, &d->pool, l, d->d_bt, d->bt_stride, d->d_pos, d->att, d->B,
+                                           d->attn_splits, d->d_attn_ws, 1);
+    if (d->profiling) {
+        rc |= hpa_event_record(d->prof_ev[1]);
+        const float ms = hpa_event_elapsed_ms(d->prof_ev[0], d->prof_ev[1]); /* waits for this launch */
+        if (ms < 0) return 1;
+        d->prof_ms += ms;
+        d->prof_launches++;
     }
     return rc;
 }
 
-/* ---- overlapped step (two lanes, one stream, hpa_lane_layer) ----
- * Lanes A and B alternate: every launch holds one lane's whole attention of
- * a layer beside the other lane's GEMM chain (attproj, fc, fcproj of the
- * previous attention, then qkv of the next layer), whose links are in-launch
- * hand-offs:
- *   embed A, B; qkv_A(0); qkv_B(0)
- *   layer l:  [attn_A(l) | chain_B(l-1) + qkv_B(l)]   (l = 0: attn_A(0) alone)
- *             [attn_B(l) | chain_A(l)   + qkv_A(l+1)]
- *   [chain_B(L-1)]; logits A, B; token choice A, B
- * Two launches per layer instead of ten. */
-static void chain_desc(GPT2* model, int li, int l, int which, HpaFusedGemm* g) {
-    lane_gemm(model, li, l, which, g);
-    g->k_slices = 0; /* the chain's tiles: no K split, 4 waves, one row block, one column tile */
-    g->waves = 4;
-    g->row_blocks = 1;
-    g->col_tiles = 1;
-}
-
-static int overlap_launch(GPT2* model, int att_lane, int att_layer, int chain_lane, int chain_layer, int with_qkv,
-                          int slot) {
-    GPT2Decode* d = model->decode;
-    const int L = model->config.num_layers;
-    HpaAttnChunk a;
-    if (att_lane >= 0) {
-        lane_attn(model, att_lane, att_layer, 0, &a);
-        a.nchunks = 1;
-    }
-    HpaFusedGemm ch[4];
-    int nph = 0;
-    if (chain_lane >= 0) {
-        chain_desc(model, chain_lane, chain_layer, G_ATTPROJ, &ch[nph++]);
-        chain_desc(model, chain_lane, chain_layer, G_FC, &ch[nph++]);
-        chain_desc(model, chain_lane, chain_layer, G_FCPROJ, &ch[nph++]);
-        if (with_qkv && chain_layer + 1 < L) chain_desc(model, chain_lane, chain_layer + 1, G_QKV, &ch[nph++]);
-    }
-    unsigned* ctl = d->d_ctl + (size_t)slot * HPA_LANE_CTL_WORDS;
-    return hpa_lane_layer(att_lane >= 0 ? &a : NULL, nph ? ch : NULL, nph, ctl, d->overlap);
-}
-
-static int dec_launch_overlap(GPT2* model) {
-    GPT2Decode* d = model->decode;
-    const int L = model->config.num_layers;
-    const int A = 0, B = 1;
-    int rc = hpa_memset_async(d->d_ctl, 0, (size_t)(2 * L + 2) * HPA_LANE_CTL_WORDS * sizeof(unsigned));
-    rc |= lane_embed(model, A);
-    rc |= lane_embed(model, B);
-    rc |= lane_gemm_run(model, A, 0, G_QKV);
-    rc |= lane_gemm_run(model, B, 0, G_QKV);
-    int slot = 0;
-    for (int l = 0; l < L && !rc; l++) {
-        rc |= overlap_launch(model, A, l, l > 0 ? B : -1, l - 1, 1, slot++);
-        rc |= overlap_launch(model, B, l, A, l, 1, slot++);
-    }
-    rc |= overlap_launch(model, -1, 0, B, L - 1, 0, slot++);
-    rc |= lane_gemm_run(model, A, 0, G_LOGITS);
-    rc |= lane_gemm_run(model, B, 0, G_LOGITS);
-    rc |= lane_pick(model, A, NULL);
-    rc |= lane_pick(model, B, NULL);
-    return rc;
-}
-
-/* all lanes: lanes 1.. fork from the launch stream, run concurrently with
- * lane 0, and join back before the step completes */
-static int dec_launch_fused(GPT2* model) {
-    GPT2Decode* d = model->decode;
-    if (d->pipeline) return dec_launch_pipelined(model);
-    if (d->overlap) return dec_launch_overlap(model);
-    if (d->split_cus) return dec_launch_split(model);
-    if (d->nlanes == 1) return dec_launch_lane(model, 0);
-    void* main_stream = hpa_get_stream();
-    int rc = hpa_event_record(d->ev_fork);
-    for (int i = 1; i < d->nlanes && !rc; i++) {
-        hpa_set_stream(d->lanes[i].stream);
-        rc |= hpa_stream_wait_event(d->ev_fork);
-        rc |= dec_launch_lane(model, i);
-        rc |= hpa_event_record(d->lanes[i].ev_join);
-    }
-    hpa_set_stream(main_stream);
-    if (rc) return rc;
-    rc |= dec_launch_lane(model, 0);
-    for (int i = 1; i < d->nlanes; i++) rc |= hpa_stream_wait_event(d->lanes[i].ev_join);
-    return rc;
-}
-
+/* the whole step on the library stream */
 static int dec_launch(GPT2* model) {
-    return model->decode->fused ? dec_launch_fused(model) : dec_launch_unfused(model);
-}
-
-/* 1: fused frag-layout path (default); 0: the unfused split-K path */
-int gpt2_decode_set_fused(GPT2* model, int enable) {
     GPT2Decode* d = model->decode;
-    if (!d) return 1;
-    if (d->graph) {
-        hpa_graph_destroy(d->graph);
-        d->graph = NULL;
+    const ParameterTensors* w = &model->params;
+    const int L = model->config.num_layers;
+    int rc = hpa_embed_frag(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, model->config.channels);
+    for (int l = 0; l < L && !rc; l++) {
+        rc |= dec_gemm(model, l, G_QKV);
+        rc |= dec_attention(model, l);
+        rc |= dec_gemm(model, l, G_ATTPROJ);
+        rc |= dec_gemm(model, l, G_FC);
+        rc |= dec_gemm(model, l, G_FCPROJ);
     }
-    if (!enable && (d->pool.dtype != HPA_F32 || d->w_bf16)) {
-        fprintf(stderr, "[paged_infer] the unfused path needs an fp32 KV pool and fp32 weights\n");
-        return 1;
-    }
-    d->fused = enable ? 1 : 0;
-    return 0;
+    rc |= dec_gemm(model, 0, G_LOGITS);
+    rc |= dec_pick(model, NULL);
+    return rc;
 }
-
-/* micro-batch lanes of the fused path (1..8; rounded to whole 16-row blocks) */
-int gpt2_decode_set_lanes(GPT2* model, int lanes) {
-    GPT2Decode* d = model->decode;
-    if (!d || lanes < 1 || lanes > DEC_MAX_LANES) return 1;
-    if (hpa_synchronize()) return 1;
-    if (d->graph) {
-        hpa_graph_destroy(d->graph);
-        d->graph = NULL;
-    }
-    d->pipeline = 0;
-    dec_split_free(d, model->config.num_layers);
-    dec_overlap_free(d);
-    return dec_lanes_alloc(d, lanes, model->config.channels, model->config.vocab_size, model->config.num_heads);
-}
-
-int gpt2_decode_lanes(GPT2* model) { return model->decode ? model->decode->nlanes : 0; }
 
 /* token choice: greedy argmax (enable = 0, the north star's), or the
  * reference driver's multinomial sampling (softmax_forward + sample_mult,
@@ -1542,13 +1184,9 @@ int gpt2_decode_set_sampling(GPT2* model, int enable, unsigned long long seed) {
     unsigned long long* h = (unsigned long long*)malloc(d->B * sizeof(unsigned long long));
     if (!h) return 1;
     for (int b = 0; b < d->B; b++) h[b] = seed + (unsigned long long)b;
-    int rc = hpa_memcpy(d->d_rng, h, d->B * sizeof(unsigned long long));
+    const int rc = hpa_memcpy(d->d_rng, h, d->B * sizeof(unsigned long long));
     free(h);
     if (rc) return 1;
-    if (enable && !d->fused) {
-        fprintf(stderr, "[paged_infer] sampling runs on the fused path\n");
-        return 1;
-    }
     d->sample = enable ? 1 : 0;
     if (d->graph) { /* recapture with the other token-choice kernel */
         hpa_graph_destroy(d->graph);
@@ -1557,112 +1195,32 @@ int gpt2_decode_set_sampling(GPT2* model, int enable, unsigned long long seed) {
     return 0;
 }
 
-/* pipelined step: two lanes on ONE stream, each lane's attention in context
- * chunks beside the other lane's GEMMs (dec_launch_pipelined).  Needs two
- * lanes of whole 16-row blocks (B > 16) and page size 8, 16 or 32. */
-int gpt2_decode_set_pipeline(GPT2* model, int enable) {
-    GPT2Decode* d = model->decode;
-    if (!d) return 1;
-    if (!enable) {
-        if (!d->pipeline) return 0;
-        return gpt2_decode_set_lanes(model, 1);
-    }
-    if (d->B <= 16 || (d->P != 8 && d->P != 16 && d->P != 32) || d->pool.dtype != HPA_F32 || d->w_bf16) {
-        fprintf(stderr, "[paged_infer] pipeline needs B > 16, page size 8/16/32, an fp32 KV pool and fp32 weights\n");
-        return 1;
-    }
-    if (gpt2_decode_set_lanes(model, 2) || d->nlanes != 2) return 1;
-    d->pipeline = 1;
-    return 0;
-}
-
-int gpt2_decode_pipeline(GPT2* model) { return model->decode ? model->decode->pipeline : 0; }
-
-/* split step (dec_launch_split): gemm_cus > 0 gives the GEMM chains that many
- * CUs and the attention the rest; 0 returns to one lane */
-int gpt2_decode_set_split(GPT2* model, int gemm_cus) {
-    GPT2Decode* d = model->decode;
-    if (!d) return 1;
-    if (gemm_cus <= 0) {
-        if (!d->split_cus) return 0;
-        return gpt2_decode_set_lanes(model, 1);
-    }
-    int ncu = 0;
-    if (hpa_device_info(NULL, 0, &ncu, NULL)) return 1;
-    if (!d->fused || d->B <= 16 || gemm_cus >= ncu) {
-        fprintf(stderr, "[paged_infer] split step needs the fused path, B > 16 and gemm_cus < %d\n", ncu);
-        return 1;
-    }
-    if (gpt2_decode_set_lanes(model, 2) || d->nlanes != 2) return 1;
-    const int L = model->config.num_layers;
-    d->sp_ev = (void**)calloc(4 * (size_t)(L + 1), sizeof(void*));
-    if (!d->sp_ev) return 1;
-    for (int i = 0; i < 4 * (L + 1); i++)
-        if (!(d->sp_ev[i] = hpa_event_create_nt())) return 1;
-    d->s_gemm = hpa_stream_create_cumask(0, gemm_cus);
-    d->s_att = hpa_stream_create_cumask(gemm_cus, ncu);
-    if (!d->s_gemm || !d->s_att) {
-        dec_split_free(d, L);
-        return 1;
-    }
-    d->split_cus = gemm_cus;
-    return 0;
-}
-
-int gpt2_decode_split(GPT2* model) { return model->decode ? model->decode->split_cus : 0; }
-
-/* overlapped step (dec_launch_overlap): chain_blocks > 0 persistent
- * workgroups run the GEMM chains beside the attention; 0 returns to one lane */
-int gpt2_decode_set_overlap(GPT2* model, int chain_blocks) {
-    GPT2Decode* d = model->decode;
-    if (!d) return 1;
-    if (chain_blocks <= 0) {
-        if (!d->overlap) return 0;
-        return gpt2_decode_set_lanes(model, 1);
-    }
-    if (!d->fused || d->B <= 16 || d->B > 128 || (d->P != 8 && d->P != 16 && d->P != 32) ||
-        d->pool.dtype != HPA_F32 || d->w_bf16) {
-        fprintf(stderr, "[paged_infer] overlapped step needs the fused path, 16 < B <= 128, page size 8/16/32, "
-                        "an fp32 KV pool and fp32 weights\n");
-        return 1;
-    }
-    if (gpt2_decode_set_lanes(model, 2) || d->nlanes != 2) return 1;
-    const int L = model->config.num_layers;
-    d->d_ctl = (unsigned*)hpa_malloc((size_t)(2 * L + 2) * HPA_LANE_CTL_WORDS * sizeof(unsigned));
-    if (!d->d_ctl) return 1;
-    d->overlap = chain_blocks;
-    return 0;
-}
-
-int gpt2_decode_overlap(GPT2* model) { return model->decode ? model->decode->overlap : 0; }
-
-/* timeout codes the overlapped step's in-launch waits left in the last step
- * (0 = none): synchronises */
-unsigned gpt2_decode_overlap_faults(GPT2* model) {
-    GPT2Decode* d = model->decode;
-    if (!d || !d->overlap || !d->d_ctl) return 0;
-    const int L = model->config.num_layers;
-    const size_t n = (size_t)(2 * L + 2) * HPA_LANE_CTL_WORDS;
-    unsigned* h = (unsigned*)malloc(n * sizeof(unsigned));
-    if (!h) return ~0u;
-    unsigned f = 0;
-    if (hpa_synchronize() || hpa_memcpy(h, d->d_ctl, n * sizeof(unsigned))) f = ~0u;
-    else
-        for (int s = 0; s < 2 * L + 2; s++) f |= h[(size_t)s * HPA_LANE_CTL_WORDS + 1];
-    free(h);
-    return f;
-}
-
 int gpt2_decode_set_graph(GPT2* model, int enable) {
     GPT2Decode* d = model->decode;
     if (!d) return 1;
     d->use_graph = enable;
     if (!enable && d->graph) {
+        hpa_synchronize();
         hpa_graph_destroy(d->graph);
         d->graph = NULL;
     }
     return 0;
 }
+
+/* 0 = by shape (hpa_attn_pick_splits), else 1..HPA_ATTN_MAX_SPLITS */
+int gpt2_decode_set_attn_splits(GPT2* model, int splits) {
+    GPT2Decode* d = model->decode;
+    if (!d) return 1;
+    if (splits == 0) {
+        int ncu = 0;
+        hpa_device_info(NULL, 0, &ncu, NULL);
+        splits = hpa_attn_pick_splits(d->B, d->pool.num_heads, d->max_ctx, ncu);
+    }
+    if (hpa_synchronize()) return 1;
+    return dec_set_splits(d, splits);
+}
+
+int gpt2_decode_attn_splits(GPT2* model) { return model->decode ? model->decode->attn_splits : 0; }
 
 static int dec_enqueue(GPT2* model, const int* tokens) {
     GPT2Decode* d = model->decode;
@@ -1676,34 +1234,30 @@ static int dec_enqueue(GPT2* model, const int* tokens) {
     }
     if (dec_ensure_pages(d)) return 1;
     if (dec_sync_block_table(d)) return 1;
-    if (tokens) {
-        if (hpa_synchronize()) return 1; /* staging buffer reuse */
-        memcpy(d->h_stage, tokens, d->B * sizeof(int));
-        if (hpa_memcpy_async(d->d_tokens, d->h_stage, d->B * sizeof(int))) return 1;
-    }
-    if (d->use_graph && !d->split_cus) {
+    if (tokens && dec_upload_tokens(d, tokens)) return 1;
+    if (d->use_graph && !d->profiling) {
         if (!d->graph) {
             if (hpa_graph_begin()) return 1;
-            int rc = dec_launch(model);
+            const int rc = dec_launch(model);
             void* g = hpa_graph_end();
             if (rc || !g) return 1;
             d->graph = g;
         }
         if (hpa_graph_launch(d->graph)) return 1;
-    } else {
-        if (dec_launch(model)) return 1;
+    } else if (dec_launch(model)) {
+        return 1;
     }
     for (int b = 0; b < d->B; b++) d->h_pos[b]++;
     return 0;
 }
 
-/* ---- prefill: T tokens of every sequence in one pass ----
- * All B*T rows go through the fused GEMMs (row r = b*T + t at absolute
+/* ---- prefill: the new tokens of every sequence in one pass ----
+ * All rows go through the fused GEMMs (row r of sequence b at absolute
  * position pos[b] + t; the QKV epilogue appends each row's K/V through its
  * sequence's block table), the causal multi-query attention runs on MFMA
- * (hpa_paged_attention_prefill), and the last row of every sequence is
- * gathered for the logits and the greedy pick.  Equivalent to T decode steps
- * with the same tokens (tested against the oracle's token-by-token decode). */
+ * (hpa_paged_attention_prefill_ragged), and the last row of every sequence
+ * is gathered for the logits and the token choice.  Equivalent to one decode
+ * step per token (tested against the oracle's token-by-token decode). */
 static int dec_prefill_reserve(GPT2* model, int R) {
     GPT2Decode* d = model->decode;
     if (R <= d->pf_cap) return 0;
@@ -1747,7 +1301,7 @@ static int prefill_gemm(GPT2* model, int l, int which, int R) {
     memset(&g, 0, sizeof(g));
     g.M = R;
     g.w_dtype = d->w_bf16 ? HPA_BF16 : HPA_F32;
-    /* B*T rows: reuse every activation fragment over 2 weight tiles and every
+    /* many rows: reuse every activation fragment over 2 weight tiles and every
      * weight fragment over 4 row blocks (MFMA-bound at this M) */
     g.waves = d->w_bf16 ? 0 : 8; /* bf16 weights: the library's shapes by (M, N, K) */
     g.row_blocks = d->w_bf16 ? 0 : 4;
@@ -1766,19 +1320,19 @@ static int prefill_gemm(GPT2* model, int l, int which, int R) {
             if (d->d_fold) { g.ln_fold_c1 = d->d_fold + 14 * lc; g.bias = g.ln_fold_c1 + 3 * C; }
             break;
         case G_ATTPROJ:
-            g.epilogue = HPA_FEPI_RESID; g.x = d->pf_att; g.K = C; g.w = wpack_at(d, e_layer * l + d->wpack_off[1]); g.N = C;
-            g.bias = w->attprojb + lc; g.out = d->pf_res2; g.res_in = d->pf_res;
+            g.epilogue = HPA_FEPI_RESID; g.x = d->pf_att; g.K = C; g.w = wpack_at(d, e_layer * l + d->wpack_off[1]);
+            g.N = C; g.bias = w->attprojb + lc; g.out = d->pf_res2; g.res_in = d->pf_res;
             g.stats_out = d->d_fold ? NULL : d->pf_st2;
             break;
         case G_FC:
             g.epilogue = HPA_FEPI_GELU; g.x = d->pf_res2; g.K = C; g.ln_stats = d->pf_st2; g.ln_ntiles = ct;
-            g.ln_w = w->ln2w + lc; g.ln_b = w->ln2b + lc; g.w = wpack_at(d, e_layer * l + d->wpack_off[2]); g.N = 4 * C;
-            g.bias = w->fcb + 4 * lc; g.out = d->pf_fch;
+            g.ln_w = w->ln2w + lc; g.ln_b = w->ln2b + lc; g.w = wpack_at(d, e_layer * l + d->wpack_off[2]);
+            g.N = 4 * C; g.bias = w->fcb + 4 * lc; g.out = d->pf_fch;
             if (d->d_fold) { g.ln_fold_c1 = d->d_fold + 14 * lc + 6 * C; g.bias = g.ln_fold_c1 + 4 * C; }
             break;
         default: /* G_FCPROJ */
-            g.epilogue = HPA_FEPI_RESID; g.x = d->pf_fch; g.K = 4 * C; g.w = wpack_at(d, e_layer * l + d->wpack_off[3]); g.N = C;
-            g.bias = w->fcprojb + lc; g.out = d->pf_res; g.res_in = d->pf_res2;
+            g.epilogue = HPA_FEPI_RESID; g.x = d->pf_fch; g.K = 4 * C; g.w = wpack_at(d, e_layer * l + d->wpack_off[3]);
+            g.N = C; g.bias = w->fcprojb + lc; g.out = d->pf_res; g.res_in = d->pf_res2;
             g.stats_out = d->d_fold && l + 1 < c.num_layers ? NULL : d->pf_st1;
             break;
     }
@@ -1786,21 +1340,15 @@ static int prefill_gemm(GPT2* model, int l, int which, int R) {
 }
 
 /* One pass over lens[b] >= 0 new tokens of every sequence b (tokens packed
- * in sequence order): all rows through the fused GEMMs (the QKV epilogue
- * appends each row's K/V through its own sequence's block table), causal
- * multi-query paged attention per sequence, then the last row of every
- * sequence with lens[b] > 0 through the logits and the greedy / sampled
- * pick.  Sequences with lens[b] = 0 are untouched (position, next token,
- * sampler state). */
+ * in sequence order): all rows through the fused GEMMs, causal multi-query
+ * paged attention per sequence, then the last row of every sequence with
+ * lens[b] > 0 through the logits and the greedy / sampled pick.  Sequences
+ * with lens[b] = 0 are untouched (position, next token, sampler state). */
 static int dec_prefill_rows(GPT2* model, const int* tokens, const int* lens, int* next_tokens) {
     GPT2Decode* d = model->decode;
     if (!d) { fprintf(stderr, "[paged_infer] gpt2_decode_init first\n"); return 1; }
     const GPT2Config c = model->config;
     const int B = d->B, C = c.channels, L = c.num_layers;
-    if (!d->fused || d->nlanes != 1 || d->pipeline) {
-        fprintf(stderr, "[paged_infer] prefill runs on the fused one-lane engine\n");
-        return 1;
-    }
     long R = 0;
     int T = 0;
     for (int b = 0; b < B; b++) {
@@ -1856,19 +1404,18 @@ static int dec_prefill_rows(GPT2* model, const int* tokens, const int* lens, int
         rc |= prefill_gemm(model, l, G_FC, (int)R);
         rc |= prefill_gemm(model, l, G_FCPROJ, (int)R);
     }
-    /* last row of every active sequence -> the one-lane engine's buffers,
-     * logits, pick; the pick advances pos by one: set pos = start + len - 1 */
-    DecLane* ln = &d->lanes[0];
+    /* last row of every active sequence -> the decode rows, logits, pick; the
+     * pick advances pos by one: set pos = start + len - 1 first */
     for (int b = 0; b < B; b++) hst[b] = d->h_pos[b] + (lens[b] > 0 ? lens[b] - 1 : 0);
     rc |= hpa_memcpy(d->d_pos, hst, B * sizeof(int));
-    rc |= hpa_gather_rows_frag(d->pf_res, d->pf_st1, Rp, d->pf_last, B, ln->res, ln->st1, ln->Mp, C);
-    rc |= lane_gemm_run(model, 0, 0, G_LOGITS);
-    rc |= lane_pick(model, 0, d_len);
+    rc |= hpa_gather_rows_frag(d->pf_res, d->pf_st1, Rp, d->pf_last, B, d->res, d->st1, d->Mp, C);
+    rc |= dec_gemm(model, 0, G_LOGITS);
+    rc |= dec_pick(model, d_len);
     if (rc) return 1;
     for (int b = 0; b < B; b++) d->h_pos[b] += lens[b];
     if (next_tokens) {
-        if (hpa_memcpy(d->h_stage + B, d->d_next, B * sizeof(int))) return 1;
-        memcpy(next_tokens, d->h_stage + B, B * sizeof(int));
+        if (hpa_memcpy(d->h_next, d->d_next, B * sizeof(int))) return 1;
+        memcpy(next_tokens, d->h_next, B * sizeof(int));
     }
     return hpa_synchronize();
 }
@@ -1908,10 +1455,25 @@ int gpt2_decode_step(GPT2* model, const int* tokens, int* next_tokens) {
     if (dec_enqueue(model, tokens)) return 1;
     GPT2Decode* d = model->decode;
     if (next_tokens) {
-        if (hpa_memcpy(d->h_stage + d->B, d->d_next, d->B * sizeof(int))) return 1;
-        memcpy(next_tokens, d->h_stage + d->B, d->B * sizeof(int));
+        if (hpa_memcpy_async(d->h_next, d->d_next, d->B * sizeof(int)) || hpa_synchronize()) return 1;
+        memcpy(next_tokens, d->h_next, d->B * sizeof(int));
     }
     return 0;
+}
+
+/* sequences the LRU policy paged out since the last call (their position
+ * restarted at 0: the caller must prefill them again); mask (nullable, [B])
+ * gets 1 for each.  Returns how many. */
+int gpt2_decode_evicted(GPT2* model, int* mask) {
+    GPT2Decode* d = model->decode;
+    if (!d) return -1;
+    int n = 0;
+    for (int b = 0; b < d->B; b++) {
+        if (mask) mask[b] = d->h_evicted[b];
+        n += d->h_evicted[b];
+        d->h_evicted[b] = 0;
+    }
+    return n;
 }
 
 int gpt2_decode_reset(GPT2* model) {
@@ -1935,7 +1497,7 @@ int gpt2_decode_fill_random(GPT2* model, int ctx, unsigned long long seed) {
     }
     if (gpt2_decode_reset(model)) return 1;
     for (int b = 0; b < d->B; b++) {
-        int need = (ctx + d->P - 1) / d->P;
+        const int need = (ctx + d->P - 1) / d->P;
         while (d->bm->prompt_block_count[b] < need)
             if (!request_block(d->bm, b)) return 1;
         d->h_pos[b] = ctx;
@@ -1948,6 +1510,7 @@ int gpt2_decode_fill_random(GPT2* model, int ctx, unsigned long long seed) {
 
 float* gpt2_decode_logits(GPT2* model) { return model->decode ? model->decode->d_logits : NULL; }
 int* gpt2_decode_next(GPT2* model) { return model->decode ? model->decode->d_next : NULL; }
+int gpt2_decode_batch(GPT2* model) { return model->decode ? model->decode->B : 0; }
 
 int gpt2_decode_positions(GPT2* model, int* host_pos) {
     GPT2Decode* d = model->decode;
@@ -1956,11 +1519,45 @@ int gpt2_decode_positions(GPT2* model, int* host_pos) {
     return 0;
 }
 
-int gpt2_decode_splits(GPT2* model, int* s4) {
+/* K/V of positions [0, n) of sequence b at layer l, in the reference's
+ * token-major layout: k, v = [n][C] host arrays (parity tests hand the same
+ * cache to the oracle) */
+int gpt2_decode_read_kv(GPT2* model, int l, int b, int n, float* k, float* v) {
     GPT2Decode* d = model->decode;
-    if (!d) return 1;
-    memcpy(s4, d->split, sizeof(d->split));
-    return 0;
+    if (!d || l < 0 || l >= model->config.num_layers || b < 0 || b >= d->B || n < 0 || n > d->h_pos[b]) return 1;
+    const int C = model->config.channels, NH = model->config.num_heads, P = d->P;
+    const size_t tile = (size_t)P * 64, eb = d->pool.elem_bytes;
+    unsigned char* buf = (unsigned char*)malloc(2 * NH * tile * eb);
+    if (!buf || hpa_synchronize()) { free(buf); return 1; }
+    int rc = 0;
+    for (int p0 = 0; p0 < n && !rc; p0 += P) {
+        const int page = d->pv.map[d->bm->prompt_block_list[b][p0 / P]];
+        rc = hpa_memcpy(buf, hpa_pool_tile(&d->pool, l, page, 0, 0), 2 * NH * tile * eb);
+        for (int t = p0; t < n && t < p0 + P && !rc; t++)
+            for (int h = 0; h < NH; h++)
+                for (int x = 0; x < 64; x++) {
+                    const int s = t - p0;
+                    /* K [chunk][slot][4|8], V [slot][64] (hip_paged_attn.h pool layout) */
+                    const size_t ki = eb == 4 ? ((size_t)(x >> 2) * P + s) * 4 + (x & 3)
+                                              : ((size_t)(x >> 3) * P + s) * 8 + (x & 7);
+                    const size_t vi = (size_t)s * 64 + x;
+                    const size_t kt = (size_t)h * tile, vt = (size_t)(NH + h) * tile;
+                    float kf, vf;
+                    if (eb == 4) {
+                        kf = ((const float*)buf)[kt + ki];
+                        vf = ((const float*)buf)[vt + vi];
+                    } else {
+                        const unsigned ku = (unsigned)((const unsigned short*)buf)[kt + ki] << 16;
+                        const unsigned vu = (unsigned)((const unsigned short*)buf)[vt + vi] << 16;
+                        memcpy(&kf, &ku, 4);
+                        memcpy(&vf, &vu, 4);
+                    }
+                    k[(size_t)t * C + h * 64 + x] = kf;
+                    v[(size_t)t * C + h * 64 + x] = vf;
+                }
+    }
+    free(buf);
+    return rc;
 }
 
 /* launch shapes of the fused GEMMs (qkv, attproj, fc, fcproj, logits):
@@ -1987,7 +1584,6 @@ int gpt2_decode_gemm_config(GPT2* model, int* waves5, int* row_blocks5, int* col
         if (row_blocks5 && row_blocks5[i]) d->frb[i] = row_blocks5[i];
         if (col_tiles5 && col_tiles5[i]) d->fct[i] = col_tiles5[i];
     }
-    if (dec_ks_alloc(d, model->config.channels)) return 1; /* split-K slabs of the new shapes */
     if (d->graph) { /* recapture with the new launch shapes */
         hpa_synchronize();
         hpa_graph_destroy(d->graph);
@@ -2011,21 +1607,23 @@ int gpt2_decode_time_attention(GPT2* model, int iters, double* ms_per_launch, do
             return 1;
         }
     int* d_p = (int*)hpa_malloc(B * sizeof(int));
+    int* h_p = (int*)malloc(B * sizeof(int));
     float* out = (float*)hpa_malloc(hpa_frag_elems(B, C) * sizeof(float));
     void* e0 = hpa_event_create();
     void* e1 = hpa_event_create();
-    int rc = !d_p || !out || !e0 || !e1;
+    int rc = !d_p || !h_p || !out || !e0 || !e1;
     if (!rc) {
-        if (hpa_synchronize()) rc = 1;
-        for (int b = 0; b < B && !rc; b++) d->h_stage[b] = d->h_pos[b] - 1;
-        rc |= hpa_memcpy(d_p, d->h_stage, B * sizeof(int));
+        for (int b = 0; b < B; b++) h_p[b] = d->h_pos[b] - 1;
+        rc |= hpa_memcpy(d_p, h_p, B * sizeof(int));
         /* warm-up launch, then the timed ones */
-        rc |= hpa_paged_attention_decode_frag(d->d_q, &d->pool, 0, d->d_bt, d->bt_stride, d_p, out, B);
+        rc |= hpa_paged_attention_decode_split(d->d_q, &d->pool, 0, d->d_bt, d->bt_stride, d_p, out, B,
+                                               d->attn_splits, d->d_attn_ws, 1);
         rc |= hpa_event_record(e0);
         for (int i = 0; i < iters && !rc; i++)
-            rc |= hpa_paged_attention_decode_frag(d->d_q, &d->pool, i % L, d->d_bt, d->bt_stride, d_p, out, B);
+            rc |= hpa_paged_attention_decode_split(d->d_q, &d->pool, i % L, d->d_bt, d->bt_stride, d_p, out, B,
+                                                   d->attn_splits, d->d_attn_ws, 1);
         rc |= hpa_event_record(e1);
-        float ms = rc ? -1.f : hpa_event_elapsed_ms(e0, e1);
+        const float ms = rc ? -1.f : hpa_event_elapsed_ms(e0, e1);
         if (ms < 0) rc = 1;
         if (!rc) {
             double kv = 0.0;
@@ -2038,6 +1636,7 @@ int gpt2_decode_time_attention(GPT2* model, int iters, double* ms_per_launch, do
     hpa_event_destroy(e1);
     hpa_free(out);
     hpa_free(d_p);
+    free(h_p);
     return rc;
 }
 
@@ -2049,23 +1648,133 @@ double gpt2_decode_step_bytes(GPT2* model, double* attn_bytes) {
     const double C = c.channels, L = c.num_layers, V = c.vocab_size, w = 4.0;
     const double wkv = (double)d->pool.elem_bytes; /* fp32 or bf16 KV storage */
     const double wm = d->w_bf16 ? 2.0 : 4.0; /* GEMM weight matrices: bf16 or fp32 */
-    double weights = (L * 12 * C * C + V * C) * wm + (L * 13 * C + 2 * C) * w;
+    const double weights = (L * 12 * C * C + V * C) * wm + (L * 13 * C + 2 * C) * w;
     double kv = 0.0;
     for (int b = 0; b < d->B; b++) kv += 2.0 * L * (d->h_pos[b] + 1) * C * wkv;
-    double append = 2.0 * L * d->B * C * wkv;
-    double logits = (double)d->B * V * 4.0;
+    const double append = 2.0 * L * d->B * C * wkv;
+    const double logits = (double)d->B * V * 4.0;
     if (attn_bytes) *attn_bytes = kv;
     return weights + d->B * C * w + kv + append + logits;
+}
+
+/* ------------------------------------------------------------------------ */
+/* sequence-sharded decode: one process per GPU, RCCL gather  */
+/* ------------------------------------------------------------------------ */
+/* This rank's engine decodes rows_per_rank[rank] sequences (its slice of the
+ * global batch, in rank order); hpa_comm_init must have bound the
+ * communicator.  The gather runs on a communication stream of its own. */
+int gpt2_decode_shard(GPT2* model, const int* rows_per_rank, int root) {
+    GPT2Decode* d = model->decode;
+    if (!d) { fprintf(stderr, "[paged_infer] gpt2_decode_init first\n"); return 1; }
+    const int n = hpa_comm_size(), rank = hpa_comm_rank();
+    if (n < 1 || rank < 0 || !rows_per_rank || root < 0 || root >= n) {
+        fprintf(stderr, "[paged_infer] gpt2_decode_shard: hpa_comm_init first, rows per rank, root\n");
+        return 1;
+    }
+    if (rows_per_rank[rank] != d->B) {
+        fprintf(stderr, "[paged_infer] gpt2_decode_shard: this rank's engine has %d sequences, not %d\n", d->B,
+                rows_per_rank[rank]);
+        return 1;
+    }
+    dec_shard_free(d);
+    DecShard* s = (DecShard*)calloc(1, sizeof(DecShard));
+    if (!s) return 1;
+    d->shard = s;
+    s->nranks = n;
+    s->rank = rank;
+    s->root = root;
+    s->last = -1;
+    s->rows = (int*)malloc(n * sizeof(int));
+    s->bytes = (size_t*)malloc(n * sizeof(size_t));
+    long total = 0;
+    if (!s->rows || !s->bytes) { dec_shard_free(d); return 1; }
+    for (int r = 0; r < n; r++) {
+        s->rows[r] = rows_per_rank[r];
+        total += rows_per_rank[r];
+    }
+    const size_t V = model->config.vocab_size;
+    s->stream = hpa_stream_create();
+    int ok = s->stream != NULL;
+    for (int k = 0; k < 2 && ok; k++) {
+        s->send[k] = (float*)hpa_malloc((size_t)d->B * V * 4);
+        s->send_ids[k] = (int*)hpa_malloc((size_t)d->B * 4);
+        if (rank == root) {
+            s->recv[k] = (float*)hpa_malloc((size_t)total * V * 4);
+            s->recv_ids[k] = (int*)hpa_malloc((size_t)total * 4);
+        }
+        s->ev_ready[k] = hpa_event_create_nt();
+        s->ev_done[k] = hpa_event_create_nt();
+        ok = s->send[k] && s->send_ids[k] && (rank != root || (s->recv[k] && s->recv_ids[k])) && s->ev_ready[k] &&
+             s->ev_done[k];
+    }
+    if (!ok) { dec_shard_free(d); return 1; }
+    return 0;
+}
+
+/* the end-of-step gather (the north star's one collective): this rank's
+ * logits (what = 0, [B][V] fp32) or greedy ids (what = 1, [B] int32) of the
+ * last enqueued step go to the root, rows in rank order.  The copy into send
+ * buffer k (k alternates) is enqueued on the compute stream; the
+ * communication stream waits for it and runs the RCCL gather, so it overlaps
+ * the next step's kernels.  Before buffer k is refilled (two gathers later)
+ * the compute stream waits for that buffer's gather.  Asynchronous: the
+ * result is read with gpt2_decode_gathered after gpt2_decode_gather_wait. */
+int gpt2_decode_gather(GPT2* model, int what) {
+    GPT2Decode* d = model->decode;
+    DecShard* s = d ? d->shard : NULL;
+    if (!s || (what != 0 && what != 1)) { fprintf(stderr, "[paged_infer] gpt2_decode_shard first\n"); return 1; }
+    const size_t V = model->config.vocab_size;
+    const size_t per = what ? sizeof(int) : V * sizeof(float);
+    const int k = s->k;
+    void* main_stream = hpa_get_stream();
+    int rc = 0;
+    if (s->pending[k]) rc |= hpa_stream_wait_event(s->ev_done[k]); /* buffer k's previous gather */
+    void* src = what ? (void*)d->d_next : (void*)d->d_logits;
+    void* snd = what ? (void*)s->send_ids[k] : (void*)s->send[k];
+    rc |= hpa_memcpy_async(snd, src, (size_t)d->B * per);
+    rc |= hpa_event_record(s->ev_ready[k]);
+    for (int r = 0; r < s->nranks; r++) s->bytes[r] = (size_t)s->rows[r] * per;
+    hpa_set_stream(s->stream);
+    rc |= hpa_stream_wait_event(s->ev_ready[k]);
+    rc |= hpa_comm_gatherv(snd, (size_t)d->B * per, what ? (void*)s->recv_ids[k] : (void*)s->recv[k], s->bytes,
+                           s->root, s->stream);
+    rc |= hpa_event_record(s->ev_done[k]);
+    hpa_set_stream(main_stream);
+    s->pending[k] = 1;
+    s->last = k;
+    s->k ^= 1;
+    return rc;
+}
+
+/* host waits for the last gather */
+int gpt2_decode_gather_wait(GPT2* model) {
+    GPT2Decode* d = model->decode;
+    if (!d || !d->shard || d->shard->last < 0) return 1;
+    return hpa_event_synchronize(d->shard->ev_done[d->shard->last]);
+}
+
+/* root: device pointer to the last gather's rows ([sum rows][V] fp32 logits
+ * or [sum rows] int32 ids); NULL elsewhere */
+void* gpt2_decode_gathered(GPT2* model, int what) {
+    GPT2Decode* d = model->decode;
+    if (!d || !d->shard || d->shard->last < 0 || d->shard->rank != d->shard->root) return NULL;
+    return what ? (void*)d->shard->recv_ids[d->shard->last] : (void*)d->shard->recv[d->shard->last];
 }
 
 /* ------------------------------------------------------------------------ */
 /* gpt2_forward (paged_infer.c:575-729) on the decode engine                */
 /* ------------------------------------------------------------------------ */
 /* inputs (B, T) hold the token window at absolute positions offset..offset+T-1
- * (the reference driver's convention, :1028-1080).  Positions not yet cached
- * are decoded in order through the engine (all L layers, absolute positions,
- * sequence b on prompt b's pages); logits/probs of row T-1 are written for
- * every b.  targets are accepted and ignored (mean_loss = -1). */
+ * (the reference driver's convention, :1028-1080: the context-filling loop
+ * calls it again and again at offset 0 with one more real token each time,
+ * then the window slides).  The engine keeps the token at every cached
+ * position; the first position whose token differs from the cached one (or
+ * is not cached yet) is where recomputation starts, one decode step per
+ * position, all L layers at absolute positions.  logits/probs rows r = 0..T-1
+ * of every b are those of position offset + r, as the reference's full
+ * window forward writes them (:727-728): rows of unchanged positions come
+ * from the per-position logits kept since they were computed.  targets are
+ * accepted and ignored (mean_loss = -1). */
 void gpt2_forward(GPT2* model, int* inputs, int* targets, size_t B, size_t T, size_t max_total,
                   int offset) {
     (void)targets;
@@ -2076,10 +1785,11 @@ void gpt2_forward(GPT2* model, int* inputs, int* targets, size_t B, size_t T, si
     const size_t V = model->config.vocab_size;
     for (size_t i = 0; i < B * T; i++) /* :591-596 */
         if (inputs[i] < 0 || (size_t)inputs[i] >= V) PI_FATAL("token out of range");
+    if (offset < 0) PI_FATAL("negative window offset");
     if (!model->acts_memory) {
         model->batch_size = (int)B;
         model->seq_len = (int)T;
-        size_t n = B * T * V;
+        const size_t n = B * T * V;
         model->acts_memory = (float*)hpa_malloc_managed(2 * n * sizeof(float));
         if (!model->acts_memory) PI_FATAL("activation allocation failed");
         memset(model->acts_memory, 0, 2 * n * sizeof(float));
@@ -2092,6 +1802,14 @@ void gpt2_forward(GPT2* model, int* inputs, int* targets, size_t B, size_t T, si
         if (maxctx < (size_t)offset + T) maxctx = (size_t)offset + T;
         if (gpt2_decode_init(model, (int)B, model->manager ? 0 : 16, (int)maxctx) != 0)
             PI_FATAL("decode engine init failed");
+        GPT2Decode* d = model->decode;
+        d->h_hist = (int*)malloc(B * (size_t)d->max_ctx * sizeof(int));
+        if (!d->h_hist) PI_FATAL("history allocation failed");
+        const double cache = (double)B * d->max_ctx * V * 4.0;
+        if (cache <= 4e9) { /* per-position logits for the rows of unchanged positions */
+            d->pos_logits = (float*)hpa_malloc((size_t)cache);
+            if (!d->pos_logits) PI_FATAL("per-position logits allocation failed");
+        }
     } else if ((int)B != model->batch_size || (int)T != model->seq_len) {
         printf("Model: B=%d T=%d, Desired: B=%d T=%d\n", model->batch_size, model->seq_len, (int)B,
                (int)T);
@@ -2099,52 +1817,68 @@ void gpt2_forward(GPT2* model, int* inputs, int* targets, size_t B, size_t T, si
     }
     memcpy(model->inputs, inputs, B * T * sizeof(int));
     GPT2Decode* d = model->decode;
-    /* all sequences share the window, so they advance together: the
-     * uncached positions cached..offset+T-1 go through the one-pass prefill
-     * (several tokens) or a decode step (one token) */
+    if (!d->h_hist) PI_FATAL("gpt2_forward: the engine was not created by gpt2_forward");
+    if ((size_t)offset + T > (size_t)d->max_ctx) PI_FATAL("window past max_total / max_seq_len");
+    /* sequences share the window, so they advance together: the first
+     * position (over all b) whose token is new or changed starts the redo */
     int cached = d->h_pos[0];
+    for (size_t b = 1; b < B; b++)
+        if (d->h_pos[b] != cached) PI_FATAL("gpt2_forward: sequences at different positions");
     if (cached < offset) PI_FATAL("window starts after uncached positions");
-    const int t0 = cached - offset, n = offset + (int)T - cached;
-    if (n > 1 && d->fused && d->nlanes == 1 && !d->pipeline) {
-        int* tok = (int*)malloc(B * (size_t)n * sizeof(int));
-        for (size_t b = 0; b < B; b++)
-            for (int t = 0; t < n; t++) tok[b * n + t] = inputs[b * T + t0 + t];
-        if (gpt2_decode_prefill(model, tok, n, NULL)) PI_FATAL("prefill failed");
-        free(tok);
-    } else {
-        int* tok = (int*)malloc(B * sizeof(int));
-        for (int t = t0; t < (int)T; t++) {
-            for (size_t b = 0; b < B; b++) tok[b] = inputs[b * T + t];
-            if (gpt2_decode_step(model, tok, NULL)) PI_FATAL("decode step failed");
+    int start = offset + (int)T;
+    for (size_t b = 0; b < B; b++)
+        for (int t = 0; t < (int)T; t++) {
+            const int p = offset + t;
+            if (p >= start) break;
+            if (p >= cached || d->h_hist[b * d->max_ctx + p] != inputs[b * T + t]) {
+                start = p;
+                break;
+            }
         }
-        free(tok);
+    if (!d->pos_logits) { /* only row T-1 is written: its position must be the last one decoded */
+        if (start < offset + (int)T - 1)
+            PI_FATAL("gpt2_forward: changed tokens before the window's last position need the per-position "
+                     "logits cache (B * max_total * V too large)");
+        if (start == offset + (int)T && cached != offset + (int)T) start = offset + (int)T - 1;
     }
+    if (start < cached) { /* rewind: pages are kept, positions >= start are rewritten */
+        int* p = (int*)malloc(B * sizeof(int));
+        for (size_t b = 0; b < B; b++) p[b] = start;
+        if (gpt2_decode_set_positions(model, p)) PI_FATAL("rewind failed");
+        free(p);
+    }
+    int* tok = (int*)malloc(B * sizeof(int));
+    for (int pos = start; pos < offset + (int)T; pos++) {
+        for (size_t b = 0; b < B; b++) {
+            tok[b] = inputs[b * T + (pos - offset)];
+            d->h_hist[b * d->max_ctx + pos] = tok[b];
+        }
+        if (gpt2_decode_step(model, tok, NULL)) PI_FATAL("decode step failed");
+        if (d->pos_logits)
+            for (size_t b = 0; b < B; b++)
+                PI_CHECK(hpa_memcpy_async(d->pos_logits + (b * d->max_ctx + pos) * V, d->d_logits + b * V,
+                                          V * sizeof(float)));
+    }
+    free(tok);
     PI_CHECK(hpa_synchronize());
-    for (size_t b = 0; b < B; b++) {
-        float* row = model->acts.logits + (b * T + (T - 1)) * V;
-        PI_CHECK(hpa_memcpy(row, d->d_logits + b * V, V * sizeof(float)));
-    }
+    /* logits rows: every position of the window when kept, else row T-1 */
+    for (size_t b = 0; b < B; b++)
+        for (int t = d->pos_logits ? 0 : (int)T - 1; t < (int)T; t++) {
+            const float* src = d->pos_logits ? d->pos_logits + (b * d->max_ctx + offset + t) * V : d->d_logits + b * V;
+            PI_CHECK(hpa_memcpy(model->acts.logits + (b * T + t) * V, src, V * sizeof(float)));
+        }
     /* probs of the same rows (softmax_forward, :259-286) */
-    for (size_t b = 0; b < B; b++) {
-        float* lg = model->acts.logits + (b * T + (T - 1)) * V;
-        float* pr = model->acts.probs + (b * T + (T - 1)) * V;
-        PI_CHECK(hpa_ref_softmax(pr, lg, 1, (int)V));
-    }
+    const int r0 = d->pos_logits ? 0 : (int)T - 1;
+    for (size_t b = 0; b < B; b++)
+        PI_CHECK(hpa_ref_softmax(model->acts.probs + (b * T + r0) * V, model->acts.logits + (b * T + r0) * V,
+                                 (int)T - r0, (int)V));
     PI_CHECK(hpa_synchronize());
     model->mean_loss = -1.0f;
 }
 
-/* paged_infer.c:736-745 (does not free model->manager, like the reference) */
+/* paged_infer.c:736-745 (does not free model->manager, like the reference;
+ * the engine hands a caller-owned manager its pages back, dec_free) */
 void gpt2_free(GPT2* model) {
-    if (model->decode) {
-        GPT2Decode* d = model->decode;
-        /* a caller-owned manager must not keep pointers into the freed pool */
-        if (!d->own_bm) {
-            for (int p = 0; p < d->bm->max_prompts; p++)
-                if (d->bm->prompt_block_count[p]) free_blocks_for_prompt(d->bm, p);
-            bm_set_backend(d->bm, NULL);
-        }
-    }
     gpt2_decode_free(model);
     hpa_free(model->params_memory);
     hpa_free(model->acts_memory);
@@ -2177,7 +1911,7 @@ int gpt2_decode_reserve(GPT2* model, int ctx) {
     GPT2Decode* d = model->decode;
     if (!d || ctx < 0 || ctx > d->max_ctx) return 1;
     for (int b = 0; b < d->B; b++) {
-        int need = (ctx + d->P - 1) / d->P;
+        const int need = (ctx + d->P - 1) / d->P;
         while (d->bm->prompt_block_count[b] < need)
             if (!request_block(d->bm, b)) return 1;
     }
@@ -2192,52 +1926,21 @@ int gpt2_decode_set_positions(GPT2* model, const int* pos) {
     for (int b = 0; b < d->B; b++) {
         if (pos[b] < 0 || pos[b] >= d->max_ctx) return 1;
         if (d->bm->prompt_block_count[b] * d->P < pos[b]) return 1;
-        d->h_pos[b] = pos[b];
     }
-    if (hpa_synchronize()) return 1;
-    memcpy(d->h_stage, pos, d->B * sizeof(int));
-    if (hpa_memcpy_async(d->d_pos, d->h_stage, d->B * sizeof(int))) return 1;
-    return hpa_synchronize();
+    for (int b = 0; b < d->B; b++) d->h_pos[b] = pos[b];
+    return hpa_memcpy(d->d_pos, d->h_pos, d->B * sizeof(int));
 }
 
 /* attention-kernel timing with HIP events on the launch stream: enable (1)
- * switches the engine to eager launches bracketed by per-layer events;
- * gpt2_decode_profile_collect() waits for the last step and adds its L
- * attention durations; read returns (total ms, launches). */
+ * switches the engine to eager launches with events around every layer's
+ * attention launch; read returns (total ms, launches). */
 int gpt2_decode_profile(GPT2* model, int enable) {
     GPT2Decode* d = model->decode;
     if (!d) return 1;
-    int L = model->config.num_layers;
-    if (!enable) {
-        if (hpa_synchronize()) return 1;
-        dec_prof_free(d, L);
-        return 0;
-    }
-    if (!d->prof_ev) {
-        d->prof_ev = (void**)calloc(2 * (size_t)L * DEC_MAX_LANES, sizeof(void*));
-        for (size_t i = 0; i < 2 * (size_t)L * DEC_MAX_LANES; i++) {
-            d->prof_ev[i] = hpa_event_create();
-            if (!d->prof_ev[i]) return 1;
-        }
-    }
-    d->use_graph = 0;
+    if (hpa_synchronize()) return 1;
+    d->profiling = enable ? 1 : 0;
     d->prof_ms = 0.0;
     d->prof_launches = 0;
-    return 0;
-}
-
-int gpt2_decode_profile_collect(GPT2* model) {
-    GPT2Decode* d = model->decode;
-    if (!d || !d->prof_ev) return 1;
-    int L = model->config.num_layers;
-    const int nl = d->fused ? d->nlanes : 1;
-    for (int l = 0; l < L; l++)
-        for (int i = 0; i < nl; i++) {
-            float ms = hpa_event_elapsed_ms(PROF_EV(d, l, i, 0), PROF_EV(d, l, i, 1));
-            if (ms < 0) return 1;
-            d->prof_ms += ms;
-            d->prof_launches++;
-        }
     return 0;
 }
 

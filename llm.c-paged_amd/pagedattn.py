@@ -50,13 +50,6 @@ class HpaKVPool(ctypes.Structure):
                 ("managed", ctypes.c_int)]
 
 
-class HpaAttnChunk(ctypes.Structure):
-    """hip_paged_attn.h HpaAttnChunk"""
-    _fields_ = [("q", _V), ("pool", _V), ("layer", ctypes.c_int), ("block_table", _V), ("bt_stride", ctypes.c_int),
-                ("pos", _V), ("state", _V), ("out_frag", _V), ("B", ctypes.c_int), ("chunk", ctypes.c_int),
-                ("nchunks", ctypes.c_int)]
-
-
 class HpaFusedGemm(ctypes.Structure):
     _fields_ = [("x", _V), ("M", ctypes.c_int), ("K", ctypes.c_int), ("ln_stats", _V),
                 ("ln_ntiles", ctypes.c_int), ("ln_w", _V), ("ln_b", _V), ("w", _V),
@@ -65,8 +58,7 @@ class HpaFusedGemm(ctypes.Structure):
                 ("pool", ctypes.POINTER(HpaKVPool)), ("layer", ctypes.c_int), ("block_table", _V),
                 ("bt_stride", ctypes.c_int), ("pos", _V), ("waves", ctypes.c_int),
                 ("row_blocks", ctypes.c_int), ("variant", ctypes.c_int), ("col_tiles", ctypes.c_int),
-                ("row_seq", _V), ("ln_fold_c1", _V), ("k_slices", ctypes.c_int), ("ks_slab", _V),
-                ("ks_count", _V), ("w_dtype", ctypes.c_int)]
+                ("row_seq", _V), ("ln_fold_c1", _V), ("w_dtype", ctypes.c_int)]
 
 
 HPA_FEPI_QKV, HPA_FEPI_RESID, HPA_FEPI_GELU, HPA_FEPI_LOGITS = 0, 1, 2, 3
@@ -96,9 +88,6 @@ def from_frag(f, rows, K):
 
 GPT2_124M = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
 GPT2_XL = dict(maxT=1024, V=50257, L=48, NH=25, C=1600)
-
-HPA_EPI_PARTIAL, HPA_EPI_BIAS, HPA_EPI_BIAS_GELU = 0, 1, 2
-
 
 def config(d):
     return GPT2Config(d["maxT"], d["V"], d["L"], d["NH"], d["C"])
@@ -139,6 +128,7 @@ def lib():
     _sig(L, "hpa_set_stream", i, [v])
     _sig(L, "hpa_get_stream", v, [])
     _sig(L, "hpa_synchronize", i, [])
+    _sig(L, "hpa_device_synchronize", i, [])
     _sig(L, "hpa_malloc", v, [sz])
     _sig(L, "hpa_malloc_managed", v, [sz])
     _sig(L, "hpa_host_alloc", v, [sz])
@@ -155,6 +145,7 @@ def lib():
     _sig(L, "hpa_stream_create", v, [])
     _sig(L, "hpa_stream_destroy", i, [v])
     _sig(L, "hpa_stream_wait_event", i, [v])
+    _sig(L, "hpa_event_synchronize", i, [v])
     _sig(L, "hpa_last_error", ctypes.c_char_p, [])
     _sig(L, "hpa_device_info", i, [ctypes.c_char_p, i, _I, ctypes.POINTER(sz)])
     _sig(L, "hpa_set_attention_waves", i, [i])
@@ -166,13 +157,16 @@ def lib():
     _sig(L, "hpa_pool_v_index", sz, [P, i, i, i, i, i])
     _sig(L, "hpa_pool_fill_random", i, [P, v, i, i, i, ctypes.c_uint64])
     _sig(L, "hpa_paged_attention_decode", i, [v, P, i, v, i, v, v, i])
-    _sig(L, "hpa_gemm_f32", i, [v, i, v, v, v, i, i, i, i, i, i])
-    _sig(L, "hpa_gemm_pick_splitk", i, [i, i, i])
-    _sig(L, "hpa_qkv_append", i, [v, i, v, v, P, i, v, i, v, i, i])
-    _sig(L, "hpa_embed_ln", i, [v, v, v, v, v, v, v, v, i, i])
-    _sig(L, "hpa_residual_ln", i, [v, i, v, v, v, v, v, v, i, i])
-    _sig(L, "hpa_bias_gelu", i, [v, i, v, v, i, i])
-    _sig(L, "hpa_argmax_advance", i, [v, i, i, v, v, v])
+    _sig(L, "hpa_attn_ws_bytes", sz, [i, i, i])
+    _sig(L, "hpa_attn_pick_splits", i, [i, i, i, i])
+    _sig(L, "hpa_paged_attention_decode_split", i, [v, P, i, v, i, v, v, i, i, v, i])
+    _sig(L, "hpa_comm_id_bytes", sz, [])
+    _sig(L, "hpa_comm_unique_id", i, [v, sz])
+    _sig(L, "hpa_comm_init", i, [i, i, v])
+    _sig(L, "hpa_comm_destroy", i, [])
+    _sig(L, "hpa_comm_size", i, [])
+    _sig(L, "hpa_comm_rank", i, [])
+    _sig(L, "hpa_comm_gatherv", i, [v, sz, v, ctypes.POINTER(sz), i, v])
     _sig(L, "hpa_ref_attention_paged", i, [v, v, v, v, v, v, i, i, i, i, i, i])
     _sig(L, "hpa_ref_matmul", i, [v, v, v, v, i, i, i, i, i])
     # block manager (block_manager.c API)
@@ -227,12 +221,20 @@ def lib():
     _sig(L, "gpt2_decode_fill_random", i, [v, i, ctypes.c_ulonglong])
     _sig(L, "gpt2_decode_set_graph", i, [v, i])
     _sig(L, "gpt2_decode_reserve", i, [v, i])
-    _sig(L, "gpt2_decode_set_fused", i, [v, i])
+    _sig(L, "gpt2_decode_set_attn_splits", i, [v, i])
+    _sig(L, "gpt2_decode_attn_splits", i, [v])
+    _sig(L, "gpt2_decode_evicted", i, [v, _I])
+    _sig(L, "gpt2_decode_read_kv", i, [v, i, i, i, _F, _F])
+    _sig(L, "gpt2_decode_batch", i, [v])
+    _sig(L, "gpt2_decode_shard", i, [v, _I, i])
+    _sig(L, "gpt2_decode_gather", i, [v, i])
+    _sig(L, "gpt2_decode_gather_wait", i, [v])
+    _sig(L, "gpt2_decode_gathered", v, [v, i])
+    _sig(L, "gpt2_decode_profile", i, [v, i])
+    _sig(L, "gpt2_decode_profile_read", ctypes.c_double, [v, ctypes.POINTER(ctypes.c_long)])
     _sig(L, "hpa_frag_elems", sz, [i, i])
     _sig(L, "hpa_pack_frag", i, [v, i, i, i, v])
     _sig(L, "hpa_ln_fold_pack", i, [v, i, i, v, v, v, v, v, v])
-    _sig(L, "hpa_fused_pick_slices", i, [i, i, i])
-    _sig(L, "hpa_fused_ks_workspace", i, [ctypes.POINTER(HpaFusedGemm), ctypes.POINTER(sz), ctypes.POINTER(sz)])
     _sig(L, "hpa_unpack_frag", i, [v, i, i, v, i])
     _sig(L, "hpa_gemm_fused", i, [ctypes.POINTER(HpaFusedGemm)])
     _sig(L, "hpa_logits_partials", i, [ctypes.POINTER(HpaFusedGemm)])
@@ -240,7 +242,6 @@ def lib():
     _sig(L, "hpa_fused_pick", None, [i, i, i, _I])
     _sig(L, "hpa_fused_pick_bf16", None, [i, i, i, _I])
     _sig(L, "hpa_fused_pick_bf16_ares", i, [i, i, i, _I])
-    _sig(L, "hpa_fused_pick_f32_ares", i, [i, i, i, _I])
     _sig(L, "hpa_embed_frag", i, [v, v, v, v, v, v, i, i])
     _sig(L, "hpa_argmax_final", i, [v, i, i, i, v, v, v, v])
     _sig(L, "hpa_sample_final", i, [v, i, i, v, v, v, v, v])
@@ -250,22 +251,9 @@ def lib():
     _sig(L, "gpt2_decode_logits", v, [v])
     _sig(L, "gpt2_decode_next", v, [v])
     _sig(L, "gpt2_decode_positions", i, [v, _I])
-    _sig(L, "gpt2_decode_splits", i, [v, _I])
     _sig(L, "gpt2_decode_gemm_config", i, [v, _I, _I, _I, i])
-    _sig(L, "gpt2_decode_set_lanes", i, [v, i])
     _sig(L, "gpt2_decode_time_attention", i, [v, i, ctypes.POINTER(ctypes.c_double),
                                               ctypes.POINTER(ctypes.c_double)])
-    _sig(L, "gpt2_decode_lanes", i, [v])
-    _sig(L, "gpt2_decode_set_pipeline", i, [v, i])
-    _sig(L, "gpt2_decode_pipeline", i, [v])
-    _sig(L, "gpt2_decode_set_split", i, [v, i])
-    _sig(L, "gpt2_decode_set_overlap", i, [v, i])
-    _sig(L, "gpt2_decode_overlap", i, [v])
-    _sig(L, "gpt2_decode_overlap_faults", ctypes.c_uint, [v])
-    _sig(L, "gpt2_decode_split", i, [v])
-    _sig(L, "hpa_stream_create_cumask", v, [i, i])
-    _sig(L, "hpa_attn_state_elems", ctypes.c_size_t, [i, i])
-    _sig(L, "hpa_attn_chunk_with_gemm", i, [ctypes.c_void_p, ctypes.c_void_p])
     _sig(L, "gpt2_decode_step_bytes", ctypes.c_double, [v, ctypes.POINTER(ctypes.c_double)])
     _sig(L, "random_u32", ctypes.c_uint, [ctypes.POINTER(ctypes.c_ulonglong)])
     _sig(L, "random_f32", f, [ctypes.POINTER(ctypes.c_ulonglong)])
@@ -534,9 +522,6 @@ class Model:
               "gpt2_decode_init")
         self.B = B
 
-    def set_fused(self, on):
-        check(lib().gpt2_decode_set_fused(self.h, int(on)), "set_fused")
-
     def set_graph(self, on):
         check(lib().gpt2_decode_set_graph(self.h, int(on)), "set_graph")
 
@@ -575,9 +560,49 @@ class Model:
         check(lib().gpt2_decode_positions(self.h, out.ctypes.data_as(_I)), "positions")
         return out
 
-    def splits(self):
-        out = np.zeros(4, np.int32)
-        check(lib().gpt2_decode_splits(self.h, out.ctypes.data_as(_I)), "splits")
+    def set_attn_splits(self, splits):
+        """context ranges per (sequence, head) of the decode attention (0 = by shape)"""
+        check(lib().gpt2_decode_set_attn_splits(self.h, int(splits)), "set_attn_splits")
+        return lib().gpt2_decode_attn_splits(self.h)
+
+    def attn_splits(self):
+        return lib().gpt2_decode_attn_splits(self.h)
+
+    def evicted(self):
+        """sequences the LRU policy paged out since the last call (bool mask)"""
+        m = np.zeros(self.B, np.int32)
+        n = lib().gpt2_decode_evicted(self.h, m.ctypes.data_as(_I))
+        if n < 0:
+            raise RuntimeError("evicted: no engine")
+        return m.astype(bool)
+
+    def read_kv(self, layer, b, n):
+        """K, V of positions [0, n) of sequence b, token-major (n, C) fp32"""
+        C = self.cfg.channels
+        k = np.zeros((n, C), np.float32)
+        v = np.zeros((n, C), np.float32)
+        check(lib().gpt2_decode_read_kv(self.h, int(layer), int(b), int(n), k.ctypes.data_as(_F),
+                                        v.ctypes.data_as(_F)), "read_kv")
+        return k, v
+
+    def shard(self, rows_per_rank, root=0):
+        """sequence-sharded decode: this rank's row count among rows_per_rank
+        (after hpa_comm_init); gather() then runs the RCCL end-of-step gather"""
+        r = np.ascontiguousarray(rows_per_rank, np.int32)
+        check(lib().gpt2_decode_shard(self.h, r.ctypes.data_as(_I), int(root)), "shard")
+
+    def gather(self, what=0):
+        check(lib().gpt2_decode_gather(self.h, int(what)), "gather")
+
+    def gathered(self, total_rows, what=0):
+        """root: host copy of the last gather (waits for it)"""
+        check(lib().gpt2_decode_gather_wait(self.h), "gather_wait")
+        ptr = lib().gpt2_decode_gathered(self.h, int(what))
+        if not ptr:
+            return None
+        out = np.empty((total_rows, self.cfg.vocab_size) if what == 0 else (total_rows,),
+                       np.float32 if what == 0 else np.int32)
+        check(lib().hpa_memcpy(out.ctypes.data, ptr, out.nbytes), "gathered download")
         return out
 
     def time_attention(self, iters=48):
@@ -616,27 +641,6 @@ class Model:
 
     def set_sampling(self, enable=True, seed=1337):
         check(lib().gpt2_decode_set_sampling(self.h, int(bool(enable)), int(seed)), "set_sampling")
-
-    def set_pipeline(self, enable=True):
-        check(lib().gpt2_decode_set_pipeline(self.h, int(bool(enable))), "set_pipeline")
-
-    def set_overlap(self, chain_blocks):
-        """overlapped step: one lane's attention beside the other lane's GEMM
-        chain in one launch per layer half (0 = off)"""
-        check(lib().gpt2_decode_set_overlap(self.h, int(chain_blocks)), "set_overlap")
-        return lib().gpt2_decode_overlap(self.h)
-
-    def overlap_faults(self):
-        return int(lib().gpt2_decode_overlap_faults(self.h))
-
-    def set_split(self, gemm_cus):
-        """split step: GEMM chains on `gemm_cus` CUs beside the attention (0 = off)"""
-        check(lib().gpt2_decode_set_split(self.h, int(gemm_cus)), "set_split")
-        return lib().gpt2_decode_split(self.h)
-
-    def set_lanes(self, lanes):
-        check(lib().gpt2_decode_set_lanes(self.h, int(lanes)), "set_lanes")
-        return lib().gpt2_decode_lanes(self.h)
 
     def gemm_config(self, waves=None, row_blocks=None, col_tiles=None):
         """fused GEMM launch shapes [qkv, attproj, fc, fcproj, logits]:

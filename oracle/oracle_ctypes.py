@@ -56,6 +56,8 @@ def lib(fast=False):
     L.oracle_paged_create.restype = ctypes.c_void_p
     L.oracle_paged_create.argtypes = [_F, OracleConfig, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_ulonglong]
+    L.oracle_paged_set_kv.restype = ctypes.c_int
+    L.oracle_paged_set_kv.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _F, _F]
     L.oracle_paged_step.restype = ctypes.c_int
     L.oracle_paged_step.argtypes = [ctypes.c_void_p, _I, _F, _I]
     L.oracle_paged_fill_random.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_ulonglong]
@@ -158,6 +160,14 @@ class PagedDecoder:
         if rc != 0:
             raise RuntimeError("oracle_paged_step failed (context full)")
         return nxt, logits
+
+    def set_kv(self, layer, b, k, v):
+        """positions [0, len(k)) of sequence b at `layer` take these K/V rows
+        (token-major (n, C)); pos[b] becomes n"""
+        k = np.ascontiguousarray(k, np.float32)
+        v = np.ascontiguousarray(v, np.float32)
+        if self.L.oracle_paged_set_kv(self.h, int(layer), int(b), k.shape[0], fp(k), fp(v)) != 0:
+            raise RuntimeError("oracle_paged_set_kv failed")
 
     def fill_random(self, ctx, seed=1):
         self.L.oracle_paged_fill_random(self.h, ctx, seed)

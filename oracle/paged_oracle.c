@@ -486,6 +486,22 @@ void oracle_paged_fill_random(OraclePaged* o, int ctx, unsigned long long seed) 
             }
 }
 
+/* parity tests: positions [0, n) of sequence b at layer l take the given
+ * K/V rows (token-major [n][C], the cache the GPU engine holds, so both
+ * sides decode from identical pages); the sequence's position becomes n */
+int oracle_paged_set_kv(OraclePaged* o, int layer, int b, int n, const float* k, const float* v) {
+    const int C = o->cfg.channels;
+    if (layer < 0 || layer >= o->cfg.num_layers || b < 0 || b >= o->B || n < 0) return -1;
+    for (int p = 0; p < n; p++) {
+        if (ensure_page(o, b, p) != 0) return -1;
+        const int page = o->block_table[(size_t)b * o->max_pages + p / o->P];
+        memcpy(page_ptr(o, o->kpool, layer, page) + (size_t)(p % o->P) * C, k + (size_t)p * C, (size_t)C * 4);
+        memcpy(page_ptr(o, o->vpool, layer, page) + (size_t)(p % o->P) * C, v + (size_t)p * C, (size_t)C * 4);
+    }
+    o->pos[b] = n;
+    return 0;
+}
+
 int oracle_paged_step(OraclePaged* o, const int* tokens, float* logits, int* next) {
     OracleConfig cfg = o->cfg;
     int B = o->B, C = cfg.channels, NH = cfg.num_heads, L = cfg.num_layers, V = cfg.vocab_size;

@@ -97,6 +97,9 @@ int  oracle_paged_step(OraclePaged* o, const int* tokens, float* logits, int* ne
  * (the bounded CPU-baseline sample; bench.py only). */
 void oracle_paged_fill_random(OraclePaged* o, int ctx, unsigned long long seed);
 int  oracle_paged_pos(const OraclePaged* o, int b);
+/* parity tests: the K/V of positions [0, n) of sequence b at layer l
+ * (token-major [n][C]); pos[b] becomes n */
+int  oracle_paged_set_kv(OraclePaged* o, int layer, int b, int n, const float* k, const float* v);
 /* bf16 KV pool semantics (BASELINE config 5): appended K/V are rounded to
  * bf16 (nearest even) and read back exactly; all arithmetic stays fp32 */
 void oracle_paged_set_kv_bf16(OraclePaged* o, int on);

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 
-def _run_case(hip, P, ctxs, NH, waves=4, seed=0, q_scale=2.0, kv=None, chunks=0, bf16=False):
+def _run_case(hip, P, ctxs, NH, waves=4, seed=0, q_scale=2.0, kv=None, splits=0, bf16=False, repeat=1):
     rng = np.random.default_rng(seed)
     L = hip.lib()
     C = NH * 64
@@ -46,19 +46,26 @@ def _run_case(hip, P, ctxs, NH, waves=4, seed=0, q_scale=2.0, kv=None, chunks=0,
     d_q = hip.DeviceBuffer.from_array(q)
     d_bt = hip.DeviceBuffer.from_array(bt)
     d_pos = hip.DeviceBuffer.from_array(pos)
-    if chunks:  # context chunks with carried softmax state (the pipelined decode)
-        import ctypes
+    if splits:  # split-context form, frag output, repeated launches over one workspace
         Mp = (B + 15) // 16 * 16
         d_out = hip.DeviceBuffer(Mp * C * 4)
-        d_state = hip.DeviceBuffer(L.hpa_attn_state_elems(B, NH) * 4)
-        a = hip.HpaAttnChunk(q=d_q.ptr, pool=ctypes.addressof(pool.s), layer=0, block_table=d_bt.ptr,
-                             bt_stride=maxp, pos=d_pos.ptr, state=d_state.ptr, out_frag=d_out.ptr, B=B,
-                             nchunks=chunks)
-        for c in range(chunks):
-            a.chunk = c
-            hip.check(L.hpa_attn_chunk_with_gemm(ctypes.byref(a), None), "attn chunk")
-        hip.check(L.hpa_synchronize())
-        out = hip.from_frag(d_out.download(Mp * C), B, C)
+        wsb = L.hpa_attn_ws_bytes(B, NH, splits)
+        d_ws = hip.DeviceBuffer(max(wsb, 4))
+        hip.check(L.hpa_memset_async(d_ws.ptr, 0, wsb))
+        hip.check(L.hpa_set_attention_waves(waves))
+        outs = []
+        for _ in range(repeat):
+            hip.check(L.hpa_paged_attention_decode_split(d_q.ptr, pool.ref, 0, d_bt.ptr, maxp, d_pos.ptr, d_out.ptr,
+                                                         B, splits, d_ws.ptr if wsb else None, 1), "split attention")
+            hip.check(L.hpa_synchronize())
+            outs.append(hip.from_frag(d_out.download(Mp * C), B, C))
+        hip.check(L.hpa_set_attention_waves(4))
+        for o in outs[1:]:  # fixed merge order: bit-identical every launch
+            assert np.array_equal(o, outs[0])
+        # the counters are left zero for the next launch
+        cnt = d_ws.download(B * NH, np.int32, offset=B * NH * splits * 68 * 4) if wsb else np.zeros(1)
+        assert not cnt.any()
+        out = outs[0]
     else:
         d_out = hip.DeviceBuffer(q.nbytes)
         hip.check(L.hpa_set_attention_waves(waves))
@@ -157,21 +164,86 @@ def test_decode_attention_full_size_subset_and_determinism(hip):
 
 
 @pytest.mark.parametrize("P", [8, 16, 32])
-@pytest.mark.parametrize("chunks", [1, 3, 4])
-def test_chunked_attention_with_carried_state(hip, P, chunks):
-    """the pipelined decode's attention: context chunks in separate launches,
-    (m, l, acc) carried through memory; ctx 1 and 2 leave most chunks empty"""
+@pytest.mark.parametrize("splits", [1, 2, 3, 4, 8, 16])
+def test_split_context_attention(hip, P, splits):
+    """flash-decoding form: each (sequence, head) cut into
+    `splits` context ranges, merged by the last range in range order; ragged
+    contexts leave ranges empty (ctx 1, 2), repeated launches are bit-identical
+    and leave the arrival counters zero"""
     ctxs = [1, 2, 5, 63, 64, 65, 200, 257, 1024]
-    out, ref = _run_case(hip, P, ctxs, NH=3, seed=P + chunks, chunks=chunks)
+    out, ref = _run_case(hip, P, ctxs, NH=3, seed=P + splits, splits=splits, repeat=3)
     assert np.abs(out - ref).max() <= TOL
 
 
-def test_chunked_attention_all_scores_below_reference_floor(hip):
+@pytest.mark.parametrize("waves", [1, 2, 8])
+def test_split_context_attention_waves(hip, waves):
+    out, ref = _run_case(hip, 16, [1, 70, 333, 1000], NH=2, waves=waves, seed=13, splits=4, repeat=2)
+    assert np.abs(out - ref).max() <= TOL
+
+
+def test_split_context_attention_floor_and_peaked(hip):
+    """every score below the -10000 floor (zero output, as the reference) and a
+    peaked softmax, across ranges"""
     def kv(ctx, C):
         return np.full((ctx, C), 10.0, np.float32), np.ones((ctx, C), np.float32)
 
-    out, ref = _run_case(hip, 16, [5, 80, 300], NH=1, seed=1, kv=kv, q_scale=1e-6, chunks=4)
+    out, ref = _run_case(hip, 16, [5, 80, 300], NH=1, seed=1, kv=kv, q_scale=1e-6, splits=4)
     assert np.abs(out - ref).max() <= TOL
+    out, ref = _run_case(hip, 16, [300, 999, 64], NH=2, seed=5, q_scale=40.0, splits=8)
+    assert np.abs(out - ref).max() <= TOL
+
+
+@pytest.mark.parametrize("splits", [2, 4, 8])
+def test_split_context_attention_bf16_pool(hip, splits):
+    ctxs = [1, 2, 7, 63, 64, 65, 200, 257, 1024]
+    out, ref = _run_case(hip, 8, ctxs, NH=3, seed=splits, bf16=True, splits=splits, repeat=2)
+    assert np.abs(out - ref).max() <= TOL
+
+
+@pytest.mark.parametrize("B", [8, 16, 32])
+def test_split_context_attention_strong_scaling_shapes(hip, B):
+    """the per-GPU batches of the metric's B = 64 at 8/4/2 GPUs (GPT-2 124M,
+    ctx 1024, page 16) at the engine's split count: every sequence vs the
+    oracle on a head subset, bit-identical on relaunch"""
+    L = hip.lib()
+    NH, P, ctx = 12, 16, 1024
+    C = NH * 64
+    S = L.hpa_attn_pick_splits(B, NH, ctx, 256)
+    assert S == {8: 8, 16: 4, 32: 2}[B]
+    maxp = ctx // P
+    pool = hip.Pool(1, NH, P, B * maxp)
+    rng = np.random.default_rng(B)
+    bt = rng.permutation(B * maxp).astype(np.int32).reshape(B, maxp)
+    d_bt = hip.DeviceBuffer.from_array(bt)
+    hip.check(L.hpa_pool_fill_random(pool.ref, d_bt.ptr, maxp, B, ctx, 99))
+    q = rng.uniform(-2, 2, (B, C)).astype(np.float32)
+    pos = np.full(B, ctx - 1, np.int32)
+    pos[::3] = rng.integers(0, ctx, len(pos[::3]))  # ragged
+    d_q = hip.DeviceBuffer.from_array(q)
+    d_pos = hip.DeviceBuffer.from_array(pos)
+    Mp = (B + 15) // 16 * 16
+    d_out = hip.DeviceBuffer(Mp * C * 4)
+    wsb = L.hpa_attn_ws_bytes(B, NH, S)
+    d_ws = hip.DeviceBuffer(wsb)
+    hip.check(L.hpa_memset_async(d_ws.ptr, 0, wsb))
+    outs = []
+    for _ in range(2):
+        hip.check(L.hpa_paged_attention_decode_split(d_q.ptr, pool.ref, 0, d_bt.ptr, maxp, d_pos.ptr, d_out.ptr, B,
+                                                     S, d_ws.ptr, 1))
+        outs.append(hip.from_frag(d_out.download(Mp * C), B, C))
+    assert np.array_equal(outs[0], outs[1])
+    for b in range(B):
+        n = int(pos[b]) + 1
+        k, v = pool.read_tokens(0, bt[b], n)
+        np_ = (n + P - 1) // P
+        kp = [np.zeros((P, C), np.float32) for _ in range(np_)]
+        vp = [np.zeros((P, C), np.float32) for _ in range(np_)]
+        for i in range(np_):
+            m = min(P, n - i * P)
+            kp[i][:m] = k[i * P:i * P + m]
+            vp[i][:m] = v[i * P:i * P + m]
+        ref = oc.attention_decode(q[b], kp, vp, n, NH)
+        assert np.abs(outs[0][b] - ref).max() <= TOL, b
 
 
 @pytest.mark.parametrize("P", [8, 16, 32])

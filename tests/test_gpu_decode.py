@@ -3,9 +3,11 @@ paged incremental decode (absolute positions, all L layers; the oracle is
 pinned bit-exact to the reference's full-L forward in test_oracle.py).
 
 Tolerances: logits <= 2e-4 max-abs (fp32, different summation order: MFMA
-k-chains + split-K + parallel LN reductions vs the reference's sequential
-dots); greedy ids bit-exact wherever the oracle's top-2 logit margin exceeds
-1e-3 (near-ties are reported, SURVEY.md 7 hard part 4).
+k-chains + parallel LN reductions vs the reference's sequential dots).
+Greedy ids bit-exact on every row except where the oracle's top-2 logit
+margin is within 2x the measured max |logit difference| of that run (a
+genuine near-tie: an order-of-summation difference of that size can flip
+it); the exempt rows are counted, printed and asserted to be few.
 """
 import numpy as np
 import pytest
@@ -15,9 +17,9 @@ import synth
 
 pytestmark = pytest.mark.gpu
 LOGIT_TOL = 2e-4
-TIE_MARGIN = 1e-3
 
 SMALL = dict(maxT=128, V=1000, L=2, NH=2, C=128)
+GPT2_124M = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
 
 
 def _margins(logits):
@@ -25,42 +27,67 @@ def _margins(logits):
     return s[:, -1] - s[:, -2]
 
 
-def _compare_run(hip, cfgd, B, P, steps, seed, graph=False, feed_greedy=False, fused=True, pipeline=False,
-                 kv_bf16=False, tol=LOGIT_TOL, w_bf16=False, tie=TIE_MARGIN):
+class IdCheck:
+    """greedy ids vs the oracle's, with the near-tie rule above"""
+
+    def __init__(self):
+        self.rows = []  # (oracle margins, ids equal) per step
+        self.worst = 0.0
+
+    def add(self, g_logits, o_logits, g_next, o_next):
+        self.worst = max(self.worst, float(np.abs(g_logits - o_logits).max()))
+        self.rows.append((_margins(o_logits), np.asarray(g_next) == np.asarray(o_next)))
+
+    def verify(self, tol, max_exempt_frac=0.02):
+        tie = 2.0 * self.worst
+        exempt = total = 0
+        for margin, same in self.rows:
+            clear = margin > tie
+            assert same[clear].all(), (margin[clear & ~same], tie)
+            exempt += int((~clear).sum())
+            total += len(margin)
+        print(f"max |logit diff| {self.worst:.3e}; tie margin {tie:.3e}; exempt rows {exempt}/{total}")
+        assert self.worst <= tol, self.worst
+        assert exempt <= max(1, max_exempt_frac * total), (exempt, total)
+        return exempt
+
+
+def _compare_run(hip, cfgd, B, P, steps, seed, graph=False, feed_greedy=False, kv_bf16=False, tol=LOGIT_TOL,
+                 w_bf16=False, splits=0, max_exempt_frac=0.02):
     params = synth.params(cfgd, seed=seed)
     model = hip.Model(cfgd, params=params)
     model.decode_init(B, P, cfgd["maxT"], kv_dtype=hip.HPA_BF16 if kv_bf16 else hip.HPA_F32,
                       w_dtype=hip.HPA_BF16 if w_bf16 else hip.HPA_F32)
-    model.set_fused(fused)
-    if pipeline:
-        model.set_pipeline(True)
+    if splits:
+        assert model.set_attn_splits(splits) == splits
     model.set_graph(graph)
     c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
     orc = oc.PagedDecoder(params, c, B, P, cfgd["maxT"], page_seed=seed + 3, kv_bf16=kv_bf16, w_bf16=w_bf16)
     rng = np.random.default_rng(seed)
     tok = rng.integers(0, cfgd["V"], B).astype(np.int32)
-    worst = 0.0
-    ties = 0
+    chk = IdCheck()
     for t in range(steps):
         o_next, o_logits = orc.step(tok)
         g_next = model.step(tok)
-        g_logits = model.logits()
-        worst = max(worst, float(np.abs(g_logits - o_logits).max()))
-        clear = _margins(o_logits) > tie
-        ties += int((~clear).sum())
-        assert np.array_equal(g_next[clear], o_next[clear]), (t, g_next, o_next)
+        chk.add(model.logits(), o_logits, g_next, o_next)
         tok = o_next if feed_greedy else rng.integers(0, cfgd["V"], B).astype(np.int32)
-    assert worst <= tol, worst
+    ties = chk.verify(tol, max_exempt_frac)
     assert np.array_equal(model.positions(), np.full(B, steps, np.int32))
     model.close()
     orc.close()
-    return worst, ties
+    return chk.worst, ties
 
 
 @pytest.mark.parametrize("P", [8, 16, 32])
-@pytest.mark.parametrize("fused", [True, False])
-def test_decode_small_model_matches_oracle(hip, P, fused):
-    _compare_run(hip, SMALL, B=3, P=P, steps=70, seed=P, fused=fused)
+def test_decode_small_model_matches_oracle(hip, P):
+    _compare_run(hip, SMALL, B=3, P=P, steps=70, seed=P)
+
+
+@pytest.mark.parametrize("splits", [2, 8, 16])
+def test_decode_with_split_context_attention_matches_oracle(hip, splits):
+    """the engine with its attention's context cut into ranges (the strong-
+    scaling shapes' path), graph replay, contexts crossing many ranges"""
+    _compare_run(hip, SMALL, B=4, P=16, steps=100, seed=80 + splits, graph=True, splits=splits)
 
 
 def test_decode_batch_over_64_rows(hip):
@@ -90,11 +117,9 @@ def test_graph_and_eager_bit_identical(hip):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("fused", [True, False])
-def test_decode_gpt2_124m_shapes(hip, fused):
+def test_decode_gpt2_124m_shapes(hip):
     """GPT-2 124M shapes (L=12, C=768, NH=12, V=50257), B=4, 24 steps"""
-    cfgd = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
-    worst, ties = _compare_run(hip, cfgd, B=4, P=16, steps=24, seed=21, fused=fused)
+    worst, ties = _compare_run(hip, GPT2_124M, B=4, P=16, steps=24, seed=21)
     print(f"124M: worst logit diff {worst:.3e}, near-ties {ties}")
 
 
@@ -138,102 +163,6 @@ def test_context_full_is_an_error(hip):
     m.close()
 
 
-@pytest.mark.parametrize("lanes,B,graph", [(2, 64, False), (4, 64, True), (3, 70, True), (8, 20, False)])
-def test_lanes_bit_identical_to_one_lane(hip, lanes, B, graph):
-    """micro-batch lanes run row groups concurrently on their own streams;
-    every row's arithmetic is unchanged, so ids and logits equal lanes=1
-    bit for bit (B=20 with 8 lanes: only 2 lanes of 16-row blocks exist)"""
-    params = synth.params(SMALL, seed=31)
-    outs = []
-    for nl in (1, lanes):
-        m = hip.Model(SMALL, params=params)
-        m.decode_init(B, 16, 128)
-        got = m.set_lanes(nl)
-        assert got == min(nl, (B + 15) // 16)
-        m.set_graph(graph)
-        rng = np.random.default_rng(5)
-        seq = [m.step(rng.integers(0, 1000, B).astype(np.int32))]
-        for _ in range(12):
-            seq.append(m.step(None))
-        seq.append(m.logits())
-        seq.append(m.positions())
-        outs.append(seq)
-        m.close()
-    for a, b in zip(*outs):
-        assert np.array_equal(a, b)
-
-
-def test_lanes_match_oracle(hip):
-    params = synth.params(SMALL, seed=8)
-    B = 40
-    model = hip.Model(SMALL, params=params)
-    model.decode_init(B, 16, SMALL["maxT"])
-    assert model.set_lanes(3) == 3
-    model.set_graph(True)
-    c = oc.cfg(SMALL["maxT"], SMALL["V"], SMALL["L"], SMALL["NH"], SMALL["C"])
-    orc = oc.PagedDecoder(params, c, B, 16, SMALL["maxT"], page_seed=11)
-    rng = np.random.default_rng(8)
-    for t in range(20):
-        tok = rng.integers(0, SMALL["V"], B).astype(np.int32)
-        o_next, o_logits = orc.step(tok)
-        g_next = model.step(tok)
-        assert np.abs(model.logits() - o_logits).max() <= LOGIT_TOL
-        clear = _margins(o_logits) > TIE_MARGIN
-        assert np.array_equal(g_next[clear], o_next[clear])
-    model.close()
-    orc.close()
-
-
-def test_set_lanes_rejects_out_of_range(hip):
-    m = hip.Model(SMALL)
-    m.decode_init(4, 16, 64)
-    with pytest.raises(RuntimeError):
-        m.set_lanes(0)
-    with pytest.raises(RuntimeError):
-        m.set_lanes(9)
-    m.close()
-
-
-@pytest.mark.parametrize("P,B", [(16, 40), (8, 33), (32, 64)])
-def test_pipelined_decode_matches_oracle(hip, P, B):
-    """two lanes on one stream, attention chunks beside the other lane's GEMMs"""
-    _compare_run(hip, SMALL, B=B, P=P, steps=40, seed=P + B, pipeline=True)
-
-
-def test_pipelined_decode_gpt2_124m_shapes(hip):
-    """124M shapes: the one-shot GEMM role (K = 768) and the looped one (fcproj)"""
-    cfgd = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
-    worst, ties = _compare_run(hip, cfgd, B=48, P=16, steps=12, seed=5, pipeline=True, graph=True)
-    print(f"124M pipelined: worst logit diff {worst:.3e}, near-ties {ties}")
-
-
-def test_pipelined_graph_equals_eager(hip):
-    params = synth.params(SMALL, seed=14)
-    outs = []
-    for graph in (False, True):
-        m = hip.Model(SMALL, params=params)
-        m.decode_init(40, 16, 128)
-        m.set_pipeline(True)
-        m.set_graph(graph)
-        rng = np.random.default_rng(2)
-        seq = [m.step(rng.integers(0, 1000, 40).astype(np.int32))]
-        for _ in range(10):
-            seq.append(m.step(None))
-        seq.append(m.logits())
-        outs.append(seq)
-        m.close()
-    for a, b in zip(*outs):
-        assert np.array_equal(a, b)
-
-
-def test_set_pipeline_needs_two_lanes(hip):
-    m = hip.Model(SMALL)
-    m.decode_init(16, 16, 64)
-    with pytest.raises(RuntimeError):
-        m.set_pipeline(True)
-    m.close()
-
-
 def test_decode_xl_width_matches_oracle(hip):
     """GPT-2 XL layer shapes (C=1600, NH=25 -> K/16 = 100 and 400: the looped
     GEMM path; page 32 as BASELINE config 3) on a 2-layer model"""
@@ -265,10 +194,6 @@ def test_decode_bf16_kv_124m_shapes(hip):
 def test_bf16_kv_guards(hip):
     m = hip.Model(SMALL)
     m.decode_init(40, 16, 64, kv_dtype=hip.HPA_BF16)
-    with pytest.raises(RuntimeError):
-        m.set_fused(False)
-    with pytest.raises(RuntimeError):
-        m.set_pipeline(True)
     m.fill_random(30, seed=2)
     m.step(np.zeros(40, np.int32))
     assert np.isfinite(m.logits()).all()
@@ -309,138 +234,6 @@ def test_sampling_off_is_greedy(hip):
     m.close()
 
 
-@pytest.mark.parametrize("gemm_cus,B", [(32, 64), (32, 40), (64, 70)])
-def test_split_step_bit_identical_to_one_lane(hip, gemm_cus, B):
-    """split step: two lanes on CU-masked streams (attention on one CU set,
-    the GEMM chains on the other); every row's arithmetic is unchanged, so
-    ids, logits and positions equal the one-lane step bit for bit"""
-    params = synth.params(SMALL, seed=41)
-    outs = []
-    for split in (0, gemm_cus):
-        m = hip.Model(SMALL, params=params)
-        m.decode_init(B, 16, 128)
-        if split:
-            assert m.set_split(split) == split
-        m.set_graph(True)  # ignored by the split step (eager)
-        rng = np.random.default_rng(6)
-        seq = [m.step(rng.integers(0, 1000, B).astype(np.int32))]
-        for _ in range(12):
-            seq.append(m.step(None))
-        seq.append(m.logits())
-        seq.append(m.positions())
-        outs.append(seq)
-        m.close()
-    for a, b in zip(*outs):
-        assert np.array_equal(a, b)
-
-
-def test_split_step_gpt2_124m_matches_oracle(hip):
-    """124M shapes through the split step against the oracle"""
-    cfgd = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
-    params = synth.params(cfgd, seed=9)
-    B = 48
-    model = hip.Model(cfgd, params=params)
-    model.decode_init(B, 16, cfgd["maxT"])
-    assert model.set_split(32) == 32
-    c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
-    orc = oc.PagedDecoder(params, c, B, 16, cfgd["maxT"], page_seed=12)
-    rng = np.random.default_rng(9)
-    tok = rng.integers(0, cfgd["V"], B).astype(np.int32)
-    for t in range(8):
-        o_next, o_logits = orc.step(tok)
-        g_next = model.step(tok)
-        assert np.abs(model.logits() - o_logits).max() <= LOGIT_TOL
-        clear = _margins(o_logits) > TIE_MARGIN
-        assert np.array_equal(g_next[clear], o_next[clear])
-        tok = o_next
-    model.close()
-    orc.close()
-
-
-def test_set_split_rejects_bad_shapes(hip):
-    m = hip.Model(SMALL)
-    m.decode_init(16, 16, 64)
-    with pytest.raises(RuntimeError):
-        m.set_split(32)  # B <= 16: no second lane
-    m.close()
-    m = hip.Model(SMALL)
-    m.decode_init(32, 16, 64)
-    with pytest.raises(RuntimeError):
-        m.set_split(100000)
-    assert m.set_split(0) == 0
-    m.close()
-
-
-@pytest.mark.parametrize("P,B,chain", [(16, 40, 64), (8, 64, 256), (32, 33, 16)])
-def test_overlap_step_matches_oracle(hip, P, B, chain):
-    """overlapped step: each launch runs one lane's attention beside the
-    other lane's GEMM chain with in-launch hand-offs (hpa_lane_layer)"""
-    params = synth.params(SMALL, seed=P + B)
-    model = hip.Model(SMALL, params=params)
-    model.decode_init(B, P, SMALL["maxT"])
-    assert model.set_overlap(chain) == chain
-    model.set_graph(True)
-    c = oc.cfg(SMALL["maxT"], SMALL["V"], SMALL["L"], SMALL["NH"], SMALL["C"])
-    orc = oc.PagedDecoder(params, c, B, P, SMALL["maxT"], page_seed=P)
-    rng = np.random.default_rng(P)
-    for t in range(30):
-        tok = rng.integers(0, SMALL["V"], B).astype(np.int32)
-        o_next, o_logits = orc.step(tok)
-        g_next = model.step(tok)
-        assert model.overlap_faults() == 0
-        assert np.abs(model.logits() - o_logits).max() <= LOGIT_TOL
-        clear = _margins(o_logits) > TIE_MARGIN
-        assert np.array_equal(g_next[clear], o_next[clear])
-    model.close()
-    orc.close()
-
-
-def test_overlap_step_gpt2_124m_matches_oracle(hip):
-    """124M shapes: one-shot chain tiles (K = 768) and the looped fcproj"""
-    cfgd = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
-    params = synth.params(cfgd, seed=19)
-    B = 64
-    model = hip.Model(cfgd, params=params)
-    model.decode_init(B, 16, cfgd["maxT"])
-    assert model.set_overlap(192) == 192
-    model.set_graph(True)
-    c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
-    orc = oc.PagedDecoder(params, c, B, 16, cfgd["maxT"], page_seed=19)
-    rng = np.random.default_rng(19)
-    tok = rng.integers(0, cfgd["V"], B).astype(np.int32)
-    worst = 0.0
-    for t in range(8):
-        o_next, o_logits = orc.step(tok)
-        g_next = model.step(tok)
-        assert model.overlap_faults() == 0
-        worst = max(worst, float(np.abs(model.logits() - o_logits).max()))
-        clear = _margins(o_logits) > TIE_MARGIN
-        assert np.array_equal(g_next[clear], o_next[clear])
-        tok = o_next
-    assert worst <= LOGIT_TOL, worst
-    model.close()
-    orc.close()
-
-
-def test_overlap_graph_equals_eager(hip):
-    params = synth.params(SMALL, seed=23)
-    outs = []
-    for graph in (False, True):
-        m = hip.Model(SMALL, params=params)
-        m.decode_init(48, 16, 128)
-        m.set_overlap(96)
-        m.set_graph(graph)
-        rng = np.random.default_rng(3)
-        seq = [m.step(rng.integers(0, 1000, 48).astype(np.int32))]
-        for _ in range(10):
-            seq.append(m.step(None))
-        seq.append(m.logits())
-        outs.append(seq)
-        m.close()
-    for a, b in zip(*outs):
-        assert np.array_equal(a, b)
-
-
 # bf16 weights ("bf16 decode", gpt2_decode_init_w): the GPU and the oracle both
 # round the GEMM weights and the GEMM input rows (after LN / attention / GELU)
 # to bf16 and sum in fp32.  The weights round identically; an input row is
@@ -449,13 +242,12 @@ def test_overlap_graph_equals_eager(hip):
 # (2^-8 relative) apart -- the same effect as the bf16 KV case, in more
 # places; the bar and the tie margin are widened for it.
 BF16W_LOGIT_TOL = 2e-2
-BF16W_TIE = 4e-2
 
 
 @pytest.mark.parametrize("P", [8, 16])
 def test_decode_bf16_weights_matches_oracle(hip, P):
     worst, ties = _compare_run(hip, SMALL, B=20, P=P, steps=40, seed=60 + P, graph=True, w_bf16=True,
-                               tol=BF16W_LOGIT_TOL, tie=BF16W_TIE)
+                               tol=BF16W_LOGIT_TOL)
     print(f"bf16 weights (small): worst logit diff {worst:.3e}, near-ties {ties}")
 
 
@@ -463,25 +255,19 @@ def test_decode_bf16_weights_and_kv_124m_shapes(hip):
     """BASELINE config 5's numerics (bf16 weights + bf16 KV) at 124M shapes"""
     cfgd = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
     worst, ties = _compare_run(hip, cfgd, B=8, P=8, steps=10, seed=9, graph=True, kv_bf16=True, w_bf16=True,
-                               tol=BF16W_LOGIT_TOL, tie=BF16W_TIE)
+                               tol=BF16W_LOGIT_TOL)
     print(f"124M bf16 weights + KV: worst logit diff {worst:.3e}, near-ties {ties}")
 
 
 def test_decode_bf16_weights_batch_over_64_rows(hip):
     """several row groups per GEMM (M = 80: 5 row blocks, row_blocks falls back to 1)"""
     _compare_run(hip, SMALL, B=80, P=16, steps=6, seed=71, graph=False, w_bf16=True,
-                 tol=BF16W_LOGIT_TOL, tie=BF16W_TIE)
+                 tol=BF16W_LOGIT_TOL)
 
 
 def test_bf16_weights_guards(hip):
     m = hip.Model(SMALL)
     m.decode_init(40, 16, 64, w_dtype=hip.HPA_BF16)
-    with pytest.raises(RuntimeError):
-        m.set_fused(False)
-    with pytest.raises(RuntimeError):
-        m.set_pipeline(True)
-    with pytest.raises(RuntimeError):
-        m.set_overlap(32)
     tot, _ = m.step_bytes()
     tot32 = None
     m.close()

@@ -144,7 +144,7 @@ def test_pack_unpack_roundtrip(hip):
 
 
 def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixed=None, variant=0, ct=0,
-         fold=False, ks=0, w_bf16=False):
+         fold=False, w_bf16=False):
     L = hip.lib()
     x = rng.uniform(-1, 1, (M, K)).astype(np.float32)
     W = rng.uniform(-0.05, 0.05, (N, K)).astype(np.float32)
@@ -239,14 +239,6 @@ def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixe
         g.block_table, g.bt_stride, g.pos = dev(bt), bt.shape[1], dev(pos)
     keep.append(out)
     keep.append(g)  # the descriptor (LOGITS: hpa_logits_partials)
-    if ks > 1:  # K split over workgroups: workspace sized by the library, counters zeroed once
-        g.k_slices = ks
-        nf, nc = ctypes.c_size_t(), ctypes.c_size_t()
-        hip.check(L.hpa_fused_ks_workspace(ctypes.byref(g), ctypes.byref(nf), ctypes.byref(nc)), "ks_ws")
-        slab = hip.DeviceBuffer(nf.value * 4)
-        cnt = hip.DeviceBuffer.from_array(np.zeros(nc.value, np.int32))
-        keep.extend([slab, cnt])
-        g.ks_slab, g.ks_count = slab.ptr, cnt.ptr
     hip.check(L.hpa_gemm_fused(ctypes.byref(g)), "gemm_fused")
     hip.check(L.hpa_synchronize())
     return out, acc, bound, keep
@@ -509,106 +501,3 @@ def test_fused_ln_fold(hip, epi, N, waves, variant, rb, ct, M):
                                  fixed=fixed, variant=1, ct=1, pool_args=pool_args, fold=True)
         got1 = out1.download((M, N // 3)) if epi == "QKV" else hip.from_frag(out1.download(Mp * N), M, N)
         assert np.array_equal(got, got1)
-
-
-def _fused_out(hip, out, epi, M, N):
-    if epi == hip.HPA_FEPI_QKV:
-        return out.download((M, N // 3))
-    if epi == hip.HPA_FEPI_LOGITS:
-        return out.download((M, N))
-    return hip.from_frag(out.download(((M + 15) // 16 * 16) * N), M, N)
-
-
-@pytest.mark.parametrize("epi,K,N,waves,rb,ct,ks,fold", [
-    ("RESID", 1600, 1600, 8, 2, 1, 2, False), ("RESID", 6400, 1600, 8, 2, 1, 4, False),
-    ("GELU", 1600, 6400, 8, 4, 2, 4, True), ("QKV", 1600, 4800, 8, 4, 2, 4, True),
-    ("GELU", 768, 3072, 4, 2, 2, 3, True), ("LOGITS", 768, 2000, 4, 2, 2, 2, False),
-    ("RESID", 768, 768, 16, 1, 1, 5, False)])
-@pytest.mark.parametrize("M", [64, 37])
-def test_fused_k_slices(hip, epi, K, N, waves, rb, ct, ks, fold, M):
-    """K split over workgroups (k_slices; the GPT-2 XL layer GEMMs): within
-    the f64 bound for every epilogue (LN folded or not); bit-identical over
-    repeated launches (the last arriver sums the slabs in slice order, so the
-    arrival order does not matter); the arrival counters are left zero; the
-    first 16 rows equal those of a 16-row launch (rows independent of M)"""
-    e = getattr(hip, "HPA_FEPI_" + epi)
-    r = np.random.default_rng(21)
-    fixed = dict(x=(r.uniform(-1, 1, (M, K)) + r.uniform(-0.5, 0.5, (M, 1))).astype(np.float32),
-                 W=r.uniform(-0.05, 0.05, (N, K)).astype(np.float32),
-                 bias=r.uniform(-0.1, 0.1, N).astype(np.float32),
-                 lw=r.uniform(0.8, 1.2, K).astype(np.float32), lb=r.uniform(-0.1, 0.1, K).astype(np.float32))
-    res = r.uniform(-1, 1, (M, N)).astype(np.float32)
-    ln = fold or (epi == "LOGITS")
-    outs = []
-    for Mrun in (M, M, 16):
-        pool_args = None
-        if epi == "QKV":
-            pool = hip.Pool(1, N // 3 // 64, 16, 4 * Mrun)
-            bt = np.arange(4 * Mrun, dtype=np.int32).reshape(Mrun, 4)
-            pos = (np.arange(Mrun, dtype=np.int32) * 7) % 64
-            pool_args = (pool, bt, pos)
-        out, acc, bound, keep = _run(hip, e, Mrun, K, N, waves, ln=ln, rng=np.random.default_rng(0),
-                                     res=res[:Mrun], rb=rb, fixed=fixed, ct=ct, variant=1,
-                                     pool_args=pool_args, fold=fold, ks=ks)
-        got = _fused_out(hip, out, e, Mrun, N)
-        if epi == "GELU":
-            ref = 0.5 * acc * (1 + np.tanh(np.sqrt(2 / np.pi) * (acc + 0.044715 * acc ** 3)))
-        elif epi == "RESID":
-            ref = acc + res[:Mrun]
-        else:
-            ref = acc[:, :got.shape[1]]
-        assert np.all(np.abs(got - ref) <= bound[:, :got.shape[1]] + 1e-6), float(np.abs(got - ref).max())
-        cnt = keep[-1]  # the counters
-        assert not np.any(cnt.download(cnt.nbytes // 4, np.int32)), "arrival counters not reset"
-        outs.append(got)
-    assert np.array_equal(outs[0], outs[1])
-    assert np.array_equal(outs[0][:16], outs[2])
-
-
-@pytest.mark.parametrize("epi,M,K,N,waves,rb,rounds,ln", [
-    ("RESID", 64, 768, 768, 8, 2, 1, True), ("RESID", 48, 1600, 1600, 8, 1, 2, True),
-    ("RESID", 37, 768, 784, 4, 1, 1, False), ("GELU", 64, 1600, 6400, 8, 1, 1, True),
-    ("GELU", 64, 768, 3072, 4, 2, 3, True), ("LOGITS", 64, 768, 50257, 8, 2, 4, True),
-    ("LOGITS", 40, 1600, 50257, 8, 1, 8, True)])
-def test_fused_f32_aresident(hip, epi, M, K, N, waves, rb, rounds, ln):
-    """fp32 A-resident kernel (variant 5, hpa_gemm_ares.hip) within the fp32
-    bound of the f64 reference, every epilogue"""
-    import torch
-    L = hip.lib()
-    e = dict(RESID=hip.HPA_FEPI_RESID, GELU=hip.HPA_FEPI_GELU, LOGITS=hip.HPA_FEPI_LOGITS)[epi]
-    rng = np.random.default_rng(M + K + rounds)
-    res = rng.uniform(-1, 1, (M, N)).astype(np.float32)
-    out, acc, bound, keep = _run(hip, e, M, K, N, waves, ln=ln, rng=rng, res=res, rb=rb, ct=rounds, variant=5)
-    Mp = (M + 15) // 16 * 16
-    if epi == "RESID":
-        got = hip.from_frag(out.download(Mp * N), M, N)
-        assert np.all(np.abs(got - (res + acc)) <= bound + 1e-6)
-    elif epi == "GELU":
-        got = hip.from_frag(out.download(Mp * N), M, N)
-        ref = torch.nn.functional.gelu(torch.from_numpy(acc), approximate="tanh").numpy()
-        assert np.all(np.abs(got - ref) <= 1.2 * bound + 2e-5)
-    else:
-        got = out.download((M, N))
-        assert np.all(np.abs(got - acc) <= bound)
-        part = keep[-3]
-        nxt = hip.DeviceBuffer(M * 4)
-        hip.check(L.hpa_argmax_final(part.ptr, (N + 15) // 16, Mp, M, nxt.ptr, None, None, None))
-        assert np.array_equal(nxt.download(M, np.int32), got.argmax(-1))
-
-
-def test_fused_f32_aresident_shape_invariant(hip):
-    """one in-order k chain per output: bit-identical for every (waves, row
-    blocks, rounds) and M"""
-    rng = np.random.default_rng(23)
-    K, N = 768, 2304
-    fixed = dict(x=rng.uniform(-1, 1, (64, K)).astype(np.float32),
-                 W=rng.uniform(-0.05, 0.05, (N, K)).astype(np.float32),
-                 bias=rng.uniform(-0.1, 0.1, N).astype(np.float32),
-                 lw=rng.uniform(0.8, 1.2, K).astype(np.float32), lb=rng.uniform(-0.1, 0.1, K).astype(np.float32))
-    outs = []
-    for waves, M, rb, rounds in [(8, 64, 2, 1), (4, 64, 1, 3), (8, 64, 1, 4), (4, 32, 2, 2)]:
-        out, _, _, keep = _run(hip, hip.HPA_FEPI_GELU, M, K, N, waves, ln=True, rng=rng, rb=rb, ct=rounds,
-                               fixed=fixed, variant=5)
-        outs.append(hip.from_frag(out.download((M + 15) // 16 * 16 * N), M, N))
-    for o in outs[1:]:
-        assert np.array_equal(o, outs[0][:o.shape[0]])

@@ -1,0 +1,128 @@
+"""The N>1 decode path with the HIP engine, on the one GPU of
+the test box.
+
+* Two processes, each a HIP engine (libpaged_hip.so on device 0) decoding
+  its shard of the batch (shard.batch_layout), exchanging through a
+  world_size-2 gloo group (RCCL refuses two ranks on one device, so the
+  transport here is gloo; the engines and the sharding are the product's).
+  Rank 0's gathered logits and greedy ids equal an unsharded HIP decode of
+  the whole batch bit for bit (same attention split count on both sides:
+  GEMM rows never depend on M, so sharding changes no arithmetic).
+* The C library's RCCL gather (hpa_comm_* + gpt2_decode_shard /
+  gpt2_decode_gather, what bench.py runs at N > 1) on a 1-rank communicator:
+  the double-buffered gather returns exactly the engine's logits and ids.
+"""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import shard
+import synth
+
+pytestmark = pytest.mark.gpu
+
+SMALL = dict(maxT=128, V=1000, L=2, NH=2, C=128)
+STEPS = 8
+SPLITS = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _tokens(B, V):
+    return np.random.default_rng(321).integers(0, V, (STEPS, B)).astype(np.int32)
+
+
+def _engine(hip, B):
+    m = hip.Model(SMALL, params=synth.params(SMALL, seed=8))
+    m.decode_init(B, 16, SMALL["maxT"])
+    assert m.set_attn_splits(SPLITS) == SPLITS
+    m.set_graph(True)
+    return m
+
+
+def _worker(rank, world, port, batch, scaling, out_path):
+    import torch
+    import torch.distributed as dist
+    import pagedattn as hip
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hip.init(0)
+        B, lo, hi = shard.batch_layout(batch, world, rank, scaling)
+        counts = [h - l for _, l, h in (shard.batch_layout(batch, world, r, scaling) for r in range(world))]
+        m = _engine(hip, hi - lo)
+        toks = _tokens(B, SMALL["V"])
+        logits, ids = [], []
+        for t in range(STEPS):
+            nxt = m.step(toks[t, lo:hi])
+            lg = torch.zeros(max(counts), SMALL["V"])
+            lg[:hi - lo] = torch.from_numpy(m.logits())
+            nx = torch.zeros(max(counts), dtype=torch.int32)
+            nx[:hi - lo] = torch.from_numpy(nxt)
+            gl = [torch.zeros_like(lg) for _ in range(world)] if rank == 0 else None
+            gi = [torch.zeros_like(nx) for _ in range(world)] if rank == 0 else None
+            dist.gather(lg, gl, dst=0)
+            dist.gather(nx, gi, dst=0)
+            if rank == 0:
+                logits.append(np.concatenate([g[:n].numpy() for g, n in zip(gl, counts)]))
+                ids.append(np.concatenate([g[:n].numpy() for g, n in zip(gi, counts)]))
+        m.close()
+        if rank == 0:
+            np.savez(out_path, logits=np.stack(logits), ids=np.stack(ids))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("batch,scaling", [(6, "strong"), (7, "strong"), (4, "weak")])
+def test_two_hip_engines_sharded_equal_unsharded(hip, tmp_path, batch, scaling):
+    world = 2
+    out = str(tmp_path / "rank0.npz")
+    mp.start_processes(_worker, args=(world, _free_port(), batch, scaling, out), nprocs=world, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    B = batch * world if scaling == "weak" else batch
+    m = _engine(hip, B)
+    toks = _tokens(B, SMALL["V"])
+    want_l, want_i = [], []
+    for t in range(STEPS):
+        want_i.append(m.step(toks[t]))
+        want_l.append(m.logits())
+    m.close()
+    assert np.array_equal(got["ids"], np.stack(want_i))
+    assert np.array_equal(got["logits"], np.stack(want_l))
+
+
+def test_rccl_gather_one_rank(hip):
+    """hpa_comm (RCCL) + gpt2_decode_shard/gather on a 1-rank communicator:
+    the asynchronous double-buffered gather of every step equals the engine's
+    own logits / ids of that step"""
+    L = hip.lib()
+    n = L.hpa_comm_id_bytes()
+    assert n >= 128
+    uid = ctypes.create_string_buffer(n)
+    hip.check(L.hpa_comm_unique_id(uid, n), "unique id")
+    hip.check(L.hpa_comm_init(1, 0, uid), "comm init")
+    try:
+        assert L.hpa_comm_size() == 1 and L.hpa_comm_rank() == 0
+        B = 5
+        m = _engine(hip, B)
+        m.shard([B], root=0)
+        toks = _tokens(B, SMALL["V"])
+        for t in range(STEPS):
+            what = t % 2
+            nxt = m.step(toks[t])
+            lg = m.logits()
+            m.gather(what)
+            got = m.gathered(B, what)
+            assert np.array_equal(got, lg if what == 0 else nxt), t
+        m.close()
+    finally:
+        hip.check(L.hpa_comm_destroy(), "comm destroy")

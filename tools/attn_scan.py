@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Paged decode attention alone vs batch size and waves per workgroup:
-GPT-2 124M shapes, synthetic K/V to ctx, back-to-back launches timed with
-HIP events (gpt2_decode_time_attention).  usage: attn_scan.py [ctx]"""
+"""Paged decode attention alone vs batch size: GPT-2 124M shapes, synthetic
+K/V to ctx, back-to-back launches timed with HIP events
+(gpt2_decode_time_attention).  For every B: the engine's split count (auto,
+hpa_attn_pick_splits) and the single pass (splits 1), then a splits sweep at
+the small batches.  usage: attn_scan.py [ctx]"""
 import os
 import sys
 
@@ -19,8 +21,10 @@ for B in (8, 16, 32, 64, 128):
     m.decode_init(B, 16, ctx)
     m.fill_random(ctx - 2, seed=3)
     m.step(np.zeros(B, np.int32))
-    for nw in (1, 2, 4, 8):
-        pa.check(L.hpa_set_attention_waves(nw), "waves")
+    auto = m.attn_splits()
+    sweep = sorted({1, auto} | ({2, 4, 8, 16} if B <= 32 else set()))
+    for s in sweep:
+        m.set_attn_splits(s)
         ms, by = m.time_attention(48)
-        print(f"B={B:4d} waves={nw}  {ms * 1e3:8.2f} us  {by / ms / 1e6:8.1f} GB/s", flush=True)
-    pa.check(L.hpa_set_attention_waves(4), "waves")
+        tag = " (engine)" if s == auto else ""
+        print(f"B={B:4d} splits={s:2d}{tag:9s} {ms * 1e3:8.2f} us  {by / ms / 1e6:8.1f} GB/s", flush=True)
