@@ -132,7 +132,8 @@ int hpa_paged_attention_decode(const float* q, const HpaKVPool* pool, int layer,
  * summation grouping), bit-identical across launches for a given splits. */
 #define HPA_ATTN_MAX_SPLITS 16
 size_t hpa_attn_ws_bytes(int B, int num_heads, int splits);
-/* the engine's choice: ~3 workgroups per CU (num_cus <= 0: 256), by shape only */
+/* the engine's choice by shape only (num_cus <= 0: 256): ranges while B*NH*S
+ * stays within one workgroup per CU, 2 between one and two per CU, else 1 */
 int hpa_attn_pick_splits(int B, int num_heads, int max_ctx, int num_cus);
 int hpa_paged_attention_decode_split(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
                                      int bt_stride, const int* pos, float* out, int B, int splits, void* ws,

@@ -195,8 +195,8 @@ int  gpt2_decode_set_positions(GPT2* model, const int* pos);
 /* capture the step into a hipGraph and replay it (1) or launch eagerly (0) */
 int  gpt2_decode_set_graph(GPT2* model, int enable);
 /* context ranges per (sequence, head) of the decode attention
- * (hpa_paged_attention_decode_split): 0 = by shape (~3 workgroups per CU:
- * 1 at B = 64 with GPT-2 124M, 2 at 32, 4 at 16, 8 at 8), else 1..16 */
+ * (hpa_paged_attention_decode_split): 0 = by shape (hpa_attn_pick_splits:
+ * GPT-2 124M 1 at B >= 64 and 16, 2 at 32 and 8), else 1..16 */
 int  gpt2_decode_set_attn_splits(GPT2* model, int splits);
 int  gpt2_decode_attn_splits(GPT2* model);
 /* attention-kernel timing with HIP events around every layer's attention

@@ -258,17 +258,23 @@ size_t hpa_attn_ws_bytes(int B, int num_heads, int splits) {
     return recs + (size_t)B * num_heads * splits * sizeof(int);  // counters ([B*NH], padded by the grid size)
 }
 
-// Splits by shape (never by context, which varies per sequence and step):
-// enough (sequence, head, range) workgroups of 4 waves for ~3 per CU, the
-// number that keeps the B = 64 single-pass kernel at 6.5 TB/s (768
-// workgroups); at most one range per 2 tiles of 64 tokens of max_ctx.
+// Splits by shape (never by context, which varies per sequence and step).
+// Measured (tools/attn_scan.py, GPT-2 124M, ctx 1024, profiles/r2/
+// attn_scan_c1024.txt): a launch costs ~6 us beyond its streaming time, and
+// a CU streams at most ~25 GB/s, so what pays is (1) more CUs streaming when
+// B*NH workgroups leave some idle, without (2) ranges so short that the
+// merge's extra round trip shows: B = 8 (96 workgroups) 16.7 us single pass,
+// 14.2 at 2 ranges, 15.0 at 4, 17.2 at 8; B = 16 (192) 20.6 single, 22.8 at 2;
+// B = 32 (384: 1.5 per CU, a second partial round) 37.4 single, 35.9 at 2;
+// B >= 64: single pass.  So: as many ranges as keep B*NH*S within one
+// workgroup per CU, or 2 when B*NH falls between one and two per CU.
 int hpa_attn_pick_splits(int B, int num_heads, int max_ctx, int num_cus) {
     if (B <= 0 || num_heads <= 0) return 1;
     if (num_cus <= 0) num_cus = 256;
     const long bh = (long)B * num_heads;
-    const long want = 3L * num_cus;
+    if (bh > num_cus && bh < 2L * num_cus) return max_ctx >= 256 ? 2 : 1;
     int s = 1;
-    while (s < HPA_ATTN_MAX_SPLITS && bh * s * 2 <= want && (long)(s * 2) * 128 <= (long)max_ctx) s *= 2;
+    while (s < HPA_ATTN_MAX_SPLITS && bh * s * 2 <= num_cus && (long)(s * 2) * 128 <= (long)max_ctx) s *= 2;
     return s;
 }
 

@@ -88,8 +88,8 @@ def test_c_driver_compiles_links_and_fails_cleanly_without_gpu(tmp_path):
     subprocess.run(["gcc", "-O2", "-Wall", "-Werror", os.path.join(repo, "examples", "decode_main.c"),
                     "-I" + os.path.join(repo, "include"), "-L" + libdir, "-lpaged_hip",
                     "-Wl,-rpath," + libdir, "-o", exe], check=True)
-    import torch
-    if torch.cuda.is_available():
+    import pagedattn  # (not torch: its own bundled HIP runtime must not share the process)
+    if pagedattn.lib().hpa_device_count() > 0:
         pytest.skip("GPU present: the failure path is not reachable")
-    r = subprocess.run([exe, "", "2", "2"], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([exe, "-b", "2", "-p", "2", "-n", "2", "-q"], capture_output=True, text=True, timeout=120)
     assert r.returncode != 0

@@ -209,7 +209,7 @@ def test_split_context_attention_strong_scaling_shapes(hip, B):
     NH, P, ctx = 12, 16, 1024
     C = NH * 64
     S = L.hpa_attn_pick_splits(B, NH, ctx, 256)
-    assert S == {8: 8, 16: 4, 32: 2}[B]
+    assert S == {8: 2, 16: 1, 32: 2}[B]
     maxp = ctx // P
     pool = hip.Pool(1, NH, P, B * maxp)
     rng = np.random.default_rng(B)
@@ -224,12 +224,12 @@ def test_split_context_attention_strong_scaling_shapes(hip, B):
     Mp = (B + 15) // 16 * 16
     d_out = hip.DeviceBuffer(Mp * C * 4)
     wsb = L.hpa_attn_ws_bytes(B, NH, S)
-    d_ws = hip.DeviceBuffer(wsb)
+    d_ws = hip.DeviceBuffer(max(wsb, 4))
     hip.check(L.hpa_memset_async(d_ws.ptr, 0, wsb))
     outs = []
     for _ in range(2):
         hip.check(L.hpa_paged_attention_decode_split(d_q.ptr, pool.ref, 0, d_bt.ptr, maxp, d_pos.ptr, d_out.ptr, B,
-                                                     S, d_ws.ptr, 1))
+                                                     S, d_ws.ptr if wsb else None, 1))
         outs.append(hip.from_frag(d_out.download(Mp * C), B, C))
     assert np.array_equal(outs[0], outs[1])
     for b in range(B):

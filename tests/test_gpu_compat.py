@@ -89,6 +89,90 @@ def test_gpt2_forward_window_driver(hip):
     m.close()
 
 
+def test_gpt2_forward_reference_main_fill_loop(hip):
+    """the reference main's FIRST loop (paged_infer.c:1028-1050): the whole
+    T-window at offset 0 is passed again and again, placeholders beyond the
+    real tokens, one more real token each call, and the caller reads probs
+    row t-1.  Every row of the window must be that position's logits, so the
+    engine recomputes from the first changed position; then the sliding
+    loop continues.  Compared with the oracle's full forward of the final
+    tokens (each row t-1 depends on tokens 0..t-1 only)."""
+    L = hip.lib()
+    cfgd = dict(maxT=64, V=1000, L=2, NH=2, C=128)
+    params = synth.params(cfgd, seed=37)
+    m = hip.Model(cfgd, params=params)
+    T, prompt, total, V = 16, 6, 24, cfgd["V"]
+    rng = np.random.default_rng(3)
+    gen = np.full(total, 999, np.int32)  # GPT2_EOT-like placeholder
+    gen[:prompt] = rng.integers(0, V, prompt)
+    c = oc.cfg(cfgd["maxT"], V, cfgd["L"], cfgd["NH"], cfgd["C"])
+    for t in range(prompt, T):  # fill loop: offset 0, row t-1
+        L.gpt2_forward(m.h, gen[:T].ctypes.data_as(_I), None, 1, T, total, 0)
+        lg = np.ctypeslib.as_array(L.gpt2_acts_logits(m.h), shape=(T, V))
+        ref = oc.gpt2_forward(params, c, gen[None, :T].copy())[0]
+        assert np.abs(lg[:t] - ref[:t]).max() <= 2e-4, t  # every real row, not only t-1
+        pr = np.ctypeslib.as_array(L.gpt2_acts_probs(m.h), shape=(T, V))
+        assert abs(float(pr[t - 1].sum()) - 1.0) < 1e-4
+        gen[t] = int(np.argmax(pr[t - 1]))
+    for t in range(T, total):  # sliding loop: offset t-T, row T-1
+        off = t - T
+        L.gpt2_forward(m.h, np.ascontiguousarray(gen[off:off + T]).ctypes.data_as(_I), None, 1, T, total, off)
+        lg = np.ctypeslib.as_array(L.gpt2_acts_logits(m.h), shape=(T, V))
+        ref = oc.gpt2_forward(params, c, gen[None, :t].copy())[0]
+        assert np.abs(lg[T - 1] - ref[t - 1]).max() <= 2e-4, t
+        assert np.abs(lg - ref[off:t]).max() <= 2e-4, t  # the whole window's rows
+        gen[t] = int(np.argmax(lg[T - 1]))
+    m.close()
+
+
+def test_external_manager_survives_engine_teardown(hip):
+    """a caller-owned manager (model.manager, paged_infer.c:986-987) gets its
+    pages back and its default backend when the engine goes away
+    (gpt2_decode_free), so later request_block / collect_kv_blocks hand out
+    live host-visible memory, never pointers into the freed pool"""
+    L = hip.lib()
+    cfgd = dict(maxT=64, V=1000, L=2, NH=2, C=128)
+    m = hip.Model(cfgd, params=synth.params(cfgd, seed=5))
+    bm = hip.BlockManager(cfgd["C"], max_prompts=4, max_blocks=16, block_size=16, max_blocks_per_prompt=4)
+    m.set_manager(bm)
+    m.decode_init(4, 16, 64)
+    m.step(np.arange(4, dtype=np.int32))
+    L.gpt2_decode_free(m.h)
+    assert L.bm_free_pages(bm.h) == 16
+    i = bm.request_block(0)
+    blk = bm.block(i)
+    keys = ctypes.cast(blk.keys, ctypes.c_void_p).value
+    assert keys and L.hpa_is_device_accessible(keys) == 1
+    for j in range(16 * cfgd["C"]):  # host writes through the fresh page
+        blk.keys[j] = float(j)
+    n = ctypes.c_int()
+    kv = L.collect_kv_blocks(bm.h, 0, ctypes.byref(n))
+    assert kv and n.value == 1
+    m.close()
+    bm.close()
+
+
+def test_lru_eviction_is_reported(hip):
+    """pool pressure: the reference policy evicts the least recently used
+    sequence whole (block_manager.c:104-113); the engine reports it through
+    gpt2_decode_evicted so the caller can re-prefill that slot"""
+    cfgd = dict(maxT=64, V=1000, L=2, NH=2, C=128)
+    m = hip.Model(cfgd, params=synth.params(cfgd, seed=6))
+    bm = hip.BlockManager(cfgd["C"], max_prompts=3, max_blocks=5, block_size=16, max_blocks_per_prompt=4)
+    m.set_manager(bm)
+    m.decode_init(3, 16, 64)
+    m.prefill_ragged([list(range(30)), [], []])  # sequence 0: 2 pages
+    m.prefill_ragged([[], list(range(30)), []])  # sequence 1: 2 pages
+    assert not m.evicted().any()
+    m.prefill_ragged([[], [], list(range(20))])  # sequence 2 needs 2 pages: only 1 free -> LRU (0) evicted
+    ev = m.evicted()
+    assert ev.tolist() == [True, False, False]
+    assert m.positions().tolist() == [0, 30, 20]
+    assert not m.evicted().any()  # reported once
+    m.close()
+    bm.close()
+
+
 def test_block_manager_managed_pages_host_roundtrip(hip):
     """block_manager_test.c's scenario with pages in HIP managed memory (the
     library's default backend): host writes, host reads back."""

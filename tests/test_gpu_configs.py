@@ -22,7 +22,7 @@ import numpy as np
 import pytest
 
 import oracle_ctypes as oc
-from test_gpu_decode import BF16W_LOGIT_TOL, LOGIT_TOL, IdCheck
+from test_gpu_decode import BF16_EXEMPT, BF16W_LOGIT_TOL, LOGIT_TOL, IdCheck
 
 pytestmark = pytest.mark.gpu
 
@@ -36,7 +36,7 @@ def _params(hip, cfgd, seed):
 
 
 def _identical_cache_run(hip, cfgd, params, B, P, ctx0, steps, seed, kv_bf16=False, w_bf16=False,
-                         tol=LOGIT_TOL):
+                         tol=LOGIT_TOL, max_exempt_frac=0.02):
     """fill the GPU pool to ctx0, give the oracle the same K/V, decode `steps`
     greedy steps from the same tokens on both; returns the IdCheck"""
     model = hip.Model(cfgd, params=params)
@@ -63,7 +63,7 @@ def _identical_cache_run(hip, cfgd, params, B, P, ctx0, steps, seed, kv_bf16=Fal
     model.close()
     orc.close()
     print(f"B={B} page {P} positions {ctx0}..{ctx0 + steps - 1}, attention splits {splits}")
-    chk.verify(tol)
+    chk.verify(tol, max_exempt_frac)
     return chk
 
 
@@ -168,4 +168,4 @@ def test_config5_end_to_end_full_context(hip):
     layers, maxT = 2048; B=8"""
     params = _params(hip, CFG_124M_2K, 55)
     _identical_cache_run(hip, CFG_124M_2K, params, B=8, P=8, ctx0=2048 - 12, steps=12, seed=55, kv_bf16=True,
-                         w_bf16=True, tol=BF16W_LOGIT_TOL)
+                         w_bf16=True, tol=BF16W_LOGIT_TOL, max_exempt_frac=BF16_EXEMPT)
