@@ -221,6 +221,7 @@ def lib():
     _sig(L, "gpt2_decode_fill_random", i, [v, i, ctypes.c_ulonglong])
     _sig(L, "gpt2_decode_set_graph", i, [v, i])
     _sig(L, "gpt2_decode_reserve", i, [v, i])
+    _sig(L, "gpt2_decode_free", None, [v])
     _sig(L, "gpt2_decode_set_attn_splits", i, [v, i])
     _sig(L, "gpt2_decode_attn_splits", i, [v])
     _sig(L, "gpt2_decode_evicted", i, [v, _I])
