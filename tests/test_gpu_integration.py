@@ -40,6 +40,7 @@ def _oracle_generate(params, c, prompts, new, sample):
     import numpy as np
     import oracle_ctypes as oc
     B, P = prompts.shape
+    c = oc.cfg(c.max_seq_len, c.vocab_size, c.num_layers, c.num_heads, c.channels)
     dec = oc.PagedDecoder(params, c, B, 16, c.max_seq_len)
     sampler = oc.Sampler(B, seed=1337) if sample else None
     margins = []
