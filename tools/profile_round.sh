@@ -1,7 +1,8 @@
 #!/bin/bash
 # The round's evidence on one GPU box: bench lines of every single-GPU
 # BASELINE config, the rocprofv3 kernel stats of the headline bench command,
-# PMC traffic (configs 2 and 5), prefill and sampling lines.
+# PMC traffic (configs 2 and 5), MFMA utilisation (configs 2 and 3, prefill),
+# the attention batch scan, prefill and sampling lines.
 # usage: tools/profile_round.sh <outdir>      (then copy into profiles/rNN/)
 set -u
 out=$1; mkdir -p "$out"
@@ -17,13 +18,25 @@ grep "^{" "$out/bench_c2.log" > "$out/bench_line.json"
 step prof_c2 400 rocprofv3 --kernel-trace --stats -d "$out/prof_c2" -o run --output-format csv -- \
   python3 bench.py --cpu-baseline off
 step pmc_c2 900 bash tools/pmc_traffic.sh "$out/pmc_c2" --steps 8 --warmup 2
-step bench_c5 500 python bench.py --batch 256 --ctx 2048 --page-size 8 --kv-dtype bf16
-step bench_c5w 500 python bench.py --batch 256 --ctx 2048 --page-size 8 --kv-dtype bf16 --w-dtype bf16 --cpu-baseline off
+step mfma_c2 400 bash tools/pmc_mfma.sh "$out/mfma_c2" --steps 6 --warmup 2
+step attn_scan 300 python tools/attn_scan.py
+step bench_c5 500 python bench.py --batch 256 --ctx 2048 --page-size 8 --kv-dtype bf16 --w-dtype bf16
 step prof_c5w 500 rocprofv3 --kernel-trace --stats -d "$out/prof_c5w" -o run --output-format csv -- \
   python3 bench.py --batch 256 --ctx 2048 --page-size 8 --kv-dtype bf16 --w-dtype bf16 --cpu-baseline off
+step pmc_c5 900 bash tools/pmc_traffic.sh "$out/pmc_c5" --batch 256 --ctx 2048 --page-size 8 --kv-dtype bf16 \
+  --w-dtype bf16 --steps 4 --warmup 1
+step bench_c5kv 500 python bench.py --batch 256 --ctx 2048 --page-size 8 --kv-dtype bf16 --cpu-baseline off
 step bench_xl 600 python bench.py --model XL --page-size 32 --cpu-baseline off
+step prof_xl 600 rocprofv3 --kernel-trace --stats -d "$out/prof_xl" -o run --output-format csv -- \
+  python3 bench.py --model XL --page-size 32 --cpu-baseline off --steps 8
+step mfma_xl 600 bash tools/pmc_mfma.sh "$out/mfma_xl" --model XL --page-size 32 --steps 3 --warmup 1
 step bench_prefill 400 python bench.py --prefill real --cpu-baseline off
+step mfma_prefill 600 bash tools/pmc_mfma.sh "$out/mfma_prefill" --prefill real --steps 3 --warmup 1
 step bench_sample 400 python bench.py --sample --cpu-baseline off
-python3 tools/kstats.py "$out/prof_c2/run_kernel_trace.csv" > "$out/kstats_c2.txt"
-python3 tools/kstats.py "$out/prof_c5w/run_kernel_trace.csv" > "$out/kstats_c5w.txt"
+for b in 8 16 32; do
+  step bench_b$b 300 python bench.py --batch $b --cpu-baseline off
+done
+python3 tools/kstats.py "$out/prof_c2/run_kernel_trace.csv" 32 > "$out/kstats_c2.txt"
+python3 tools/kstats.py "$out/prof_c5w/run_kernel_trace.csv" 32 > "$out/kstats_c5w.txt"
+python3 tools/kstats.py "$out/prof_xl/run_kernel_trace.csv" 8 > "$out/kstats_xl.txt"
 echo done
