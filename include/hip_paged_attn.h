@@ -204,7 +204,13 @@ typedef struct {
                              4 = LOGITS only: activation-resident persistent kernel
                              (K = 768, rows <= 64; 16 waves; else as 1);
                              5 = bf16 weights only: A-resident kernel (col_tiles = rounds,
-                             K <= 3200) */
+                             K <= 3200);
+                             6 = stream-K (hpa_gemm_sk.hip; M <= 64, fp32 weights): one
+                             16-wave workgroup per CU walks an equal contiguous share of
+                             the (32-column super-tile, k16) steps, all M rows at once;
+                             tiles split between workgroups are summed in workgroup
+                             order by the last to arrive (sk_slab / sk_count).  LN only
+                             folded (ln_fold_c1 with ln_stats from the producer) */
     int col_tiles;        /* 16-column tiles per workgroup: 1; 2 (waves 4/8, row_blocks
                              2/4); 4 (waves 4, row_blocks 4); 0 = by shape.  A hint:
                              where M's row blocks or the waves cannot carry it, 1 */
@@ -218,6 +224,9 @@ typedef struct {
                              the workgroup already holds (K = the LN width).  No LN
                              prologue and no statistics loads; ln_stats, ln_w and
                              ln_b are not read. */
+    float* sk_slab;       /* variant 6: hpa_gemm_sk_workspace floats */
+    int* sk_count;        /* variant 6: per-super-tile counters, zero before the first launch
+                             (every launch leaves them zero) */
     int w_dtype;          /* HPA_F32 (0): w is fp32 frag layout.  HPA_BF16: w points at bf16
                              weights in the bf16 frag layout (hpa_pack_frag_bf16), K % 32 == 0;
                              A is rounded to bf16 (RNE) after the LayerNorm, products are
@@ -233,6 +242,9 @@ typedef struct {
 int hpa_ln_fold_pack(const float* W, int N, int K, const float* ln_w, const float* ln_b, const float* bias,
                      float* dst_frag, float* c1, float* c2);
 int hpa_gemm_fused(const HpaFusedGemm* g);
+/* variant 6 workspace: slab floats and counters for an (N) GEMM on this
+ * device's CU count (enough for any K and M <= 64) */
+int hpa_gemm_sk_workspace(int N, size_t* slab_floats, size_t* counters);
 /* argmax partials per row a LOGITS launch of g writes into part_out (the
  * `ntiles` of hpa_argmax_final): N/16 tiles, or one per workgroup of the
  * activation-resident kernel (variant 4) on the current stream; -1 if g is

@@ -824,6 +824,7 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
         return launch_b16(p, g->epilogue, nw, mt, ntw);
     }
     HPA_REQUIRE(g->w_dtype == HPA_F32, "gemm_fused: w_dtype must be HPA_F32 or HPA_BF16");
+    if (g->variant == 6) return launch_sk(p, g->epilogue);  // stream-K (hpa_gemm_sk.hip)
     HPA_REQUIRE(g->row_blocks == 0 || g->row_blocks == 1 || g->row_blocks == 2 || g->row_blocks == 4,
                 "gemm_fused: row_blocks must be 1, 2 or 4");
     looped_shape(g, p.Mp, &nw, &mt, &ntw);

@@ -36,6 +36,8 @@ struct FG {
     const int* row_seq;  // QKV: block-table row per GEMM row (NULL: the row)
     const float* fold_c1;  // LN folded into w: out = rstd*(acc - mean*c1) + bias (bias = c2)
     int gx, gy;  // column-tile groups x row groups of the launch
+    float* sk_slab;  // stream-K (variant 6): [workgroup][2][super-tile] partials
+    int* sk_cnt;     // stream-K: [super-tile] arrival counters (zero between launches)
 };
 
 // XCD-aware workgroup order (MI355X_MICROARCH.md "Workgroup dispatch":
@@ -609,6 +611,8 @@ int launch_b16(const FG& p, int epi, int nw, int mt, int ntw);
 // A-resident bf16 variant (variant 5): waves 4/8, row_blocks (mt) 1/2/4 with
 // mt*K <= 3200; each workgroup takes waves*rounds column tiles
 int launch_b16_ares(const FG& p, int epi, int nw, int mt, int rounds);
+// stream-K fp32 kernel (hpa_gemm_sk.hip, variant 6): M <= 64
+int launch_sk(const FG& p, int epi);
 
 static inline int fused_prepare(const HpaFusedGemm* g, FG* p) {
     HPA_REQUIRE(g && g->x && g->w && g->out, "gemm_fused: null operand");
@@ -642,6 +646,8 @@ static inline int fused_prepare(const HpaFusedGemm* g, FG* p) {
     p->pos = g->pos;
     p->row_seq = g->row_seq;
     p->fold_c1 = g->ln_fold_c1;
+    p->sk_slab = g->sk_slab;
+    p->sk_cnt = g->sk_count;
     HPA_REQUIRE(!g->ln_fold_c1 || g->epilogue != HPA_FEPI_LOGITS, "gemm_fused: ln_fold_c1 with LOGITS");
     if (g->epilogue == HPA_FEPI_QKV) {
         const HpaKVPool* pool = g->pool;

@@ -1,0 +1,285 @@
+// hpa_gemm_sk.hip -- stream-K fused GEMM for the decode rows (M <= 64),
+// variant 6 of hpa_gemm_fused: the GPT-2 XL layer GEMMs and logits.
+//
+// Why (measured, profiles/r2/mfma_xl.txt): the tile-per-workgroup kernels
+// keep the XL GEMMs at 24-31 % of the fp32 MFMA peak.  Their grids are one
+// wave of 100-400 column tiles over 256 CUs, so either CUs idle (150-200
+// workgroups) or a second partial round runs; and each workgroup's pipeline
+// is short next to the first-load latency.  The weights (123 MB per XL layer)
+// must stream from HBM once at <= ~25 GB/s per CU (MI355X_MICROARCH.md), so
+// the work has to be spread evenly over EVERY CU, each streaming its own
+// contiguous share of the weights for the whole kernel.
+//
+// How:
+//  * work = (32-column super-tile, 16-deep k-step) pairs in super-tile-major
+//    order; one 8-wave workgroup per CU takes an equal contiguous range of
+//    them, its waves equal contiguous sub-ranges.  A step loads the two
+//    weight fragments of the super-tile (1 KiB each, streamed in order) and
+//    the <= 4 activation fragments of all M rows (L2-resident), and issues
+//    32 v_mfma_f32_16x16x4_f32 into 8 accumulators (4 row blocks x 2 column
+//    tiles): every weight byte is fetched from HBM exactly once.  Loads run
+//    SK_D steps ahead in a register ring.
+//  * a wave's sub-range covers at most 2 super-tiles (it is shorter than
+//    K/16 steps); it leaves each one's partial tile in LDS.  The workgroup
+//    then folds, per super-tile it touched, the partials of its waves in wave
+//    order.  A super-tile wholly inside the workgroup's range goes straight
+//    to the epilogue; one split between workgroups is published as a
+//    write-through slab (sc1 stores, drained) with an arrival ticket
+//    (agent-scope atomic add), and the last of its workgroups to arrive sums
+//    the slabs in workgroup order (sc1 loads: MI355X_MICROARCH.md "Valid
+//    forms", row 1) and runs the epilogue, then rewinds the counter.
+//    Summation order: k in order within a wave, waves in order, workgroups in
+//    order -- fixed by the shape and the CU count, never by M or timing.
+//  * epilogues are the shared Epi (QKV + KV append, RESID + statistics, GELU,
+//    LOGITS + argmax partials).  The LayerNorm of qkv / fc is folded into the
+//    weights; its row statistics come from the producer's 16-column partials
+//    (ln_stats), since no workgroup sees a whole row's K.
+#include <math.h>
+
+#include "hpa_gemm_body.h"
+
+namespace {
+using namespace hpa_gemm;
+
+constexpr int SK_NW = 8;           // waves per workgroup (2 per SIMD)
+constexpr int SK_MT = 4;           // row blocks: all M <= 64 rows
+constexpr int SK_NTW = 2;          // column tiles per super-tile
+constexpr int SK_TE = SK_MT * 256;  // elements per column tile (64 rows x 16 cols)
+constexpr int SK_STE = SK_NTW * SK_TE;  // elements per super-tile
+constexpr int SK_D = 3;            // steps in flight per wave
+constexpr int SK_NT = SK_NW * 64;
+// LDS: [wave][2 slots][super-tile] partials, then row statistics [NW][64][2],
+// the epilogue's row-statistics scratch [NTW * 64][17], a broadcast word
+constexpr int SK_LDS_FLOATS = SK_NW * 2 * SK_STE + SK_NW * 64 * 2 + SK_NTW * 64 * 17 + 4;
+
+__device__ __forceinline__ long long sk_start(long long F, int G, int g) { return F * g / G; }
+
+// the workgroup whose range holds step u
+__device__ __forceinline__ int sk_owner(long long F, int G, long long u) {
+    int g = (int)((u * G) / F);
+    while (g + 1 < G && sk_start(F, G, g + 1) <= u) ++g;
+    while (g > 0 && sk_start(F, G, g) > u) --g;
+    return g;
+}
+
+__device__ __forceinline__ float sk_ld(const float* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sk_st(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
+    extern __shared__ __attribute__((aligned(16))) float sk_smem[];
+    float* part = sk_smem;                         // [NW][2][STE]
+    float* wsum = part + SK_NW * 2 * SK_STE;       // [NW][64][2] (slot 0 = row totals, others 0)
+    float* tile = wsum + SK_NW * 64 * 2;           // [NTW*64][17]
+    int* bcast = reinterpret_cast<int*>(tile + SK_NTW * 64 * 17);
+
+    const int G = gridDim.x, g = blockIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int K16 = p.K16, MTv = p.Mp >> 4;
+    const int nst = (p.ntn + SK_NTW - 1) / SK_NTW;
+    const long long F = (long long)nst * K16;
+    const long long g_lo = sk_start(F, G, g), g_hi = sk_start(F, G, g + 1);
+    const long long n_g = g_hi - g_lo;
+    const long long a = g_lo + n_g * w / SK_NW, b = g_lo + n_g * (w + 1) / SK_NW;  // this wave's steps
+
+    // ---- row statistics of the folded LayerNorm: the producer's partials in tile order
+    if (p.fold_c1) {
+        for (int i = threadIdx.x; i < SK_NW * 64 * 2; i += SK_NT) wsum[i] = 0.f;
+        __syncthreads();
+        if (threadIdx.x < 64 && (int)threadIdx.x < p.M) {
+            const int row = threadIdx.x;
+            float s1 = 0.f, s2 = 0.f;
+            for (int t = 0; t < p.ln_ntiles; ++t) {
+                s1 += p.ln_stats[((size_t)t * p.Mp + row) * 2];
+                s2 += p.ln_stats[((size_t)t * p.Mp + row) * 2 + 1];
+            }
+            wsum[2 * row] = s1;
+            wsum[2 * row + 1] = s2;
+        }
+    }
+
+    // ---- the wave's steps: a register ring SK_D steps deep
+    const float4* __restrict__ W4 = reinterpret_cast<const float4*>(p.w);
+    const float4* __restrict__ X4 = reinterpret_cast<const float4*>(p.x);
+    struct Step {
+        float4 w[SK_NTW], x[SK_MT];
+    };
+    auto load = [&](Step& s, long long u) {
+        u = u < b ? u : b - 1;  // clamped, unconditional
+        const int st = (int)(u / K16), k = (int)(u - (long long)st * K16);
+#pragma unroll
+        for (int j = 0; j < SK_NTW; ++j) {
+            const int t = min(st * SK_NTW + j, p.ntn - 1);  // tail tile past ntn: re-read, never stored
+            const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(W4 + ((size_t)t * K16 + k) * 64 + lane));
+            s.w[j] = make_float4(v.x, v.y, v.z, v.w);
+        }
+#pragma unroll
+        for (int r = 0; r < SK_MT; ++r) s.x[r] = X4[((size_t)min(r, MTv - 1) * K16 + k) * 64 + lane];
+    };
+    f32x4 acc[SK_NTW * SK_MT];
+#pragma unroll
+    for (int i = 0; i < SK_NTW * SK_MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int st_first = b > a ? (int)(a / K16) : 0;
+    int st_cur = st_first;
+    auto flush = [&](int slot) {  // accumulators -> part[w][slot] in the epilogue's element order
+        float* d = part + ((size_t)w * 2 + slot) * SK_STE;
+#pragma unroll
+        for (int j = 0; j < SK_NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < SK_MT; ++r)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) d[j * SK_TE + (r * 4 + q) * 64 + lane] = acc[j * SK_MT + r][q];
+#pragma unroll
+        for (int i = 0; i < SK_NTW * SK_MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    if (b > a) {
+        Step ring[SK_D];
+#pragma unroll
+        for (int d = 0; d < SK_D; ++d) load(ring[d], a + d);
+        for (long long u0 = a; u0 < b; u0 += SK_D) {
+#pragma unroll
+            for (int d = 0; d < SK_D; ++d) {
+                const long long u = u0 + d;
+                if (u < b) {
+                    const int st = (int)(u / K16);
+                    if (st != st_cur) {  // at most once per wave: its first super-tile is done
+                        flush(0);
+                        st_cur = st;
+                    }
+                    Step s = ring[d];
+                    load(ring[d], u + SK_D);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+#pragma unroll
+                        for (int j = 0; j < SK_NTW; ++j)
+#pragma unroll
+                            for (int r = 0; r < SK_MT; ++r) {
+                                if (r >= MTv) continue;  // uniform: rows past M
+                                const float xs = q == 0 ? s.x[r].x : q == 1 ? s.x[r].y : q == 2 ? s.x[r].z : s.x[r].w;
+                                const float ws = q == 0 ? s.w[j].x : q == 1 ? s.w[j].y : q == 2 ? s.w[j].z : s.w[j].w;
+                                acc[j * SK_MT + r] =
+                                    __builtin_amdgcn_mfma_f32_16x16x4f32(xs, ws, acc[j * SK_MT + r], 0, 0, 0);
+                            }
+                }
+            }
+        }
+        flush(st_cur == st_first ? 0 : 1);
+    }
+    __syncthreads();
+
+    // ---- per super-tile this workgroup touched: fold its waves, finish or hand off
+    if (n_g <= 0) return;
+    const int st_lo = (int)(g_lo / K16), st_hi = (int)((g_hi - 1) / K16);
+    Epi<SK_NW, EPI, SK_MT, SK_NTW> epi;
+    constexpr int EPT = Epi<SK_NW, EPI, SK_MT, SK_NTW>::EPT;
+    for (int st = st_lo; st <= st_hi; ++st) {
+        epi.prefetch(p, st * SK_NTW, 0);
+        float vals[EPT];
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) vals[i] = 0.f;
+        for (int ww = 0; ww < SK_NW; ++ww) {  // waves in order
+            const long long wa = g_lo + n_g * ww / SK_NW, wb = g_lo + n_g * (ww + 1) / SK_NW;
+            if (wb <= wa) continue;
+            const int fs = (int)(wa / K16), ls = (int)((wb - 1) / K16);
+            if (st < fs || st > ls) continue;
+            const float* src = part + ((size_t)ww * 2 + (st == fs ? 0 : 1)) * SK_STE;
+#pragma unroll
+            for (int i = 0; i < EPT; ++i) {
+                const int e = threadIdx.x + i * SK_NT;
+                if (e < SK_STE) vals[i] += src[e];
+            }
+        }
+        const long long t_lo = (long long)st * K16, t_hi = t_lo + K16;
+        if (t_lo < g_lo || t_hi > g_hi) {  // split between workgroups: hand off
+            const int slot = st == st_lo ? 0 : 1;
+            float* mine = p.sk_slab + ((size_t)g * 2 + slot) * SK_STE;
+#pragma unroll
+            for (int i = 0; i < EPT; ++i) {
+                const int e = threadIdx.x + i * SK_NT;
+                if (e < SK_STE) sk_st(mine + e, vals[i]);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every slab store drained before the ticket
+            __syncthreads();
+            const int g0 = sk_owner(F, G, t_lo), g1 = sk_owner(F, G, t_hi - 1);
+            if (threadIdx.x == 0)
+                bcast[0] = __hip_atomic_fetch_add(p.sk_cnt + st, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            const int ticket = bcast[0];
+            __syncthreads();
+            if (ticket != g1 - g0) continue;  // not the last: the last arriver finishes this tile
+            if (threadIdx.x == 0) __hip_atomic_store(p.sk_cnt + st, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int i = 0; i < EPT; ++i) vals[i] = 0.f;
+            for (int gg = g0; gg <= g1; ++gg) {  // workgroups in order
+                const int s_slot = st == (int)(sk_start(F, G, gg) / K16) ? 0 : 1;
+                const float* src = p.sk_slab + ((size_t)gg * 2 + s_slot) * SK_STE;
+#pragma unroll
+                for (int i = 0; i < EPT; ++i) {
+                    const int e = threadIdx.x + i * SK_NT;
+                    if (e < SK_STE) vals[i] += sk_ld(src + e);
+                }
+            }
+        }
+        epi.apply(p, vals, tile, st * SK_NTW, 0, wsum);
+        __syncthreads();  // tile scratch reuse by the next super-tile
+    }
+}
+
+template <int EPI>
+int launch_sk_t(const FG& p, int G) {
+    const size_t lds = (size_t)SK_LDS_FLOATS * sizeof(float);
+    static bool attr_set = false;
+    if (!attr_set) {
+        HPA_CHECK(hipFuncSetAttribute((const void*)gemm_sk_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds));
+        attr_set = true;
+    }
+    gemm_sk_kernel<EPI><<<G, SK_NT, lds, hpa_stream()>>>(p);
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+int g_sk_cus = 0;
+int sk_grid() {
+    if (g_sk_cus <= 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&g_sk_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            g_sk_cus = 256;
+    }
+    return g_sk_cus;
+}
+
+}  // namespace
+
+namespace hpa_gemm {
+int launch_sk(const FG& p, int epi) {
+    HPA_REQUIRE(p.Mp <= 64, "gemm_fused stream-K: M <= 64");
+    HPA_REQUIRE(p.sk_slab && p.sk_cnt, "gemm_fused stream-K: sk_slab / sk_count workspace");
+    HPA_REQUIRE(!p.ln_stats || p.fold_c1, "gemm_fused stream-K: LayerNorm only folded (ln_fold_c1)");
+    HPA_REQUIRE(!p.fold_c1 || p.ln_stats, "gemm_fused stream-K: folded LayerNorm needs ln_stats");
+    const int G = sk_grid();
+    const long long nst = (p.ntn + SK_NTW - 1) / SK_NTW, F = nst * p.K16;
+    // a wave's sub-range must span at most two super-tiles
+    HPA_REQUIRE((F + (long long)G * SK_NW - 1) / ((long long)G * SK_NW) + 1 <= p.K16,
+                "gemm_fused stream-K: too few steps per super-tile for this grid");
+    switch (epi) {
+        case HPA_FEPI_QKV: return launch_sk_t<HPA_FEPI_QKV>(p, G);
+        case HPA_FEPI_RESID: return launch_sk_t<HPA_FEPI_RESID>(p, G);
+        case HPA_FEPI_GELU: return launch_sk_t<HPA_FEPI_GELU>(p, G);
+        case HPA_FEPI_LOGITS: return launch_sk_t<HPA_FEPI_LOGITS>(p, G);
+        default: return hpa_fail(__FILE__, __LINE__, "gemm_fused stream-K: unknown epilogue");
+    }
+}
+}  // namespace hpa_gemm
+
+extern "C" int hpa_gemm_sk_workspace(int N, size_t* slab_floats, size_t* counters) {
+    HPA_REQUIRE(N > 0 && slab_floats && counters, "gemm_sk_workspace: arguments");
+    *slab_floats = (size_t)sk_grid() * 2 * SK_STE;
+    *counters = (size_t)((N + 15) / 16 + SK_NTW - 1) / SK_NTW;
+    return 0;
+}

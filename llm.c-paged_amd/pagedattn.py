@@ -58,7 +58,8 @@ class HpaFusedGemm(ctypes.Structure):
                 ("pool", ctypes.POINTER(HpaKVPool)), ("layer", ctypes.c_int), ("block_table", _V),
                 ("bt_stride", ctypes.c_int), ("pos", _V), ("waves", ctypes.c_int),
                 ("row_blocks", ctypes.c_int), ("variant", ctypes.c_int), ("col_tiles", ctypes.c_int),
-                ("row_seq", _V), ("ln_fold_c1", _V), ("w_dtype", ctypes.c_int)]
+                ("row_seq", _V), ("ln_fold_c1", _V), ("sk_slab", _V), ("sk_count", _V),
+                ("w_dtype", ctypes.c_int)]
 
 
 HPA_FEPI_QKV, HPA_FEPI_RESID, HPA_FEPI_GELU, HPA_FEPI_LOGITS = 0, 1, 2, 3
@@ -238,6 +239,7 @@ def lib():
     _sig(L, "hpa_ln_fold_pack", i, [v, i, i, v, v, v, v, v, v])
     _sig(L, "hpa_unpack_frag", i, [v, i, i, v, i])
     _sig(L, "hpa_gemm_fused", i, [ctypes.POINTER(HpaFusedGemm)])
+    _sig(L, "hpa_gemm_sk_workspace", i, [i, ctypes.POINTER(sz), ctypes.POINTER(sz)])
     _sig(L, "hpa_logits_partials", i, [ctypes.POINTER(HpaFusedGemm)])
     _sig(L, "hpa_fused_pick_waves", i, [i, i, i])
     _sig(L, "hpa_fused_pick", None, [i, i, i, _I])

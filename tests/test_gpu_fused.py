@@ -239,6 +239,13 @@ def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixe
         g.block_table, g.bt_stride, g.pos = dev(bt), bt.shape[1], dev(pos)
     keep.append(out)
     keep.append(g)  # the descriptor (LOGITS: hpa_logits_partials)
+    if variant == 6:  # stream-K: slab + counters (zeroed once; every launch leaves them zero)
+        nf, nc = ctypes.c_size_t(), ctypes.c_size_t()
+        hip.check(L.hpa_gemm_sk_workspace(N, ctypes.byref(nf), ctypes.byref(nc)), "sk workspace")
+        slab = hip.DeviceBuffer(nf.value * 4)
+        cnt = hip.DeviceBuffer.from_array(np.zeros(nc.value, np.int32))
+        keep.extend([slab, cnt])
+        g.sk_slab, g.sk_count = slab.ptr, cnt.ptr
     hip.check(L.hpa_gemm_fused(ctypes.byref(g)), "gemm_fused")
     hip.check(L.hpa_synchronize())
     return out, acc, bound, keep
@@ -501,3 +508,62 @@ def test_fused_ln_fold(hip, epi, N, waves, variant, rb, ct, M):
                                  fixed=fixed, variant=1, ct=1, pool_args=pool_args, fold=True)
         got1 = out1.download((M, N // 3)) if epi == "QKV" else hip.from_frag(out1.download(Mp * N), M, N)
         assert np.array_equal(got, got1)
+
+
+@pytest.mark.parametrize("epi,K,N,fold", [("GELU", 1600, 6400, True), ("QKV", 1600, 4800, True),
+                                          ("RESID", 6400, 1600, False), ("RESID", 1600, 1600, False),
+                                          ("LOGITS", 1600, 1000, False), ("GELU", 768, 3072, True),
+                                          ("RESID", 3072, 768, False), ("GELU", 256, 80, False)])
+@pytest.mark.parametrize("M", [64, 37, 16, 1])
+def test_fused_stream_k(hip, epi, K, N, fold, M):
+    """stream-K kernel (variant 6, hpa_gemm_sk.hip): every epilogue within the
+    f64 bound, LayerNorm folded with the producer's row statistics; odd
+    column-tile counts (N = 1000, 80: a half-filled last super-tile); tiles
+    split between workgroups summed by the last to arrive; a relaunch is bit
+    identical and leaves the counters zero"""
+    e = getattr(hip, "HPA_FEPI_" + epi)
+    rng = np.random.default_rng(K + N + M)
+    res = rng.uniform(-1, 1, (M, N)).astype(np.float32) if epi == "RESID" else None
+    pool_args = None
+    if epi == "QKV":
+        pool = hip.Pool(1, N // 3 // 64, 16, 4 * M)
+        bt = np.arange(4 * M, dtype=np.int32).reshape(M, 4)
+        pos = (np.arange(M, dtype=np.int32) * 7) % 64
+        pool_args = (pool, bt, pos)
+    out, acc, bound, keep = _run(hip, e, M, K, N, 8, ln=fold, rng=rng, res=res, pool_args=pool_args, variant=6,
+                                 fold=fold)
+    Mp = (M + 15) // 16 * 16
+    if epi == "QKV":
+        C = N // 3
+        got = out.download((M, C))
+        assert np.all(np.abs(got - acc[:, :C]) <= bound[:, :C])
+        for b in (0, M - 1):
+            k, v = pool.read_tokens(0, bt[b], pos[b] + 1)
+            assert np.all(np.abs(k[pos[b]] - acc[b, C:2 * C]) <= bound[b, C:2 * C])
+            assert np.all(np.abs(v[pos[b]] - acc[b, 2 * C:]) <= bound[b, 2 * C:])
+    elif epi == "LOGITS":
+        got = out.download((M, N))
+        assert np.all(np.abs(got - acc) <= bound)
+    else:
+        got = hip.from_frag(out.download(Mp * N), M, N)
+        if epi == "GELU":
+            ref = 0.5 * acc * (1 + np.tanh(np.sqrt(2 / np.pi) * (acc + 0.044715 * acc ** 3)))
+            assert np.all(np.abs(got - ref) <= bound + 1e-6)
+        else:
+            assert np.all(np.abs(got - (acc + res)) <= bound + 1e-6)
+    # relaunch: bit-identical (fixed summation order), counters back at zero
+    g = [k for k in keep if isinstance(k, hip.HpaFusedGemm)][0]
+    hip.check(hip.lib().hpa_gemm_fused(ctypes.byref(g)), "relaunch")
+    hip.check(hip.lib().hpa_synchronize())
+    again = out.download((M, N // 3)) if epi == "QKV" else out.download((M, N)) if epi == "LOGITS" else \
+        hip.from_frag(out.download(Mp * N), M, N)
+    assert np.array_equal(again, got)
+    cnt = [k for k in keep if isinstance(k, hip.DeviceBuffer)][-1]
+    assert not cnt.download((cnt.nbytes // 4,), np.int32).any()
+
+
+def test_fused_stream_k_rejects_operand_layernorm(hip):
+    """stream-K sees no whole row: an LN on the operand path (not folded) is refused"""
+    with pytest.raises(RuntimeError):
+        _run(hip, hip.HPA_FEPI_GELU, 16, 768, 3072, 8, ln=True, rng=np.random.default_rng(1), variant=6)
+
