@@ -67,13 +67,7 @@ __device__ __forceinline__ bool split_merge(float* __restrict__ rec_bh, int* __r
         st_wt(rec + 1, l);
     }
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        float* d = rec + 4 + 4 * (K * lane + k);
-        st_wt(d, acc[k].x);
-        st_wt(d + 1, acc[k].y);
-        st_wt(d + 2, acc[k].z);
-        st_wt(d + 3, acc[k].w);
-    }
+    for (int k = 0; k < K; ++k) hpa::store_wt16(rec, (4 + 4 * (K * lane + k)) * 4, acc[k]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every record store drained before the ticket
     int ticket = 0;
     if (lane == 0) ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -92,11 +86,11 @@ __device__ __forceinline__ bool split_merge(float* __restrict__ rec_bh, int* __r
         L = fmaf(ld_wt(r + 1), f, L);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const float* d = r + 4 + 4 * (K * lane + k);
-            O[k].x = fmaf(ld_wt(d), f, O[k].x);
-            O[k].y = fmaf(ld_wt(d + 1), f, O[k].y);
-            O[k].z = fmaf(ld_wt(d + 2), f, O[k].z);
-            O[k].w = fmaf(ld_wt(d + 3), f, O[k].w);
+            const float4 a = hpa::load_wt16(r, (4 + 4 * (K * lane + k)) * 4);
+            O[k].x = fmaf(a.x, f, O[k].x);
+            O[k].y = fmaf(a.y, f, O[k].y);
+            O[k].z = fmaf(a.z, f, O[k].z);
+            O[k].w = fmaf(a.w, f, O[k].w);
         }
     }
     m = M;

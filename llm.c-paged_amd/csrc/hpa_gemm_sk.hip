@@ -62,13 +62,6 @@ __device__ __forceinline__ int sk_owner(long long F, int G, long long u) {
     return g;
 }
 
-__device__ __forceinline__ float sk_ld(const float* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void sk_st(float* p, float v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 template <int EPI>
 __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
     extern __shared__ __attribute__((aligned(16))) float sk_smem[];
@@ -195,13 +188,11 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
         }
         const long long t_lo = (long long)st * K16, t_hi = t_lo + K16;
         if (t_lo < g_lo || t_hi > g_hi) {  // split between workgroups: hand off
+            static_assert(EPT == 4, "slab rows: one float4 per thread");
             const int slot = st == st_lo ? 0 : 1;
-            float* mine = p.sk_slab + ((size_t)g * 2 + slot) * SK_STE;
-#pragma unroll
-            for (int i = 0; i < EPT; ++i) {
-                const int e = threadIdx.x + i * SK_NT;
-                if (e < SK_STE) sk_st(mine + e, vals[i]);
-            }
+            // thread-major slab: thread t's four elements as one 16-B write-through store
+            hpa::store_wt16(p.sk_slab + ((size_t)g * 2 + slot) * SK_STE, (int)threadIdx.x * 16,
+                            make_float4(vals[0], vals[1], vals[2], vals[3]));
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every slab store drained before the ticket
             __syncthreads();
             const int g0 = sk_owner(F, G, t_lo), g1 = sk_owner(F, G, t_hi - 1);
@@ -210,18 +201,22 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
             __syncthreads();
             const int ticket = bcast[0];
             __syncthreads();
-            if (ticket != g1 - g0) continue;  // not the last: the last arriver finishes this tile
+            int arrivals = 0;  // workgroups with steps in this tile (with fewer steps than
+            for (int gg = g0; gg <= g1; ++gg)  // workgroups, some ranges are empty)
+                arrivals += sk_start(F, G, gg + 1) > sk_start(F, G, gg);
+            if (ticket != arrivals - 1) continue;  // not the last: the last arriver finishes this tile
             if (threadIdx.x == 0) __hip_atomic_store(p.sk_cnt + st, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
             for (int i = 0; i < EPT; ++i) vals[i] = 0.f;
             for (int gg = g0; gg <= g1; ++gg) {  // workgroups in order
+                if (sk_start(F, G, gg + 1) == sk_start(F, G, gg)) continue;  // empty range: no slab
                 const int s_slot = st == (int)(sk_start(F, G, gg) / K16) ? 0 : 1;
-                const float* src = p.sk_slab + ((size_t)gg * 2 + s_slot) * SK_STE;
-#pragma unroll
-                for (int i = 0; i < EPT; ++i) {
-                    const int e = threadIdx.x + i * SK_NT;
-                    if (e < SK_STE) vals[i] += sk_ld(src + e);
-                }
+                const float4 v =
+                    hpa::load_wt16(p.sk_slab + ((size_t)gg * 2 + s_slot) * SK_STE, (int)threadIdx.x * 16);
+                vals[0] += v.x;
+                vals[1] += v.y;
+                vals[2] += v.z;
+                vals[3] += v.w;
             }
         }
         epi.apply(p, vals, tile, st * SK_NTW, 0, wsum);

@@ -29,6 +29,24 @@ hipStream_t hpa_stream();
 namespace hpa {
 constexpr int kWave = 64;
 
+// 16-byte write-through (sc1) store / L1-bypassing (sc1) load at
+// base + byte_off (base wave-uniform, byte_off per lane, 16-B aligned): the
+// hand-off forms of MI355X_MICROARCH.md "Valid forms" row 1 at full width
+// (4-byte sc1 stores are one fabric write each, several times slower per byte)
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kCpolSc1 = 16;  // gfx940+ cache policy: SC1
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void store_wt16(void* base, int byte_off, float4 v) {
+    const u32x4 d = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(d, wt_rsrc(base), byte_off, 0, kCpolSc1);
+}
+__device__ __forceinline__ float4 load_wt16(const void* base, int byte_off) {
+    const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(wt_rsrc(base), byte_off, 0, kCpolSc1);
+    return make_float4(__uint_as_float(d.x), __uint_as_float(d.y), __uint_as_float(d.z), __uint_as_float(d.w));
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
