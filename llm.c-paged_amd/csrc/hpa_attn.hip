@@ -46,13 +46,6 @@ using namespace hpa_attn;
 // [B*NH] int arrival counters (zero between launches)
 constexpr int kRec = 68;
 
-__device__ __forceinline__ void st_wt(float* p, float v) {  // write-through (sc1) store
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_wt(const float* p) {  // L1-bypassing (sc1) load
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // Range s of S: publish this workgroup's folded state (K float4 chunks per
 // lane in wave 0: chunk k of lane j holds dims 4*(K*j + k)..+3 -- K = 1 for
 // the fp32 fold, lanes 0..15; K = 2 for the bf16 fold, lanes 0..7); the last
@@ -62,10 +55,7 @@ __device__ __forceinline__ bool split_merge(float* __restrict__ rec_bh, int* __r
                                             float& m, float& l, float4* acc) {
     const int lane = threadIdx.x & 63;
     float* rec = rec_bh + (size_t)s * kRec;
-    if (lane == 0) {
-        st_wt(rec, m);
-        st_wt(rec + 1, l);
-    }
+    if (lane == 0) hpa::store_wt16(rec, 0, make_float4(m, l, 0.f, 0.f));
 #pragma unroll
     for (int k = 0; k < K; ++k) hpa::store_wt16(rec, (4 + 4 * (K * lane + k)) * 4, acc[k]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every record store drained before the ticket
@@ -74,23 +64,45 @@ __device__ __forceinline__ bool split_merge(float* __restrict__ rec_bh, int* __r
     ticket = __builtin_amdgcn_readfirstlane(ticket);
     if (ticket != S - 1) return false;
     if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    // every record's (m, l) head, all in flight together (one after another
+    // each would be a cross-XCD round trip), then the acc chunks 8 ranges at a time
+    float4 head[HPA_ATTN_MAX_SPLITS];
+#pragma unroll
+    for (int i = 0; i < HPA_ATTN_MAX_SPLITS; ++i) head[i] = hpa::load_wt16(rec_bh + (size_t)min(i, S - 1) * kRec, 0);
     float M = -INFINITY;
-    for (int i = 0; i < S; ++i) M = fmaxf(M, ld_wt(rec_bh + (size_t)i * kRec));
+#pragma unroll
+    for (int i = 0; i < HPA_ATTN_MAX_SPLITS; ++i)
+        if (i < S) M = fmaxf(M, head[i].x);
     float L = 0.f;
     float4 O[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) O[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int i = 0; i < S; ++i) {  // ranges in order: independent of arrival order
-        const float* r = rec_bh + (size_t)i * kRec;
-        const float f = exp2f(ld_wt(r) - M);
-        L = fmaf(ld_wt(r + 1), f, L);
+    for (int i0 = 0; i0 < S; i0 += 8) {  // ranges in order: independent of arrival order
+        float4 a[8][K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const float4 a = hpa::load_wt16(r, (4 + 4 * (K * lane + k)) * 4);
-            O[k].x = fmaf(a.x, f, O[k].x);
-            O[k].y = fmaf(a.y, f, O[k].y);
-            O[k].z = fmaf(a.z, f, O[k].z);
-            O[k].w = fmaf(a.w, f, O[k].w);
+        for (int q = 0; q < 8; ++q)
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                a[q][k] = hpa::load_wt16(rec_bh + (size_t)min(i0 + q, S - 1) * kRec, (4 + 4 * (K * lane + k)) * 4);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (i0 + q >= S) break;
+            float hm = head[0].x, hl = head[0].y;
+#pragma unroll
+            for (int i = 1; i < HPA_ATTN_MAX_SPLITS; ++i)
+                if (i == i0 + q) {
+                    hm = head[i].x;
+                    hl = head[i].y;
+                }
+            const float f = exp2f(hm - M);
+            L = fmaf(hl, f, L);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                O[k].x = fmaf(a[q][k].x, f, O[k].x);
+                O[k].y = fmaf(a[q][k].y, f, O[k].y);
+                O[k].z = fmaf(a[q][k].z, f, O[k].z);
+                O[k].w = fmaf(a[q][k].w, f, O[k].w);
+            }
         }
     }
     m = M;

@@ -208,15 +208,27 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
             if (threadIdx.x == 0) __hip_atomic_store(p.sk_cnt + st, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
             for (int i = 0; i < EPT; ++i) vals[i] = 0.f;
-            for (int gg = g0; gg <= g1; ++gg) {  // workgroups in order
-                if (sk_start(F, G, gg + 1) == sk_start(F, G, gg)) continue;  // empty range: no slab
-                const int s_slot = st == (int)(sk_start(F, G, gg) / K16) ? 0 : 1;
-                const float4 v =
-                    hpa::load_wt16(p.sk_slab + ((size_t)gg * 2 + s_slot) * SK_STE, (int)threadIdx.x * 16);
-                vals[0] += v.x;
-                vals[1] += v.y;
-                vals[2] += v.z;
-                vals[3] += v.w;
+            // workgroups in order, 8 slabs in flight at a time (each load is a
+            // cross-XCD round trip: issued one after another they serialise)
+            for (int gb = g0; gb <= g1; gb += 8) {
+                float4 v[8];
+                bool has[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int gg = min(gb + q, g1);
+                    const long long s0 = sk_start(F, G, gg);
+                    has[q] = gb + q <= g1 && sk_start(F, G, gg + 1) > s0;  // empty range: no slab
+                    const int s_slot = st == (int)(s0 / K16) ? 0 : 1;
+                    v[q] = hpa::load_wt16(p.sk_slab + ((size_t)gg * 2 + s_slot) * SK_STE, (int)threadIdx.x * 16);
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    if (has[q]) {
+                        vals[0] += v[q].x;
+                        vals[1] += v[q].y;
+                        vals[2] += v[q].z;
+                        vals[3] += v[q].w;
+                    }
             }
         }
         epi.apply(p, vals, tile, st * SK_NTW, 0, wsum);
