@@ -48,19 +48,24 @@ constexpr int SK_TE = SK_MT * 256;  // elements per column tile (64 rows x 16 co
 constexpr int SK_STE = SK_NTW * SK_TE;  // elements per super-tile
 constexpr int SK_D = 3;            // steps in flight per wave
 constexpr int SK_NT = SK_NW * 64;
+constexpr int SK_MAXG = 1024;      // workgroups (one per CU)
 // LDS: [wave][2 slots][super-tile] partials, then row statistics [NW][64][2],
-// the epilogue's row-statistics scratch [NTW * 64][17], a broadcast word
-constexpr int SK_LDS_FLOATS = SK_NW * 2 * SK_STE + SK_NW * 64 * 2 + SK_NTW * 64 * 17 + 4;
+// the epilogue's row-statistics scratch [NTW * 64][17], a broadcast word (+3
+// pad), the per-wave super-tile span [NW][2] and the range table [SK_MAXG + 1]
+constexpr int SK_LDS_FLOATS = SK_NW * 2 * SK_STE + SK_NW * 64 * 2 + SK_NTW * 64 * 17 + 4 + 2 * SK_NW + SK_MAXG + 4;
 
-__device__ __forceinline__ long long sk_start(long long F, int G, int g) { return F * g / G; }
+// workgroup g owns steps [F*g/G, F*(g+1)/G); all index math is 32-bit
+// (F*G < 2^31, checked on the host): the 64-bit divisions this replaced cost
+// ~15 us per launch (tools/sk_trace.py)
+__device__ __forceinline__ int sk_start(int F, int G, int g) { return (int)((unsigned)(F * g) / (unsigned)G); }
 
-// the workgroup whose range holds step u
-__device__ __forceinline__ int sk_owner(long long F, int G, long long u) {
-    int g = (int)((u * G) / F);
-    while (g + 1 < G && sk_start(F, G, g + 1) <= u) ++g;
-    while (g > 0 && sk_start(F, G, g) > u) --g;
-    return g;
-}
+#ifdef HPA_SK_TRACE  // phase timestamps per workgroup (tools/sk_trace.py; A/B build only)
+__device__ unsigned long long sk_tr[1024 * 16];
+#define SK_T(i) \
+    do { if (threadIdx.x == 0) sk_tr[blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define SK_T(i) do {} while (0)
+#endif
 
 template <int EPI>
 __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
@@ -69,31 +74,22 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
     float* wsum = part + SK_NW * 2 * SK_STE;       // [NW][64][2] (slot 0 = row totals, others 0)
     float* tile = wsum + SK_NW * 64 * 2;           // [NTW*64][17]
     int* bcast = reinterpret_cast<int*>(tile + SK_NTW * 64 * 17);
+    int* wst = bcast + 4;  // [NW][2]: first and last super-tile of each wave's steps (-1: none)
+    int* bnd = wst + 2 * SK_NW;  // [G + 1]: sk_start of every workgroup
 
+    SK_T(0);
     const int G = gridDim.x, g = blockIdx.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int K16 = p.K16, MTv = p.Mp >> 4;
     const int nst = (p.ntn + SK_NTW - 1) / SK_NTW;
-    const long long F = (long long)nst * K16;
-    const long long g_lo = sk_start(F, G, g), g_hi = sk_start(F, G, g + 1);
-    const long long n_g = g_hi - g_lo;
-    const long long a = g_lo + n_g * w / SK_NW, b = g_lo + n_g * (w + 1) / SK_NW;  // this wave's steps
-
-    // ---- row statistics of the folded LayerNorm: the producer's partials in tile order
-    if (p.fold_c1) {
-        for (int i = threadIdx.x; i < SK_NW * 64 * 2; i += SK_NT) wsum[i] = 0.f;
-        __syncthreads();
-        if (threadIdx.x < 64 && (int)threadIdx.x < p.M) {
-            const int row = threadIdx.x;
-            float s1 = 0.f, s2 = 0.f;
-            for (int t = 0; t < p.ln_ntiles; ++t) {
-                s1 += p.ln_stats[((size_t)t * p.Mp + row) * 2];
-                s2 += p.ln_stats[((size_t)t * p.Mp + row) * 2 + 1];
-            }
-            wsum[2 * row] = s1;
-            wsum[2 * row + 1] = s2;
-        }
-    }
+    const int F = nst * K16;
+    for (int i = threadIdx.x; i <= G; i += SK_NT) bnd[i] = sk_start(F, G, i);
+    const int g_lo = sk_start(F, G, g), g_hi = sk_start(F, G, g + 1);
+    const int n_g = g_hi - g_lo;
+    const int a = g_lo + n_g * w / SK_NW, b = g_lo + n_g * (w + 1) / SK_NW;  // this wave's steps
+    // folded LayerNorm: wsum slot 0 gets the row totals (below), the other slots 0
+    if (p.fold_c1)
+        for (int i = 128 + threadIdx.x; i < SK_NW * 64 * 2; i += SK_NT) wsum[i] = 0.f;
 
     // ---- the wave's steps: a register ring SK_D steps deep
     const float4* __restrict__ W4 = reinterpret_cast<const float4*>(p.w);
@@ -101,9 +97,9 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
     struct Step {
         float4 w[SK_NTW], x[SK_MT];
     };
-    auto load = [&](Step& s, long long u) {
+    auto load = [&](Step& s, int u) {
         u = u < b ? u : b - 1;  // clamped, unconditional
-        const int st = (int)(u / K16), k = (int)(u - (long long)st * K16);
+        const int st = (int)((unsigned)u / (unsigned)K16), k = u - st * K16;
 #pragma unroll
         for (int j = 0; j < SK_NTW; ++j) {
             const int t = min(st * SK_NTW + j, p.ntn - 1);  // tail tile past ntn: re-read, never stored
@@ -116,7 +112,7 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
     f32x4 acc[SK_NTW * SK_MT];
 #pragma unroll
     for (int i = 0; i < SK_NTW * SK_MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int st_first = b > a ? (int)(a / K16) : 0;
+    const int st_first = b > a ? (int)((unsigned)a / (unsigned)K16) : 0;
     int st_cur = st_first;
     auto flush = [&](int slot) {  // accumulators -> part[w][slot] in the epilogue's element order
         float* d = part + ((size_t)w * 2 + slot) * SK_STE;
@@ -133,12 +129,12 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
         Step ring[SK_D];
 #pragma unroll
         for (int d = 0; d < SK_D; ++d) load(ring[d], a + d);
-        for (long long u0 = a; u0 < b; u0 += SK_D) {
+        for (int u0 = a; u0 < b; u0 += SK_D) {
 #pragma unroll
             for (int d = 0; d < SK_D; ++d) {
-                const long long u = u0 + d;
+                const int u = u0 + d;
                 if (u < b) {
-                    const int st = (int)(u / K16);
+                    const int st = (int)((unsigned)u / (unsigned)K16);
                     if (st != st_cur) {  // at most once per wave: its first super-tile is done
                         flush(0);
                         st_cur = st;
@@ -162,11 +158,33 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
         }
         flush(st_cur == st_first ? 0 : 1);
     }
+    if (lane == 0) {
+        wst[2 * w] = b > a ? st_first : -1;
+        wst[2 * w + 1] = st_cur;
+    }
+    // the folded LayerNorm's row totals: the producer's 16-column partials
+    // summed in tile order, by the last wave after its steps
+    if (p.fold_c1 && w == SK_NW - 1) {
+        float s1 = 0.f, s2 = 0.f;
+        if (lane < p.M) {
+            const float2* ls2 = reinterpret_cast<const float2*>(p.ln_stats);
+#pragma unroll 8
+            for (int t = 0; t < p.ln_ntiles; ++t) {
+                const float2 v = ls2[(size_t)t * p.Mp + lane];
+                s1 += v.x;
+                s2 += v.y;
+            }
+        }
+        wsum[2 * lane] = s1;
+        wsum[2 * lane + 1] = s2;
+    }
+    SK_T(1);
     __syncthreads();
+    SK_T(2);
 
     // ---- per super-tile this workgroup touched: fold its waves, finish or hand off
     if (n_g <= 0) return;
-    const int st_lo = (int)(g_lo / K16), st_hi = (int)((g_hi - 1) / K16);
+    const int st_lo = g_lo / K16, st_hi = (g_hi - 1) / K16;
     Epi<SK_NW, EPI, SK_MT, SK_NTW> epi;
     constexpr int EPT = Epi<SK_NW, EPI, SK_MT, SK_NTW>::EPT;
     for (int st = st_lo; st <= st_hi; ++st) {
@@ -175,10 +193,8 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
 #pragma unroll
         for (int i = 0; i < EPT; ++i) vals[i] = 0.f;
         for (int ww = 0; ww < SK_NW; ++ww) {  // waves in order
-            const long long wa = g_lo + n_g * ww / SK_NW, wb = g_lo + n_g * (ww + 1) / SK_NW;
-            if (wb <= wa) continue;
-            const int fs = (int)(wa / K16), ls = (int)((wb - 1) / K16);
-            if (st < fs || st > ls) continue;
+            const int fs = wst[2 * ww], ls = wst[2 * ww + 1];
+            if (fs < 0 || st < fs || st > ls) continue;
             const float* src = part + ((size_t)ww * 2 + (st == fs ? 0 : 1)) * SK_STE;
 #pragma unroll
             for (int i = 0; i < EPT; ++i) {
@@ -186,7 +202,8 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
                 if (e < SK_STE) vals[i] += src[e];
             }
         }
-        const long long t_lo = (long long)st * K16, t_hi = t_lo + K16;
+        SK_T(3 + 4 * (st - st_lo));
+        const int t_lo = st * K16, t_hi = t_lo + K16;
         if (t_lo < g_lo || t_hi > g_hi) {  // split between workgroups: hand off
             static_assert(EPT == 4, "slab rows: one float4 per thread");
             const int slot = st == st_lo ? 0 : 1;
@@ -195,15 +212,19 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
                             make_float4(vals[0], vals[1], vals[2], vals[3]));
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every slab store drained before the ticket
             __syncthreads();
-            const int g0 = sk_owner(F, G, t_lo), g1 = sk_owner(F, G, t_hi - 1);
+            // the workgroups whose ranges meet this tile: g0 owns t_lo, g1 owns t_hi - 1
+            int g0 = g, g1 = g;
+            while (g0 > 0 && bnd[g0] > t_lo) --g0;
+            while (g1 + 1 < G && bnd[g1 + 1] <= t_hi - 1) ++g1;
             if (threadIdx.x == 0)
                 bcast[0] = __hip_atomic_fetch_add(p.sk_cnt + st, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __syncthreads();
             const int ticket = bcast[0];
+            SK_T(4 + 4 * (st - st_lo));
             __syncthreads();
             int arrivals = 0;  // workgroups with steps in this tile (with fewer steps than
             for (int gg = g0; gg <= g1; ++gg)  // workgroups, some ranges are empty)
-                arrivals += sk_start(F, G, gg + 1) > sk_start(F, G, gg);
+                arrivals += bnd[gg + 1] > bnd[gg];
             if (ticket != arrivals - 1) continue;  // not the last: the last arriver finishes this tile
             if (threadIdx.x == 0) __hip_atomic_store(p.sk_cnt + st, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
@@ -216,9 +237,8 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
                     const int gg = min(gb + q, g1);
-                    const long long s0 = sk_start(F, G, gg);
-                    has[q] = gb + q <= g1 && sk_start(F, G, gg + 1) > s0;  // empty range: no slab
-                    const int s_slot = st == (int)(s0 / K16) ? 0 : 1;
+                    has[q] = gb + q <= g1 && bnd[gg + 1] > bnd[gg];  // empty range: no slab
+                    const int s_slot = bnd[gg] >= t_lo ? 0 : 1;  // its first tile, or its second
                     v[q] = hpa::load_wt16(p.sk_slab + ((size_t)gg * 2 + s_slot) * SK_STE, (int)threadIdx.x * 16);
                 }
 #pragma unroll
@@ -231,8 +251,10 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
                     }
             }
         }
+        SK_T(5 + 4 * (st - st_lo));
         epi.apply(p, vals, tile, st * SK_NTW, 0, wsum);
         __syncthreads();  // tile scratch reuse by the next super-tile
+        SK_T(6 + 4 * (st - st_lo));
     }
 }
 
@@ -271,6 +293,7 @@ int launch_sk(const FG& p, int epi) {
     HPA_REQUIRE(!p.fold_c1 || p.ln_stats, "gemm_fused stream-K: folded LayerNorm needs ln_stats");
     const int G = sk_grid();
     const long long nst = (p.ntn + SK_NTW - 1) / SK_NTW, F = nst * p.K16;
+    HPA_REQUIRE(G <= SK_MAXG && F * G < (1LL << 31), "gemm_fused stream-K: grid or step count too large");
     // a wave's sub-range must span at most two super-tiles
     HPA_REQUIRE((F + (long long)G * SK_NW - 1) / ((long long)G * SK_NW) + 1 <= p.K16,
                 "gemm_fused stream-K: too few steps per super-tile for this grid");
@@ -283,6 +306,17 @@ int launch_sk(const FG& p, int epi) {
     }
 }
 }  // namespace hpa_gemm
+
+#ifdef HPA_SK_TRACE
+extern "C" int hpa_sk_trace_read(unsigned long long* host) {
+    HPA_CHECK(hipDeviceSynchronize());
+    HPA_CHECK(hipMemcpyFromSymbol(host, HIP_SYMBOL(sk_tr), sizeof(sk_tr)));
+    void* d = nullptr;
+    HPA_CHECK(hipGetSymbolAddress(&d, HIP_SYMBOL(sk_tr)));
+    HPA_CHECK(hipMemset(d, 0, sizeof(sk_tr)));
+    return 0;
+}
+#endif
 
 extern "C" int hpa_gemm_sk_workspace(int N, size_t* slab_floats, size_t* counters) {
     HPA_REQUIRE(N > 0 && slab_floats && counters, "gemm_sk_workspace: arguments");
