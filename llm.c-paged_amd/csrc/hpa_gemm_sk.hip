@@ -46,7 +46,7 @@ constexpr int SK_MT = 4;           // row blocks: all M <= 64 rows
 constexpr int SK_NTW = 2;          // column tiles per super-tile
 constexpr int SK_TE = SK_MT * 256;  // elements per column tile (64 rows x 16 cols)
 constexpr int SK_STE = SK_NTW * SK_TE;  // elements per super-tile
-constexpr int SK_D = 3;            // steps in flight per wave
+constexpr int SK_D = 4;            // steps in flight per wave
 constexpr int SK_NT = SK_NW * 64;
 constexpr int SK_MAXG = 1024;      // workgroups (one per CU)
 // LDS: [wave][2 slots][super-tile] partials, then row statistics [NW][64][2],
@@ -67,7 +67,9 @@ __device__ unsigned long long sk_tr[1024 * 16];
 #define SK_T(i) do {} while (0)
 #endif
 
-template <int EPI>
+// MT: row blocks computed (1, 2 or 4; compile-time, so the step body has no
+// branches -- a runtime row-block test put one around every MFMA)
+template <int EPI, int MT>
 __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
     extern __shared__ __attribute__((aligned(16))) float sk_smem[];
     float* part = sk_smem;                         // [NW][2][STE]
@@ -79,7 +81,8 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
 
     SK_T(0);
     const int G = gridDim.x, g = blockIdx.x;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: scalar step bounds and branches
     const int K16 = p.K16, MTv = p.Mp >> 4;
     const int nst = (p.ntn + SK_NTW - 1) / SK_NTW;
     const int F = nst * K16;
@@ -95,7 +98,7 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
     const float4* __restrict__ W4 = reinterpret_cast<const float4*>(p.w);
     const float4* __restrict__ X4 = reinterpret_cast<const float4*>(p.x);
     struct Step {
-        float4 w[SK_NTW], x[SK_MT];
+        float4 w[SK_NTW], x[MT];
     };
     auto load = [&](Step& s, int u) {
         u = u < b ? u : b - 1;  // clamped, unconditional
@@ -107,7 +110,7 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
             s.w[j] = make_float4(v.x, v.y, v.z, v.w);
         }
 #pragma unroll
-        for (int r = 0; r < SK_MT; ++r) s.x[r] = X4[((size_t)min(r, MTv - 1) * K16 + k) * 64 + lane];
+        for (int r = 0; r < MT; ++r) s.x[r] = X4[((size_t)min(r, MTv - 1) * K16 + k) * 64 + lane];
     };
     f32x4 acc[SK_NTW * SK_MT];
 #pragma unroll
@@ -126,34 +129,47 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
         for (int i = 0; i < SK_NTW * SK_MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
     if (b > a) {
+        // Branch-free body: every ring slot is consumed by its step's MFMAs
+        // and only then reloaded (same registers, no copies).  A load inside a
+        // conditional, or one issued before its slot's old value was used,
+        // made the compiler move the new data into the ring at the join,
+        // i.e. wait for it within the same step (measured: half the MFMA rate).
+        // Steps past b (the last group's tail) run with zero weights.
         Step ring[SK_D];
 #pragma unroll
         for (int d = 0; d < SK_D; ++d) load(ring[d], a + d);
+        int next_st = (st_first + 1) * K16;  // first step of the next super-tile
         for (int u0 = a; u0 < b; u0 += SK_D) {
 #pragma unroll
             for (int d = 0; d < SK_D; ++d) {
                 const int u = u0 + d;
-                if (u < b) {
-                    const int st = (int)((unsigned)u / (unsigned)K16);
-                    if (st != st_cur) {  // at most once per wave: its first super-tile is done
-                        flush(0);
-                        st_cur = st;
-                    }
-                    Step s = ring[d];
-                    load(ring[d], u + SK_D);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-#pragma unroll
-                        for (int j = 0; j < SK_NTW; ++j)
-#pragma unroll
-                            for (int r = 0; r < SK_MT; ++r) {
-                                if (r >= MTv) continue;  // uniform: rows past M
-                                const float xs = q == 0 ? s.x[r].x : q == 1 ? s.x[r].y : q == 2 ? s.x[r].z : s.x[r].w;
-                                const float ws = q == 0 ? s.w[j].x : q == 1 ? s.w[j].y : q == 2 ? s.w[j].z : s.w[j].w;
-                                acc[j * SK_MT + r] =
-                                    __builtin_amdgcn_mfma_f32_16x16x4f32(xs, ws, acc[j * SK_MT + r], 0, 0, 0);
-                            }
+                const bool live = u < b;  // uniform
+                if (live && u == next_st) {  // at most once per wave: its first super-tile is done
+                    flush(0);
+                    ++st_cur;
+                    next_st += K16;
                 }
+                const float wm = live ? 1.f : 0.f;  // select, not a branch
+#pragma unroll
+                for (int j = 0; j < SK_NTW; ++j) {
+                    ring[d].w[j].x *= wm;
+                    ring[d].w[j].y *= wm;
+                    ring[d].w[j].z *= wm;
+                    ring[d].w[j].w *= wm;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int j = 0; j < SK_NTW; ++j)
+#pragma unroll
+                        for (int r = 0; r < MT; ++r) {
+                            const Step& s = ring[d];
+                            const float xs = q == 0 ? s.x[r].x : q == 1 ? s.x[r].y : q == 2 ? s.x[r].z : s.x[r].w;
+                            const float ws = q == 0 ? s.w[j].x : q == 1 ? s.w[j].y : q == 2 ? s.w[j].z : s.w[j].w;
+                            acc[j * SK_MT + r] =
+                                __builtin_amdgcn_mfma_f32_16x16x4f32(xs, ws, acc[j * SK_MT + r], 0, 0, 0);
+                        }
+                load(ring[d], u + SK_D);
             }
         }
         flush(st_cur == st_first ? 0 : 1);
@@ -258,18 +274,24 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
     }
 }
 
-template <int EPI>
-int launch_sk_t(const FG& p, int G) {
+template <int EPI, int MT>
+int launch_sk_mt(const FG& p, int G) {
     const size_t lds = (size_t)SK_LDS_FLOATS * sizeof(float);
     static bool attr_set = false;
     if (!attr_set) {
-        HPA_CHECK(hipFuncSetAttribute((const void*)gemm_sk_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)lds));
+        HPA_CHECK(hipFuncSetAttribute((const void*)gemm_sk_kernel<EPI, MT>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         attr_set = true;
     }
-    gemm_sk_kernel<EPI><<<G, SK_NT, lds, hpa_stream()>>>(p);
+    gemm_sk_kernel<EPI, MT><<<G, SK_NT, lds, hpa_stream()>>>(p);
     HPA_LAUNCH_CHECK();
     return 0;
+}
+
+template <int EPI>
+int launch_sk_t(const FG& p, int G) {
+    const int mtv = p.Mp >> 4;
+    return mtv == 1 ? launch_sk_mt<EPI, 1>(p, G) : mtv == 2 ? launch_sk_mt<EPI, 2>(p, G) : launch_sk_mt<EPI, 4>(p, G);
 }
 
 int g_sk_cus = 0;
