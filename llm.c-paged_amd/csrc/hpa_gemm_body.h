@@ -345,7 +345,10 @@ __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
     int cx, ry;
     if (!xcd_tile(p, bid, cx, ry)) return;
     const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
+    // uniform wave index: the step bounds below live in SGPRs and every
+    // per-step test is a scalar branch (with a VGPR index the compiler made
+    // them divergent and waited for loads at each join)
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nt0 = cx * NTW;
     const int rb0 = ry * MT;
     const int row0 = rb0 * 16;
@@ -431,11 +434,14 @@ __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
             }
         }
     };
+    // loads are unconditional (a trip past the end re-reads the last step's
+    // fragments, never used): a load under a branch left its buffer to be
+    // copied at the join, i.e. waited for in the same trip
     for (int t = 0; t < trips; t += 2) {
-        if (t + 1 < trips) load(Bb, t + 1);
+        load(Bb, t + 1);
         comp(A, t);
         if (t + 1 >= trips) break;
-        if (t + 2 < trips) load(A, t + 2);
+        load(A, t + 2);
         comp(Bb, t + 1);
     }
 

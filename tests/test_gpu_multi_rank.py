@@ -13,13 +13,12 @@ the test box.
   the double-buffered gather returns exactly the engine's logits and ids.
 """
 import ctypes
+import multiprocessing
 import os
 import socket
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
-
 import shard
 import synth
 
@@ -85,8 +84,16 @@ def _worker(rank, world, port, batch, scaling, out_path):
 def test_two_hip_engines_sharded_equal_unsharded(hip, tmp_path, batch, scaling):
     world = 2
     out = str(tmp_path / "rank0.npz")
-    mp.start_processes(_worker, args=(world, _free_port(), batch, scaling, out), nprocs=world, join=True,
-                       start_method="spawn")
+    # stdlib spawn: torch is imported by the ranks only, never in the pytest
+    # process (its bundled HIP runtime beside the library's aborts at exit)
+    ctx = multiprocessing.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, batch, scaling, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     got = np.load(out)
     B = batch * world if scaling == "weak" else batch
     m = _engine(hip, B)
