@@ -28,7 +28,8 @@ def main():
     for name, M, K, N, epi in [("124M attproj", 64, 768, 768, pa.HPA_FEPI_RESID),
                                ("124M fc", 64, 768, 3072, pa.HPA_FEPI_GELU),
                                ("XL qkv", 64, 1600, 4800, pa.HPA_FEPI_GELU),
-                               ("XL attproj", 64, 1600, 1600, pa.HPA_FEPI_RESID)]:
+                               ("XL attproj", 64, 1600, 1600, pa.HPA_FEPI_RESID),
+                               ("XL logits", 64, 1600, 50257, pa.HPA_FEPI_LOGITS)]:
         g = shape_inputs(M, K, N, epi, False)
         nf, nc = ctypes.c_size_t(), ctypes.c_size_t()
         pa.check(L.hpa_gemm_sk_workspace(N, ctypes.byref(nf), ctypes.byref(nc)), "ws")
