@@ -160,12 +160,17 @@ def main():
         args.gpus = world
     dist = None
     if world > 1:  # rendezvous only; the data path's collective is RCCL in the C library
+        if os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
+            # one node: bootstrap sockets on loopback (the container hostname may
+            # not resolve); RCCL's data path is xGMI either way
+            os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         import torch.distributed as dist
         dist.init_process_group("gloo")
     import pagedattn
     import shard
     L = pagedattn.lib()
-    pagedattn.init(local_rank)
+    pagedattn.init(int(os.environ.get("HPA_DEVICE", local_rank)))  # HPA_DEVICE: rehearse N ranks on one GPU
     if world > 1 and args.gather != "none":
         n = L.hpa_comm_id_bytes()
         uid = ctypes.create_string_buffer(n)
@@ -174,7 +179,14 @@ def main():
         obj = [uid.raw]
         dist.broadcast_object_list(obj, src=0)
         uid = ctypes.create_string_buffer(obj[0], n)
-        pagedattn.check(L.hpa_comm_init(world, rank, uid), "comm_init (RCCL)")
+        ok = L.hpa_comm_init(world, rank, uid) == 0
+        oks = [None] * world
+        dist.all_gather_object(oks, ok)
+        if not all(oks):  # report the run without the gather rather than no run at all
+            print(f"[bench] rank {rank}: RCCL communicator init failed "
+                  f"({L.hpa_last_error().decode(errors='replace')}); "
+                  "running without the end-of-step gather", file=sys.stderr, flush=True)
+            args.gather = "none (RCCL init failed)"
     pagedattn.check(L.hpa_set_attention_waves(args.attn_waves), "attention waves")
 
     cfgd = dict(pagedattn.GPT2_124M if args.model == "124M" else pagedattn.GPT2_XL)
@@ -224,7 +236,7 @@ def main():
         for _ in range(start):
             model.step(rng.integers(0, cfgd["V"], B_local).astype(np.int32), want_next=False)
     model.set_graph(not args.no_graph)
-    gather = world > 1 and args.gather != "none"
+    gather = world > 1 and not args.gather.startswith("none")
     if gather:
         model.shard(counts, root=0)
     what = 0 if args.gather == "logits" else 1
@@ -331,7 +343,8 @@ def main():
                        "decode_positions": f"{start}..{start + args.warmup + args.steps - 1}",
                        "parallelism": f"seq-shard x{world}" + (f" + RCCL gather({args.gather}) to rank 0 in the C "
                                                                "library, overlapped with the next step"
-                                                               if gather else ""),
+                                                               if gather else
+                                                               f" (gather: {args.gather})" if world > 1 else ""),
                        "hip_graph": not args.no_graph, "attn_splits": splits,
                        "token_choice": "multinomial (reference sample_mult)" if args.sample else "greedy",
                        "gemm_waves": [int(x) for x in model.gemm_config()[0]],
