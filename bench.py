@@ -56,8 +56,9 @@ def pmc_traffic(kernel_prefix, batch_per_gpu, ctx, page_size, dtype):
         except (OSError, ValueError):
             continue
         c = d.get("config") or {}
-        if (c.get("batch_per_gpu"), c.get("seq_len"), c.get("page_size"), c.get("dtype", "fp32")) != \
-                (batch_per_gpu, ctx, page_size, dtype):
+        # the attention kernel's bytes depend on the KV storage type, not on the weights'
+        if (c.get("batch_per_gpu"), c.get("seq_len"), c.get("page_size"), "bf16 KV" in c.get("dtype", "fp32")) != \
+                (batch_per_gpu, ctx, page_size, "bf16 KV" in dtype):
             continue
         for name, k in d["kernels"].items():
             if name.startswith(kernel_prefix):
