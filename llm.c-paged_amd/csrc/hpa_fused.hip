@@ -732,8 +732,8 @@ void hpa_fused_pick(int M, int N, int K, int* out3) {
         out3[0] = 8;
         out3[1] = 4;
         out3[2] = 2;
-    } else if (ntn >= 96 && k16 >= 96) {  // GPT-2 XL attproj / fcproj
-        out3[0] = 8;
+    } else if (ntn >= 96 && k16 >= 96) {  // GPT-2 XL attproj / fcproj (round 2 sweep: 4 waves
+        out3[0] = 4;                        // 8.8 / 23.4 us vs 9.4 / 24.5 at 8, profiles/r2/gemm_tune_xl.log)
         out3[1] = 2;
         out3[2] = 1;
     } else {  // GPT-2 124M layer GEMMs: one row block per workgroup (one-shot where K allows)
