@@ -830,6 +830,10 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
     looped_shape(g, p.Mp, &nw, &mt, &ntw);
     HPA_REQUIRE(g->variant >= 0 && g->variant <= 4 && g->variant != 3, "gemm_fused: variant must be 0, 1, 2 or 4");
     if (g->variant == 4 && logits_resident_eligible(p, g->epilogue)) return launch_logits_resident(p);
+    // variant 4 elsewhere (GPT-2 XL logits, K = 1600): stream-K when the caller
+    // gave its workspace (120 vs 143 us at M = 64, profiles/r2/sk_tune_xl.txt)
+    if (g->variant == 4 && g->epilogue == HPA_FEPI_LOGITS && p.Mp <= 64 && p.sk_slab && p.sk_cnt)
+        return launch_sk(p, g->epilogue);
     HPA_REQUIRE(g->col_tiles == 0 || g->col_tiles == 1 || g->col_tiles == 2 || g->col_tiles == 4,
                 "gemm_fused: col_tiles must be 1, 2 or 4");
     if (g->variant == 2 || (g->variant == 0 && mt == 1 && p.ntn < 1024 && g->col_tiles <= 1)) {

@@ -49,10 +49,19 @@ constexpr int SK_STE = SK_NTW * SK_TE;  // elements per super-tile
 constexpr int SK_D = 4;            // steps in flight per wave
 constexpr int SK_NT = SK_NW * 64;
 constexpr int SK_MAXG = 1024;      // workgroups (one per CU)
+// LayerNorm applied on load (ln_stats without a fold): its weight / bias
+// [2][HPA_FUSED_LN_KMAX] overlay the row-statistics and epilogue-scratch areas
+// (dead during the steps) plus SK_LNX_GB more floats, then ln_prologue's
+// statistics [64][2] and scratch [256][2]
+constexpr int SK_LNX_GB = 2 * HPA_FUSED_LN_KMAX - (SK_NW * 64 * 2 + SK_NTW * 64 * 17);
+constexpr int SK_LNX = SK_LNX_GB + 2 * 64 + 8 * 64;
 // LDS: [wave][2 slots][super-tile] partials, then row statistics [NW][64][2],
-// the epilogue's row-statistics scratch [NTW * 64][17], a broadcast word (+3
-// pad), the per-wave super-tile span [NW][2] and the range table [SK_MAXG + 1]
-constexpr int SK_LDS_FLOATS = SK_NW * 2 * SK_STE + SK_NW * 64 * 2 + SK_NTW * 64 * 17 + 4 + 2 * SK_NW + SK_MAXG + 4;
+// the epilogue's row-statistics scratch [NTW * 64][17], the LN area, a
+// broadcast word (+3 pad), the per-wave super-tile span [NW][2] and the range
+// table [SK_MAXG + 1]
+constexpr int SK_LDS_FLOATS =
+    SK_NW * 2 * SK_STE + SK_NW * 64 * 2 + SK_NTW * 64 * 17 + SK_LNX + 4 + 2 * SK_NW + SK_MAXG + 4;
+static_assert(SK_LNX_GB >= 0 && SK_LDS_FLOATS * 4 <= 160 * 1024, "stream-K LDS");
 
 // workgroup g owns steps [F*g/G, F*(g+1)/G); all index math is 32-bit
 // (F*G < 2^31, checked on the host): the 64-bit divisions this replaced cost
@@ -68,14 +77,16 @@ __device__ unsigned long long sk_tr[1024 * 16];
 #endif
 
 // MT: row blocks computed (1, 2 or 4; compile-time, so the step body has no
-// branches -- a runtime row-block test put one around every MFMA)
-template <int EPI, int MT>
+// branches -- a runtime row-block test put one around every MFMA); LN: the
+// LayerNorm applied to the A fragments on load (the logits' LNf)
+template <int EPI, int MT, bool LN>
 __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
     extern __shared__ __attribute__((aligned(16))) float sk_smem[];
     float* part = sk_smem;                         // [NW][2][STE]
     float* wsum = part + SK_NW * 2 * SK_STE;       // [NW][64][2] (slot 0 = row totals, others 0)
     float* tile = wsum + SK_NW * 64 * 2;           // [NTW*64][17]
-    int* bcast = reinterpret_cast<int*>(tile + SK_NTW * 64 * 17);
+    float* lnx = tile + SK_NTW * 64 * 17;          // LN area (with wsum and tile)
+    int* bcast = reinterpret_cast<int*>(lnx + SK_LNX);
     int* wst = bcast + 4;  // [NW][2]: first and last super-tile of each wave's steps (-1: none)
     int* bnd = wst + 2 * SK_NW;  // [G + 1]: sk_start of every workgroup
 
@@ -93,16 +104,26 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
     // folded LayerNorm: wsum slot 0 gets the row totals (below), the other slots 0
     if (p.fold_c1)
         for (int i = 128 + threadIdx.x; i < SK_NW * 64 * 2; i += SK_NT) wsum[i] = 0.f;
+    // LayerNorm on load: weight / bias into LDS over wsum.., mean / rstd of the
+    // rows (l & 15) + 16 r of lane l (the looped kernel's prologue)
+    float mu[MT], rs[MT];
+#pragma unroll
+    for (int r = 0; r < MT; ++r) mu[r] = rs[r] = 0.f;
+    if (LN) ln_prologue<SK_NW, MT>(p, wsum, lnx + SK_LNX_GB, lnx + SK_LNX_GB + 128, 0, true, mu, rs);
+    const float4* lng4 = reinterpret_cast<const float4*>(wsum) + (lane >> 4);
+    const float4* lnb4 = reinterpret_cast<const float4*>(wsum + HPA_FUSED_LN_KMAX) + (lane >> 4);
 
     // ---- the wave's steps: a register ring SK_D steps deep
     const float4* __restrict__ W4 = reinterpret_cast<const float4*>(p.w);
     const float4* __restrict__ X4 = reinterpret_cast<const float4*>(p.x);
     struct Step {
         float4 w[SK_NTW], x[MT];
+        int k;  // k-step within the super-tile
     };
     auto load = [&](Step& s, int u) {
         u = u < b ? u : b - 1;  // clamped, unconditional
         const int st = (int)((unsigned)u / (unsigned)K16), k = u - st * K16;
+        s.k = k;
 #pragma unroll
         for (int j = 0; j < SK_NTW; ++j) {
             const int t = min(st * SK_NTW + j, p.ntn - 1);  // tail tile past ntn: re-read, never stored
@@ -148,6 +169,11 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
                     flush(0);
                     ++st_cur;
                     next_st += K16;
+                }
+                if (LN) {  // compile-time
+                    const float4 gg = lng4[4 * ring[d].k], bb = lnb4[4 * ring[d].k];
+#pragma unroll
+                    for (int r = 0; r < MT; ++r) ring[d].x[r] = ln4(ring[d].x[r], mu[r], rs[r], gg, bb);
                 }
                 const float wm = live ? 1.f : 0.f;  // select, not a branch
 #pragma unroll
@@ -274,24 +300,31 @@ __global__ __launch_bounds__(SK_NT) void gemm_sk_kernel(FG p) {
     }
 }
 
-template <int EPI, int MT>
+template <int EPI, int MT, bool LN>
 int launch_sk_mt(const FG& p, int G) {
     const size_t lds = (size_t)SK_LDS_FLOATS * sizeof(float);
     static bool attr_set = false;
     if (!attr_set) {
-        HPA_CHECK(hipFuncSetAttribute((const void*)gemm_sk_kernel<EPI, MT>,
+        HPA_CHECK(hipFuncSetAttribute((const void*)gemm_sk_kernel<EPI, MT, LN>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         attr_set = true;
     }
-    gemm_sk_kernel<EPI, MT><<<G, SK_NT, lds, hpa_stream()>>>(p);
+    gemm_sk_kernel<EPI, MT, LN><<<G, SK_NT, lds, hpa_stream()>>>(p);
     HPA_LAUNCH_CHECK();
     return 0;
 }
 
+template <int EPI, bool LN>
+int launch_sk_ln(const FG& p, int G) {
+    const int mtv = p.Mp >> 4;
+    return mtv == 1   ? launch_sk_mt<EPI, 1, LN>(p, G)
+           : mtv == 2 ? launch_sk_mt<EPI, 2, LN>(p, G)
+                      : launch_sk_mt<EPI, 4, LN>(p, G);
+}
+
 template <int EPI>
 int launch_sk_t(const FG& p, int G) {
-    const int mtv = p.Mp >> 4;
-    return mtv == 1 ? launch_sk_mt<EPI, 1>(p, G) : mtv == 2 ? launch_sk_mt<EPI, 2>(p, G) : launch_sk_mt<EPI, 4>(p, G);
+    return p.ln_stats && !p.fold_c1 ? launch_sk_ln<EPI, true>(p, G) : launch_sk_ln<EPI, false>(p, G);
 }
 
 int g_sk_cus = 0;
@@ -311,7 +344,7 @@ namespace hpa_gemm {
 int launch_sk(const FG& p, int epi) {
     HPA_REQUIRE(p.Mp <= 64, "gemm_fused stream-K: M <= 64");
     HPA_REQUIRE(p.sk_slab && p.sk_cnt, "gemm_fused stream-K: sk_slab / sk_count workspace");
-    HPA_REQUIRE(!p.ln_stats || p.fold_c1, "gemm_fused stream-K: LayerNorm only folded (ln_fold_c1)");
+    HPA_REQUIRE(!p.ln_stats || p.fold_c1 || p.K <= HPA_FUSED_LN_KMAX, "gemm_fused stream-K: LayerNorm K too large");
     HPA_REQUIRE(!p.fold_c1 || p.ln_stats, "gemm_fused stream-K: folded LayerNorm needs ln_stats");
     const int G = sk_grid();
     const long long nst = (p.ntn + SK_NTW - 1) / SK_NTW, F = nst * p.K16;

@@ -622,6 +622,8 @@ struct GPT2Decode {
     float* d_logits;  /* [B][V] */
     /* frag-layout activations [Mp][*] (padded rows stay zero) and LN statistics */
     float *res, *res2, *att, *fch, *st1, *st2, *part;
+    float* sk_slab;   /* stream-K logits workspace (fp32 weights, B <= 64, C != 768), else NULL */
+    int* sk_cnt;
     float* d_wpack;   /* packed qkvw, attprojw, fcw, fcprojw of every layer, then wte */
     int w_bf16;       /* weights packed bf16 (hpa_pack_frag_bf16; offsets in elements) */
     size_t wpack_off[5]; /* per-layer offsets (0..3) and wte offset (4) */
@@ -745,6 +747,7 @@ static void dec_free(GPT2Decode* d) {
     hpa_free(d->d_q); hpa_free(d->d_logits);
     hpa_free(d->res); hpa_free(d->res2); hpa_free(d->att); hpa_free(d->fch);
     hpa_free(d->st1); hpa_free(d->st2); hpa_free(d->part);
+    hpa_free(d->sk_slab); hpa_free(d->sk_cnt);
     hpa_free(d->d_wpack);
     hpa_free(d->d_fold);
     hpa_free(d->d_attn_ws);
@@ -949,6 +952,17 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
     d->part = (float*)hpa_malloc((size_t)((V + 15) / 16) * Mp * 2 * 4);
     int ok = d->d_bt && d->d_pos && d->d_tokens && d->d_next && d->h_pos && d->h_evicted && d->h_next && d->d_q &&
              d->d_logits && d->res && d->res2 && d->att && d->fch && d->st1 && d->st2 && d->part;
+    /* logits GEMM: the activation-resident kernel takes C = 768; other widths
+     * (XL) run stream-K at B <= 64, which needs a slab and zeroed counters */
+    if (ok && w_dtype != HPA_BF16 && Mp <= 64 && C != 768) {
+        size_t nf = 0, nc = 0;
+        ok = hpa_gemm_sk_workspace(V, &nf, &nc) == 0;
+        if (ok) {
+            d->sk_slab = (float*)hpa_malloc(nf * sizeof(float));
+            d->sk_cnt = (int*)hpa_malloc(nc * sizeof(int));
+            ok = d->sk_slab && d->sk_cnt && hpa_memset_async(d->sk_cnt, 0, nc * sizeof(int)) == 0;
+        }
+    }
     for (int k = 0; k < 2 && ok; k++) {
         d->h_tok[k] = (int*)hpa_host_alloc(B * sizeof(int));
         d->h_bt[k] = (int*)hpa_host_alloc(btn * sizeof(int));
@@ -1110,7 +1124,8 @@ static void dec_gemm_desc(GPT2* model, int l, int which, HpaFusedGemm* g) {
             g->x = d->res; g->K = C; g->ln_stats = d->st1; g->ln_ntiles = ct;
             g->ln_w = w->lnfw; g->ln_b = w->lnfb; g->w = wpack_at(d, d->wpack_off[4]); g->N = V;
             g->out = d->d_logits; g->part_out = d->part; g->layer = 0;
-            g->variant = 4; /* activation-resident kernel where the shape allows (hpa_logits.hip) */
+            g->variant = 4; /* activation-resident kernel where the shape allows (hpa_logits.hip), */
+            g->sk_slab = d->sk_slab; g->sk_count = d->sk_cnt; /* else stream-K with this workspace */
             break;
     }
 }

@@ -151,7 +151,7 @@ def test_pack_unpack_roundtrip(hip):
 
 
 def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixed=None, variant=0, ct=0,
-         fold=False, w_bf16=False):
+         fold=False, w_bf16=False, sk_ws=False):
     L = hip.lib()
     x = rng.uniform(-1, 1, (M, K)).astype(np.float32)
     W = rng.uniform(-0.05, 0.05, (N, K)).astype(np.float32)
@@ -246,7 +246,7 @@ def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixe
         g.block_table, g.bt_stride, g.pos = dev(bt), bt.shape[1], dev(pos)
     keep.append(out)
     keep.append(g)  # the descriptor (LOGITS: hpa_logits_partials)
-    if variant == 6:  # stream-K: slab + counters (zeroed once; every launch leaves them zero)
+    if variant == 6 or sk_ws:  # stream-K: slab + counters (zeroed once; every launch leaves them zero)
         nf, nc = ctypes.c_size_t(), ctypes.c_size_t()
         hip.check(L.hpa_gemm_sk_workspace(N, ctypes.byref(nf), ctypes.byref(nc)), "sk workspace")
         slab = hip.DeviceBuffer(nf.value * 4)
@@ -519,14 +519,17 @@ def test_fused_ln_fold(hip, epi, N, waves, variant, rb, ct, M):
 @pytest.mark.parametrize("epi,K,N,fold", [("GELU", 1600, 6400, True), ("QKV", 1600, 4800, True),
                                           ("RESID", 6400, 1600, False), ("RESID", 1600, 1600, False),
                                           ("LOGITS", 1600, 1000, False), ("GELU", 768, 3072, True),
-                                          ("RESID", 3072, 768, False), ("GELU", 256, 80, False)])
+                                          ("RESID", 3072, 768, False), ("GELU", 256, 80, False),
+                                          ("LOGITS", 1600, 1000, "apply"), ("GELU", 768, 3072, "apply"),
+                                          ("LOGITS", 1600, 50257, "apply")])
 @pytest.mark.parametrize("M", [64, 37, 16, 1])
 def test_fused_stream_k(hip, epi, K, N, fold, M):
     """stream-K kernel (variant 6, hpa_gemm_sk.hip): every epilogue within the
-    f64 bound, LayerNorm folded with the producer's row statistics; odd
-    column-tile counts (N = 1000, 80: a half-filled last super-tile); tiles
-    split between workgroups summed by the last to arrive; a relaunch is bit
-    identical and leaves the counters zero"""
+    f64 bound; LayerNorm folded with the producer's row statistics (True) or
+    applied to the A fragments on load ("apply": the XL logits' LNf);
+    odd column-tile counts (N = 1000, 80: a half-filled last super-tile);
+    tiles split between workgroups summed by the last to arrive; a relaunch is
+    bit identical and leaves the counters zero"""
     e = getattr(hip, "HPA_FEPI_" + epi)
     rng = np.random.default_rng(K + N + M)
     res = rng.uniform(-1, 1, (M, N)).astype(np.float32) if epi == "RESID" else None
@@ -536,8 +539,8 @@ def test_fused_stream_k(hip, epi, K, N, fold, M):
         bt = np.arange(4 * M, dtype=np.int32).reshape(M, 4)
         pos = (np.arange(M, dtype=np.int32) * 7) % 64
         pool_args = (pool, bt, pos)
-    out, acc, bound, keep = _run(hip, e, M, K, N, 8, ln=fold, rng=rng, res=res, pool_args=pool_args, variant=6,
-                                 fold=fold)
+    out, acc, bound, keep = _run(hip, e, M, K, N, 8, ln=bool(fold), rng=rng, res=res, pool_args=pool_args,
+                                 variant=6, fold=fold is True)
     Mp = (M + 15) // 16 * 16
     if epi == "QKV":
         C = N // 3
@@ -568,8 +571,23 @@ def test_fused_stream_k(hip, epi, K, N, fold, M):
     assert not cnt.download((cnt.nbytes // 4,), np.int32).any()
 
 
-def test_fused_stream_k_rejects_operand_layernorm(hip):
-    """stream-K sees no whole row: an LN on the operand path (not folded) is refused"""
+def test_fused_stream_k_rejects_wide_layernorm(hip):
+    """LN applied on load stages its weights in LDS: K > 2048 is refused"""
     with pytest.raises(RuntimeError):
-        _run(hip, hip.HPA_FEPI_GELU, 16, 768, 3072, 8, ln=True, rng=np.random.default_rng(1), variant=6)
+        _run(hip, hip.HPA_FEPI_GELU, 16, 3072, 768, 8, ln=True, rng=np.random.default_rng(1), variant=6)
+
+
+def test_logits_variant4_takes_stream_k_with_workspace(hip):
+    """variant 4 at K = 1600 (not the resident kernel's shape): with a stream-K
+    workspace it runs stream-K (bit-identical to variant 6), without one the
+    looped kernel; both within the f64 bound"""
+    M, K, N = 64, 1600, 3000
+    outs = []
+    for variant, ws in ((6, True), (4, True), (4, False)):
+        out, acc, bound, keep = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, 8, ln=True,
+                                     rng=np.random.default_rng(5), variant=variant, sk_ws=ws)
+        got = out.download((M, N))
+        assert np.all(np.abs(got - acc) <= bound)
+        outs.append(got)
+    assert np.array_equal(outs[0], outs[1])
 
