@@ -1,8 +1,11 @@
 // hpa_gemm_sk.hip -- stream-K fused GEMM for the decode rows (M <= 64),
-// variant 6 of hpa_gemm_fused: the GPT-2 XL layer GEMMs and logits.
+// variant 6 of hpa_gemm_fused; the engine's logits GEMM where the resident
+// kernel does not fit (GPT-2 XL).  On the layer GEMMs it measured slower than
+// the looped / one-shot kernels (the slab hand-off), so they keep
+// those.
 //
 // Why (measured, profiles/r2/mfma_xl.txt): the tile-per-workgroup kernels
-// keep the XL GEMMs at 24-31 % of the fp32 MFMA peak.  Their grids are one
+// keep the XL GEMMs at 19-48 % of the fp32 MFMA peak.  Their grids are one
 // wave of 100-400 column tiles over 256 CUs, so either CUs idle (150-200
 // workgroups) or a second partial round runs; and each workgroup's pipeline
 // is short next to the first-load latency.  The weights (123 MB per XL layer)
@@ -31,9 +34,10 @@
 //    Summation order: k in order within a wave, waves in order, workgroups in
 //    order -- fixed by the shape and the CU count, never by M or timing.
 //  * epilogues are the shared Epi (QKV + KV append, RESID + statistics, GELU,
-//    LOGITS + argmax partials).  The LayerNorm of qkv / fc is folded into the
-//    weights; its row statistics come from the producer's 16-column partials
-//    (ln_stats), since no workgroup sees a whole row's K.
+//    LOGITS + argmax partials).  A LayerNorm is either folded into the weights
+//    (qkv / fc: row statistics from the producer's 16-column partials, since
+//    no workgroup sees a whole row's K) or applied to the A fragments on load
+//    (logits' LNf: the looped kernel's prologue, weights staged in LDS).
 #include <math.h>
 
 #include "hpa_gemm_body.h"
