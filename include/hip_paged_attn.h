@@ -202,15 +202,16 @@ typedef struct {
                              2 = one-shot (every operand load issued up front; one
                              row block; (waves, K/16) in {(4,48),(8,48),(16,48),(8,192),(16,192),(10,100)});
                              4 = LOGITS only: activation-resident persistent kernel
-                             (K = 768, rows <= 64; 16 waves; else as 1);
+                             (K = 768, rows <= 64; 16 waves); else stream-K (6) when
+                             sk_slab / sk_count are given and rows <= 64; else as 1;
                              5 = bf16 weights only: A-resident kernel (col_tiles = rounds,
                              K <= 3200);
                              6 = stream-K (hpa_gemm_sk.hip; M <= 64, fp32 weights): one
-                             16-wave workgroup per CU walks an equal contiguous share of
+                             8-wave workgroup per CU walks an equal contiguous share of
                              the (32-column super-tile, k16) steps, all M rows at once;
                              tiles split between workgroups are summed in workgroup
-                             order by the last to arrive (sk_slab / sk_count).  LN only
-                             folded (ln_fold_c1 with ln_stats from the producer) */
+                             order by the last to arrive (sk_slab / sk_count).  LN
+                             folded (ln_fold_c1) or applied on load (K <= 2048) */
     int col_tiles;        /* 16-column tiles per workgroup: 1; 2 (waves 4/8, row_blocks
                              2/4); 4 (waves 4, row_blocks 4); 0 = by shape.  A hint:
                              where M's row blocks or the waves cannot carry it, 1 */
