@@ -1,0 +1,43 @@
+"""bench.py's contract on the GPU: one JSON line with the metric of
+BASELINE.json, a positive whole-job value, the attention-kernel roofline and
+the config fields the driver reads (a short run: 3 timed steps)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args):
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup", "1",
+                        "--cpu-baseline", "off", *args], capture_output=True, text=True, timeout=300, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_default_line():
+    d = _bench()
+    base = json.load(open(os.path.join(REPO, "BASELINE.json")))
+    assert d["metric"] == base["metric"]
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["warmup"] == 1
+    assert d["value"] > 0 and d["ms_per_step"] > 0 and d["higher_is_better"] is True
+    assert abs(d["value"] - 64 * 1000.0 / d["ms_per_step"]) / d["value"] < 1e-3  # B=64 tokens per step
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and 0 < r["frac"] < 1
+    assert abs(r["achieved"] / r["peak"] - r["frac"]) < 1e-3
+    c = d["config"]
+    assert c["global_batch"] == 64 and c["seq_len"] == 1024 and c["page_size"] == 16 and c["hip_graph"]
+
+
+def test_bench_small_batch_split_attention_line():
+    """B=8 (the per-GPU batch of strong scaling at N=8): the split-context
+    attention is in use and the line is well formed"""
+    d = _bench("--batch", "8")
+    assert d["config"]["global_batch"] == 8 and d["config"]["attn_splits"] >= 2
+    assert d["value"] > 0 and 0 < d["roofline"]["frac"] < 1
