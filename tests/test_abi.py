@@ -93,3 +93,26 @@ def test_c_driver_compiles_links_and_fails_cleanly_without_gpu(tmp_path):
         pytest.skip("GPU present: the failure path is not reachable")
     r = subprocess.run([exe, "-b", "2", "-p", "2", "-n", "2", "-q"], capture_output=True, text=True, timeout=120)
     assert r.returncode != 0
+
+
+def test_integration_c_snippets_compile(tmp_path):
+    """the C fragments INTEGRATION.md documents (the reference-style driver of
+    section 1 and the multi-rank gather of section 4) compile against the
+    headers with -Wall -Werror"""
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    blocks = re.findall(r"```c\n(.*?)```", text, re.S)
+    assert len(blocks) >= 2
+    body = []
+    for b in blocks:
+        lines = [ln for ln in b.splitlines() if not ln.startswith("#include")]
+        body.append("    {\n" + "\n".join("        " + ln for ln in lines) + "\n    }")
+    src = ("#include <stddef.h>\n#include \"block_manager.h\"\n#include \"paged_infer.h\"\n"
+           "#include \"hip_paged_attn.h\"\n"
+           "int snippets(int B, int N, int rank, const int* rows, int steps, const int* tokens, int* next_ids) {\n"
+           + "\n".join(body) + "\n    return 0;\n}\n")
+    path = tmp_path / "snippets.c"
+    path.write_text(src)
+    r = subprocess.run(["gcc", "-std=gnu11", "-fsyntax-only", "-Wall", "-Werror", "-Wno-unused-variable",
+                        "-Wno-unused-but-set-variable", "-I" + os.path.join(REPO, "include"), str(path)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr + "\n" + src
