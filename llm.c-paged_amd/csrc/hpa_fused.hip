@@ -624,18 +624,25 @@ int launch16(FG p, int epi) {
     return 0;
 }
 
-template <int NW, int S>
-int launch16_os(FG p, int epi) {
-    dim3 grid = xcd_grid(p, p.ntn, p.Mp / 16), block(NW * 64);
+template <int NW, int S, bool NT>
+int launch16_os_nt(const FG& p, int epi, dim3 grid, dim3 block) {
     switch (epi) {
-        case HPA_FEPI_QKV: gemm16_os_kernel<NW, HPA_FEPI_QKV, S><<<grid, block, 0, hpa_stream()>>>(p); break;
-        case HPA_FEPI_RESID: gemm16_os_kernel<NW, HPA_FEPI_RESID, S><<<grid, block, 0, hpa_stream()>>>(p); break;
-        case HPA_FEPI_GELU: gemm16_os_kernel<NW, HPA_FEPI_GELU, S><<<grid, block, 0, hpa_stream()>>>(p); break;
-        case HPA_FEPI_LOGITS: gemm16_os_kernel<NW, HPA_FEPI_LOGITS, S><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_QKV: gemm16_os_kernel<NW, HPA_FEPI_QKV, S, NT><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_RESID: gemm16_os_kernel<NW, HPA_FEPI_RESID, S, NT><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_GELU: gemm16_os_kernel<NW, HPA_FEPI_GELU, S, NT><<<grid, block, 0, hpa_stream()>>>(p); break;
+        case HPA_FEPI_LOGITS: gemm16_os_kernel<NW, HPA_FEPI_LOGITS, S, NT><<<grid, block, 0, hpa_stream()>>>(p); break;
         default: return hpa_fail(__FILE__, __LINE__, "gemm_fused: unknown epilogue");
     }
     HPA_LAUNCH_CHECK();
     return 0;
+}
+
+// weights non-temporal where each tile has one reader (one 16-row block)
+template <int NW, int S>
+int launch16_os(FG p, int epi) {
+    dim3 grid = xcd_grid(p, p.ntn, p.Mp / 16), block(NW * 64);
+    return p.Mp == 16 ? launch16_os_nt<NW, S, true>(p, epi, grid, block)
+                      : launch16_os_nt<NW, S, false>(p, epi, grid, block);
 }
 
 // one-shot instances: (NW, S) with K16 = NW * S for K = 768 (K16 = 48) and 3072 (192)

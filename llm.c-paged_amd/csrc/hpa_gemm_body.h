@@ -470,7 +470,11 @@ constexpr int gemm16_os_lds_floats() {
     return 2 * HPA_FUSED_LN_KMAX + NW * 256 + 16 * 17 + 2 * 16;
 }
 
-template <int NW, int EPI, int S>
+// WNT: the weight loads non-temporal -- where every weight tile is read by ONE
+// workgroup (a single 16-row block, B <= 16: MI355X_MICROARCH.md nt-weights;
+// B = 8 decode step 0.522 -> 0.506 ms); with several row blocks the tile is
+// re-read from L2 by its row-block neighbours and the default policy is faster
+template <int NW, int EPI, int S, bool WNT = false>
 __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem) {
     constexpr int NT = NW * 64;
     float* lngb = smem;                         // LN weight [K], bias [K]
@@ -519,7 +523,12 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
     float4 wv[S], xv[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-        wv[s] = wf[s * 64];  // default policy: nt measured no faster here
+        if (WNT) {  // compile-time
+            const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(wf + s * 64));
+            wv[s] = make_float4(v.x, v.y, v.z, v.w);
+        } else {
+            wv[s] = wf[s * 64];
+        }
         xv[s] = xf[s * 64];
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -597,10 +606,10 @@ __device__ __forceinline__ void gemm16_os_body(const FG& p, int bid, float* smem
     epi.finish(p, acc, red, tile, nt, row0, lngb);
 }
 
-template <int NW, int EPI, int S>
+template <int NW, int EPI, int S, bool WNT>
 __global__ __launch_bounds__(NW * 64) void gemm16_os_kernel(FG p) {
     __shared__ __attribute__((aligned(16))) float smem[gemm16_os_lds_floats<NW>()];
-    gemm16_os_body<NW, EPI, S>(p, blockIdx.x, smem);
+    gemm16_os_body<NW, EPI, S, WNT>(p, blockIdx.x, smem);
 }
 
 
