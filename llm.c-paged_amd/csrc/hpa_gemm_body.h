@@ -329,15 +329,6 @@ constexpr int gemm16_lds_floats() {
     return 2 * HPA_FUSED_LN_KMAX + NW * MT * NTW * 256 + NTW * MT * 16 * 17 + 10 * MT * 16;
 }
 
-// operand ring depth of the looped GEMM (trips in flight + 1)
-#ifndef HPA_RING_DEPTH
-#define HPA_RING_DEPTH 2
-#endif
-template <int NW, int MT, int NTW>
-constexpr int gemm16_ring_depth() {
-    return NW >= 16 ? 2 : HPA_RING_DEPTH;  // 16 waves: 4 per SIMD, 128 VGPRs each
-}
-
 // body of the looped GEMM workgroup `bid` of the XCD-ordered 1-D grid
 // (gemm16_kernel, and the GEMM role of the pipelined combo launches)
 template <int NW, int EPI, int MT, int NTW>
@@ -381,10 +372,7 @@ __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
     struct Buf {
         float4 w[U][NTW], x[U][MT];
     };
-    constexpr int D = gemm16_ring_depth<NW, MT, NTW>();
-    Buf ring[D];
-    Buf& A = ring[0];
-    Buf& Bb = ring[1];
+    Buf A, Bb;
     auto load = [&](Buf& f, int t) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -453,25 +441,11 @@ __device__ __forceinline__ void gemm16_body(const FG& p, int bid, float* smem) {
     // header with the second buffer's loads still pending, and the waitcnt
     // pass then drains every load (vmcnt(0)) before each trip's issue; an odd
     // trip count runs one empty half instead (comp skips steps >= nsteps)
-    if constexpr (D == 2) {
-        for (int t = 0; t < trips; t += 2) {
-            load(Bb, t + 1);
-            comp(A, t);
-            load(A, t + 2);
-            comp(Bb, t + 1);
-        }
-    } else {  // D-deep ring: trip t's operands issued D-1 trips ahead
-        if (trips > 0) {
-#pragma unroll
-            for (int d = 1; d < D - 1; ++d) load(ring[d], d);
-        }
-        for (int t = 0; t < trips; t += D) {
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                load(ring[(d + D - 1) % D], t + d + D - 1);
-                comp(ring[d], t + d);
-            }
-        }
+    for (int t = 0; t < trips; t += 2) {
+        load(Bb, t + 1);
+        comp(A, t);
+        load(A, t + 2);
+        comp(Bb, t + 1);
     }
 
     if (fold)  // [NW][R][2] over the LN weight area (unused when folded)
