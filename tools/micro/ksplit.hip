@@ -5,7 +5,9 @@
 // range.  MODE 0 writes each range's partial tile (no combine: the load-side
 // floor of the tiling); MODE 1 (S = 2) publishes the partial, takes an
 // agent-scope ticket and the second arriver adds the first's partial (exact
-// in either order: fp32 a + b == b + a) -- the combine's cost.
+// in either order: fp32 a + b == b + a) -- the combine's cost.  MODE 2: the
+// same loads, no MFMAs (one VALU add per fragment keeps them live); MODE 3:
+// the MFMAs on operands loaded once (no loads in the loop).
 // Build: hipcc --offload-arch=gfx950 -O3 -o ksplit tools/micro/ksplit.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -42,6 +44,7 @@ __global__ __launch_bounds__(NW * 64) void ks_kernel(const float* __restrict__ x
     const int n = max(0, ke - kb);
     float4 wa[NTW], xa[MT], wb[NTW], xb[MT];
     auto load = [&](float4* wr, float4* xr, int s) {
+        if (MODE == 3 && s > 0) return;
         const int k = kb + min(s, max(n - 1, 0));
 #pragma unroll
         for (int j = 0; j < NTW; ++j) wr[j] = w4[((size_t)j * K16 + k) * 64];
@@ -49,6 +52,14 @@ __global__ __launch_bounds__(NW * 64) void ks_kernel(const float* __restrict__ x
         for (int r = 0; r < MT; ++r) xr[r] = x4[((size_t)r * K16 + k) * 64];
     };
     auto comp = [&](const float4* wr, const float4* xr, int s) {
+        if (MODE == 2) {
+            if (s < n)
+#pragma unroll
+                for (int j = 0; j < NTW; ++j)
+#pragma unroll
+                    for (int r = 0; r < MT; ++r) acc[j * MT + r][0] += xr[r].x + wr[j].y;
+            return;
+        }
         if (s < n) {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -63,6 +74,12 @@ __global__ __launch_bounds__(NW * 64) void ks_kernel(const float* __restrict__ x
         }
     };
     if (n > 0) load(wa, xa, 0);
+    if (MODE == 3) {
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) wb[j] = wa[j];
+#pragma unroll
+        for (int r = 0; r < MT; ++r) xb[r] = xa[r];
+    }
     for (int s = 0; s < n; s += 2) {
         load(wb, xb, s + 1);
         comp(wa, xa, s);
@@ -84,7 +101,7 @@ __global__ __launch_bounds__(NW * 64) void ks_kernel(const float* __restrict__ x
         v[i] = a;
     }
     float* mine = slab + (size_t)bid * E;
-    if (MODE == 0 || S == 1) {
+    if (MODE != 1 || S == 1) {
 #pragma unroll
         for (int i = 0; i < E / NT; ++i) mine[threadIdx.x + i * NT] = v[i];
         return;
@@ -160,6 +177,13 @@ int main() {
     run<1, 4, 0>("fcproj", 3072, 768, 8, x, w, slab, out, cnt);
     // GPT-2 XL, B = 64 (product looped: qkv 24.8, attproj 8.8, fc 25.4, fcproj 23.2 us isolated)
     run<2, 8, 0>("xl_fc", 1600, 6400, 1, x, w, slab, out, cnt);
+    run<2, 8, 2>("xl_fc", 1600, 6400, 1, x, w, slab, out, cnt);
+    run<2, 8, 3>("xl_fc", 1600, 6400, 1, x, w, slab, out, cnt);
+    run<1, 4, 2>("qkv", 768, 2304, 1, x, w, slab, out, cnt);
+    run<1, 4, 3>("qkv", 768, 2304, 1, x, w, slab, out, cnt);
+    run<1, 4, 0>("xl_fcproj", 6400, 1600, 1, x, w, slab, out, cnt);
+    run<1, 4, 2>("xl_fcproj", 6400, 1600, 1, x, w, slab, out, cnt);
+    run<1, 4, 3>("xl_fcproj", 6400, 1600, 1, x, w, slab, out, cnt);
     run<2, 4, 0>("xl_fc", 1600, 6400, 2, x, w, slab, out, cnt);
     run<2, 4, 1>("xl_fc", 1600, 6400, 2, x, w, slab, out, cnt);
     run<1, 4, 1>("xl_fc", 1600, 6400, 2, x, w, slab, out, cnt);
