@@ -7,7 +7,9 @@
 // agent-scope ticket and the second arriver adds the first's partial (exact
 // in either order: fp32 a + b == b + a) -- the combine's cost.  MODE 2: the
 // same loads, no MFMAs (one VALU add per fragment keeps them live); MODE 3:
-// the MFMAs on operands loaded once (no loads in the loop).
+// the MFMAs on operands loaded once (no loads in the loop); MODE 4: MODE 0
+// with s_setprio(1) around each MFMA cluster; MODE 5: MODE 0 with the
+// younger half of the waves at priority 1 (cdna_hip_programming.md T5).
 // Build: hipcc --offload-arch=gfx950 -O3 -o ksplit tools/micro/ksplit.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -61,6 +63,7 @@ __global__ __launch_bounds__(NW * 64) void ks_kernel(const float* __restrict__ x
             return;
         }
         if (s < n) {
+            if (MODE == 4) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -71,8 +74,10 @@ __global__ __launch_bounds__(NW * 64) void ks_kernel(const float* __restrict__ x
                         const float ws = q == 0 ? wr[j].x : q == 1 ? wr[j].y : q == 2 ? wr[j].z : wr[j].w;
                         acc[j * MT + r] = __builtin_amdgcn_mfma_f32_16x16x4f32(xs, ws, acc[j * MT + r], 0, 0, 0);
                     }
+            if (MODE == 4) __builtin_amdgcn_s_setprio(0);
         }
     };
+    if (MODE == 5 && wv >= NW / 2) __builtin_amdgcn_s_setprio(1);
     if (n > 0) load(wa, xa, 0);
     if (MODE == 3) {
 #pragma unroll
@@ -179,6 +184,11 @@ int main() {
     run<2, 8, 0>("xl_fc", 1600, 6400, 1, x, w, slab, out, cnt);
     run<2, 8, 2>("xl_fc", 1600, 6400, 1, x, w, slab, out, cnt);
     run<2, 8, 3>("xl_fc", 1600, 6400, 1, x, w, slab, out, cnt);
+    run<2, 8, 4>("xl_fc", 1600, 6400, 1, x, w, slab, out, cnt);
+    run<2, 8, 5>("xl_fc", 1600, 6400, 1, x, w, slab, out, cnt);
+    run<2, 4, 0>("xl_fc", 1600, 6400, 1, x, w, slab, out, cnt);
+    run<2, 4, 4>("xl_fc", 1600, 6400, 1, x, w, slab, out, cnt);
+    run<1, 4, 4>("qkv", 768, 2304, 1, x, w, slab, out, cnt);
     run<1, 4, 2>("qkv", 768, 2304, 1, x, w, slab, out, cnt);
     run<1, 4, 3>("qkv", 768, 2304, 1, x, w, slab, out, cnt);
     run<1, 4, 0>("xl_fcproj", 6400, 1600, 1, x, w, slab, out, cnt);
