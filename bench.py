@@ -10,8 +10,9 @@ sequences per GPU (BASELINE configs[3]: B = 512 at 8 GPUs).  The one
 collective is the end-of-step gather of the logits to rank 0 (--gather ids:
 the greedy ids only), run by the C library over RCCL/xGMI
 (gpt2_decode_gather: double-buffered on its own stream, so step k's gather
-overlaps step k+1).  torch.distributed (gloo) is only the launcher's
-rendezvous: the RCCL id exchange, barriers and the max-over-ranks time.
+overlaps step k+1).  No torch in the measuring processes: the RCCL id goes
+through a file, and the timing barriers and the max-over-ranks time run on
+the library's own communicator (hpa_comm_barrier / hpa_comm_allreduce_max).
 
 One "step" = one decode step of the whole batch: every sequence gets one new
 token at its absolute position, all layers (QKV + KV append into the HBM page
@@ -67,6 +68,49 @@ def pmc_traffic(kernel_prefix, batch_per_gpu, ctx, page_size, dtype):
     return None, None
 
 
+def comm_id_path():
+    """the RCCL id's rendezvous file: one per launch (the launcher's pid is
+    every worker's parent) and master port, on the node's local disk"""
+    port = os.environ.get("MASTER_PORT", "0")
+    return os.path.join(os.environ.get("TMPDIR", "/tmp"), f"hpa_rccl_id_{os.getppid()}_{port}")
+
+
+def comm_init(L, pagedattn, world, rank):
+    """N > 1: the library's own RCCL communicator (libpaged_hip.so, built
+    against /opt/rocm's RCCL), no torch in this process.  Rank 0 writes the
+    ncclUniqueId to a file, the others read it; the communicator then carries
+    the end-of-step gather, the timing barriers and the max-over-ranks time.
+    A rank whose communicator cannot be created exits non-zero and no value
+    is reported (a scaling line without the north star's collective would
+    leave work out of the timed region)."""
+    n = L.hpa_comm_id_bytes()
+    path = comm_id_path()
+    uid = ctypes.create_string_buffer(n)
+    if rank == 0:
+        pagedattn.check(L.hpa_comm_unique_id(uid, n), "comm_unique_id")
+        tmp = path + ".tmp"
+        with open(tmp, "wb") as f:
+            f.write(uid.raw)
+        os.replace(tmp, path)
+    else:
+        t0 = time.time()
+        while not (os.path.exists(path) and os.path.getsize(path) == n):
+            if time.time() - t0 > 120:
+                print(f"[bench] rank {rank}: no RCCL id from rank 0 in 120 s ({path})", file=sys.stderr, flush=True)
+                sys.exit(3)
+            time.sleep(0.01)
+        with open(path, "rb") as f:
+            uid = ctypes.create_string_buffer(f.read(), n)
+    if L.hpa_comm_init(world, rank, uid) != 0:
+        print(f"[bench] rank {rank}: RCCL communicator init failed "
+              f"({L.hpa_last_error().decode(errors='replace')}); no value reported", file=sys.stderr, flush=True)
+        sys.exit(4)
+    maps = open("/proc/self/maps").read().split("\n")
+    libs = sorted({ln.split()[-1] for ln in maps if ("librccl" in ln or "libamdhip64" in ln) and "/" in ln})
+    print(f"[bench] rank {rank}: RCCL communicator {rank}/{world}; loaded: {', '.join(libs)}", file=sys.stderr,
+          flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -94,6 +138,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="per CPU build (strict and -Ofast)")
     ap.add_argument("--attn-waves", type=int, default=4)
     ap.add_argument("--attn-splits", type=int, default=0, help="attention context ranges (0 = by shape)")
+    ap.add_argument("--layer-kernel", type=int, default=-1, choices=[-1, 0, 1, 2],
+                    help="layer loop: 0 five launches per layer, 1 persistent where it measured faster (B <= 32), "
+                         "2 persistent wherever it applies; -1 the engine's default (HPA_LAYER_KERNEL or 1)")
     ap.add_argument("--sample", action="store_true",
                     help="multinomial sampling as the reference driver (default: greedy argmax)")
     ap.add_argument("--gemm-waves", default="", help="fused GEMM waves qkv,attproj,fc,fcproj,logits (0 = auto)")
@@ -159,35 +206,12 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and args.gpus != world:
         args.gpus = world
-    dist = None
-    if world > 1:  # rendezvous only; the data path's collective is RCCL in the C library
-        if os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
-            # one node: bootstrap sockets on loopback (the container hostname may
-            # not resolve); RCCL's data path is xGMI either way
-            os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
-            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
     import pagedattn
     import shard
     L = pagedattn.lib()
     pagedattn.init(int(os.environ.get("HPA_DEVICE", local_rank)))  # HPA_DEVICE: rehearse N ranks on one GPU
-    if world > 1 and args.gather != "none":
-        n = L.hpa_comm_id_bytes()
-        uid = ctypes.create_string_buffer(n)
-        if rank == 0:
-            pagedattn.check(L.hpa_comm_unique_id(uid, n), "comm_unique_id")
-        obj = [uid.raw]
-        dist.broadcast_object_list(obj, src=0)
-        uid = ctypes.create_string_buffer(obj[0], n)
-        ok = L.hpa_comm_init(world, rank, uid) == 0
-        oks = [None] * world
-        dist.all_gather_object(oks, ok)
-        if not all(oks):  # report the run without the gather rather than no run at all
-            print(f"[bench] rank {rank}: RCCL communicator init failed "
-                  f"({L.hpa_last_error().decode(errors='replace')}); "
-                  "running without the end-of-step gather", file=sys.stderr, flush=True)
-            args.gather = "none (RCCL init failed)"
+    if world > 1:
+        comm_init(L, pagedattn, world, rank)
     pagedattn.check(L.hpa_set_attention_waves(args.attn_waves), "attention waves")
 
     cfgd = dict(pagedattn.GPT2_124M if args.model == "124M" else pagedattn.GPT2_XL)
@@ -210,6 +234,8 @@ def main():
                       w_dtype=pagedattn.HPA_BF16 if w_bf16 else pagedattn.HPA_F32)
     if args.attn_splits:
         model.set_attn_splits(args.attn_splits)
+    if args.layer_kernel >= 0:
+        model.set_layer_kernel(args.layer_kernel)
     if args.sample:
         model.set_sampling(True, seed=1337 + lo)
     if args.gemm_waves or args.gemm_rows or args.gemm_cols:
@@ -261,7 +287,7 @@ def main():
         one_step(None)
     sync()
     if world > 1:
-        dist.barrier()
+        pagedattn.check(L.hpa_comm_barrier(), "comm barrier")  # RCCL all-reduce + wait
     sync()
     bytes_before, _ = model.step_bytes()
     t0 = time.perf_counter()
@@ -269,15 +295,14 @@ def main():
         one_step(None)
     sync()
     if world > 1:
-        dist.barrier()
+        pagedattn.check(L.hpa_comm_barrier(), "comm barrier")
     t1 = time.perf_counter()
     bytes_after, _ = model.step_bytes()
     elapsed = t1 - t0
-    if world > 1:
-        import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    if world > 1:  # max over ranks, through the library's RCCL communicator
+        el = ctypes.c_double(elapsed)
+        pagedattn.check(L.hpa_comm_allreduce_max(ctypes.byref(el)), "comm max")
+        elapsed = el.value
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
     tokens_per_s = B * args.steps / elapsed  # whole job: every rank's sequences
 
@@ -347,6 +372,8 @@ def main():
                                                                if gather else
                                                                f" (gather: {args.gather})" if world > 1 else ""),
                        "hip_graph": not args.no_graph, "attn_splits": splits,
+                       "layer_loop": ("one persistent launch per layer (hpa_decode_layer)" if model.layer_kernel()
+                                      else "five launches per layer"),
                        "token_choice": "multinomial (reference sample_mult)" if args.sample else "greedy",
                        "gemm_waves": [int(x) for x in model.gemm_config()[0]],
                        "gemm_row_blocks": [int(x) for x in model.gemm_config()[1]],
@@ -362,10 +389,13 @@ def main():
         print(json.dumps(result), flush=True)
     model.close()
     if world > 1:
-        if gather:
-            L.hpa_comm_destroy()
-        dist.barrier()
-        dist.destroy_process_group()
+        pagedattn.check(L.hpa_comm_barrier(), "comm barrier")
+        L.hpa_comm_destroy()
+        if rank == 0:
+            try:
+                os.unlink(comm_id_path())
+            except OSError:
+                pass
 
 
 if __name__ == "__main__":

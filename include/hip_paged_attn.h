@@ -263,6 +263,64 @@ void hpa_fused_pick_bf16(int M, int N, int K, int* out3);
  * out3 = {waves, row_blocks, rounds}; returns 1 where variant 0 uses it */
 int hpa_fused_pick_bf16_ares(int M, int N, int K, int* out3);
 int hpa_fused_pick_waves(int M, int N, int K);
+/* ---------------- persistent decode layer (hpa_layer.hip) ----------------
+ * The decode step's layer loop (reference gpt2_forward, paged_infer.c:659-722)
+ * as ONE launch per layer l instead of five:
+ *   attention(l) -> attproj(l) -> fc(l) -> fcproj(l) -> qkv(l+1)
+ * One 16-wave workgroup per CU, all resident; the phases hand off through
+ * write-through (sc1) stores and agent-scope arrival counters inside the
+ * launch.  Each workgroup owns a fixed slice ("granule": a 16-column tile and
+ * a K range) of every GEMM; the attproj / fc / fcproj slices are copied into
+ * its LDS while the attention streams K/V, so the GEMM phases read only the
+ * activations.  attproj and fcproj are split over K (parts), and the last part
+ * of a (row block, column tile) to arrive sums the parts in part order.  qkv
+ * and fc use the one-shot kernel's summation order (4 waves x K/4, folded in
+ * wave order): their rows are bit-identical to the launch path.
+ * fp32 frag-packed weights with the LayerNorms folded (hpa_ln_fold_pack);
+ * C = 128 or 768 (num_heads 2 or 12), B <= 64, B*num_heads*splits <= 3 x CUs.
+ * Every spin is bounded (200 ms): a timeout stores a nonzero code in *err and
+ * ends the launch (the outputs are then garbage). */
+typedef struct {
+    int B, C, num_heads, splits;  /* splits: context ranges of the attention */
+    int last;                     /* 1: no qkv(l+1) phase (last layer) */
+    const HpaKVPool* pool;
+    int layer;
+    const int* block_table;
+    int bt_stride;
+    const int* pos;
+    const float* q;               /* q of layer l [B][C] row-major (read) */
+    float* att;                   /* attention output, frag [Mp][C] */
+    float* res;                   /* residual in (frag [Mp][C]); fcproj writes the next */
+    float* res2;                  /* res + attproj, frag [Mp][C] */
+    float* fch;                   /* gelu(fc), frag [Mp][4C] */
+    const float* w_ap;            /* frag-packed attprojw [C][C] */
+    const float* b_ap;
+    const float* w_fc;            /* LN2-folded fcw [4C][C] */
+    const float* fc_c1;
+    const float* fc_c2;
+    const float* w_fp;            /* frag-packed fcprojw [C][4C] */
+    const float* b_fp;
+    const float* w_qkv;           /* layer l+1, LN1-folded qkvw [3C][C] (unused when last) */
+    const float* qkv_c1;
+    const float* qkv_c2;
+    float* q_out;                 /* q of layer l+1 [B][C]; its K/V go into layer l+1's pages */
+    float* stats_out;             /* last layer: LNf statistics [C/16][Mp][2] of res; else NULL */
+    float* rec;                   /* attention split records (hpa_decode_layer_sizes) */
+    float* slab;                  /* K-part partial sums */
+    int* counters;                /* this layer's counter block, zero before the launch */
+    int* err;                     /* 0, or the code of the first timed-out wait */
+} HpaLayerArgs;
+/* 1 if the persistent layer applies (shape, CU count, residency), else 0 */
+int hpa_decode_layer_eligible(int B, int C, int num_heads, int splits);
+/* splits the persistent layer uses by default for this batch */
+int hpa_decode_layer_pick_splits(int B, int num_heads, int max_ctx);
+/* sizes: out[0] = rec floats, out[1] = slab floats, out[2] = counter ints per layer */
+int hpa_decode_layer_sizes(int B, int C, int num_heads, int splits, size_t* out3);
+int hpa_decode_layer(const HpaLayerArgs* a);
+/* diagnostic builds (-DHPA_LAYER_TRACE) only, else returns 1: per-(layer,
+ * workgroup) event stamps [layers][256][16] of the last launches (10 ns
+ * ticks); host = NULL clears them */
+int hpa_decode_layer_trace(unsigned long long* host, int layers);
 /* residual = wte[tok] + wpe[pos] in frag layout [Mp][C], stats (1 tile) */
 int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const float* wpe,
                    float* res_frag, float* stats, int B, int C);
@@ -312,7 +370,7 @@ int hpa_gather_rows_frag(const float* src, const float* src_stats, int src_Mp, c
 /* ---------------- multi-GPU: RCCL over xGMI (hpa_comm.hip) ----------------
  * One process per GPU.  Rank 0 makes the id
  * (hpa_comm_unique_id), the launcher hands it to every rank (any out-of-band
- * channel: torch.distributed's store, a file, MPI), and each rank binds its
+ * channel: a file -- bench.py --, sockets, MPI), and each rank binds its
  * current device with hpa_comm_init.  The decode engine's end-of-step gather
  * (gpt2_decode_gather) runs on it. */
 size_t hpa_comm_id_bytes(void);                     /* sizeof(ncclUniqueId) = 128 */
@@ -325,6 +383,24 @@ int    hpa_comm_rank(void);                         /* -1 before hpa_comm_init *
  * uneven sizes allowed) on `stream` (NULL = the library stream), async */
 int    hpa_comm_gatherv(const void* send, size_t send_bytes, void* recv, const size_t* bytes_per_rank, int root,
                         void* stream);
+/* the gather's layout, host arithmetic only (what hpa_comm_gatherv posts):
+ * recv_off[r] = byte offset of rank r's rows in root's buffer (rank order);
+ * returns the number of ncclRecv the root posts (ranks != root with bytes),
+ * or 1 / 0 on a non-root rank (it sends iff its bytes are nonzero); -1 on bad
+ * arguments.  *own_off = root's own rows' offset (its local copy). */
+int    hpa_comm_gather_layout(int nranks, int rank, int root, const size_t* bytes_per_rank, size_t* recv_off,
+                              size_t* own_off);
+/* timing helpers over the communicator (RCCL all-reduce on the library
+ * stream, then a host wait): a barrier, and the maximum of one host double
+ * over the ranks (bench.py's max-over-ranks step time) */
+int    hpa_comm_barrier(void);
+int    hpa_comm_allreduce_max(double* value);
+/* single-process form (one process driving ndev GPUs,
+ * ncclCommInitAll): communicators for devices devs[0..ndev-1], rank i =
+ * devs[i]; hpa_comm_use(i) makes comm i (and device devs[i]) current for the
+ * calls above.  Exclusive with hpa_comm_init. */
+int    hpa_comm_init_all(int ndev, const int* devs);
+int    hpa_comm_use(int index);
 
 /* ---------------- reference-layout kernels (drop-in compat) ----------------
  * Pages in the reference layout: token-major [block_size][C] per page

@@ -42,75 +42,6 @@
 namespace {
 using namespace hpa_attn;
 
-// split-context records: [B*NH][S][kRec] floats (m, l, -, -, acc[64]), then
-// [B*NH] int arrival counters (zero between launches)
-constexpr int kRec = 68;
-
-// Range s of S: publish this workgroup's folded state (K float4 chunks per
-// lane in wave 0: chunk k of lane j holds dims 4*(K*j + k)..+3 -- K = 1 for
-// the fp32 fold, lanes 0..15; K = 2 for the bf16 fold, lanes 0..7); the last
-// arriver merges every range in order and returns true with the merged state.
-template <int K>
-__device__ __forceinline__ bool split_merge(float* __restrict__ rec_bh, int* __restrict__ cnt, int S, int s,
-                                            float& m, float& l, float4* acc) {
-    const int lane = threadIdx.x & 63;
-    float* rec = rec_bh + (size_t)s * kRec;
-    if (lane == 0) hpa::store_wt16(rec, 0, make_float4(m, l, 0.f, 0.f));
-#pragma unroll
-    for (int k = 0; k < K; ++k) hpa::store_wt16(rec, (4 + 4 * (K * lane + k)) * 4, acc[k]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every record store drained before the ticket
-    int ticket = 0;
-    if (lane == 0) ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ticket = __builtin_amdgcn_readfirstlane(ticket);
-    if (ticket != S - 1) return false;
-    if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-    // every record's (m, l) head, all in flight together (one after another
-    // each would be a cross-XCD round trip), then the acc chunks 8 ranges at a time
-    float4 head[HPA_ATTN_MAX_SPLITS];
-#pragma unroll
-    for (int i = 0; i < HPA_ATTN_MAX_SPLITS; ++i) head[i] = hpa::load_wt16(rec_bh + (size_t)min(i, S - 1) * kRec, 0);
-    float M = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < HPA_ATTN_MAX_SPLITS; ++i)
-        if (i < S) M = fmaxf(M, head[i].x);
-    float L = 0.f;
-    float4 O[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) O[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int i0 = 0; i0 < S; i0 += 8) {  // ranges in order: independent of arrival order
-        float4 a[8][K];
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                a[q][k] = hpa::load_wt16(rec_bh + (size_t)min(i0 + q, S - 1) * kRec, (4 + 4 * (K * lane + k)) * 4);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            if (i0 + q >= S) break;
-            float hm = head[0].x, hl = head[0].y;
-#pragma unroll
-            for (int i = 1; i < HPA_ATTN_MAX_SPLITS; ++i)
-                if (i == i0 + q) {
-                    hm = head[i].x;
-                    hl = head[i].y;
-                }
-            const float f = exp2f(hm - M);
-            L = fmaf(hl, f, L);
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                O[k].x = fmaf(a[q][k].x, f, O[k].x);
-                O[k].y = fmaf(a[q][k].y, f, O[k].y);
-                O[k].z = fmaf(a[q][k].z, f, O[k].z);
-                O[k].w = fmaf(a[q][k].w, f, O[k].w);
-            }
-        }
-    }
-    m = M;
-    l = L;
-#pragma unroll
-    for (int k = 0; k < K; ++k) acc[k] = O[k];
-    return true;
-}
 
 template <int P, int NW, bool FRAG, bool BF16>
 __global__ __launch_bounds__(NW * 64, 3) void paged_attn_decode_f32(
@@ -149,7 +80,7 @@ __global__ __launch_bounds__(NW * 64, 3) void paged_attn_decode_f32(
         attn_tiles_bf16<P, NW>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, page_elems, bt, bt_stride, ctx,
                                it0, n_it, qscale, m, l, acc);
         if (!attn_fold_bf16<NW>(m, l, acc, s_m, s_l, s_acc)) return;
-        if (S > 1 && !split_merge<2>(rec_bh, cnt, S, sr, m, l, acc)) return;
+        if (S > 1 && !split_merge<2>(rec_bh, cnt, S, sr, m, l, acc, true)) return;
         const float inv = l == 0.f ? 0.f : 1.f / l;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {  // dims 8*lane + 4k .. +3
@@ -164,7 +95,7 @@ __global__ __launch_bounds__(NW * 64, 3) void paged_attn_decode_f32(
         attn_tiles<P, NW>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, page_elems, bt, bt_stride, ctx,
                           it0, n_it, qscale, m, l, acc);
         if (!attn_fold<NW>(m, l, acc, s_m, s_l, s_acc)) return;
-        if (S > 1 && !split_merge<1>(rec_bh, cnt, S, sr, m, l, &acc)) return;
+        if (S > 1 && !split_merge<1>(rec_bh, cnt, S, sr, m, l, &acc, true)) return;
         // out[b][h*64 + 4*lane .. +3]: row-major, or the frag layout the next
         // GEMM reads (4 consecutive columns stay one contiguous float4 there)
         const size_t oi =

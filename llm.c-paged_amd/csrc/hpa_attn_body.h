@@ -43,10 +43,10 @@ template <int P, int NW>
 __device__ __forceinline__ void attn_tiles(const float* __restrict__ qh, const float* __restrict__ kbase,
                                            const float* __restrict__ vbase, size_t page_elems,
                                            const int* __restrict__ bt, int bt_len, int ctx, int it_begin,
-                                           int it_end, float qscale, float& m, float& l, float4& acc) {
+                                           int it_end, float qscale, float& m, float& l, float4& acc,
+                                           int w = (int)(threadIdx.x >> 6)) {
     static_assert(P % 4 == 0 && 64 % P == 0, "page size must divide 64 and be a multiple of 4");
     const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
     const int g = lane >> 4;
     const int d4 = lane & 15;
     const int v_lane_off = g * HS + d4 * 4;
@@ -127,10 +127,10 @@ __device__ __forceinline__ void attn_tiles_bf16(const float* __restrict__ qh,
                                                 const unsigned short* __restrict__ kbase,
                                                 const unsigned short* __restrict__ vbase, size_t page_elems,
                                                 const int* __restrict__ bt, int bt_len, int ctx, int it_begin,
-                                                int it_end, float qscale, float& m, float& l, float4* acc) {
+                                                int it_end, float qscale, float& m, float& l, float4* acc,
+                                                int w = (int)(threadIdx.x >> 6)) {
     static_assert(P % 8 == 0 && 64 % P == 0, "bf16 pages: page size 8, 16, 32 or 64");
     const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
     const int g = lane >> 3;
     const int d8 = lane & 7;
     const int v_lane_off = g * HS + d8 * 8;
@@ -299,6 +299,77 @@ __device__ __forceinline__ bool attn_fold(float& m, float& l, float4& acc, float
         acc = O;
         return true;
     }
+}
+
+// split-context records: [B*NH][S][kRec] floats (m, l, -, -, acc[64]), then
+// [B*NH] int arrival counters (zero between launches)
+constexpr int kRec = 68;
+
+// Range s of S: publish this workgroup's folded state (K float4 chunks per
+// lane in wave 0: chunk k of lane j holds dims 4*(K*j + k)..+3 -- K = 1 for
+// the fp32 fold, lanes 0..15; K = 2 for the bf16 fold, lanes 0..7); the last
+// arriver merges every range in order and returns true with the merged state
+// (rewind: it also zeroes the counter for the next launch).
+template <int K>
+__device__ __forceinline__ bool split_merge(float* __restrict__ rec_bh, int* __restrict__ cnt, int S, int s,
+                                            float& m, float& l, float4* acc, bool rewind) {
+    const int lane = threadIdx.x & 63;
+    float* rec = rec_bh + (size_t)s * kRec;
+    if (lane == 0) hpa::store_wt16(rec, 0, make_float4(m, l, 0.f, 0.f));
+#pragma unroll
+    for (int k = 0; k < K; ++k) hpa::store_wt16(rec, (4 + 4 * (K * lane + k)) * 4, acc[k]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every record store drained before the ticket
+    int ticket = 0;
+    if (lane == 0) ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ticket = __builtin_amdgcn_readfirstlane(ticket);
+    if (ticket != S - 1) return false;
+    if (rewind && lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    // every record's (m, l) head, all in flight together (one after another
+    // each would be a cross-XCD round trip), then the acc chunks 8 ranges at a time
+    float4 head[HPA_ATTN_MAX_SPLITS];
+#pragma unroll
+    for (int i = 0; i < HPA_ATTN_MAX_SPLITS; ++i) head[i] = hpa::load_wt16(rec_bh + (size_t)min(i, S - 1) * kRec, 0);
+    float M = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < HPA_ATTN_MAX_SPLITS; ++i)
+        if (i < S) M = fmaxf(M, head[i].x);
+    float L = 0.f;
+    float4 O[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) O[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i0 = 0; i0 < S; i0 += 8) {  // ranges in order: independent of arrival order
+        float4 a[8][K];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                a[q][k] = hpa::load_wt16(rec_bh + (size_t)min(i0 + q, S - 1) * kRec, (4 + 4 * (K * lane + k)) * 4);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (i0 + q >= S) break;
+            float hm = head[0].x, hl = head[0].y;
+#pragma unroll
+            for (int i = 1; i < HPA_ATTN_MAX_SPLITS; ++i)
+                if (i == i0 + q) {
+                    hm = head[i].x;
+                    hl = head[i].y;
+                }
+            const float f = exp2f(hm - M);
+            L = fmaf(hl, f, L);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                O[k].x = fmaf(a[q][k].x, f, O[k].x);
+                O[k].y = fmaf(a[q][k].y, f, O[k].y);
+                O[k].z = fmaf(a[q][k].z, f, O[k].z);
+                O[k].w = fmaf(a[q][k].w, f, O[k].w);
+            }
+        }
+    }
+    m = M;
+    l = L;
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = O[k];
+    return true;
 }
 
 }  // namespace hpa_attn

@@ -9,6 +9,7 @@
 // reference has no collective outside the PyTorch trainer
 // (train_gpt2.py:400-412).
 #include <rccl/rccl.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "hpa_internal.h"
@@ -16,6 +17,10 @@
 namespace {
 ncclComm_t g_comm = nullptr;
 int g_nranks = 0, g_rank = -1;
+// single-process form (hpa_comm_init_all): one communicator per device
+ncclComm_t* g_all = nullptr;
+int* g_all_dev = nullptr;
+int g_all_n = 0;
 }  // namespace
 
 #define HPA_NCCL(call)                                                                          \
@@ -49,6 +54,23 @@ int hpa_comm_init(int nranks, int rank, const void* id) {
 }
 
 int hpa_comm_destroy(void) {
+    if (g_all) {  // the single-process set: every device's communicator
+        ncclResult_t r = ncclSuccess;
+        for (int i = 0; i < g_all_n; ++i)
+            if (g_all[i]) {
+                const ncclResult_t ri = ncclCommDestroy(g_all[i]);
+                if (r == ncclSuccess) r = ri;
+            }
+        free(g_all);
+        free(g_all_dev);
+        g_all = nullptr;
+        g_all_dev = nullptr;
+        g_all_n = 0;
+        g_comm = nullptr;
+        g_nranks = 0;
+        g_rank = -1;
+        return r == ncclSuccess ? 0 : hpa_fail(__FILE__, __LINE__, ncclGetErrorString(r));
+    }
     if (!g_comm) return 0;
     const ncclResult_t r = ncclCommDestroy(g_comm);
     g_comm = nullptr;
@@ -60,9 +82,24 @@ int hpa_comm_destroy(void) {
 int hpa_comm_size(void) { return g_nranks; }
 int hpa_comm_rank(void) { return g_rank; }
 
+int hpa_comm_gather_layout(int nranks, int rank, int root, const size_t* bytes_per_rank, size_t* recv_off,
+                           size_t* own_off) {
+    if (nranks < 1 || rank < 0 || rank >= nranks || root < 0 || root >= nranks || !bytes_per_rank) return -1;
+    size_t off = 0;
+    int posts = 0;
+    for (int r = 0; r < nranks; ++r) {
+        if (recv_off) recv_off[r] = off;
+        if (r == root && own_off) *own_off = off;
+        if (r != root && bytes_per_rank[r]) ++posts;
+        off += bytes_per_rank[r];
+    }
+    if (rank != root) return bytes_per_rank[rank] ? 1 : 0;
+    return posts;
+}
+
 // Rank r sends its send_bytes to root, which places them at offset
-// sum(bytes_per_rank[0..r-1]) of recv (rank order).  Enqueued on `stream`
-// (NULL = the library stream); asynchronous.
+// sum(bytes_per_rank[0..r-1]) of recv (rank order; hpa_comm_gather_layout).
+// Enqueued on `stream` (NULL = the library stream); asynchronous.
 int hpa_comm_gatherv(const void* send, size_t send_bytes, void* recv, const size_t* bytes_per_rank, int root,
                      void* stream) {
     HPA_REQUIRE(g_comm, "comm_gatherv: hpa_comm_init first");
@@ -74,18 +111,70 @@ int hpa_comm_gatherv(const void* send, size_t send_bytes, void* recv, const size
         return 0;
     }
     HPA_REQUIRE(recv, "comm_gatherv: root needs a receive buffer");
-    size_t off = 0;
-    HPA_NCCL(ncclGroupStart());
-    for (int r = 0; r < g_nranks; ++r) {
-        if (r != root && bytes_per_rank[r])
-            HPA_NCCL(ncclRecv((char*)recv + off, bytes_per_rank[r], ncclChar, r, g_comm, s));
-        off += bytes_per_rank[r];
+    size_t* off = (size_t*)malloc((size_t)g_nranks * sizeof(size_t));
+    HPA_REQUIRE(off, "comm_gatherv: out of host memory");
+    size_t own = 0;
+    hpa_comm_gather_layout(g_nranks, g_rank, root, bytes_per_rank, off, &own);
+    ncclResult_t r = ncclGroupStart();
+    for (int q = 0; q < g_nranks && r == ncclSuccess; ++q)
+        if (q != root && bytes_per_rank[q]) r = ncclRecv((char*)recv + off[q], bytes_per_rank[q], ncclChar, q, g_comm, s);
+    const ncclResult_t r2 = ncclGroupEnd();
+    free(off);
+    HPA_NCCL(r);
+    HPA_NCCL(r2);
+    if (send_bytes && (char*)recv + own != send)
+        HPA_CHECK(hipMemcpyAsync((char*)recv + own, send, send_bytes, hipMemcpyDeviceToDevice, s));
+    return 0;
+}
+
+// (a device word per call: rare calls -- timing --, and the current device
+// may change between them in the single-process form)
+int hpa_comm_allreduce_max(double* value) {
+    HPA_REQUIRE(g_comm && value, "comm_allreduce_max: hpa_comm_init first");
+    double* w = nullptr;
+    HPA_CHECK(hipMalloc(&w, sizeof(double)));
+    hipStream_t s = hpa_stream();
+    int rc = hipMemcpyAsync(w, value, sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess;
+    const ncclResult_t r = rc ? ncclSuccess : ncclAllReduce(w, w, 1, ncclFloat64, ncclMax, g_comm, s);
+    rc |= r != ncclSuccess;
+    rc |= !rc && hipMemcpyAsync(value, w, sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess;
+    rc |= hipStreamSynchronize(s) != hipSuccess;
+    (void)hipFree(w);
+    if (r != ncclSuccess) return hpa_fail(__FILE__, __LINE__, ncclGetErrorString(r));
+    HPA_REQUIRE(!rc, "comm_allreduce_max: copy / sync failed");
+    return 0;
+}
+
+int hpa_comm_barrier(void) {
+    double v = 0.0;
+    return hpa_comm_allreduce_max(&v);
+}
+
+int hpa_comm_init_all(int ndev, const int* devs) {
+    HPA_REQUIRE(ndev >= 1 && devs, "comm_init_all: devices");
+    HPA_REQUIRE(!g_comm && !g_all, "comm_init_all: a communicator exists (hpa_comm_destroy first)");
+    g_all = (ncclComm_t*)calloc(ndev, sizeof(ncclComm_t));
+    g_all_dev = (int*)malloc(ndev * sizeof(int));
+    HPA_REQUIRE(g_all && g_all_dev, "comm_init_all: out of host memory");
+    memcpy(g_all_dev, devs, ndev * sizeof(int));
+    const ncclResult_t r = ncclCommInitAll(g_all, ndev, devs);
+    if (r != ncclSuccess) {
+        free(g_all);
+        free(g_all_dev);
+        g_all = nullptr;
+        g_all_dev = nullptr;
+        return hpa_fail(__FILE__, __LINE__, ncclGetErrorString(r));
     }
-    HPA_NCCL(ncclGroupEnd());
-    off = 0;
-    for (int r = 0; r < root; ++r) off += bytes_per_rank[r];
-    if (send_bytes && (char*)recv + off != send)
-        HPA_CHECK(hipMemcpyAsync((char*)recv + off, send, send_bytes, hipMemcpyDeviceToDevice, s));
+    g_all_n = ndev;
+    return hpa_comm_use(0);
+}
+
+int hpa_comm_use(int index) {
+    HPA_REQUIRE(g_all && index >= 0 && index < g_all_n, "comm_use: hpa_comm_init_all first / index");
+    if (hpa_get_device() != g_all_dev[index]) HPA_REQUIRE(hpa_init(g_all_dev[index]) == 0, "comm_use: device");
+    g_comm = g_all[index];
+    g_nranks = g_all_n;
+    g_rank = index;
     return 0;
 }
 

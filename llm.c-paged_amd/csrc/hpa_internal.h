@@ -47,6 +47,15 @@ __device__ __forceinline__ float4 load_wt16(const void* base, int byte_off) {
     return make_float4(__uint_as_float(d.x), __uint_as_float(d.y), __uint_as_float(d.z), __uint_as_float(d.w));
 }
 
+// 4-byte forms (one float per lane; a wave's 64 consecutive floats are one
+// 256-B write-through burst)
+__device__ __forceinline__ void store_wt4(void* base, int byte_off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), wt_rsrc(base), byte_off, 0, kCpolSc1);
+}
+__device__ __forceinline__ float load_wt4(const void* base, int byte_off) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wt_rsrc(base), byte_off, 0, kCpolSc1));
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

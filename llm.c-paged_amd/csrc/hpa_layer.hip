@@ -1,0 +1,807 @@
+// hpa_layer.hip -- the decode step's layer as ONE persistent launch (gfx950).
+//
+// Replaces five launches per layer of the reference layer loop
+// (gpt2_forward, paged_infer.c:659-722, one decode row per sequence):
+//   A  attention(l)   attention_paged :163-240 (split context, hpa_attn_body.h)
+//   B  attproj(l)     matmul_forward :716 + residual_forward :717
+//   C  fc(l)          layernorm_forward :718 (folded) + matmul :719 + gelu :720
+//   D  fcproj(l)      matmul_forward :721 + residual_forward :722
+//   E  qkv(l+1)       layernorm :696 (folded) + matmul_cached :706 + add_to_cache :710
+// so a step is embed, qkv(0), L of these, logits, token choice.
+//
+// Why ("Persistent layer"): every launch of the
+// five-kernel layer pays a fixed dispatch + first-HBM-round-trip + drain cost
+// (~3 us) and the GEMMs fetch their weights from HBM only after the previous
+// kernel has ended.  Here the workgroup of each CU copies its slices of the
+// attproj / fc / fcproj weights into LDS while the attention streams K/V
+// (slot 3 below), so the GEMM phases read only the activations, and the seams
+// between phases are in-launch hand-offs.
+//
+// Geometry: one workgroup of 16 waves per CU (grid = CU count), all resident
+// (checked with the occupancy API).  In phase A the waves form four 4-wave
+// slots; slots 0..2 each run one attention unit (sequence, head, context
+// range: the split-context decomposition of hpa_attn.hip, with its
+// last-arriver merge), slot 3 stages the weights.  In the GEMM phases the
+// waves form four row-block groups (group g = rows 16g..16g+15), each of 4
+// waves splitting the granule's K range exactly like the one-shot kernel
+// (gemm16_os_kernel<4, *, K16/4>), so qkv and fc rows are bit-identical to the
+// launch path.
+//
+// Granules (fixed per workgroup, i.e. per CU):
+//   attproj  (column tile j, K part p of AP)   on workgroups [0, N_AP)
+//   fc       (column tile j, all K)            on workgroups [0, N_FC)
+//   fcproj   (column tile j, K part p of 4)    on workgroups [G - N_FP, G)
+//   qkv      (column tile j, all K)            on workgroups [0, N_QKV)
+// K-part partial tiles go to a slab with write-through stores; the last part
+// of a (row block, column tile) to draw its ticket sums the parts in part
+// order (results independent of arrival order), adds bias and residual.
+//
+// Hand-offs (MI355X_MICROARCH.md "Valid forms", row 1; cdna_hip_programming.md
+// Guideline 16): every byte handed over inside the launch is stored sc1
+// (write-through) and loaded sc1 (L1 bypass); each storing wave drains
+// (s_waitcnt vmcnt(0)), the workgroup barrier follows, then ONE lane adds to
+// the phase counter, sharded over 8 lines by workgroup % 8; the consumer's
+// wave 0 polls every shard with sc1 loads, the other waves wait at a barrier.
+// Counters are zeroed before every step (a memset node), one block per layer.
+// Every spin is bounded: on timeout *err gets the phase code and the launch
+// ends (outputs garbage, reported by the host).
+#include <math.h>
+
+#include "hpa_attn_body.h"
+#include "hpa_gemm_body.h"
+
+namespace {
+using hpa_attn::HS;
+using hpa_attn::kRec;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kPad = 32;                // ints per counter shard (one 128-B line)
+constexpr int kCtrInts = 4 * 8 * kPad;  // counters ATT, X1, H, X2 x 8 shards
+enum { CT_ATT = 0, CT_X1 = 1, CT_H = 2, CT_X2 = 3 };
+constexpr long long kSpinTicks = 20000000;  // s_memrealtime is 100 MHz: 200 ms
+
+template <int NH>
+struct LD {
+    static constexpr int C = 64 * NH;
+    static constexpr int K16 = C / 16;  // k16 steps of K = C; also the column tiles of N = C
+    static constexpr int NCT = C / 16;
+    static constexpr int FP = 4;   // fcproj K parts (C each)
+    static constexpr int SW = NH;  // k16 steps per wave: K = C over a slot's 4 waves
+};
+
+template <int NH>
+struct Smem {
+    float red[12 * 256];     // [wave][4 regs][64 lanes] accumulators
+    float wsum[12 * 32];     // [wave][16 rows][2] LN row partial sums
+    float tile[3 * 16 * 17]; // last layer: [slot][16 rows][17] for the LNf statistics
+    float s_m[3][4], s_l[3][4];
+    float4 s_acc[3][64];     // [slot][4 waves x 16 lanes] (fp32) / [4 waves x 8 lanes][2] (bf16)
+    int s_cnt[3];
+    int s_ok;
+    int s_last[3];
+};
+
+struct KA {
+    int B, Mp, R, S, G, last, layer;
+    const float* q;
+    const void* kv;       // layer l of the pool
+    void* kv_next;        // layer l+1
+    size_t page_elems;
+    const int* bt;
+    int bt_stride;
+    const int* pos;
+    float qscale, m_init;
+    float *att, *res, *res2, *fch;
+    const float *w_ap, *b_ap, *w_fc, *fc_c1, *fc_c2, *w_fp, *b_fp, *w_qkv, *qkv_c1, *qkv_c2;
+    float* q_out;
+    float* stats_out;
+    float* rec;
+    float* slab_fp;
+    int* ctr;
+    int* err;
+};
+
+// diagnostic build (-DHPA_LAYER_TRACE, tools/pl_trace.py): s_memrealtime of
+// workgroup-level events per (layer, workgroup); never in the product library
+#ifdef HPA_LAYER_TRACE
+// (the stamp intrinsic counts as a memory clobber: the trace build loads q
+// through vector loads + readfirstlane, HPA_PL_QREG, ~1 us later than the
+// product's scalar loads)
+#ifndef HPA_PL_QREG
+#define HPA_PL_QREG 1
+#endif
+__device__ unsigned long long g_pl_trace[64][256][16];
+#define PL_MARK(k)                                                                                     \
+    do {                                                                                               \
+        if (threadIdx.x == 0 && a.layer < 64 && blockIdx.x < 256)                                      \
+            g_pl_trace[a.layer][blockIdx.x][k] = (unsigned long long)__builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+// stamps taken before the attention are stored after it: a global store in
+// front of the q loads would cost them their scalar (s_load) form
+#define PL_STAMP(var) const unsigned long long var = (unsigned long long)__builtin_amdgcn_s_memrealtime()
+#define PL_STORE(k, var)                                                           \
+    do {                                                                           \
+        if (threadIdx.x == 0 && a.layer < 64 && blockIdx.x < 256) g_pl_trace[a.layer][blockIdx.x][k] = var; \
+    } while (0)
+#else
+#define PL_MARK(k) \
+    do {           \
+    } while (0)
+#define PL_STAMP(var) \
+    do {              \
+    } while (0)
+#define PL_STORE(k, var) \
+    do {                 \
+    } while (0)
+#endif
+
+__device__ __forceinline__ int wave_sum_int(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// every thread of the workgroup calls; wave 0 polls the 8 shards of counter
+// `which` until they sum to `expected` (bounded), the rest wait at the barrier
+template <int NH>
+__device__ __forceinline__ bool wait_ctr(const KA& a, int which, int expected, int code, Smem<NH>& sm) {
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wv == 0) {
+        const int lane = threadIdx.x & 63;
+        const int* c = a.ctr + which * 8 * kPad;
+        int ok = 0;
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        for (unsigned it = 0;; ++it) {
+#ifndef HPA_PL_POLL
+#define HPA_PL_POLL 0
+#endif
+#if HPA_PL_POLL == 2  /* experiment: returning atomic add of 0 (served at the memory side) */
+            int v = lane < 8 ? __hip_atomic_fetch_add(const_cast<int*>(c) + lane * kPad, 0, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT)
+                             : 0;
+#elif HPA_PL_POLL == 3  /* experiment: system-scope (sc0 sc1) loads */
+            int v = lane < 8 ? __hip_atomic_load(c + lane * kPad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0;
+#else
+            int v = lane < 8 ? __hip_atomic_load(c + lane * kPad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+#endif
+            v = __builtin_amdgcn_readfirstlane(wave_sum_int(v));
+            if (v >= expected) {
+                ok = 1;
+                break;
+            }
+            if ((it & 7) == 7) {
+                const int e = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if (e) break;  // another workgroup gave up: follow at once
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+                    if (lane == 0) atomicCAS(a.err, 0, code);
+                    break;
+                }
+            }
+#ifndef HPA_PL_NOSLEEP
+            __builtin_amdgcn_s_sleep(1);
+#endif
+        }
+        if (lane == 0) sm.s_ok = ok;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // no VMEM drain (see lds_barrier)
+    const bool ok = sm.s_ok != 0;
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // s_ok read before the next wait rewrites it
+    return ok;
+}
+
+// one lane, after every storing wave's drain and the workgroup barrier
+__device__ __forceinline__ void arrive(const KA& a, int which, int n) {
+    __hip_atomic_fetch_add(a.ctr + which * 8 * kPad + (blockIdx.x & 7) * kPad, n, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ float4 ld_nt(const float4* p) {
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
+// ------------------------------------------------------------------ phase A
+// attention unit u = (sequence, head) x context range, run by the 4 waves of
+// `slot`; the slot folds through LDS with a last-arriving-wave counter (no
+// workgroup barrier: the other slots and the staging waves run on)
+// q of unit u's (sequence, head) as wave-uniform values (SGPRs): loaded
+// before the weight DMA is issued (behind an LDS-DMA the compiler no longer
+// proves q unclobbered and would keep it in 64 VGPRs)
+template <int NH>
+__device__ __forceinline__ void load_q(const KA& a, int u, float (&qv)[HS]) {
+    const float4* q4 = reinterpret_cast<const float4*>(a.q + (size_t)(u / a.S) * HS);
+#pragma unroll
+    for (int i = 0; i < HS / 4; ++i) {
+        const float4 t = q4[i];
+        qv[4 * i + 0] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(t.x)));
+        qv[4 * i + 1] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(t.y)));
+        qv[4 * i + 2] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(t.z)));
+        qv[4 * i + 3] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(t.w)));
+    }
+}
+
+template <int NH, int P, bool BF>
+__device__ __forceinline__ void attn_unit(const KA& a, int u, int slot, int wq, Smem<NH>& sm, const float (&qv)[HS]) {
+    constexpr int C = LD<NH>::C;
+    constexpr int TILE = P * HS;
+    constexpr int K = BF ? 2 : 1;    // float4 chunks of the folded state per lane
+    constexpr int NL = 16 / K;       // lanes holding it
+    const int lane = threadIdx.x & 63;
+    const int S = a.S;
+    const int bh = u / S;
+    const int sr = u - bh * S;
+    const int b = bh / NH;
+    const int h = bh - b * NH;
+    const int ctx = a.pos[b] + 1;
+#ifdef HPA_PL_QREG
+    const float* qh = qv;
+#else
+    (void)qv;
+    const float* __restrict__ qh = a.q + (size_t)bh * HS;  // scalar loads beside the first page ids
+#endif
+    const int* bt = a.bt + (size_t)b * a.bt_stride;
+    const int n_all = (ctx + 63) >> 6;
+    const int it0 = (int)((long long)sr * n_all / S);
+    const int it1 = (int)((long long)(sr + 1) * n_all / S);
+    float m = a.m_init, l = 0.f;
+    float4 acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (BF) {
+        const unsigned short* base = reinterpret_cast<const unsigned short*>(a.kv);
+        hpa_attn::attn_tiles_bf16<P, 4>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, a.page_elems, bt,
+                                        a.bt_stride, ctx, it0, it1, a.qscale, m, l, acc, wq);
+#pragma unroll
+        for (int o = 8; o <= 32; o <<= 1)
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                acc[k].x += __shfl_xor(acc[k].x, o, 64);
+                acc[k].y += __shfl_xor(acc[k].y, o, 64);
+                acc[k].z += __shfl_xor(acc[k].z, o, 64);
+                acc[k].w += __shfl_xor(acc[k].w, o, 64);
+            }
+    } else {
+        const float* base = reinterpret_cast<const float*>(a.kv);
+        hpa_attn::attn_tiles<P, 4>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, a.page_elems, bt,
+                                   a.bt_stride, ctx, it0, it1, a.qscale, m, l, acc[0], wq);
+#pragma unroll
+        for (int o = 16; o <= 32; o <<= 1) {
+            acc[0].x += __shfl_xor(acc[0].x, o, 64);
+            acc[0].y += __shfl_xor(acc[0].y, o, 64);
+            acc[0].z += __shfl_xor(acc[0].z, o, 64);
+            acc[0].w += __shfl_xor(acc[0].w, o, 64);
+        }
+    }
+    l = hpa::wave_sum(l);
+    if (lane == 0) {
+        sm.s_m[slot][wq] = m;
+        sm.s_l[slot][wq] = l;
+    }
+    if (lane < NL)
+#pragma unroll
+        for (int k = 0; k < K; ++k) sm.s_acc[slot][(wq * NL + lane) * K + k] = acc[k];
+    int old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(&sm.s_cnt[slot], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old != 3 || lane >= NL) return;
+    // the last wave of the slot: the 4 waves' states in wave order (hpa_attn::attn_fold)
+    float M = sm.s_m[slot][0];
+#pragma unroll
+    for (int i = 1; i < 4; ++i) M = fmaxf(M, sm.s_m[slot][i]);
+    float L = 0.f;
+    float4 O[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) O[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float f = exp2f(sm.s_m[slot][i] - M);
+        L = fmaf(sm.s_l[slot][i], f, L);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const float4 v = sm.s_acc[slot][(i * NL + lane) * K + k];
+            O[k].x = fmaf(v.x, f, O[k].x);
+            O[k].y = fmaf(v.y, f, O[k].y);
+            O[k].z = fmaf(v.z, f, O[k].z);
+            O[k].w = fmaf(v.w, f, O[k].w);
+        }
+    }
+    m = M;
+    l = L;
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = O[k];
+    if (S > 1) {
+        int* tick = a.ctr + kCtrInts + 2 * a.R * LD<NH>::NCT + bh;  // zeroed per step: no rewind
+        if (!hpa_attn::split_merge<K>(a.rec + (size_t)bh * S * kRec, tick, S, sr, m, l, acc, false)) return;
+    }
+    const float inv = l == 0.f ? 0.f : 1.f / l;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {  // dims (16/NL)*lane + 4k .. +3 of head h, frag layout
+        const int col = h * HS + (64 / NL) * lane + 4 * k;
+        hpa::store_wt16(a.att, (int)(hpa::frag_index(b, col, C) * 4),
+                        make_float4(acc[k].x * inv, acc[k].y * inv, acc[k].z * inv, acc[k].w * inv));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this (the only storing) wave drained
+    if (lane == 0) arrive(a, CT_ATT, 1);
+}
+
+// ------------------------------------------------------------------ GEMM units
+// A unit is one 16x16 output tile (column tile j, row block rb) over a K range
+// of C (the whole K of qkv / attproj / fc, one of 4 parts of fcproj's 4C),
+// computed by one 4-wave slot exactly like gemm16_os_kernel<4, *, K16/4>:
+// wave wq takes k16 steps [wq*SW, wq*SW+SW), one accumulator chain in k
+// order, the 4 waves folded in wave order.  Phase X's units are numbered
+// v = (part*R + rb)*NJ + j and dealt v -> workgroup v % G, slot v / G: with
+// NJ and G multiples of 8 the row blocks and parts of one weight tile land on
+// one XCD (blocks b, b+8 share an XCD) and re-read it from that L2.
+// The slot's weight fragments are loaded into registers BEFORE the phase's
+// wait (prefetch across the seam); the barriers between phases wait for LDS
+// only (lds_barrier), so those loads stay in flight.
+
+// workgroup barrier that does not drain the vector-memory counter (the
+// prefetched weights stay in flight); LDS accesses before it are complete
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+struct Unit {
+    int j, rb, p;
+    bool has;
+};
+__device__ __forceinline__ Unit unit_of(int v, int n, int NJ, int R) {
+    Unit u;
+    u.has = v < n;
+    const int vv = u.has ? v : 0;
+    u.j = vv % NJ;
+    const int q = vv / NJ;
+    u.rb = q % R;
+    u.p = q / R;
+    return u;
+}
+
+// the wave's weight fragments of column tile j, k16 steps kb + wq*SW ..
+// (K16W steps per tile row); non-temporal where one row block reads the tile
+template <int SW>
+__device__ __forceinline__ void load_w(const float* W, int K16W, int j, int kb, int wq, bool nt, float4 (&wr)[SW]) {
+    const float4* wf = reinterpret_cast<const float4*>(W) + ((size_t)j * K16W + kb + wq * SW) * 64 + (threadIdx.x & 63);
+    if (nt) {
+#pragma unroll
+        for (int s = 0; s < SW; ++s) wr[s] = ld_nt(wf + s * 64);
+    } else {
+#pragma unroll
+        for (int s = 0; s < SW; ++s) wr[s] = wf[s * 64];
+    }
+}
+
+// the wave's A fragments (activation written in this launch: sc1 loads),
+// then the one-shot kernel's chain and (STATS) its LN row partial sums
+template <int SW, bool STATS>
+__device__ __forceinline__ f32x4 unit_mfma(const float* A, int K16A, int rb, int kb, int wq, const float4 (&wr)[SW],
+                                           float& fs1, float& fs2) {
+    float4 xv[SW];
+    const int off = ((rb * K16A + kb + wq * SW) * 64 + (int)(threadIdx.x & 63)) * 16;
+#pragma unroll
+    for (int s = 0; s < SW; ++s) xv[s] = hpa::load_wt16(A, off + s * 1024);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < SW; ++s) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s].x, wr[s].x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s].y, wr[s].y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s].z, wr[s].z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s].w, wr[s].w, acc, 0, 0, 0);
+    }
+    if (STATS)
+#pragma unroll
+        for (int s = 0; s < SW; ++s) hpa_gemm::row_sums_add(xv[s], fs1, fs2);
+    return acc;
+}
+
+__device__ __forceinline__ void put_red(float* red, int wv, f32x4 acc) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) red[wv * 256 + g * 64 + lane] = acc[g];
+}
+
+// element e = wq*64 + lane of the slot's tile, its 4 waves in wave order
+// (Epi<4,...>::finish): row 4*(lane>>4) + wq, column lane & 15
+__device__ __forceinline__ float fold4(const float* red, int slot, int e) {
+    const float* r = red + slot * 4 * 256 + e;
+    float v = r[0];
+    v += r[256];
+    v += r[512];
+    v += r[768];
+    return v;
+}
+
+// LayerNorm-folded value: rstd*(acc - mean*c1) + c2 (Epi::apply's order)
+__device__ __forceinline__ float ln_fold_val(const float* wsum, int slot, int lrow, int K, float val, float c1,
+                                             float c2) {
+    const float* ws = wsum + slot * 4 * 32;
+    float S1 = ws[2 * lrow], S2 = ws[2 * lrow + 1];
+#pragma unroll
+    for (int ww = 1; ww < 4; ++ww) {
+        S1 += ws[ww * 32 + 2 * lrow];
+        S2 += ws[ww * 32 + 2 * lrow + 1];
+    }
+    const float m = S1 / K;
+    const float rstd = 1.0f / sqrtf(fmaxf(S2 / K - m * m, 0.f) + 1e-5f);
+    val = rstd * (val - m * c1);
+    val += c2;
+    return val;
+}
+
+// slots of workgroup bid that hold one of n units
+__device__ __forceinline__ int slots_with(int bid, int G, int n) {
+    return (bid < n) + (bid + G < n) + (bid + 2 * G < n);
+}
+
+// every storing wave drained, then one lane counts the slots that stored
+__device__ __forceinline__ void publish(const KA& a, int which, int nslots) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    if (threadIdx.x == 0 && nslots) arrive(a, which, nslots);
+}
+
+// ------------------------------------------------------------------ the kernel
+template <int NH, int P, bool BF>
+__global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
+    using D = LD<NH>;
+    constexpr int C = D::C, SW = D::SW, NCT = D::NCT;
+    // fields read where used from the kernarg segment (not all hoisted into
+    // SGPRs at entry: the attention keeps q in 64 SGPRs)
+    const KA& a = *(const KA*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
+    (void)args;
+    __shared__ Smem<NH> sm;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int slot = wv >> 2, wq = wv & 3;
+    const int lane = threadIdx.x & 63;
+    const int bid = blockIdx.x;
+    const int R = a.R, G = a.G;
+    const int v = bid + slot * G;          // this slot's unit index in every phase
+    const int e = wq * 64 + lane;           // the tile element this thread finishes
+    const int lrow = 4 * (lane >> 4) + wq, lcol = lane & 15;
+    const bool nt = R == 1;                 // one row block: every weight tile read once
+    PL_STAMP(t_start);
+    if (threadIdx.x < 3) sm.s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+
+    // A: attention, one unit (sequence, head, context range) per slot
+    {
+        const bool has = v < a.B * NH * a.S;
+        float qv[HS];
+#ifdef HPA_PL_QREG
+        if (has) load_q<NH>(a, v, qv);
+#endif
+        PL_STAMP(t_issued);
+        if (has) attn_unit<NH, P, BF>(a, v, slot, wq, sm, qv);
+        PL_MARK(2);
+        PL_STORE(0, t_start);
+        PL_STORE(1, t_issued);
+    }
+    float4 wr[SW];
+    float fs1, fs2;
+    // B: attproj(l): res2 = res + att . Wap^T + b
+    {
+        const Unit u = unit_of(v, NCT * R, NCT, R);
+        if (u.has) load_w<SW>(a.w_ap, D::K16, u.j, 0, wq, nt, wr);
+        lds_barrier();
+        PL_MARK(3);
+        if (!wait_ctr<NH>(a, CT_ATT, a.B * NH, 1, sm)) return;
+        PL_MARK(4);
+        const int row = u.rb * 16 + lrow, col = u.j * 16 + lcol;
+        const int fi = (int)(hpa::frag_index(row, col, C) * 4);
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        float bv = 0.f, rv = 0.f;
+        if (u.has) {
+            bv = a.b_ap[col];
+            rv = hpa::load_wt4(a.res, fi);
+            acc = unit_mfma<SW, false>(a.att, D::K16, u.rb, 0, wq, wr, fs1, fs2);
+        }
+        put_red(sm.red, wv, acc);
+        lds_barrier();
+        if (u.has) {
+            float val = fold4(sm.red, slot, e);
+            val += bv;
+            val = row < a.B ? rv + val : 0.f;  // residual_forward(out, res, proj)
+            hpa::store_wt4(a.res2, fi, val);
+        }
+        publish(a, CT_X1, slots_with(bid, G, NCT * R));
+    }
+    PL_MARK(5);
+    // C: fc(l): fch = gelu(LN2(res2) . Wfc^T + b), LN folded
+    {
+        const Unit u = unit_of(v, 4 * NCT * R, 4 * NCT, R);
+        if (u.has) load_w<SW>(a.w_fc, D::K16, u.j, 0, wq, nt, wr);
+        if (!wait_ctr<NH>(a, CT_X1, NCT * R, 2, sm)) return;
+        PL_MARK(6);
+        const int row = u.rb * 16 + lrow, col = u.j * 16 + lcol;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        float c1 = 0.f, c2 = 0.f;
+        fs1 = fs2 = 0.f;
+        if (u.has) {
+            c1 = a.fc_c1[col];
+            c2 = a.fc_c2[col];
+            acc = unit_mfma<SW, true>(a.res2, D::K16, u.rb, 0, wq, wr, fs1, fs2);
+        }
+        hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + wv * 32);
+        put_red(sm.red, wv, acc);
+        lds_barrier();
+        if (u.has) {
+            float val = fold4(sm.red, slot, e);
+            val = ln_fold_val(sm.wsum, slot, lrow, C, val, c1, c2);
+            hpa::store_wt4(a.fch, (int)(hpa::frag_index(row, col, 4 * C) * 4), row < a.B ? hpa::gelu_ref(val) : 0.f);
+        }
+        publish(a, CT_H, slots_with(bid, G, 4 * NCT * R));
+        PL_MARK(7);
+    }
+    // D: fcproj(l), K part p of 4: partial tiles -> slab; the last part of
+    // (rb, j) adds the parts in order + bias + res2 -> res
+    {
+        const Unit u = unit_of(v, NCT * R * D::FP, NCT, R);
+        if (u.has) load_w<SW>(a.w_fp, 4 * D::K16, u.j, u.p * D::K16, wq, nt, wr);
+        if (!wait_ctr<NH>(a, CT_H, 4 * NCT * R, 3, sm)) return;
+        PL_MARK(8);
+        const int row = u.rb * 16 + lrow, col = u.j * 16 + lcol;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        if (u.has) acc = unit_mfma<SW, false>(a.fch, 4 * D::K16, u.rb, u.p * D::K16, wq, wr, fs1, fs2);
+        put_red(sm.red, wv, acc);
+        lds_barrier();
+        float val = 0.f;
+        const int sofs = ((u.p * R + u.rb) * NCT + u.j) * 256 + e;
+        if (u.has) {
+            val = fold4(sm.red, slot, e);
+            hpa::store_wt4(a.slab_fp, sofs * 4, val);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        if (u.has && wq == 0 && lane == 0) {
+            const int t = __hip_atomic_fetch_add(a.ctr + kCtrInts + R * NCT + u.rb * NCT + u.j, 1, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            sm.s_last[slot] = t == D::FP - 1;
+        }
+        lds_barrier();
+        const bool last = u.has && sm.s_last[slot] != 0;
+        if (last) {
+            float pv[D::FP];
+#pragma unroll
+            for (int q = 0; q < D::FP; ++q)
+                pv[q] = q == u.p ? val : hpa::load_wt4(a.slab_fp, (((q * R + u.rb) * NCT + u.j) * 256 + e) * 4);
+            const int fi = (int)(hpa::frag_index(row, col, C) * 4);
+            const float rv = hpa::load_wt4(a.res2, fi);
+            float tot = pv[0];
+#pragma unroll
+            for (int q = 1; q < D::FP; ++q) tot += pv[q];
+            tot += a.b_fp[col];
+            tot = row < a.B ? rv + tot : 0.f;
+            hpa::store_wt4(a.res, fi, tot);
+            if (a.stats_out) sm.tile[(slot * 16 + lrow) * 17 + lcol] = tot;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        if (a.stats_out && wq == 0 && lane < 16 && last) {  // 16-column LNf partial sums of the tile's rows
+            const float* tr = sm.tile + (slot * 16 + lane) * 17;
+            float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+                s1 += tr[c];
+                s2 += tr[c] * tr[c];
+            }
+            const int r = u.rb * 16 + lane;
+            a.stats_out[((size_t)u.j * a.Mp + r) * 2] = s1;
+            a.stats_out[((size_t)u.j * a.Mp + r) * 2 + 1] = s2;
+        }
+        if (threadIdx.x == 0) {
+            int nd = 0;
+            for (int s2 = 0; s2 < 3; ++s2) nd += sm.s_last[s2] != 0 && bid + s2 * G < NCT * R * D::FP;
+            if (nd) arrive(a, CT_X2, nd);
+        }
+        PL_MARK(9);
+    }
+    // E: qkv(l+1): LN1 folded, q + K/V appended into layer l+1's pages
+    if (!a.last) {
+        const Unit u = unit_of(v, 3 * NCT * R, 3 * NCT, R);
+        if (u.has) load_w<SW>(a.w_qkv, D::K16, u.j, 0, wq, nt, wr);
+        if (!wait_ctr<NH>(a, CT_X2, NCT * R, 4, sm)) return;
+        PL_MARK(10);
+        const int row = u.rb * 16 + lrow, col = u.j * 16 + lcol;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        float c1 = 0.f, c2 = 0.f;
+        fs1 = fs2 = 0.f;
+        if (u.has) {
+            c1 = a.qkv_c1[col];
+            c2 = a.qkv_c2[col];
+            acc = unit_mfma<SW, true>(a.res, D::K16, u.rb, 0, wq, wr, fs1, fs2);
+        }
+        hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + wv * 32);
+        put_red(sm.red, wv, acc);
+        lds_barrier();
+        if (u.has && row < a.B) {
+            float val = fold4(sm.red, slot, e);
+            val = ln_fold_val(sm.wsum, slot, lrow, C, val, c1, c2);
+            if (col < C) {
+                a.q_out[(size_t)row * C + col] = val;
+            } else {  // K/V of this token into the sequence's page of layer l+1 (add_to_cache)
+                const int kv = col >= 2 * C;
+                const int c = col - (kv ? 2 * C : C);
+                const int hh = c >> 6, d = c & 63;
+                const int ps = a.pos[row];
+                const int page = a.bt[(size_t)row * a.bt_stride + ps / P];
+                if (page >= 0) {
+                    const int pslot = ps % P;
+                    const size_t toff = (size_t)page * a.page_elems + ((size_t)kv * NH + hh) * P * 64;
+                    if constexpr (BF) {
+                        unsigned short* kvt = reinterpret_cast<unsigned short*>(a.kv_next) + toff;
+                        kvt[kv == 0 ? ((d >> 3) * P + pslot) * 8 + (d & 7) : pslot * 64 + d] = hpa::f32_to_bf16(val);
+                    } else {
+                        float* kvt = reinterpret_cast<float*>(a.kv_next) + toff;
+                        if (kv == 0)
+                            kvt[((d >> 2) * P + pslot) * 4 + (d & 3)] = val;
+                        else
+                            kvt[pslot * 64 + d] = val;
+                    }
+                }
+            }
+        }
+    }
+    PL_MARK(11);
+}
+
+int g_ncu = 0;
+
+int num_cus() {
+    if (!g_ncu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return 0;
+        hipDeviceProp_t pr;
+        if (hipGetDeviceProperties(&pr, dev) != hipSuccess) return 0;
+        g_ncu = pr.multiProcessorCount;
+    }
+    return g_ncu;
+}
+
+template <int NH>
+bool shape_ok(int B, int S, int G) {
+    // one unit per slot in every phase: attention B*NH*S, fc and fcproj
+    // 4*(C/16)*R units; grid and unit numbering assume G % 8 == 0
+    const int R = (B + 15) / 16;
+    return B >= 1 && B <= 64 && S >= 1 && S <= HPA_ATTN_MAX_SPLITS && G % 8 == 0 && (long)B * NH * S <= 3L * G &&
+           4L * LD<NH>::NCT * R <= 3L * G;
+}
+
+template <int NH, int P, bool BF>
+int launch(const HpaLayerArgs* h, int G) {
+    static int resident = -1;  // blocks per CU of this instantiation (occupancy API)
+    if (resident < 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, decode_layer_kernel<NH, P, BF>, 768, 0) != hipSuccess)
+            nb = 0;
+        resident = nb;
+    }
+    HPA_REQUIRE(resident >= 1, "decode layer: the persistent workgroup does not fit a CU");
+    const HpaKVPool* pool = h->pool;
+    KA a;
+    a.B = h->B;
+    a.Mp = (h->B + 15) / 16 * 16;
+    a.R = a.Mp / 16;
+    a.S = h->splits;
+    a.G = G;
+    a.last = h->last;
+    a.layer = h->layer;
+    a.q = h->q;
+    a.kv = (const char*)pool->base + (size_t)h->layer * pool->layer_elems * pool->elem_bytes;
+    a.kv_next = h->last ? nullptr : (char*)pool->base + (size_t)(h->layer + 1) * pool->layer_elems * pool->elem_bytes;
+    a.page_elems = pool->page_elems;
+    a.bt = h->block_table;
+    a.bt_stride = h->bt_stride;
+    a.pos = h->pos;
+    const float log2e = 1.4426950408889634f;
+    a.qscale = (float)(1.0 / sqrt((double)HS)) * log2e;
+    a.m_init = -10000.0f * log2e;
+    a.att = h->att;
+    a.res = h->res;
+    a.res2 = h->res2;
+    a.fch = h->fch;
+    a.w_ap = h->w_ap;
+    a.b_ap = h->b_ap;
+    a.w_fc = h->w_fc;
+    a.fc_c1 = h->fc_c1;
+    a.fc_c2 = h->fc_c2;
+    a.w_fp = h->w_fp;
+    a.b_fp = h->b_fp;
+    a.w_qkv = h->w_qkv;
+    a.qkv_c1 = h->qkv_c1;
+    a.qkv_c2 = h->qkv_c2;
+    a.q_out = h->q_out;
+    a.stats_out = h->stats_out;
+    a.rec = h->rec;
+    a.slab_fp = h->slab;
+    a.ctr = h->counters;
+    a.err = h->err;
+    decode_layer_kernel<NH, P, BF><<<G, 768, 0, hpa_stream()>>>(a);
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int NH>
+int dispatch(const HpaLayerArgs* h, int G) {
+    const bool bf = h->pool->dtype == HPA_BF16;
+    switch (h->pool->page_size) {
+        case 8: return bf ? launch<NH, 8, true>(h, G) : launch<NH, 8, false>(h, G);
+        case 16: return bf ? launch<NH, 16, true>(h, G) : launch<NH, 16, false>(h, G);
+        case 32: return bf ? launch<NH, 32, true>(h, G) : launch<NH, 32, false>(h, G);
+        case 64: return bf ? launch<NH, 64, true>(h, G) : launch<NH, 64, false>(h, G);
+        default: return hpa_fail(__FILE__, __LINE__, "decode layer: page size must be 8, 16, 32 or 64");
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int hpa_decode_layer_eligible(int B, int C, int num_heads, int splits) {
+    const int G = num_cus();
+    if (G <= 0 || C != 64 * num_heads) return 0;
+    if (num_heads == 12) return shape_ok<12>(B, splits, G) ? 1 : 0;
+    if (num_heads == 2) return shape_ok<2>(B, splits, G) ? 1 : 0;
+    return 0;
+}
+
+// the split count measured best for the stand-alone attention
+// (hpa_attn_pick_splits: a range of >= 4 tiles per 4-wave unit; short ranges
+// pay the merge), halved until every unit has a slot (B*NH*S <= 3 x CUs)
+int hpa_decode_layer_pick_splits(int B, int num_heads, int max_ctx) {
+    const int G = num_cus();
+    if (G <= 0 || B <= 0 || num_heads <= 0) return 1;
+    int s = hpa_attn_pick_splits(B, num_heads, max_ctx, G);
+    while (s > 1 && (long)B * num_heads * s > 3L * G) s /= 2;
+    return s;
+}
+
+int hpa_decode_layer_sizes(int B, int C, int num_heads, int splits, size_t* out3) {
+    HPA_REQUIRE(out3 && B > 0 && C == 64 * num_heads && splits >= 1, "decode layer sizes: bad arguments");
+    const int R = (B + 15) / 16, nct = C / 16;
+    out3[0] = (size_t)B * num_heads * splits * kRec;
+    out3[1] = (size_t)4 * R * nct * 256;  // fcproj K-part partial tiles
+    const size_t ints = (size_t)kCtrInts + 2 * (size_t)R * nct + (size_t)B * num_heads;
+    out3[2] = (ints + 31) / 32 * 32;  // whole 128-B lines (memset in multiples of 16 B)
+    return 0;
+}
+
+// trace build only: copy the per-(layer, workgroup) event stamps of the last
+// launches ([layers][256][16] u64, s_memrealtime ticks of 10 ns); host NULL
+// clears them.  Returns 1 in the product build.
+int hpa_decode_layer_trace(unsigned long long* host, int layers) {
+#ifdef HPA_LAYER_TRACE
+    HPA_REQUIRE(layers >= 0 && layers <= 64, "trace: layers 0..64");
+    if (!host) {
+        static unsigned long long zero[64 * 256 * 16];
+        HPA_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_pl_trace), zero, sizeof(zero)));
+        return 0;
+    }
+    HPA_CHECK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pl_trace), (size_t)layers * 256 * 16 * 8));
+    return 0;
+#else
+    (void)host;
+    (void)layers;
+    return 1;
+#endif
+}
+
+int hpa_decode_layer(const HpaLayerArgs* h) {
+    HPA_REQUIRE(h && h->pool && h->pool->base, "decode layer: pool");
+    const HpaKVPool* pool = h->pool;
+    HPA_REQUIRE(pool->dtype == HPA_F32 || pool->dtype == HPA_BF16, "decode layer: fp32 or bf16 pool");
+    HPA_REQUIRE(pool->head_size == HS && h->C == h->num_heads * HS, "decode layer: head size 64");
+    HPA_REQUIRE(h->layer >= 0 && h->layer < pool->num_layers && (h->last || h->layer + 1 < pool->num_layers),
+                "decode layer: layer out of range");
+    HPA_REQUIRE(h->q && h->att && h->res && h->res2 && h->fch && h->w_ap && h->b_ap && h->w_fc && h->fc_c1 &&
+                    h->fc_c2 && h->w_fp && h->b_fp && h->block_table && h->pos && h->rec && h->slab &&
+                    h->counters && h->err,
+                "decode layer: null operand");
+    HPA_REQUIRE(h->last || (h->w_qkv && h->qkv_c1 && h->qkv_c2 && h->q_out), "decode layer: qkv(l+1) operands");
+    HPA_REQUIRE(h->splits >= 1 && h->splits <= HPA_ATTN_MAX_SPLITS, "decode layer: splits 1..16");
+    const int G = num_cus();
+    HPA_REQUIRE(hpa_decode_layer_eligible(h->B, h->C, h->num_heads, h->splits), "decode layer: shape not supported");
+    if (h->num_heads == 12) return dispatch<12>(h, G);
+    return dispatch<2>(h, G);
+}
+
+}  // extern "C"

@@ -17,6 +17,8 @@ int hpa_fail(const char* file, int line, const char* what) {
     return 1;
 }
 
+constexpr int kMaxDevices = 64;
+hipStream_t g_dev_streams[kMaxDevices];
 hipStream_t hpa_stream() { return g_stream; }
 
 extern "C" {
@@ -34,12 +36,16 @@ int hpa_init(int device) {
     HPA_CHECK(hipGetDeviceCount(&n));
     HPA_REQUIRE(n > 0, "no HIP device visible");
     HPA_REQUIRE(device >= 0 && device < n, "device index out of range");
+    HPA_REQUIRE(device < kMaxDevices, "device index beyond the library's table");
     HPA_CHECK(hipSetDevice(device));
-    if (g_device != device || !g_default_stream) {
-        HPA_CHECK(hipStreamCreateWithFlags(&g_default_stream, hipStreamNonBlocking));
-        g_device = device;
-    }
-    if (!g_stream) g_stream = g_default_stream;
+    // one default stream per device (the single-process multi-GPU form,
+    // hpa_comm_use, switches devices); a current stream that was the old
+    // device's default follows the switch
+    if (!g_dev_streams[device]) HPA_CHECK(hipStreamCreateWithFlags(&g_dev_streams[device], hipStreamNonBlocking));
+    const bool follow = !g_stream || g_stream == g_default_stream;
+    g_default_stream = g_dev_streams[device];
+    g_device = device;
+    if (follow) g_stream = g_default_stream;
     return 0;
 }
 

@@ -648,6 +648,14 @@ struct GPT2Decode {
     double prof_ms;
     long prof_launches;
     DecShard* shard;
+    /* persistent layer (hpa_decode_layer): one launch per layer */
+    int pl_want;      /* gpt2_decode_set_layer_kernel */
+    int pl_on;        /* in use: wanted and eligible */
+    int pl_splits;
+    float* pl_rec;
+    float* pl_slab;
+    int* pl_ctr;      /* [L][pl_ctr_ints], zeroed at the start of every step */
+    size_t pl_ctr_ints;
     /* gpt2_forward: token at every cached position [B][max_ctx] and, when it
      * fits, the logits of every position [B][max_ctx][V] (managed) */
     int* h_hist;
@@ -751,6 +759,7 @@ static void dec_free(GPT2Decode* d) {
     hpa_free(d->d_wpack);
     hpa_free(d->d_fold);
     hpa_free(d->d_attn_ws);
+    hpa_free(d->pl_rec); hpa_free(d->pl_slab); hpa_free(d->pl_ctr);
     hpa_free(d->d_rng);
     hpa_free(d->pos_logits);
     hpa_host_free(d->h_next);
@@ -849,6 +858,85 @@ static int dec_set_splits(GPT2Decode* d, int splits) {
     return 0;
 }
 
+static const float* wpack_at(const GPT2Decode* d, size_t off);
+
+/* the persistent layer's workspace, where it applies (fp32 LN-folded weights,
+ * the shapes hpa_decode_layer_eligible accepts) */
+static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
+    const GPT2Config c = model->config;
+    d->pl_on = 0;
+    if (!d->pl_want || d->w_bf16 || !d->d_fold) return 0;
+    /* auto (1): where it measured faster than five launches per layer --
+     * B <= 32 (profiles/r3/pl_ab.txt: B 8/16/32 -1.7/-2.3/-0.4 %, B 48/64
+     * +1.2/0 %); 2 forces it at any eligible batch */
+    if (d->pl_want == 1 && d->B > 32) return 0;
+    int splits = hpa_decode_layer_pick_splits(d->B, c.num_heads, d->max_ctx);
+    const char* env = getenv("HPA_LAYER_SPLITS");
+    if (env && atoi(env) > 0) splits = atoi(env);
+    if (!hpa_decode_layer_eligible(d->B, c.channels, c.num_heads, splits)) return 0;
+    size_t sz[3];
+    if (hpa_decode_layer_sizes(d->B, c.channels, c.num_heads, splits, sz)) return 1;
+    if (!d->pl_rec || d->pl_splits != splits) { /* records depend on the split count */
+        hpa_free(d->pl_rec);
+        d->pl_rec = (float*)hpa_malloc(sz[0] * sizeof(float));
+    }
+    if (!d->pl_slab) d->pl_slab = (float*)hpa_malloc(sz[1] * sizeof(float));
+    if (!d->pl_ctr) {
+        d->pl_ctr_ints = sz[2];
+        d->pl_ctr = (int*)hpa_malloc((size_t)c.num_layers * sz[2] * sizeof(int));
+    }
+    if (!d->pl_rec || !d->pl_slab || !d->pl_ctr) return 1;
+    d->pl_splits = splits;
+    d->pl_on = 1;
+    return 0;
+}
+
+/* layer l of the persistent path: attention(l) .. fcproj(l), qkv(l+1) */
+static int dec_layer(GPT2* model, int l) {
+    GPT2Decode* d = model->decode;
+    const GPT2Config c = model->config;
+    const int C = c.channels, L = c.num_layers;
+    const ParameterTensors* w = &model->params;
+    const size_t lc = (size_t)l * C;
+    const size_t e_layer = d->wpack_off[3] + hpa_frag_elems(C, 4 * C);
+    HpaLayerArgs a;
+    memset(&a, 0, sizeof(a));
+    a.B = d->B;
+    a.C = C;
+    a.num_heads = c.num_heads;
+    a.splits = d->pl_splits;
+    a.last = l + 1 == L;
+    a.pool = &d->pool;
+    a.layer = l;
+    a.block_table = d->d_bt;
+    a.bt_stride = d->bt_stride;
+    a.pos = d->d_pos;
+    a.q = d->d_q;
+    a.att = d->att;
+    a.res = d->res;
+    a.res2 = d->res2;
+    a.fch = d->fch;
+    a.w_ap = wpack_at(d, e_layer * l + d->wpack_off[1]);
+    a.b_ap = w->attprojb + lc;
+    a.w_fc = wpack_at(d, e_layer * l + d->wpack_off[2]);
+    a.fc_c1 = d->d_fold + 14 * lc + 6 * C;
+    a.fc_c2 = a.fc_c1 + 4 * C;
+    a.w_fp = wpack_at(d, e_layer * l + d->wpack_off[3]);
+    a.b_fp = w->fcprojb + lc;
+    if (!a.last) {
+        a.w_qkv = wpack_at(d, e_layer * (l + 1) + d->wpack_off[0]);
+        a.qkv_c1 = d->d_fold + 14 * (lc + C);
+        a.qkv_c2 = a.qkv_c1 + 3 * C;
+        a.q_out = d->d_q; /* every read of q(l) is done before the first qkv(l+1) store */
+    }
+    a.stats_out = a.last ? d->st1 : NULL; /* LNf statistics for the logits */
+    a.rec = d->pl_rec;
+    a.slab = d->pl_slab;
+    a.counters = d->pl_ctr + (size_t)l * d->pl_ctr_ints;
+    a.err = d->d_next + d->B;
+    return hpa_decode_layer(&a);
+}
+
 int gpt2_decode_init(GPT2* model, int B, int page_size, int max_ctx) {
     return gpt2_decode_init_ex(model, B, page_size, max_ctx, HPA_F32);
 }
@@ -937,10 +1025,10 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
     d->d_bt = (int*)hpa_malloc(btn * sizeof(int));
     d->d_pos = (int*)hpa_malloc(B * sizeof(int));
     d->d_tokens = (int*)hpa_malloc(B * sizeof(int));
-    d->d_next = (int*)hpa_malloc(B * sizeof(int));
+    d->d_next = (int*)hpa_malloc((B + 1) * sizeof(int)); /* [B]: persistent-layer error word */
     d->h_pos = (int*)calloc(B, sizeof(int));
     d->h_evicted = (char*)calloc(B, 1);
-    d->h_next = (int*)hpa_host_alloc(B * sizeof(int));
+    d->h_next = (int*)hpa_host_alloc((B + 1) * sizeof(int));
     d->d_q = (float*)hpa_malloc((size_t)B * C * 4);
     d->d_logits = (float*)hpa_malloc((size_t)B * V * 4);
     d->res = (float*)hpa_malloc(Mp * C * 4);
@@ -985,8 +1073,17 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
         dec_free(d);
         return 1;
     }
+    {
+        const char* env = getenv("HPA_LAYER_KERNEL");
+        d->pl_want = env && (env[0] == '0' || env[0] == '2') ? env[0] - '0' : 1;
+    }
+    if (dec_layer_setup(model, d)) {
+        dec_free(d);
+        return 1;
+    }
     for (size_t i = 0; i < btn; i++) d->h_bt[0][i] = -1;
     if (hpa_memcpy(d->d_bt, d->h_bt[0], btn * sizeof(int)) || hpa_memset_async(d->d_pos, 0, B * sizeof(int)) ||
+        hpa_memset_async(d->d_next, 0, (B + 1) * sizeof(int)) ||
         hpa_memset_async(d->d_tokens, 0, B * sizeof(int)) || hpa_synchronize()) {
         dec_free(d);
         return 1;
@@ -1172,6 +1269,14 @@ static int dec_launch(GPT2* model) {
     const ParameterTensors* w = &model->params;
     const int L = model->config.num_layers;
     int rc = hpa_embed_frag(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, model->config.channels);
+    if (d->pl_on && !d->profiling) { /* qkv(0), then one persistent launch per layer */
+        rc |= dec_gemm(model, 0, G_QKV);
+        rc |= hpa_memset_async(d->pl_ctr, 0, (size_t)L * d->pl_ctr_ints * sizeof(int));
+        for (int l = 0; l < L && !rc; l++) rc |= dec_layer(model, l);
+        rc |= dec_gemm(model, 0, G_LOGITS);
+        rc |= dec_pick(model, NULL);
+        return rc;
+    }
     for (int l = 0; l < L && !rc; l++) {
         rc |= dec_gemm(model, l, G_QKV);
         rc |= dec_attention(model, l);
@@ -1470,11 +1575,42 @@ int gpt2_decode_step(GPT2* model, const int* tokens, int* next_tokens) {
     if (dec_enqueue(model, tokens)) return 1;
     GPT2Decode* d = model->decode;
     if (next_tokens) {
-        if (hpa_memcpy_async(d->h_next, d->d_next, d->B * sizeof(int)) || hpa_synchronize()) return 1;
+        if (hpa_memcpy_async(d->h_next, d->d_next, (d->B + 1) * sizeof(int)) || hpa_synchronize()) return 1;
+        if (d->h_next[d->B]) return gpt2_decode_status(model) ? 1 : 1;
         memcpy(next_tokens, d->h_next, d->B * sizeof(int));
     }
     return 0;
 }
+
+int gpt2_decode_status(GPT2* model) {
+    GPT2Decode* d = model->decode;
+    if (!d) return -1;
+    if (hpa_memcpy_async(d->h_next, d->d_next, (d->B + 1) * sizeof(int)) || hpa_synchronize()) return -1;
+    const int code = d->h_next[d->B];
+    if (code) {
+        static const char* what[] = {"", "attention", "attproj", "fc", "fcproj"};
+        fprintf(stderr, "[paged_infer] persistent layer: in-launch wait for %s timed out (code %d); step invalid\n",
+                code >= 1 && code <= 4 ? what[code] : "?", code);
+        const int zero = 0;
+        if (hpa_memcpy(d->d_next + d->B, &zero, sizeof(int))) return -1;
+    }
+    return code;
+}
+
+int gpt2_decode_set_layer_kernel(GPT2* model, int enable) {
+    GPT2Decode* d = model->decode;
+    if (!d) return 1;
+    if (hpa_synchronize()) return 1;
+    d->pl_want = enable < 0 ? 0 : enable > 2 ? 2 : enable;
+    if (dec_layer_setup(model, d)) return 1;
+    if (d->graph) { /* recapture with the other step */
+        hpa_graph_destroy(d->graph);
+        d->graph = NULL;
+    }
+    return 0;
+}
+
+int gpt2_decode_layer_kernel(GPT2* model) { return model->decode ? model->decode->pl_on : 0; }
 
 /* sequences the LRU policy paged out since the last call (their position
  * restarted at 0: the caller must prefill them again); mask (nullable, [B])

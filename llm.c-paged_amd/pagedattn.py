@@ -168,6 +168,11 @@ def lib():
     _sig(L, "hpa_comm_size", i, [])
     _sig(L, "hpa_comm_rank", i, [])
     _sig(L, "hpa_comm_gatherv", i, [v, sz, v, ctypes.POINTER(sz), i, v])
+    _sig(L, "hpa_comm_gather_layout", i, [i, i, i, ctypes.POINTER(sz), ctypes.POINTER(sz), ctypes.POINTER(sz)])
+    _sig(L, "hpa_comm_barrier", i, [])
+    _sig(L, "hpa_comm_allreduce_max", i, [ctypes.POINTER(ctypes.c_double)])
+    _sig(L, "hpa_comm_init_all", i, [i, ctypes.POINTER(i)])
+    _sig(L, "hpa_comm_use", i, [i])
     _sig(L, "hpa_ref_attention_paged", i, [v, v, v, v, v, v, i, i, i, i, i, i])
     _sig(L, "hpa_ref_matmul", i, [v, v, v, v, i, i, i, i, i])
     # block manager (block_manager.c API)
@@ -225,6 +230,12 @@ def lib():
     _sig(L, "gpt2_decode_free", None, [v])
     _sig(L, "gpt2_decode_set_attn_splits", i, [v, i])
     _sig(L, "gpt2_decode_attn_splits", i, [v])
+    _sig(L, "gpt2_decode_set_layer_kernel", i, [v, i])
+    _sig(L, "gpt2_decode_layer_kernel", i, [v])
+    _sig(L, "gpt2_decode_status", i, [v])
+    _sig(L, "hpa_decode_layer_eligible", i, [i, i, i, i])
+    _sig(L, "hpa_decode_layer_pick_splits", i, [i, i, i])
+    _sig(L, "hpa_decode_layer_trace", i, [v, i])
     _sig(L, "gpt2_decode_evicted", i, [v, _I])
     _sig(L, "gpt2_decode_read_kv", i, [v, i, i, i, _F, _F])
     _sig(L, "gpt2_decode_batch", i, [v])
@@ -570,6 +581,22 @@ class Model:
 
     def attn_splits(self):
         return lib().gpt2_decode_attn_splits(self.h)
+
+    def set_layer_kernel(self, on):
+        """one persistent launch per layer (1: where it measured faster, B <= 32;
+        2: wherever it applies, B <= 64) or five (0); returns whether the
+        persistent layer is now in use"""
+        check(lib().gpt2_decode_set_layer_kernel(self.h, int(on)), "set_layer_kernel")
+        return bool(lib().gpt2_decode_layer_kernel(self.h))
+
+    def layer_kernel(self):
+        return bool(lib().gpt2_decode_layer_kernel(self.h))
+
+    def status(self):
+        """waits for queued work; raises if a persistent-layer wait timed out"""
+        code = lib().gpt2_decode_status(self.h)
+        if code:
+            raise RuntimeError(f"decode step failed (status {code})")
 
     def evicted(self):
         """sequences the LRU policy paged out since the last call (bool mask)"""

@@ -1,0 +1,176 @@
+"""The persistent decode layer (hpa_layer.hip: attention -> attproj -> fc ->
+fcproj -> next qkv as one launch per layer) against the five-launch layer and
+the oracle.
+
+* Decode parity vs the oracle runs through every test of test_gpu_decode.py /
+  test_gpu_configs.py, where the persistent layer is the engine's default for
+  B <= 64; here the two engine paths are compared directly at GPT-2 124M
+  shapes with ~1000-token contexts (the bench's regime), at batches 64, 32,
+  16 and 8 (split counts 1, 2, 4, 8), fp32 and bf16 pools.
+* Tolerance: the qkv and fc rows are bit-identical to the launch path by
+  construction (same per-row summation order); attproj / fcproj are summed
+  over K parts here (4 partial tiles added in part order) instead of 4 or 8
+  waves, so logits differ by fp32 reassociation only: <= 2e-5 max-abs.
+* Rows never depend on the batch: engines of B = 6 and of its two halves give
+  bit-identical logits at the same split count (the sharded-decode property).
+* Every step reports status 0 (no in-launch wait timed out).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as oc
+import synth
+
+pytestmark = pytest.mark.gpu
+
+SMALL = dict(maxT=256, V=1000, L=2, NH=2, C=128)
+GPT2_124M = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
+
+
+def _model(hip, cfgd, params, B, P, layer, kv_dtype=0, splits_env=None):
+    if splits_env is not None:
+        os.environ["HPA_LAYER_SPLITS"] = str(splits_env)
+    try:
+        m = hip.Model(cfgd, params=params)
+        m.decode_init(B, P, cfgd["maxT"], kv_dtype=kv_dtype)
+    finally:
+        os.environ.pop("HPA_LAYER_SPLITS", None)
+    assert m.set_layer_kernel(2 if layer else 0) == bool(layer)  # 2: at every batch it supports
+    m.set_graph(True)
+    return m
+
+
+@pytest.mark.parametrize("B", [64, 32, 16, 8])
+def test_persistent_layer_matches_launch_path_124m(hip, B):
+    params = synth.params(GPT2_124M, seed=31)
+    ctx = 990
+    rng = np.random.default_rng(B)
+    toks = rng.integers(0, GPT2_124M["V"], (6, B)).astype(np.int32)
+    out = []
+    for layer in (1, 0):
+        m = _model(hip, GPT2_124M, params, B, 16, layer)
+        hip.check(hip.lib().gpt2_decode_fill_random(m.h, ctx, 5), "fill_random")
+        lg, ids = [], []
+        for t in range(toks.shape[0]):
+            ids.append(m.step(toks[t]))
+            lg.append(m.logits())
+        m.status()
+        assert np.array_equal(m.positions(), np.full(B, ctx + toks.shape[0], np.int32))
+        m.close()
+        out.append((np.stack(lg), np.stack(ids)))
+    (lp, ip), (ll, il) = out
+    diff = float(np.abs(lp - ll).max())
+    s = np.sort(ll, axis=-1)
+    margin = s[..., -1] - s[..., -2]
+    clear = margin > 4 * diff
+    print(f"B={B}: max |logit diff| persistent vs launches {diff:.3e}; near-ties {int((~clear).sum())}")
+    assert diff <= 2e-5, diff
+    assert np.array_equal(ip[clear], il[clear])
+
+
+@pytest.mark.parametrize("P", [8, 16, 32, 64])
+def test_persistent_layer_small_model_matches_oracle(hip, P):
+    """greedy decode across page boundaries and many 64-token attention tiles"""
+    params = synth.params(SMALL, seed=40 + P)
+    B, steps = 5, 150
+    m = _model(hip, SMALL, params, B, P, 1)
+    c = oc.cfg(SMALL["maxT"], SMALL["V"], SMALL["L"], SMALL["NH"], SMALL["C"])
+    orc = oc.PagedDecoder(params, c, B, P, SMALL["maxT"], page_seed=P)
+    tok = np.random.default_rng(P).integers(0, SMALL["V"], B).astype(np.int32)
+    worst = 0.0
+    for t in range(steps):
+        o_next, o_logits = orc.step(tok)
+        g_next = m.step(tok)
+        g_logits = m.logits()
+        worst = max(worst, float(np.abs(g_logits - o_logits).max()))
+        s = np.sort(o_logits, axis=-1)
+        clear = (s[:, -1] - s[:, -2]) > 4e-4
+        assert np.array_equal(g_next[clear], o_next[clear]), t
+        tok = o_next
+    m.status()
+    print(f"P={P}: max |logit diff| vs oracle {worst:.3e}")
+    assert worst <= 2e-4
+    m.close()
+    orc.close()
+
+
+@pytest.mark.parametrize("splits", [1, 3, 16])
+def test_persistent_layer_split_counts(hip, splits):
+    """context ranges per (sequence, head) forced: 1, a count that does not
+    divide the tiles, and the maximum (ranges with no tile at short context)"""
+    params = synth.params(SMALL, seed=60 + splits)
+    B = 4
+    m = _model(hip, SMALL, params, B, 16, 1, splits_env=splits)
+    c = oc.cfg(SMALL["maxT"], SMALL["V"], SMALL["L"], SMALL["NH"], SMALL["C"])
+    orc = oc.PagedDecoder(params, c, B, 16, SMALL["maxT"], page_seed=splits)
+    rng = np.random.default_rng(splits)
+    worst = 0.0
+    for t in range(140):
+        tok = rng.integers(0, SMALL["V"], B).astype(np.int32)
+        _, o_logits = orc.step(tok)
+        m.step(tok)
+        worst = max(worst, float(np.abs(m.logits() - o_logits).max()))
+    m.status()
+    assert worst <= 2e-4, worst
+    m.close()
+    orc.close()
+
+
+def test_persistent_layer_bf16_pool_matches_launch_path(hip):
+    params = synth.params(SMALL, seed=77)
+    B, steps = 9, 40
+    rng = np.random.default_rng(77)
+    toks = rng.integers(0, SMALL["V"], (steps, B)).astype(np.int32)
+    res = []
+    for layer in (1, 0):
+        m = _model(hip, SMALL, params, B, 8, layer, kv_dtype=hip.HPA_BF16)
+        lg = []
+        for t in range(steps):
+            m.step(toks[t])
+            lg.append(m.logits())
+        m.status()
+        m.close()
+        res.append(np.stack(lg))
+    diff = float(np.abs(res[0] - res[1]).max())
+    assert diff <= 1e-4, diff  # fp32 reassociation of attproj / fcproj (3e-5 measured)
+
+
+def test_persistent_layer_rows_independent_of_batch(hip):
+    """B = 6 vs its halves B = 3 + 3 at the same split count: bit-identical
+    logits (what makes sequence-sharded decode equal the unsharded run)"""
+    params = synth.params(SMALL, seed=90)
+    steps = 30
+    toks = np.random.default_rng(90).integers(0, SMALL["V"], (steps, 6)).astype(np.int32)
+
+    def run(lo, hi):
+        m = _model(hip, SMALL, params, hi - lo, 16, 1, splits_env=4)
+        lg = []
+        for t in range(steps):
+            m.step(toks[t, lo:hi])
+            lg.append(m.logits())
+        m.status()
+        m.close()
+        return np.stack(lg)
+
+    full = run(0, 6)
+    assert np.array_equal(full[:, :3], run(0, 3))
+    assert np.array_equal(full[:, 3:], run(3, 6))
+
+
+def test_persistent_layer_eager_equals_graph(hip):
+    params = synth.params(SMALL, seed=5)
+    toks = np.random.default_rng(5).integers(0, SMALL["V"], (12, 7)).astype(np.int32)
+    outs = []
+    for graph in (False, True):
+        m = _model(hip, SMALL, params, 7, 16, 1)
+        m.set_graph(graph)
+        lg = []
+        for t in range(12):
+            m.step(toks[t])
+            lg.append(m.logits())
+        m.status()
+        m.close()
+        outs.append(np.stack(lg))
+    assert np.array_equal(outs[0], outs[1])

@@ -42,6 +42,10 @@ def _tokens(B, V):
 def _engine(hip, B):
     m = hip.Model(SMALL, params=synth.params(SMALL, seed=8))
     m.decode_init(B, 16, SMALL["maxT"])
+    # five launches per layer: two processes share the one GPU here, and the
+    # persistent layer needs every CU for itself (test_gpu_layer.py covers
+    # its sharded == unsharded property in one process)
+    m.set_layer_kernel(0)
     assert m.set_attn_splits(SPLITS) == SPLITS
     m.set_graph(True)
     return m

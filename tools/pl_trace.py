@@ -1,0 +1,71 @@
+"""Phase timeline of the persistent decode layer (hpa_layer.hip), from the
+trace build's per-(layer, workgroup) s_memrealtime stamps.
+
+usage: HPA_LIB=llm.c-paged_amd/libpaged_hip_trace.so python tools/pl_trace.py [B] [ctx]
+
+Prints, per event, the min / median / max over workgroups of the time since
+the earliest kernel-start stamp of that layer (us), averaged over layers 1..L-2
+of the last step, plus the span of one launch.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(HERE, ".."), os.path.join(HERE, "..", "llm.c-paged_amd"), os.path.join(HERE, "..", "tests")]
+import pagedattn as hip  # noqa: E402
+import synth  # noqa: E402
+
+EVENTS = ["start", "A issued", "A unit done", "A barrier", "B wait done", "B done", "C wait done", "C done",
+          "D wait done", "D done", "E wait done", "end"]
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+    ctx = int(sys.argv[2]) if len(sys.argv) > 2 else 990
+    cfg = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
+    hip.init(0)
+    m = hip.Model(cfg, params=synth.params(cfg, seed=3))
+    m.decode_init(B, 16, cfg["maxT"])
+    assert m.set_layer_kernel(2), "persistent layer not in use"
+    m.set_graph(True)
+    hip.check(hip.lib().gpt2_decode_fill_random(m.h, ctx, 5), "fill")
+    toks = np.random.default_rng(1).integers(0, cfg["V"], B).astype(np.int32)
+    for _ in range(8):
+        m.step(toks)
+    L = hip.lib()
+    if L.hpa_decode_layer_trace(None, 0) != 0:
+        raise SystemExit("not a trace build (make XFLAGS=-DHPA_LAYER_TRACE)")
+    m.step(toks)
+    m.status()
+    buf = np.zeros((cfg["L"], 256, 16), np.uint64)
+    hip.check(L.hpa_decode_layer_trace(buf.ctypes.data_as(ctypes.c_void_p), cfg["L"]), "trace")
+    rows = {k: [] for k in range(len(EVENTS))}
+    spans = []
+    for layer in range(1, cfg["L"] - 1):
+        t = buf[layer].astype(np.int64)
+        t0 = t[:, 0][t[:, 0] > 0].min()
+        spans.append((t[:, 11][t[:, 11] > 0].max() - t0) / 100.0)
+        for k in range(len(EVENTS)):
+            v = t[:, k]
+            v = v[v > 0]
+            if len(v):
+                rows[k].append(((v - t0) / 100.0))
+    print(f"B={B} ctx={ctx}: launch span (first start -> last end) {np.mean(spans):.1f} us "
+          f"(layers 1..{cfg['L'] - 2}, last step)")
+    print(f"{'event':14s} {'n':>4s} {'min':>7s} {'med':>7s} {'max':>7s}  us")
+    for k, name in enumerate(EVENTS):
+        if not rows[k]:
+            continue
+        n = int(np.mean([len(r) for r in rows[k]]))
+        mn = np.mean([r.min() for r in rows[k]])
+        md = np.mean([np.median(r) for r in rows[k]])
+        mx = np.mean([r.max() for r in rows[k]])
+        print(f"{name:14s} {n:4d} {mn:7.2f} {md:7.2f} {mx:7.2f}")
+    m.close()
+
+
+if __name__ == "__main__":
+    main()
