@@ -101,14 +101,13 @@ def comm_init(L, pagedattn, world, rank):
             time.sleep(0.01)
         with open(path, "rb") as f:
             uid = ctypes.create_string_buffer(f.read(), n)
+    maps = open("/proc/self/maps").read().split("\n")
+    libs = sorted({ln.split()[-1] for ln in maps if ("librccl" in ln or "libamdhip64" in ln) and "/" in ln})
+    print(f"[bench] rank {rank}/{world}: process loaded {', '.join(libs)}", file=sys.stderr, flush=True)
     if L.hpa_comm_init(world, rank, uid) != 0:
         print(f"[bench] rank {rank}: RCCL communicator init failed "
               f"({L.hpa_last_error().decode(errors='replace')}); no value reported", file=sys.stderr, flush=True)
         sys.exit(4)
-    maps = open("/proc/self/maps").read().split("\n")
-    libs = sorted({ln.split()[-1] for ln in maps if ("librccl" in ln or "libamdhip64" in ln) and "/" in ln})
-    print(f"[bench] rank {rank}: RCCL communicator {rank}/{world}; loaded: {', '.join(libs)}", file=sys.stderr,
-          flush=True)
 
 
 def parse():

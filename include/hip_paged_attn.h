@@ -251,6 +251,11 @@ int hpa_gemm_sk_workspace(int N, size_t* slab_floats, size_t* counters);
  * activation-resident kernel (variant 4) on the current stream; -1 if g is
  * not a valid LOGITS descriptor */
 int hpa_logits_partials(const HpaFusedGemm* g);
+/* the kernel a variant-4 fp32 LOGITS GEMM of this shape runs (LN applied):
+ * 4 = activation-resident, 6 = stream-K (when given its workspace), 1 =
+ * looped; -1 on a bad shape.  The engine allocates the stream-K workspace
+ * exactly when this says 6. */
+int hpa_logits_kernel(int M, int N, int K);
 /* the launch shape hpa_gemm_fused picks when waves / row_blocks / col_tiles
  * are 0: out3 = {waves, row_blocks, col_tiles} */
 void hpa_fused_pick(int M, int N, int K, int* out3);

@@ -29,6 +29,7 @@
 //    latency overlaps it.
 #include <math.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "hpa_gemm_body.h"
 
@@ -839,8 +840,8 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
     if (g->variant == 4 && logits_resident_eligible(p, g->epilogue)) return launch_logits_resident(p);
     // variant 4 elsewhere (GPT-2 XL logits, K = 1600): stream-K when the caller
     // gave its workspace (120 vs 143 us at M = 64, profiles/r2/sk_tune_xl.txt)
-    if (g->variant == 4 && g->epilogue == HPA_FEPI_LOGITS && p.Mp <= 64 && p.sk_slab && p.sk_cnt)
-        return launch_sk(p, g->epilogue);
+    if (g->variant == 4 && g->epilogue == HPA_FEPI_LOGITS && p.sk_slab && p.sk_cnt && sk_eligible(p.Mp, p.ntn, p.K16))
+        return launch_sk(p, g->epilogue);  // else the looped kernel below
     HPA_REQUIRE(g->col_tiles == 0 || g->col_tiles == 1 || g->col_tiles == 2 || g->col_tiles == 4,
                 "gemm_fused: col_tiles must be 1, 2 or 4");
     if (g->variant == 2 || (g->variant == 0 && mt == 1 && p.ntn < 1024 && g->col_tiles <= 1)) {
@@ -856,6 +857,22 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
             return launch16_mt<16>(p, g->epilogue, mt, ntw);
         default: return hpa_fail(__FILE__, __LINE__, "gemm_fused: waves must be 4, 8 or 16");
     }
+}
+
+int hpa_logits_kernel(int M, int N, int K) {
+    if (M <= 0 || N <= 0 || K <= 0 || K % 16) return -1;
+    const int Mp = (M + 15) / 16 * 16, K16 = K / 16, ntn = (N + 15) / 16;
+    FG p;
+    memset(&p, 0, sizeof(p));
+    p.M = M;
+    p.Mp = Mp;
+    p.K = K;
+    p.K16 = K16;
+    p.N = N;
+    p.ntn = ntn;
+    p.ln_stats = reinterpret_cast<const float*>(16);  // "LN present": only its presence is read
+    if (logits_resident_eligible(p, HPA_FEPI_LOGITS)) return 4;
+    return sk_eligible(Mp, ntn, K16) ? 6 : 1;
 }
 
 int hpa_logits_partials(const HpaFusedGemm* g) {

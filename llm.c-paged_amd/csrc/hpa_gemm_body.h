@@ -631,6 +631,7 @@ int launch_b16(const FG& p, int epi, int nw, int mt, int ntw);
 int launch_b16_ares(const FG& p, int epi, int nw, int mt, int rounds);
 // stream-K fp32 kernel (hpa_gemm_sk.hip, variant 6): M <= 64
 int launch_sk(const FG& p, int epi);
+bool sk_eligible(int Mp, int ntn, int K16);
 
 static inline int fused_prepare(const HpaFusedGemm* g, FG* p) {
     HPA_REQUIRE(g && g->x && g->w && g->out, "gemm_fused: null operand");

@@ -345,6 +345,14 @@ int sk_grid() {
 }  // namespace
 
 namespace hpa_gemm {
+// the shapes launch_sk accepts (its checks, as a predicate for the dispatch)
+bool sk_eligible(int Mp, int ntn, int K16) {
+    const int G = sk_grid();
+    const long long nst = (ntn + SK_NTW - 1) / SK_NTW, F = nst * K16;
+    return Mp <= 64 && G <= SK_MAXG && F * G < (1LL << 31) &&
+           (F + (long long)G * SK_NW - 1) / ((long long)G * SK_NW) + 1 <= K16;
+}
+
 int launch_sk(const FG& p, int epi) {
     HPA_REQUIRE(p.Mp <= 64, "gemm_fused stream-K: M <= 64");
     HPA_REQUIRE(p.sk_slab && p.sk_cnt, "gemm_fused stream-K: sk_slab / sk_count workspace");

@@ -652,6 +652,7 @@ struct GPT2Decode {
     int pl_want;      /* gpt2_decode_set_layer_kernel */
     int pl_on;        /* in use: wanted and eligible */
     int pl_splits;
+    int pl_global_B;  /* sharded: the whole batch's size (picks follow it); else 0 */
     float* pl_rec;
     float* pl_slab;
     int* pl_ctr;      /* [L][pl_ctr_ints], zeroed at the start of every step */
@@ -869,8 +870,9 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
     /* auto (1): where it measured faster than five launches per layer --
      * B <= 32 (profiles/r3/pl_ab.txt: B 8/16/32 -1.7/-2.3/-0.4 %, B 48/64
      * +1.2/0 %); 2 forces it at any eligible batch */
-    if (d->pl_want == 1 && d->B > 32) return 0;
-    int splits = hpa_decode_layer_pick_splits(d->B, c.num_heads, d->max_ctx);
+    const int Bg = d->pl_global_B > 0 ? d->pl_global_B : d->B; /* the batch the picks follow */
+    if (Bg > 64 || (d->pl_want == 1 && Bg > 32)) return 0;
+    int splits = hpa_decode_layer_pick_splits(Bg, c.num_heads, d->max_ctx);
     const char* env = getenv("HPA_LAYER_SPLITS");
     if (env && atoi(env) > 0) splits = atoi(env);
     if (!hpa_decode_layer_eligible(d->B, c.channels, c.num_heads, splits)) return 0;
@@ -1040,9 +1042,10 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
     d->part = (float*)hpa_malloc((size_t)((V + 15) / 16) * Mp * 2 * 4);
     int ok = d->d_bt && d->d_pos && d->d_tokens && d->d_next && d->h_pos && d->h_evicted && d->h_next && d->d_q &&
              d->d_logits && d->res && d->res2 && d->att && d->fch && d->st1 && d->st2 && d->part;
-    /* logits GEMM: the activation-resident kernel takes C = 768; other widths
-     * (XL) run stream-K at B <= 64, which needs a slab and zeroed counters */
-    if (ok && w_dtype != HPA_BF16 && Mp <= 64 && C != 768) {
+    /* logits GEMM: the activation-resident kernel where it applies (C = 768,
+     * B <= 64); stream-K where its shape limits allow (XL at B <= 64), which
+     * needs a slab and zeroed counters; else the looped kernel */
+    if (ok && w_dtype != HPA_BF16 && hpa_logits_kernel(B, V, C) == 6) {
         size_t nf = 0, nc = 0;
         ok = hpa_gemm_sk_workspace(V, &nf, &nc) == 0;
         if (ok) {
@@ -1828,6 +1831,25 @@ int gpt2_decode_shard(GPT2* model, const int* rows_per_rank, int root) {
         return 1;
     }
     dec_shard_free(d);
+    {   /* the arithmetic follows the GLOBAL batch, so a sharded decode equals
+         * the unsharded one bit for bit: the attention split
+         * count and the layer loop's form are what the unsharded engine of
+         * sum(rows) sequences picks (row results never depend on M beyond
+         * those two choices) */
+        long tot = 0;
+        for (int r = 0; r < n; r++) tot += rows_per_rank[r];
+        const GPT2Config c = model->config;
+        int ncu = 0;
+        hpa_device_info(NULL, 0, &ncu, NULL);
+        if (hpa_synchronize() || dec_set_splits(d, hpa_attn_pick_splits((int)tot, c.num_heads, d->max_ctx, ncu)))
+            return 1;
+        d->pl_global_B = (int)tot;
+        if (dec_layer_setup(model, d)) return 1;
+        if (d->graph) {
+            hpa_graph_destroy(d->graph);
+            d->graph = NULL;
+        }
+    }
     DecShard* s = (DecShard*)calloc(1, sizeof(DecShard));
     if (!s) return 1;
     d->shard = s;
@@ -2005,6 +2027,9 @@ void gpt2_forward(GPT2* model, int* inputs, int* targets, size_t B, size_t T, si
             d->h_hist[b * d->max_ctx + pos] = tok[b];
         }
         if (gpt2_decode_step(model, tok, NULL)) PI_FATAL("decode step failed");
+        /* every sequence of the window is live: an LRU eviction inside the
+         * loop would restart one at position 0 mid-window */
+        if (gpt2_decode_evicted(model, NULL) > 0) PI_FATAL("gpt2_forward: page pool too small, a sequence was evicted");
         if (d->pos_logits)
             for (size_t b = 0; b < B; b++)
                 PI_CHECK(hpa_memcpy_async(d->pos_logits + (b * d->max_ctx + pos) * V, d->d_logits + b * V,

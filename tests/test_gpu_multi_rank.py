@@ -137,3 +137,31 @@ def test_rccl_gather_one_rank(hip):
         m.close()
     finally:
         hip.check(L.hpa_comm_destroy(), "comm destroy")
+
+
+def test_rccl_single_process_init_all_barrier_and_max(hip):
+    """SURVEY.md 8e's single-process form (ncclCommInitAll over the devices
+    one process drives; here the box's one device), the timing helpers
+    bench.py uses at N > 1 (hpa_comm_barrier / hpa_comm_allreduce_max), and
+    the engine's gather on that communicator"""
+    L = hip.lib()
+    devs = (ctypes.c_int * 1)(0)
+    hip.check(L.hpa_comm_init_all(1, devs), "init_all")
+    try:
+        assert L.hpa_comm_size() == 1 and L.hpa_comm_rank() == 0
+        hip.check(L.hpa_comm_use(0), "use")
+        hip.check(L.hpa_comm_barrier(), "barrier")
+        v = ctypes.c_double(3.25)
+        hip.check(L.hpa_comm_allreduce_max(ctypes.byref(v)), "max")
+        assert v.value == 3.25
+        B = 3
+        m = _engine(hip, B)
+        m.shard([B], root=0)
+        toks = _tokens(B, SMALL["V"])
+        for t in range(3):
+            nxt = m.step(toks[t])
+            m.gather(1)
+            assert np.array_equal(m.gathered(B, 1), nxt)
+        m.close()
+    finally:
+        hip.check(L.hpa_comm_destroy(), "comm destroy")
