@@ -190,7 +190,7 @@ def cpu_baseline(cfgd, B, P, start_ctx, end_ctx, budget_s, kv_bf16=False, w_bf16
     return {"value": runs[1]["value"], "unit": "tokens/s", "cores": threads, "kind": "port",
             "nproc": os.cpu_count(), "affinity_cores": affinity,
             "sample": f"oracle/ C restatement of the same paged decode (OpenMP, {threads} threads = the cores "
-                      f"this process may use; nproc {os.cpu_count()}), GPT-2 124M"
+                      f"this process may use; nproc {os.cpu_count()}), GPT-2 {'XL' if cfgd['C'] == 1600 else '124M'}"
                       f"{' bf16-rounded weights and GEMM inputs' if w_bf16 else ' fp32'}"
                       f"{' (bf16 KV)' if kv_bf16 else ''}, B={B}, page {P}, decode steps at the GPU's positions "
                       f"after a synthetic K/V fill, <= {budget_s:.0f} s per build; value = the -Ofast build; "
@@ -318,11 +318,14 @@ def main():
     if rank == 0:
         cpu = None
         want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
-        if want_cpu and args.model == "124M":
+        if want_cpu:
             try:
                 # bounded sample: the oracle keeps an fp32 pool of B*ctx*C*L*2 floats, so
                 # beyond config 2's B*ctx the sample takes a subset of the sequences
+                # (GPT-2 XL: one sequence -- 0.6 GB of pool, 6 GB of weights on the host)
                 cpu_B = B_local if B_local * ctx <= 65536 else max(1, 16384 // ctx)
+                if args.model == "XL":
+                    cpu_B = 1
                 cpu = cpu_baseline(cfgd, cpu_B, P, start, ctx, args.cpu_seconds, kv_bf16, w_bf16)
                 if cpu_B != B_local:
                     cpu["sample"] += f" (a {cpu_B}-sequence subset of the {B_local}-sequence batch)"

@@ -143,6 +143,10 @@ int hpa_paged_attention_decode_split(const float* q, const HpaKVPool* pool, int 
  * from a counter-based hash (attention microbench / bench synthetic prefill) */
 int hpa_pool_fill_random(const HpaKVPool* pool, const int* block_table, int bt_stride, int B,
                          int ctx, uint64_t seed);
+/* the same for sequences seq_offset .. seq_offset+B-1 of a larger batch (a
+ * shard fills exactly the rows the unsharded batch would get) */
+int hpa_pool_fill_random_ex(const HpaKVPool* pool, const int* block_table, int bt_stride, int B,
+                            int ctx, uint64_t seed, int seq_offset);
 
 /* ---------------- fused decode-layer GEMMs (the engine's path) ----------------
  * "frag" layout: a [rows][K] fp32 matrix with rows padded to a multiple of 16

@@ -188,6 +188,9 @@ int  gpt2_decode_step_async(GPT2* model, const int* tokens);
 int  gpt2_decode_reset(GPT2* model);
 /* synthetic K/V for positions [0, ctx) of every sequence (benchmark prefill) */
 int  gpt2_decode_fill_random(GPT2* model, int ctx, unsigned long long seed);
+/* the same with the K/V of global sequences seq_offset.. (a shard of a larger
+ * batch gets exactly its rows of the unsharded fill) */
+int  gpt2_decode_fill_random_ex(GPT2* model, int ctx, unsigned long long seed, int seq_offset);
 /* allocate the pages of positions [0, ctx) up front (no host work per step) */
 int  gpt2_decode_reserve(GPT2* model, int ctx);
 /* rewind/advance positions (pages kept) */

@@ -310,6 +310,15 @@ constexpr int kRec = 68;
 // the fp32 fold, lanes 0..15; K = 2 for the bf16 fold, lanes 0..7); the last
 // arriver merges every range in order and returns true with the merged state
 // (rewind: it also zeroes the counter for the next launch).
+// Memory model: gfx950 only.  The hand-off is MI355X_MICROARCH.md "Valid
+// forms" row 1: 16-byte sc1 (write-through) record stores, drained by
+// s_waitcnt vmcnt(0), then an agent-scope relaxed ticket, and sc1 loads by
+// the last arriver (L1 bypass); no acquire/release fences, so it relies on
+// gfx950's sc1 semantics and on the buffer-load builtins not being speculated
+// above the ticket (they are data-dependent on it through the branch).  A
+// launch that aborts part-way leaves counters non-zero: the engine re-zeroes
+// them after a failure and before a graph recapture (paged_infer.c
+// dec_rezero).
 template <int K>
 __device__ __forceinline__ bool split_merge(float* __restrict__ rec_bh, int* __restrict__ cnt, int S, int s,
                                             float& m, float& l, float4* acc, bool rewind) {

@@ -622,8 +622,9 @@ struct GPT2Decode {
     float* d_logits;  /* [B][V] */
     /* frag-layout activations [Mp][*] (padded rows stay zero) and LN statistics */
     float *res, *res2, *att, *fch, *st1, *st2, *part;
-    float* sk_slab;   /* stream-K logits workspace (fp32 weights, B <= 64, C != 768), else NULL */
+    float* sk_slab;   /* stream-K logits workspace (hpa_logits_kernel == 6), else NULL */
     int* sk_cnt;
+    size_t sk_cnt_n;
     float* d_wpack;   /* packed qkvw, attprojw, fcw, fcprojw of every layer, then wte */
     int w_bf16;       /* weights packed bf16 (hpa_pack_frag_bf16; offsets in elements) */
     size_t wpack_off[5]; /* per-layer offsets (0..3) and wte offset (4) */
@@ -939,6 +940,17 @@ static int dec_layer(GPT2* model, int l) {
     return hpa_decode_layer(&a);
 }
 
+/* the in-launch arrival counters of the attention's split merge and of the
+ * stream-K logits back to zero: every completed launch leaves them zero, a
+ * launch that failed part-way may not.  Called before a graph is
+ * recaptured and after a reported failure. */
+static int dec_rezero(GPT2Decode* d) {
+    int rc = 0;
+    if (d->d_attn_ws) rc |= hpa_memset_async(d->d_attn_ws, 0, d->attn_ws_bytes);
+    if (d->sk_cnt && d->sk_cnt_n) rc |= hpa_memset_async(d->sk_cnt, 0, d->sk_cnt_n * sizeof(int));
+    return rc;
+}
+
 int gpt2_decode_init(GPT2* model, int B, int page_size, int max_ctx) {
     return gpt2_decode_init_ex(model, B, page_size, max_ctx, HPA_F32);
 }
@@ -1051,6 +1063,7 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
         if (ok) {
             d->sk_slab = (float*)hpa_malloc(nf * sizeof(float));
             d->sk_cnt = (int*)hpa_malloc(nc * sizeof(int));
+            d->sk_cnt_n = nc;
             ok = d->sk_slab && d->sk_cnt && hpa_memset_async(d->sk_cnt, 0, nc * sizeof(int)) == 0;
         }
     }
@@ -1314,6 +1327,7 @@ int gpt2_decode_set_sampling(GPT2* model, int enable, unsigned long long seed) {
     if (d->graph) { /* recapture with the other token-choice kernel */
         hpa_graph_destroy(d->graph);
         d->graph = NULL;
+        if (dec_rezero(d)) return 1;
     }
     return 0;
 }
@@ -1595,7 +1609,7 @@ int gpt2_decode_status(GPT2* model) {
         fprintf(stderr, "[paged_infer] persistent layer: in-launch wait for %s timed out (code %d); step invalid\n",
                 code >= 1 && code <= 4 ? what[code] : "?", code);
         const int zero = 0;
-        if (hpa_memcpy(d->d_next + d->B, &zero, sizeof(int))) return -1;
+        if (hpa_memcpy(d->d_next + d->B, &zero, sizeof(int)) || dec_rezero(d)) return -1;
     }
     return code;
 }
@@ -1609,6 +1623,7 @@ int gpt2_decode_set_layer_kernel(GPT2* model, int enable) {
     if (d->graph) { /* recapture with the other step */
         hpa_graph_destroy(d->graph);
         d->graph = NULL;
+        if (dec_rezero(d)) return 1;
     }
     return 0;
 }
@@ -1643,6 +1658,10 @@ int gpt2_decode_reset(GPT2* model) {
 }
 
 int gpt2_decode_fill_random(GPT2* model, int ctx, unsigned long long seed) {
+    return gpt2_decode_fill_random_ex(model, ctx, seed, 0);
+}
+
+int gpt2_decode_fill_random_ex(GPT2* model, int ctx, unsigned long long seed, int seq_offset) {
     GPT2Decode* d = model->decode;
     if (!d) return 1;
     if (ctx < 0 || ctx >= d->max_ctx) {
@@ -1657,7 +1676,7 @@ int gpt2_decode_fill_random(GPT2* model, int ctx, unsigned long long seed) {
         d->h_pos[b] = ctx;
     }
     if (dec_sync_block_table(d)) return 1;
-    if (hpa_pool_fill_random(&d->pool, d->d_bt, d->bt_stride, d->B, ctx, seed)) return 1;
+    if (hpa_pool_fill_random_ex(&d->pool, d->d_bt, d->bt_stride, d->B, ctx, seed, seq_offset)) return 1;
     if (hpa_memcpy(d->d_pos, d->h_pos, d->B * sizeof(int))) return 1;
     return 0;
 }

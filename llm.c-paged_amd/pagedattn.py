@@ -231,6 +231,9 @@ def lib():
     _sig(L, "gpt2_decode_set_attn_splits", i, [v, i])
     _sig(L, "gpt2_decode_attn_splits", i, [v])
     _sig(L, "gpt2_decode_set_layer_kernel", i, [v, i])
+    _sig(L, "gpt2_decode_fill_random_ex", i, [v, i, ctypes.c_uint64, i])
+    _sig(L, "hpa_pool_fill_random_ex", i, [P, v, i, i, i, ctypes.c_uint64, i])
+    _sig(L, "hpa_logits_kernel", i, [i, i, i])
     _sig(L, "gpt2_decode_layer_kernel", i, [v])
     _sig(L, "gpt2_decode_status", i, [v])
     _sig(L, "hpa_decode_layer_eligible", i, [i, i, i, i])
@@ -700,8 +703,10 @@ class Model:
         pos = np.ascontiguousarray(pos, np.int32)
         check(lib().gpt2_decode_set_positions(self.h, pos.ctypes.data_as(_I)), "set_positions")
 
-    def fill_random(self, ctx, seed=1):
-        check(lib().gpt2_decode_fill_random(self.h, ctx, seed), "fill_random")
+    def fill_random(self, ctx, seed=1, seq_offset=0):
+        """synthetic K/V of positions [0, ctx); seq_offset: this engine's rows
+        are sequences seq_offset.. of a larger (sharded) batch"""
+        check(lib().gpt2_decode_fill_random_ex(self.h, ctx, seed, seq_offset), "fill_random")
 
     def close(self):
         if self.h:

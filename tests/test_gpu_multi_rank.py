@@ -165,3 +165,63 @@ def test_rccl_single_process_init_all_barrier_and_max(hip):
         m.close()
     finally:
         hip.check(L.hpa_comm_destroy(), "comm destroy")
+
+
+# ---- BASELINE config 4's per-rank work at model size:
+# GPT-2 124M, B = 64 split 32 / 32 over two engine processes on the one GPU,
+# identical K/V (the fill hashes the global sequence index) to ~1000 tokens,
+# 8 steps; every row's logits and greedy id equal the unsharded B = 64 engine
+# bit for bit.  Both sides use five launches per layer with the global batch's
+# attention split count (what gpt2_decode_shard picks), so the arithmetic is
+# the same; the shards hand their rows over by file (the RCCL gather of this
+# path is tested above on a 1-rank communicator).
+GPT2_124M = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
+C4_CTX, C4_STEPS, C4_B = 990, 8, 64
+
+
+def _c4_engine(hip, B, lo):
+    m = hip.Model(GPT2_124M, params=synth.params(GPT2_124M, seed=41))
+    m.decode_init(B, 16, GPT2_124M["maxT"])
+    m.set_layer_kernel(0)
+    m.set_attn_splits(hip.lib().hpa_attn_pick_splits(C4_B, GPT2_124M["NH"], GPT2_124M["maxT"], 0))
+    m.set_graph(True)
+    m.fill_random(C4_CTX, seed=7, seq_offset=lo)
+    return m
+
+
+def _c4_tokens():
+    return np.random.default_rng(44).integers(0, GPT2_124M["V"], (C4_STEPS, C4_B)).astype(np.int32)
+
+
+def _c4_worker(lo, hi, out_path):
+    import pagedattn as hip
+    hip.init(0)
+    m = _c4_engine(hip, hi - lo, lo)
+    toks = _c4_tokens()
+    ids, lg = [], []
+    for t in range(C4_STEPS):
+        ids.append(m.step(toks[t, lo:hi]))
+        lg.append(m.logits())
+    m.close()
+    np.savez(out_path, ids=np.stack(ids), logits=np.stack(lg))
+
+
+def test_config4_shards_at_model_size_equal_unsharded(hip, tmp_path):
+    ctx = multiprocessing.get_context("spawn")
+    halves = [(0, 32), (32, 64)]
+    outs = [str(tmp_path / f"shard{r}.npz") for r in range(2)]
+    procs = [ctx.Process(target=_c4_worker, args=(lo, hi, o)) for (lo, hi), o in zip(halves, outs)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    got = [np.load(o) for o in outs]
+    m = _c4_engine(hip, C4_B, 0)
+    toks = _c4_tokens()
+    for t in range(C4_STEPS):
+        want_ids = m.step(toks[t])
+        want_lg = m.logits()
+        assert np.array_equal(np.concatenate([g["ids"][t] for g in got]), want_ids), t
+        assert np.array_equal(np.concatenate([g["logits"][t] for g in got]), want_lg), t
+    m.close()
