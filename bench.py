@@ -374,8 +374,10 @@ def main():
                                                                if gather else
                                                                f" (gather: {args.gather})" if world > 1 else ""),
                        "hip_graph": not args.no_graph, "attn_splits": splits,
-                       "layer_loop": ("one persistent launch per layer (hpa_decode_layer)" if model.layer_kernel()
-                                      else "five launches per layer"),
+                       "layer_loop": {0: "five launches per layer",
+                                      1: "one persistent launch per layer (hpa_decode_layer)",
+                                      2: "attention launch + one persistent launch of the GEMM chain "
+                                         "(hpa_decode_layer chain_only)"}[model.layer_form()],
                        "token_choice": "multinomial (reference sample_mult)" if args.sample else "greedy",
                        "gemm_waves": [int(x) for x in model.gemm_config()[0]],
                        "gemm_row_blocks": [int(x) for x in model.gemm_config()[1]],

@@ -292,6 +292,9 @@ int hpa_fused_pick_waves(int M, int N, int K);
 typedef struct {
     int B, C, num_heads, splits;  /* splits: context ranges of the attention */
     int last;                     /* 1: no qkv(l+1) phase (last layer) */
+    int chain_only;               /* 1: no attention phase -- the caller launched the decode
+                                     attention (frag output into att) before: the launch is
+                                     attproj -> fc -> fcproj -> qkv(l+1) */
     const HpaKVPool* pool;
     int layer;
     const int* block_table;

@@ -202,15 +202,18 @@ int  gpt2_decode_set_graph(GPT2* model, int enable);
  * GPT-2 124M 1 at B >= 64 and 16, 2 at 32 and 8), else 1..16 */
 int  gpt2_decode_set_attn_splits(GPT2* model, int splits);
 int  gpt2_decode_attn_splits(GPT2* model);
-/* the layer loop as one persistent launch per layer (hpa_decode_layer:
- * attention -> attproj -> fc -> fcproj -> next qkv) or five launches per
- * layer (0).  1 (default, "auto"): persistent where it measured faster (fp32
- * weights, C = 128 / 768, B <= 32); 2: persistent at every batch it supports
- * (B <= 64).  HPA_LAYER_KERNEL=0/1/2 in the environment sets the default.
- * The persistent launch needs every CU for its 12-wave workgroup: a GPU
- * shared with another process's persistent kernels should use 0. */
+/* the layer loop's form: 0 five launches per layer; 2 one persistent launch
+ * per layer (hpa_decode_layer: attention -> attproj -> fc -> fcproj -> next
+ * qkv); 3 the decode attention's own launch + one persistent launch of the
+ * GEMM chain (attproj -> fc -> fcproj -> next qkv); 1 (default, "auto") the
+ * form measured fastest for the batch (profiles/r3).  The persistent forms
+ * need fp32 weights, C = 128 / 768 and B <= 64 (else five launches).
+ * HPA_LAYER_KERNEL=0..3 in the environment sets the default.  A persistent
+ * launch needs every CU for its 12-wave workgroups: a GPU shared with
+ * another process's persistent kernels should use 0. */
 int  gpt2_decode_set_layer_kernel(GPT2* model, int enable);
-/* 1 while the persistent layer is in use */
+/* the form in use: 0 five launches, 1 full persistent layer, 2 attention
+ * launch + persistent chain */
 int  gpt2_decode_layer_kernel(GPT2* model);
 /* waits for the queued work; 0, or the code of a timed-out in-launch wait of
  * the persistent layer (the step's outputs are then invalid), which it clears */

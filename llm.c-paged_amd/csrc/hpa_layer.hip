@@ -441,7 +441,10 @@ __device__ __forceinline__ void publish(const KA& a, int which, int nslots) {
 }
 
 // ------------------------------------------------------------------ the kernel
-template <int NH, int P, bool BF>
+// ATTN = false: the chain only (attproj -> fc -> fcproj -> next qkv); the
+// attention ran as its own launch just before (hpa_paged_attention_decode_split
+// writing `att` in frag layout), so phase B needs no in-launch wait
+template <int NH, int P, bool BF, bool ATTN>
 __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
     using D = LD<NH>;
     constexpr int C = D::C, SW = D::SW, NCT = D::NCT;
@@ -464,7 +467,7 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
     __syncthreads();
 
     // A: attention, one unit (sequence, head, context range) per slot
-    {
+    if constexpr (ATTN) {
         const bool has = v < a.B * NH * a.S;
         float qv[HS];
 #ifdef HPA_PL_QREG
@@ -473,9 +476,9 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         PL_STAMP(t_issued);
         if (has) attn_unit<NH, P, BF>(a, v, slot, wq, sm, qv);
         PL_MARK(2);
-        PL_STORE(0, t_start);
         PL_STORE(1, t_issued);
     }
+    PL_STORE(0, t_start);
     float4 wr[SW];
     float fs1, fs2;
     // B: attproj(l): res2 = res + att . Wap^T + b
@@ -484,7 +487,7 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         if (u.has) load_w<SW>(a.w_ap, D::K16, u.j, 0, wq, nt, wr);
         lds_barrier();
         PL_MARK(3);
-        if (!wait_ctr<NH>(a, CT_ATT, a.B * NH, 1, sm)) return;
+        if (ATTN && !wait_ctr<NH>(a, CT_ATT, a.B * NH, 1, sm)) return;
         PL_MARK(4);
         const int row = u.rb * 16 + lrow, col = u.j * 16 + lcol;
         const int fi = (int)(hpa::frag_index(row, col, C) * 4);
@@ -666,12 +669,13 @@ bool shape_ok(int B, int S, int G) {
            4L * LD<NH>::NCT * R <= 3L * G;
 }
 
-template <int NH, int P, bool BF>
+template <int NH, int P, bool BF, bool ATTN>
 int launch(const HpaLayerArgs* h, int G) {
     static int resident = -1;  // blocks per CU of this instantiation (occupancy API)
     if (resident < 0) {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, decode_layer_kernel<NH, P, BF>, 768, 0) != hipSuccess)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, decode_layer_kernel<NH, P, BF, ATTN>, 768, 0) !=
+            hipSuccess)
             nb = 0;
         resident = nb;
     }
@@ -715,21 +719,26 @@ int launch(const HpaLayerArgs* h, int G) {
     a.slab_fp = h->slab;
     a.ctr = h->counters;
     a.err = h->err;
-    decode_layer_kernel<NH, P, BF><<<G, 768, 0, hpa_stream()>>>(a);
+    decode_layer_kernel<NH, P, BF, ATTN><<<G, 768, 0, hpa_stream()>>>(a);
     HPA_LAUNCH_CHECK();
     return 0;
 }
 
-template <int NH>
-int dispatch(const HpaLayerArgs* h, int G) {
+template <int NH, bool ATTN>
+int dispatch_p(const HpaLayerArgs* h, int G) {
     const bool bf = h->pool->dtype == HPA_BF16;
     switch (h->pool->page_size) {
-        case 8: return bf ? launch<NH, 8, true>(h, G) : launch<NH, 8, false>(h, G);
-        case 16: return bf ? launch<NH, 16, true>(h, G) : launch<NH, 16, false>(h, G);
-        case 32: return bf ? launch<NH, 32, true>(h, G) : launch<NH, 32, false>(h, G);
-        case 64: return bf ? launch<NH, 64, true>(h, G) : launch<NH, 64, false>(h, G);
+        case 8: return bf ? launch<NH, 8, true, ATTN>(h, G) : launch<NH, 8, false, ATTN>(h, G);
+        case 16: return bf ? launch<NH, 16, true, ATTN>(h, G) : launch<NH, 16, false, ATTN>(h, G);
+        case 32: return bf ? launch<NH, 32, true, ATTN>(h, G) : launch<NH, 32, false, ATTN>(h, G);
+        case 64: return bf ? launch<NH, 64, true, ATTN>(h, G) : launch<NH, 64, false, ATTN>(h, G);
         default: return hpa_fail(__FILE__, __LINE__, "decode layer: page size must be 8, 16, 32 or 64");
     }
+}
+
+template <int NH>
+int dispatch(const HpaLayerArgs* h, int G) {
+    return h->chain_only ? dispatch_p<NH, false>(h, G) : dispatch_p<NH, true>(h, G);
 }
 
 }  // namespace

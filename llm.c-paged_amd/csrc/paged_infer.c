@@ -650,8 +650,8 @@ struct GPT2Decode {
     long prof_launches;
     DecShard* shard;
     /* persistent layer (hpa_decode_layer): one launch per layer */
-    int pl_want;      /* gpt2_decode_set_layer_kernel */
-    int pl_on;        /* in use: wanted and eligible */
+    int pl_want;      /* gpt2_decode_set_layer_kernel: 0 off, 1 auto, 2 full, 3 chain */
+    int pl_on;        /* in use: 0 five launches, 1 full persistent layer, 2 attention launch + chain */
     int pl_splits;
     int pl_global_B;  /* sharded: the whole batch's size (picks follow it); else 0 */
     float* pl_rec;
@@ -868,14 +868,18 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
     const GPT2Config c = model->config;
     d->pl_on = 0;
     if (!d->pl_want || d->w_bf16 || !d->d_fold) return 0;
-    /* auto (1): where it measured faster than five launches per layer --
-     * B <= 32 (profiles/r3/pl_ab.txt: B 8/16/32 -1.7/-2.3/-0.4 %, B 48/64
-     * +1.2/0 %); 2 forces it at any eligible batch */
     const int Bg = d->pl_global_B > 0 ? d->pl_global_B : d->B; /* the batch the picks follow */
-    if (Bg > 64 || (d->pl_want == 1 && Bg > 32)) return 0;
+    if (Bg > 64) return 0;
+    /* auto (1): the form measured fastest (profiles/r3/pl_ab.txt): the
+     * attention's own launch + the persistent chain, at every batch it
+     * supports (B 64 / 32 / 16 / 8: -2.3 / -0.9 / -4.9 / -4.0 % per step
+     * against five launches; the full persistent layer -0.1 / +0.2 / -2.3 /
+     * -1.7 %) */
+    const int mode = d->pl_want == 2 ? 1 : 2;
     int splits = hpa_decode_layer_pick_splits(Bg, c.num_heads, d->max_ctx);
     const char* env = getenv("HPA_LAYER_SPLITS");
     if (env && atoi(env) > 0) splits = atoi(env);
+    if (mode == 2) splits = 1; /* no attention phase: no split records */
     if (!hpa_decode_layer_eligible(d->B, c.channels, c.num_heads, splits)) return 0;
     size_t sz[3];
     if (hpa_decode_layer_sizes(d->B, c.channels, c.num_heads, splits, sz)) return 1;
@@ -890,7 +894,7 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
     }
     if (!d->pl_rec || !d->pl_slab || !d->pl_ctr) return 1;
     d->pl_splits = splits;
-    d->pl_on = 1;
+    d->pl_on = mode;
     return 0;
 }
 
@@ -909,6 +913,7 @@ static int dec_layer(GPT2* model, int l) {
     a.num_heads = c.num_heads;
     a.splits = d->pl_splits;
     a.last = l + 1 == L;
+    a.chain_only = d->pl_on == 2;
     a.pool = &d->pool;
     a.layer = l;
     a.block_table = d->d_bt;
@@ -1091,7 +1096,7 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
     }
     {
         const char* env = getenv("HPA_LAYER_KERNEL");
-        d->pl_want = env && (env[0] == '0' || env[0] == '2') ? env[0] - '0' : 1;
+        d->pl_want = env && env[0] >= '0' && env[0] <= '3' ? env[0] - '0' : 1;
     }
     if (dec_layer_setup(model, d)) {
         dec_free(d);
@@ -1288,7 +1293,10 @@ static int dec_launch(GPT2* model) {
     if (d->pl_on && !d->profiling) { /* qkv(0), then one persistent launch per layer */
         rc |= dec_gemm(model, 0, G_QKV);
         rc |= hpa_memset_async(d->pl_ctr, 0, (size_t)L * d->pl_ctr_ints * sizeof(int));
-        for (int l = 0; l < L && !rc; l++) rc |= dec_layer(model, l);
+        for (int l = 0; l < L && !rc; l++) {
+            if (d->pl_on == 2) rc |= dec_attention(model, l); /* chain form: the attention's own launch */
+            rc |= dec_layer(model, l);
+        }
         rc |= dec_gemm(model, 0, G_LOGITS);
         rc |= dec_pick(model, NULL);
         return rc;
@@ -1618,7 +1626,7 @@ int gpt2_decode_set_layer_kernel(GPT2* model, int enable) {
     GPT2Decode* d = model->decode;
     if (!d) return 1;
     if (hpa_synchronize()) return 1;
-    d->pl_want = enable < 0 ? 0 : enable > 2 ? 2 : enable;
+    d->pl_want = enable < 0 ? 0 : enable > 3 ? 3 : enable;
     if (dec_layer_setup(model, d)) return 1;
     if (d->graph) { /* recapture with the other step */
         hpa_graph_destroy(d->graph);

@@ -586,14 +586,18 @@ class Model:
         return lib().gpt2_decode_attn_splits(self.h)
 
     def set_layer_kernel(self, on):
-        """one persistent launch per layer (1: where it measured faster, B <= 32;
-        2: wherever it applies, B <= 64) or five (0); returns whether the
-        persistent layer is now in use"""
+        """layer loop: 0 five launches, 2 full persistent layer, 3 attention
+        launch + persistent chain, 1 the form measured fastest for the batch;
+        returns whether a persistent form is now in use"""
         check(lib().gpt2_decode_set_layer_kernel(self.h, int(on)), "set_layer_kernel")
         return bool(lib().gpt2_decode_layer_kernel(self.h))
 
     def layer_kernel(self):
         return bool(lib().gpt2_decode_layer_kernel(self.h))
+
+    def layer_form(self):
+        """0 five launches per layer, 1 full persistent layer, 2 attention launch + persistent chain"""
+        return int(lib().gpt2_decode_layer_kernel(self.h))
 
     def status(self):
         """waits for queued work; raises if a persistent-layer wait timed out"""

@@ -29,7 +29,7 @@ SMALL = dict(maxT=256, V=1000, L=2, NH=2, C=128)
 GPT2_124M = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
 
 
-def _model(hip, cfgd, params, B, P, layer, kv_dtype=0, splits_env=None):
+def _model(hip, cfgd, params, B, P, layer, kv_dtype=0, splits_env=None, mode=2):
     if splits_env is not None:
         os.environ["HPA_LAYER_SPLITS"] = str(splits_env)
     try:
@@ -37,20 +37,22 @@ def _model(hip, cfgd, params, B, P, layer, kv_dtype=0, splits_env=None):
         m.decode_init(B, P, cfgd["maxT"], kv_dtype=kv_dtype)
     finally:
         os.environ.pop("HPA_LAYER_SPLITS", None)
-    assert m.set_layer_kernel(2 if layer else 0) == bool(layer)  # 2: at every batch it supports
+    # mode 2: the full persistent layer at every batch it supports; 3: the
+    # attention's own launch + the persistent GEMM chain
+    assert m.set_layer_kernel(mode if layer else 0) == bool(layer)
     m.set_graph(True)
     return m
 
 
-@pytest.mark.parametrize("B", [64, 32, 16, 8])
-def test_persistent_layer_matches_launch_path_124m(hip, B):
+@pytest.mark.parametrize("B,mode", [(64, 2), (32, 2), (16, 2), (8, 2), (64, 3), (40, 3), (8, 3)])
+def test_persistent_layer_matches_launch_path_124m(hip, B, mode):
     params = synth.params(GPT2_124M, seed=31)
     ctx = 990
     rng = np.random.default_rng(B)
     toks = rng.integers(0, GPT2_124M["V"], (6, B)).astype(np.int32)
     out = []
     for layer in (1, 0):
-        m = _model(hip, GPT2_124M, params, B, 16, layer)
+        m = _model(hip, GPT2_124M, params, B, 16, layer, mode=mode)
         hip.check(hip.lib().gpt2_decode_fill_random(m.h, ctx, 5), "fill_random")
         lg, ids = [], []
         for t in range(toks.shape[0]):
@@ -65,17 +67,17 @@ def test_persistent_layer_matches_launch_path_124m(hip, B):
     s = np.sort(ll, axis=-1)
     margin = s[..., -1] - s[..., -2]
     clear = margin > 4 * diff
-    print(f"B={B}: max |logit diff| persistent vs launches {diff:.3e}; near-ties {int((~clear).sum())}")
+    print(f"B={B} mode {mode}: max |logit diff| persistent vs launches {diff:.3e}; near-ties {int((~clear).sum())}")
     assert diff <= 2e-5, diff
     assert np.array_equal(ip[clear], il[clear])
 
 
-@pytest.mark.parametrize("P", [8, 16, 32, 64])
-def test_persistent_layer_small_model_matches_oracle(hip, P):
+@pytest.mark.parametrize("P,mode", [(8, 2), (16, 2), (32, 2), (64, 2), (16, 3), (8, 3)])
+def test_persistent_layer_small_model_matches_oracle(hip, P, mode):
     """greedy decode across page boundaries and many 64-token attention tiles"""
     params = synth.params(SMALL, seed=40 + P)
     B, steps = 5, 150
-    m = _model(hip, SMALL, params, B, P, 1)
+    m = _model(hip, SMALL, params, B, P, 1, mode=mode)
     c = oc.cfg(SMALL["maxT"], SMALL["V"], SMALL["L"], SMALL["NH"], SMALL["C"])
     orc = oc.PagedDecoder(params, c, B, P, SMALL["maxT"], page_seed=P)
     tok = np.random.default_rng(P).integers(0, SMALL["V"], B).astype(np.int32)

@@ -1,7 +1,8 @@
 """Phase timeline of the persistent decode layer (hpa_layer.hip), from the
 trace build's per-(layer, workgroup) s_memrealtime stamps.
 
-usage: HPA_LIB=llm.c-paged_amd/libpaged_hip_trace.so python tools/pl_trace.py [B] [ctx]
+usage: HPA_LIB=llm.c-paged_amd/libpaged_hip_trace.so python tools/pl_trace.py [B] [ctx] [mode]
+(mode: 2 full persistent layer, default; 3 attention launch + persistent chain)
 
 Prints, per event, the min / median / max over workgroups of the time since
 the earliest kernel-start stamp of that layer (us), averaged over layers 1..L-2
@@ -25,11 +26,12 @@ EVENTS = ["start", "A issued", "A unit done", "A barrier", "B wait done", "B don
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
     ctx = int(sys.argv[2]) if len(sys.argv) > 2 else 990
+    mode = int(sys.argv[3]) if len(sys.argv) > 3 else 2
     cfg = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
     hip.init(0)
     m = hip.Model(cfg, params=synth.params(cfg, seed=3))
     m.decode_init(B, 16, cfg["maxT"])
-    assert m.set_layer_kernel(2), "persistent layer not in use"
+    assert m.set_layer_kernel(mode), "persistent layer not in use"
     m.set_graph(True)
     hip.check(hip.lib().gpt2_decode_fill_random(m.h, ctx, 5), "fill")
     toks = np.random.default_rng(1).integers(0, cfg["V"], B).astype(np.int32)
@@ -53,7 +55,7 @@ def main():
             v = v[v > 0]
             if len(v):
                 rows[k].append(((v - t0) / 100.0))
-    print(f"B={B} ctx={ctx}: launch span (first start -> last end) {np.mean(spans):.1f} us "
+    print(f"B={B} ctx={ctx} mode={mode}: launch span (first start -> last end) {np.mean(spans):.1f} us "
           f"(layers 1..{cfg['L'] - 2}, last step)")
     print(f"{'event':14s} {'n':>4s} {'min':>7s} {'med':>7s} {'max':>7s}  us")
     for k, name in enumerate(EVENTS):
