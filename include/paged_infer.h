@@ -184,6 +184,9 @@ int  gpt2_decode_prefill_ragged(GPT2* model, const int* tokens, const int* lens,
 int  gpt2_decode_release(GPT2* model, int seq);
 /* the same, but enqueue only (no host sync; next ids stay on device) */
 int  gpt2_decode_step_async(GPT2* model, const int* tokens);
+/* one eager step that also copies the residual stream entering every layer
+ * and the final one to host_x, row-major [L+1][B][C] (per-layer parity tests) */
+int  gpt2_decode_step_traced(GPT2* model, const int* tokens, int* next_tokens, float* host_x);
 /* free every sequence's pages and rewind positions to 0 */
 int  gpt2_decode_reset(GPT2* model);
 /* synthetic K/V for positions [0, ctx) of every sequence (benchmark prefill) */

@@ -662,6 +662,9 @@ struct GPT2Decode {
      * fits, the logits of every position [B][max_ctx][V] (managed) */
     int* h_hist;
     float* pos_logits;
+    /* gpt2_decode_step_traced: the residual stream entering every layer and
+     * the final one, row-major [L+1][B][C], written during that one step */
+    float* trace_x;
 };
 
 /* the manager's page index -> pool slot: a fixed pseudo-random permutation,
@@ -1289,13 +1292,18 @@ static int dec_launch(GPT2* model) {
     GPT2Decode* d = model->decode;
     const ParameterTensors* w = &model->params;
     const int L = model->config.num_layers;
-    int rc = hpa_embed_frag(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, model->config.channels);
+    const int C = model->config.channels;
+    int rc = hpa_embed_frag(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C);
+#define DEC_TRACE(i) \
+    if (d->trace_x) rc |= hpa_unpack_frag(d->res, d->B, C, d->trace_x + (size_t)(i) * d->B * C, C)
+    DEC_TRACE(0);
     if (d->pl_on && !d->profiling) { /* qkv(0), then one persistent launch per layer */
         rc |= dec_gemm(model, 0, G_QKV);
         rc |= hpa_memset_async(d->pl_ctr, 0, (size_t)L * d->pl_ctr_ints * sizeof(int));
         for (int l = 0; l < L && !rc; l++) {
             if (d->pl_on == 2) rc |= dec_attention(model, l); /* chain form: the attention's own launch */
             rc |= dec_layer(model, l);
+            DEC_TRACE(l + 1);
         }
         rc |= dec_gemm(model, 0, G_LOGITS);
         rc |= dec_pick(model, NULL);
@@ -1307,7 +1315,9 @@ static int dec_launch(GPT2* model) {
         rc |= dec_gemm(model, l, G_ATTPROJ);
         rc |= dec_gemm(model, l, G_FC);
         rc |= dec_gemm(model, l, G_FCPROJ);
+        DEC_TRACE(l + 1);
     }
+#undef DEC_TRACE
     rc |= dec_gemm(model, 0, G_LOGITS);
     rc |= dec_pick(model, NULL);
     return rc;
@@ -1380,7 +1390,7 @@ static int dec_enqueue(GPT2* model, const int* tokens) {
     if (dec_ensure_pages(d)) return 1;
     if (dec_sync_block_table(d)) return 1;
     if (tokens && dec_upload_tokens(d, tokens)) return 1;
-    if (d->use_graph && !d->profiling) {
+    if (d->use_graph && !d->profiling && !d->trace_x) {
         if (!d->graph) {
             if (hpa_graph_begin()) return 1;
             const int rc = dec_launch(model);
@@ -1605,6 +1615,23 @@ int gpt2_decode_step(GPT2* model, const int* tokens, int* next_tokens) {
         memcpy(next_tokens, d->h_next, d->B * sizeof(int));
     }
     return 0;
+}
+
+/* one step, eager, that also writes the residual stream entering every
+ * layer and the final one (the rows LNf reads) to host_x [L+1][B][C]: the
+ * per-layer parity tests hand it to the oracle (oracle_paged_step_ex) so that
+ * each layer is checked on the GPU's own input */
+int gpt2_decode_step_traced(GPT2* model, const int* tokens, int* next_tokens, float* host_x) {
+    GPT2Decode* d = model->decode;
+    if (!d || !host_x) return 1;
+    const size_t n = (size_t)(model->config.num_layers + 1) * d->B * model->config.channels;
+    d->trace_x = (float*)hpa_malloc(n * sizeof(float));
+    if (!d->trace_x) return 1;
+    int rc = gpt2_decode_step(model, tokens, next_tokens);
+    rc |= hpa_memcpy(host_x, d->trace_x, n * sizeof(float));
+    hpa_free(d->trace_x);
+    d->trace_x = NULL;
+    return rc;
 }
 
 int gpt2_decode_status(GPT2* model) {

@@ -223,6 +223,7 @@ def lib():
     _sig(L, "hpa_gather_rows_frag", i, [_F, _F, i, _I, i, _F, _F, i, i])
     _sig(L, "gpt2_decode_step", i, [v, _I, _I])
     _sig(L, "gpt2_decode_step_async", i, [v, _I])
+    _sig(L, "gpt2_decode_step_traced", i, [v, _I, _I, _F])
     _sig(L, "gpt2_decode_reset", i, [v])
     _sig(L, "gpt2_decode_fill_random", i, [v, i, ctypes.c_ulonglong])
     _sig(L, "gpt2_decode_set_graph", i, [v, i])
@@ -552,6 +553,19 @@ class Model:
         check(lib().gpt2_decode_step(self.h, tp, nxt.ctypes.data_as(_I) if want_next else None),
               "gpt2_decode_step")
         return nxt
+
+    def step_traced(self, tokens=None):
+        """one eager step; returns (next ids, the residual stream entering every
+        layer and the final one, (L+1, B, C))"""
+        nxt = np.zeros(self.B, np.int32)
+        xs = np.zeros((self.cfg.num_layers + 1, self.B, self.cfg.channels), np.float32)
+        tp = None
+        if tokens is not None:
+            tokens = np.ascontiguousarray(tokens, np.int32)
+            tp = tokens.ctypes.data_as(_I)
+        check(lib().gpt2_decode_step_traced(self.h, tp, nxt.ctypes.data_as(_I), xs.ctypes.data_as(_F)),
+              "gpt2_decode_step_traced")
+        return nxt, xs
 
     def step_async(self, tokens=None):
         tp = None

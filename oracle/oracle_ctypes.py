@@ -60,6 +60,8 @@ def lib(fast=False):
     L.oracle_paged_set_kv.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _F, _F]
     L.oracle_paged_step.restype = ctypes.c_int
     L.oracle_paged_step.argtypes = [ctypes.c_void_p, _I, _F, _I]
+    L.oracle_paged_step_ex.restype = ctypes.c_int
+    L.oracle_paged_step_ex.argtypes = [ctypes.c_void_p, _I, _F, _F, _F, _I]
     L.oracle_paged_fill_random.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_ulonglong]
     L.oracle_paged_pos.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.oracle_paged_pos.restype = ctypes.c_int
@@ -160,6 +162,24 @@ class PagedDecoder:
         if rc != 0:
             raise RuntimeError("oracle_paged_step failed (context full)")
         return nxt, logits
+
+    def step_forced(self, tokens, forced_x):
+        """one step with layer l's input taken from forced_x[l] ((L+1, B, C):
+        the GPU engine's residual stream, gpt2_decode_step_traced; forced_x[L]
+        feeds LNf); returns next ids, logits and every layer's output (L, B, C)"""
+        tokens = np.ascontiguousarray(tokens, np.int32)
+        Lc, C = self.c.num_layers, self.c.channels
+        fx = None
+        if forced_x is not None:  # None: the decoder's own stream (layer outputs still returned)
+            fx = np.ascontiguousarray(forced_x, np.float32)
+            assert fx.shape == (Lc + 1, self.B, C)
+        nxt = np.zeros(self.B, np.int32)
+        logits = np.zeros((self.B, self.c.vocab_size), np.float32)
+        out = np.zeros((Lc, self.B, C), np.float32)
+        if self.L.oracle_paged_step_ex(self.h, ip(tokens), fp(fx) if fx is not None else None, fp(out), fp(logits),
+                                       ip(nxt)) != 0:
+            raise RuntimeError("oracle_paged_step_ex failed (context full)")
+        return nxt, logits, out
 
     def set_kv(self, layer, b, k, v):
         """positions [0, len(k)) of sequence b at `layer` take these K/V rows

@@ -503,6 +503,17 @@ int oracle_paged_set_kv(OraclePaged* o, int layer, int b, int n, const float* k,
 }
 
 int oracle_paged_step(OraclePaged* o, const int* tokens, float* logits, int* next) {
+    return oracle_paged_step_ex(o, tokens, NULL, NULL, logits, next);
+}
+
+/* forced_x (nullable, [L+1][B][C]): the residual stream entering layer l is
+ * taken from forced_x[l] (and the final one, LNf's input, from forced_x[L])
+ * instead of this decoder's own previous layer -- each layer then runs on the
+ * GPU engine's input (gpt2_decode_step_traced), so a per-layer comparison is
+ * not compounded over layers; layer_out (nullable, [L][B][C]) receives every
+ * layer's output.  The K/V appended are those computed from the forced input. */
+int oracle_paged_step_ex(OraclePaged* o, const int* tokens, const float* forced_x, float* layer_out,
+                         float* logits, int* next) {
     OracleConfig cfg = o->cfg;
     int B = o->B, C = cfg.channels, NH = cfg.num_heads, L = cfg.num_layers, V = cfg.vocab_size;
     int hs = C / NH;
@@ -527,6 +538,7 @@ int oracle_paged_step(OraclePaged* o, const int* tokens, float* logits, int* nex
         const float* fcb = P + o->off[11] + (size_t)l * 4 * C;
         const float* fpw = PW + o->off[12] + (size_t)l * C * 4 * C;
         const float* fpb = P + o->off[13] + (size_t)l * C;
+        if (forced_x) memcpy(o->x, forced_x + (size_t)l * B * C, (size_t)B * C * 4);
         oracle_layernorm_forward(o->ln, NULL, NULL, o->x, ln1w, ln1b, B, 1, C);
         round_bf16_n(o, o->ln, (size_t)B * C);
         /* decode QKV = matmul_cached's last row (paged_infer.c:117-160) */
@@ -575,7 +587,9 @@ int oracle_paged_step(OraclePaged* o, const int* tokens, float* logits, int* nex
         round_bf16_n(o, o->fchg, (size_t)B * 4 * C);
         matmul_rows_ocpar(o->tmp, o->fchg, fpw, fpb, B, 4 * C, C);
         oracle_residual_forward(o->x, o->res2, o->tmp, B * C);
+        if (layer_out) memcpy(layer_out + (size_t)l * B * C, o->x, (size_t)B * C * 4);
     }
+    if (forced_x) memcpy(o->x, forced_x + (size_t)L * B * C, (size_t)B * C * 4);
     oracle_layernorm_forward(o->ln, NULL, NULL, o->x, P + o->off[14], P + o->off[15], B, 1, C);
     round_bf16_n(o, o->ln, (size_t)B * C);
     float* lg = logits ? logits : o->logits;

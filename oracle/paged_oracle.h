@@ -93,6 +93,10 @@ OraclePaged* oracle_paged_create(const float* params, OracleConfig cfg, int B, i
  * (matmul_forward with wte, :727); next[b] = argmax(logits[b]).  logits may
  * be NULL.  Returns 0, or -1 when a sequence would exceed max_ctx. */
 int  oracle_paged_step(OraclePaged* o, const int* tokens, float* logits, int* next);
+/* the step with each layer's input taken from forced_x [L+1][B][C] (nullable)
+ * and every layer's output written to layer_out [L][B][C] (nullable) */
+int  oracle_paged_step_ex(OraclePaged* o, const int* tokens, const float* forced_x, float* layer_out,
+                          float* logits, int* next);
 /* synthetic K/V fill: set every pos[b] = ctx and fill those slots with U(-1,1)
  * (the bounded CPU-baseline sample; bench.py only). */
 void oracle_paged_fill_random(OraclePaged* o, int ctx, unsigned long long seed);

@@ -157,3 +157,39 @@ def test_oracle_bf16_kv_decode_is_close_to_fp32():
     a.close()
     b.close()
     assert 0.0 < worst < 5e-2
+
+
+@pytest.mark.parametrize("w_bf16", [False, True])
+def test_forced_step_on_own_stream_is_the_plain_step(w_bf16):
+    """oracle_paged_step_ex fed its own residual stream (embedding, then each
+    layer's output) reproduces the plain step bit for bit: the forced input is
+    the only thing it changes, so a per-layer GPU check through it measures
+    one layer's arithmetic at a time"""
+    g = load("forward_golden.npz")
+    c = oc.cfg(*[int(x) for x in g["cfg"]])
+    params = g["params"]
+    tokens = g["tokens"]
+    B, T = tokens.shape
+    Cn = c.channels
+    off = (ctypes_offsets(c))
+    wte = params[off[0]:off[0] + c.vocab_size * Cn].reshape(c.vocab_size, Cn)
+    wpe = params[off[1]:off[1] + c.max_seq_len * Cn].reshape(c.max_seq_len, Cn)
+    a = oc.PagedDecoder(params, c, B, 8, 64, page_seed=3, w_bf16=w_bf16)
+    b = oc.PagedDecoder(params, c, B, 8, 64, page_seed=3, w_bf16=w_bf16)
+    for t in range(T):
+        na, la, outs = a.step_forced(tokens[:, t], None)
+        emb = wte[tokens[:, t]] + wpe[t]
+        xs = np.concatenate([emb[None], outs], axis=0)
+        nb, lb, outs_b = b.step_forced(tokens[:, t], xs)
+        assert np.array_equal(la, lb) and np.array_equal(na, nb) and np.array_equal(outs, outs_b), t
+        if not w_bf16:
+            assert np.array_equal(la, g["logits"][:, t]), t
+    a.close()
+    b.close()
+
+
+def ctypes_offsets(c):
+    import ctypes
+    off = (ctypes.c_size_t * 16)()
+    oc.lib().oracle_param_offsets(c, off)
+    return [int(x) for x in off]
