@@ -276,15 +276,20 @@ int hpa_fused_pick_waves(int M, int N, int K);
  * The decode step's layer loop (reference gpt2_forward, paged_infer.c:659-722)
  * as ONE launch per layer l instead of five:
  *   attention(l) -> attproj(l) -> fc(l) -> fcproj(l) -> qkv(l+1)
- * One 16-wave workgroup per CU, all resident; the phases hand off through
- * write-through (sc1) stores and agent-scope arrival counters inside the
- * launch.  Each workgroup owns a fixed slice ("granule": a 16-column tile and
- * a K range) of every GEMM; the attproj / fc / fcproj slices are copied into
- * its LDS while the attention streams K/V, so the GEMM phases read only the
- * activations.  attproj and fcproj are split over K (parts), and the last part
- * of a (row block, column tile) to arrive sums the parts in part order.  qkv
- * and fc use the one-shot kernel's summation order (4 waves x K/4, folded in
- * wave order): their rows are bit-identical to the launch path.
+ * or, chain_only, the decode attention as its own launch before and one
+ * launch of attproj(l) -> fc(l) -> fcproj(l) -> qkv(l+1) (the engine's
+ * default form: measured faster at every batch, profiles/r3/pl_ab.txt).
+ * One 12-wave workgroup per CU (grid = CU count, residency checked with the
+ * occupancy API), split into three 4-wave slots; every phase deals its units
+ * (a 16x16 output tile over a K range, or an attention unit) one per slot.
+ * Each slot loads its next phase's weight fragments into registers BEFORE
+ * that phase's wait, so the weight stream overlaps the hand-off.  Hand-offs
+ * inside the launch: write-through (sc1) stores, drained, one agent-scope
+ * arrival per workgroup on a counter sharded 8 ways, polled with sc1 loads
+ * (MI355X_MICROARCH.md "Valid forms", row 1).  fcproj is split over K into 4
+ * parts and the last part of a tile to draw its ticket adds the parts in part
+ * order.  qkv and fc follow the one-shot kernel's summation order (4 waves x
+ * K/4, folded in wave order): their rows are bit-identical to the launch path.
  * fp32 frag-packed weights with the LayerNorms folded (hpa_ln_fold_pack);
  * C = 128 or 768 (num_heads 2 or 12), B <= 64, B*num_heads*splits <= 3 x CUs.
  * Every spin is bounded (200 ms): a timeout stores a nonzero code in *err and

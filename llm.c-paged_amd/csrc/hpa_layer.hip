@@ -10,31 +10,25 @@
 // so a step is embed, qkv(0), L of these, logits, token choice.
 //
 // Why ("Persistent layer"): every launch of the
-// five-kernel layer pays a fixed dispatch + first-HBM-round-trip + drain cost
-// (~3 us) and the GEMMs fetch their weights from HBM only after the previous
-// kernel has ended.  Here the workgroup of each CU copies its slices of the
-// attproj / fc / fcproj weights into LDS while the attention streams K/V
-// (slot 3 below), so the GEMM phases read only the activations, and the seams
+// five-kernel layer pays a dispatch + first-round-trip + drain cost, and each
+// GEMM starts fetching its weights only after the previous kernel ended.
+// Here every phase's weight fragments are loaded into registers before the
+// phase's wait, so the weight stream overlaps the hand-off, and the seams
 // between phases are in-launch hand-offs.
 //
-// Geometry: one workgroup of 16 waves per CU (grid = CU count), all resident
-// (checked with the occupancy API).  In phase A the waves form four 4-wave
-// slots; slots 0..2 each run one attention unit (sequence, head, context
-// range: the split-context decomposition of hpa_attn.hip, with its
-// last-arriver merge), slot 3 stages the weights.  In the GEMM phases the
-// waves form four row-block groups (group g = rows 16g..16g+15), each of 4
-// waves splitting the granule's K range exactly like the one-shot kernel
-// (gemm16_os_kernel<4, *, K16/4>), so qkv and fc rows are bit-identical to the
-// launch path.
-//
-// Granules (fixed per workgroup, i.e. per CU):
-//   attproj  (column tile j, K part p of AP)   on workgroups [0, N_AP)
-//   fc       (column tile j, all K)            on workgroups [0, N_FC)
-//   fcproj   (column tile j, K part p of 4)    on workgroups [G - N_FP, G)
-//   qkv      (column tile j, all K)            on workgroups [0, N_QKV)
-// K-part partial tiles go to a slab with write-through stores; the last part
-// of a (row block, column tile) to draw its ticket sums the parts in part
-// order (results independent of arrival order), adds bias and residual.
+// Geometry: one workgroup of 12 waves per CU (grid = CU count, residency
+// checked with the occupancy API), three 4-wave slots.  A phase's units are
+// numbered v and dealt v -> (workgroup v % G, slot v / G):
+//   A  attention unit (sequence, head, context range; hpa_attn_body.h tiles,
+//      folded through LDS by the slot's last wave, split_merge across ranges)
+//   B..E  a 16x16 output tile (row block rb, column tile j) over K = C (fc,
+//      qkv, attproj) or one of 4 K parts of 4C (fcproj), 4 waves x K/4 each
+//      -- the one-shot GEMM kernel's summation order.
+// ATTN = false (chain form, the engine's default): no phase A; the attention
+// ran as its own launch just before, writing att in frag layout.
+// fcproj's K-part partial tiles go to a slab with write-through stores; the
+// last part of a tile to draw its ticket sums the parts in part order
+// (results independent of arrival order), adds bias and residual.
 //
 // Hand-offs (MI355X_MICROARCH.md "Valid forms", row 1; cdna_hip_programming.md
 // Guideline 16): every byte handed over inside the launch is stored sc1
