@@ -70,7 +70,9 @@ int   hpa_graph_begin(void);
 void* hpa_graph_end(void);               /* instantiated executable graph, NULL on failure */
 int   hpa_graph_launch(void* graph_exec);
 int   hpa_graph_destroy(void* graph_exec);
-/* waves per (sequence, head) workgroup of the decode attention: 1, 2, 4, 8 */
+/* waves per (sequence, head) workgroup of every decode attention launch of
+ * the process: 1, 2, 4, 8 (an override for timing tools); 0 (default): the
+ * caller's choice (the engine's hpa_attn_pick_waves, else 4) */
 int   hpa_set_attention_waves(int nw);
 int   hpa_device_info(char* name, int name_len, int* num_cus, size_t* total_mem);
 
@@ -135,6 +137,13 @@ size_t hpa_attn_ws_bytes(int B, int num_heads, int splits);
 /* the engine's choice by shape only (num_cus <= 0: 256): ranges while B*NH*S
  * stays within one workgroup per CU, 2 between one and two per CU, else 1 */
 int hpa_attn_pick_splits(int B, int num_heads, int max_ctx, int num_cus);
+/* the same with the waves per workgroup (0: 4; 1, 2, 4 or 8) -- the engine
+ * passes hpa_attn_pick_waves of its (global) batch */
+int hpa_paged_attention_decode_split_w(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
+                                       int bt_stride, const int* pos, float* out, int B, int splits, void* ws,
+                                       int out_frag, int waves);
+/* 8 when the B*num_heads*splits workgroups fit one per CU, else 4 */
+int hpa_attn_pick_waves(int B, int num_heads, int splits, int num_cus);
 int hpa_paged_attention_decode_split(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
                                      int bt_stride, const int* pos, float* out, int B, int splits, void* ws,
                                      int out_frag);

@@ -135,21 +135,33 @@ int launch_decode(const float* q, const HpaKVPool* pool, int layer, const int* b
     return 0;
 }
 
-int g_attn_waves = 4;
+int g_attn_waves = 0;  // hpa_set_attention_waves: a process-wide override (0: the caller's choice)
 
 }  // namespace
 
 extern "C" {
 
-// waves per (sequence, head) workgroup: 1, 2, 4 (default) or 8
+// waves per (sequence, head) workgroup for every launch of the process: 1,
+// 2, 4 or 8 (timing tools); 0 restores the callers' choice
 int hpa_set_attention_waves(int nw) {
-    HPA_REQUIRE(nw == 1 || nw == 2 || nw == 4 || nw == 8, "attention waves must be 1, 2, 4 or 8");
+    HPA_REQUIRE(nw == 0 || nw == 1 || nw == 2 || nw == 4 || nw == 8, "attention waves must be 0, 1, 2, 4 or 8");
     g_attn_waves = nw;
     return 0;
 }
 
+// 8 waves when the B*NH*S workgroups leave CUs without one (each workgroup
+// then has a CU's memory pipe to itself and its tiles take half the trips),
+// else 4.  tools/attn_scan_r3.py, profiles/r3/attn_scan_r3.txt (ctx 1020):
+// B = 8, S = 2: 13.02 vs 13.66 us; B = 16, S = 1: 19.11 vs 20.26; B = 32,
+// S = 2 (768 workgroups): 38.65 vs 35.33
+int hpa_attn_pick_waves(int B, int num_heads, int splits, int num_cus) {
+    if (num_cus <= 0) num_cus = 256;
+    return (long)B * num_heads * splits <= num_cus ? 8 : 4;
+}
+
 static int attn_dispatch(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
-                         int bt_stride, const int* pos, float* out, int B, bool frag, int S, void* ws) {
+                         int bt_stride, const int* pos, float* out, int B, bool frag, int S, void* ws,
+                         int waves = 0) {
     HPA_REQUIRE(pool && pool->base, "pool not created");
     HPA_REQUIRE(pool->dtype == HPA_F32 || pool->dtype == HPA_BF16, "decode attention: fp32 or bf16 pool");
     HPA_REQUIRE(pool->head_size == HS, "decode attention requires head_size 64");
@@ -159,7 +171,8 @@ static int attn_dispatch(const float* q, const HpaKVPool* pool, int layer, const
     HPA_REQUIRE(S >= 1 && S <= HPA_ATTN_MAX_SPLITS && (S == 1 || ws), "decode attention: splits 1..16, workspace");
     const bool bf = pool->dtype == HPA_BF16;
     float* w = (float*)ws;
-    const int nw = g_attn_waves;
+    HPA_REQUIRE(waves == 0 || waves == 1 || waves == 2 || waves == 4 || waves == 8, "attention waves 1, 2, 4, 8");
+    const int nw = g_attn_waves ? g_attn_waves : waves ? waves : 4;
 #define HPA_ATTN_CASE(PS)                                                                                      \
     case PS:                                                                                                    \
         if (bf)                                                                                                 \
@@ -219,6 +232,12 @@ int hpa_paged_attention_decode_split(const float* q, const HpaKVPool* pool, int 
                                      int bt_stride, const int* pos, float* out, int B, int splits, void* ws,
                                      int out_frag) {
     return attn_dispatch(q, pool, layer, block_table, bt_stride, pos, out, B, out_frag != 0, splits, ws);
+}
+
+int hpa_paged_attention_decode_split_w(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
+                                       int bt_stride, const int* pos, float* out, int B, int splits, void* ws,
+                                       int out_frag, int waves) {
+    return attn_dispatch(q, pool, layer, block_table, bt_stride, pos, out, B, out_frag != 0, splits, ws, waves);
 }
 
 }  // extern "C"

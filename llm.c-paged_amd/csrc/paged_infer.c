@@ -634,6 +634,7 @@ struct GPT2Decode {
     int frb[5];       /* 16-row blocks per workgroup, same order */
     int fct[5];       /* 16-column tiles per workgroup, same order */
     int attn_splits;  /* context ranges per (sequence, head) of the decode attention */
+    int attn_waves;   /* waves per attention workgroup (hpa_attn_pick_waves of the global batch) */
     void* d_attn_ws;  /* split records + counters (hpa_attn_ws_bytes at HPA_ATTN_MAX_SPLITS) */
     size_t attn_ws_bytes;
     int sample;       /* 0: greedy argmax; 1: multinomial with per-sequence xorshift */
@@ -855,6 +856,11 @@ static int dec_set_splits(GPT2Decode* d, int splits) {
     }
     if (d->d_attn_ws && hpa_memset_async(d->d_attn_ws, 0, d->attn_ws_bytes)) return 1;
     d->attn_splits = splits;
+    {   /* the waves follow the batch the picks follow (sharded: the global one) */
+        int ncu = 0;
+        hpa_device_info(NULL, 0, &ncu, NULL);
+        d->attn_waves = hpa_attn_pick_waves(d->pl_global_B > 0 ? d->pl_global_B : d->B, d->pool.num_heads, splits, ncu);
+    }
     if (d->graph) { /* recapture with the new grid */
         hpa_synchronize();
         hpa_graph_destroy(d->graph);
@@ -1275,8 +1281,8 @@ static int dec_attention(GPT2* model, int l) {
     GPT2Decode* d = model->decode;
     int rc = 0;
     if (d->profiling) rc |= hpa_event_record(d->prof_ev[0]);
-    rc |= hpa_paged_attention_decode_split(d->d_q, &d->pool, l, d->d_bt, d->bt_stride, d->d_pos, d->att, d->B,
-                                           d->attn_splits, d->d_attn_ws, 1);
+    rc |= hpa_paged_attention_decode_split_w(d->d_q, &d->pool, l, d->d_bt, d->bt_stride, d->d_pos, d->att, d->B,
+                                             d->attn_splits, d->d_attn_ws, 1, d->attn_waves);
     if (d->profiling) {
         rc |= hpa_event_record(d->prof_ev[1]);
         const float ms = hpa_event_elapsed_ms(d->prof_ev[0], d->prof_ev[1]); /* waits for this launch */
@@ -1824,12 +1830,12 @@ int gpt2_decode_time_attention(GPT2* model, int iters, double* ms_per_launch, do
         for (int b = 0; b < B; b++) h_p[b] = d->h_pos[b] - 1;
         rc |= hpa_memcpy(d_p, h_p, B * sizeof(int));
         /* warm-up launch, then the timed ones */
-        rc |= hpa_paged_attention_decode_split(d->d_q, &d->pool, 0, d->d_bt, d->bt_stride, d_p, out, B,
-                                               d->attn_splits, d->d_attn_ws, 1);
+        rc |= hpa_paged_attention_decode_split_w(d->d_q, &d->pool, 0, d->d_bt, d->bt_stride, d_p, out, B,
+                                                 d->attn_splits, d->d_attn_ws, 1, d->attn_waves);
         rc |= hpa_event_record(e0);
         for (int i = 0; i < iters && !rc; i++)
-            rc |= hpa_paged_attention_decode_split(d->d_q, &d->pool, i % L, d->d_bt, d->bt_stride, d_p, out, B,
-                                                   d->attn_splits, d->d_attn_ws, 1);
+            rc |= hpa_paged_attention_decode_split_w(d->d_q, &d->pool, i % L, d->d_bt, d->bt_stride, d_p, out, B,
+                                                     d->attn_splits, d->d_attn_ws, 1, d->attn_waves);
         rc |= hpa_event_record(e1);
         const float ms = rc ? -1.f : hpa_event_elapsed_ms(e0, e1);
         if (ms < 0) rc = 1;
@@ -1895,9 +1901,9 @@ int gpt2_decode_shard(GPT2* model, const int* rows_per_rank, int root) {
         const GPT2Config c = model->config;
         int ncu = 0;
         hpa_device_info(NULL, 0, &ncu, NULL);
+        d->pl_global_B = (int)tot;
         if (hpa_synchronize() || dec_set_splits(d, hpa_attn_pick_splits((int)tot, c.num_heads, d->max_ctx, ncu)))
             return 1;
-        d->pl_global_B = (int)tot;
         if (dec_layer_setup(model, d)) return 1;
         if (d->graph) {
             hpa_graph_destroy(d->graph);

@@ -59,7 +59,7 @@ def _run_case(hip, P, ctxs, NH, waves=4, seed=0, q_scale=2.0, kv=None, splits=0,
                                                          B, splits, d_ws.ptr if wsb else None, 1), "split attention")
             hip.check(L.hpa_synchronize())
             outs.append(hip.from_frag(d_out.download(Mp * C), B, C))
-        hip.check(L.hpa_set_attention_waves(4))
+        hip.check(L.hpa_set_attention_waves(0))  # back to the callers' choice
         for o in outs[1:]:  # fixed merge order: bit-identical every launch
             assert np.array_equal(o, outs[0])
         # the counters are left zero for the next launch
@@ -71,7 +71,7 @@ def _run_case(hip, P, ctxs, NH, waves=4, seed=0, q_scale=2.0, kv=None, splits=0,
         hip.check(L.hpa_set_attention_waves(waves))
         hip.check(L.hpa_paged_attention_decode(d_q.ptr, pool.ref, 0, d_bt.ptr, maxp, d_pos.ptr, d_out.ptr, B))
         hip.check(L.hpa_synchronize())
-        hip.check(L.hpa_set_attention_waves(4))
+        hip.check(L.hpa_set_attention_waves(0))  # back to the callers' choice
         out = d_out.download((B, C))
     ref = np.zeros_like(out)
     for b, ctx in enumerate(ctxs):
