@@ -150,6 +150,7 @@ def lib():
     _sig(L, "hpa_last_error", ctypes.c_char_p, [])
     _sig(L, "hpa_device_info", i, [ctypes.c_char_p, i, _I, ctypes.POINTER(sz)])
     _sig(L, "hpa_set_attention_waves", i, [i])
+    _sig(L, "hpa_attn_pick_waves", i, [i, i, i, i])
     # pool + kernels
     _sig(L, "hpa_pool_create", i, [P, i, i, i, i, i, i, i])
     _sig(L, "hpa_pool_destroy", None, [P])

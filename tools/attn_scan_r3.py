@@ -26,7 +26,7 @@ for B in batches:
         for s in (1, 2, 4, 8):
             m.set_attn_splits(s)
             ms, by = m.time_attention(48)
-            tag = " (engine)" if s == auto and nw == 4 else ""
+            tag = " (engine)" if s == auto and nw == pa.lib().hpa_attn_pick_waves(B, cfg["NH"], s, 0) else ""
             print(f"B={B:3d} waves={nw} S={s}{tag:9s} {ms * 1e3:7.2f} us {by / ms / 1e6:7.1f} GB/s", flush=True)
     pa.check(pa.lib().hpa_set_attention_waves(0), "waves")  # back to the engine's pick
 m.close()
