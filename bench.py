@@ -135,7 +135,8 @@ def parse():
                     help="attention roofline timing: prof_steps x L back-to-back launches (0 = off)")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="per CPU build (strict and -Ofast)")
-    ap.add_argument("--attn-waves", type=int, default=4)
+    ap.add_argument("--attn-waves", type=int, default=0,
+                    help="waves per attention workgroup for every launch (0 = the engine's pick by batch)")
     ap.add_argument("--attn-splits", type=int, default=0, help="attention context ranges (0 = by shape)")
     ap.add_argument("--layer-kernel", type=int, default=-1, choices=[-1, 0, 1, 2],
                     help="layer loop: 0 five launches per layer, 1 persistent where it measured faster (B <= 32), "
@@ -374,6 +375,7 @@ def main():
                                                                if gather else
                                                                f" (gather: {args.gather})" if world > 1 else ""),
                        "hip_graph": not args.no_graph, "attn_splits": splits,
+                       "attn_waves": args.attn_waves or int(L.hpa_attn_pick_waves(B, cfgd["NH"], splits, cus)),
                        "layer_loop": {0: "five launches per layer",
                                       1: "one persistent launch per layer (hpa_decode_layer)",
                                       2: "attention launch + one persistent launch of the GEMM chain "
