@@ -347,6 +347,10 @@ int hpa_decode_layer(const HpaLayerArgs* a);
  * workgroup) event stamps [layers][256][16] of the last launches (10 ns
  * ticks); host = NULL clears them */
 int hpa_decode_layer_trace(unsigned long long* host, int layers);
+/* diagnostic builds (-DHPA_RG_TRACE) only, else returns 1: the ring logits
+ * kernel's per-workgroup stamps of the last launch: [2][256][24] u64, s_memrealtime
+ * (10 ns ticks) then s_memtime (shader clock) */
+int hpa_logits_trace(unsigned long long* host);
 /* residual = wte[tok] + wpe[pos] in frag layout [Mp][C], stats (1 tile) */
 int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const float* wpe,
                    float* res_frag, float* stats, int B, int C);

@@ -871,6 +871,7 @@ int hpa_logits_kernel(int M, int N, int K) {
     p.N = N;
     p.ntn = ntn;
     p.ln_stats = reinterpret_cast<const float*>(16);  // "LN present": only its presence is read
+    p.ln_ntiles = K16;                                 // the engine's statistics: one per 16 columns
     if (logits_resident_eligible(p, HPA_FEPI_LOGITS)) return 4;
     return sk_eligible(Mp, ntn, K16) ? 6 : 1;
 }

@@ -27,6 +27,8 @@
 // waves of 3 k-steps 62.7 us per launch, of which the LDS fold was ~30 us
 // that the MFMAs could not hide (tools/logits_exp.sh: 33.9 us without the
 // fold, 36.6 us without the MFMAs); 8 waves halve the fold.
+#include <type_traits>
+
 #include "hpa_gemm_body.h"
 #ifndef HPA_RES_EXP
 #define HPA_RES_EXP 0  // timing experiments (tools/logits_exp.sh); 0 in the product
@@ -249,11 +251,389 @@ __global__ __launch_bounds__(kResNW * 64) void logits_resident_kernel(FG p) {
     }
 }
 
+// ---- ring form (round 3): rows split over waves, wte through an LDS ring ----
+// The 16-wave form above splits K over 16 waves, so every 16x16 output tile
+// is folded from 16 partial tiles through LDS behind a barrier that all
+// waves reach together: the matrix pipes idle through each fold (MFMA busy
+// 50 %, profiles/r3/mfma_c2.txt).  Here the ROWS are split instead:
+//   * 8 waves (2 per SIMD); at 64 rows wave w owns row block w & 3 and K
+//     parts {2h, 2h+1} (h = w >> 2) of the 4 parts of 192, i.e. 96 VGPRs of
+//     LNf(x), with one accumulator per part (two independent MFMA chains);
+//   * the column tile's 48 KiB of wte is streamed ONCE per workgroup into a
+//     3-stage LDS ring by LDS-DMA (global_load_lds_dwordx4, non-temporal),
+//     two tiles ahead, by the upper four waves (12 wave-instructions each
+//     per tile, one per k-step); every wave reads its B fragments of the
+//     tile from the ring with ds_read_b128 right after the tile's barrier;
+//   * a tile's result is (p0 + p1) + (p2 + p3) over the 4 K parts: the wave
+//     of h = 1 publishes (p2 + p3) (1 KiB) into a double-buffered fold slot;
+//     the owner (h = 0) adds it in the NEXT iteration, after that
+//     iteration's one barrier, so the epilogue (store, running argmax)
+//     overlaps the partner's MFMAs; the per-row argmax keeps a running
+//     (max, column) per lane and reduces the 16 lanes once at the end.
+// Fewer rows (16 / 32) keep the same per-row arithmetic: one part per wave
+// and three published partials, summed in the same order, so a row's logits
+// are bit-identical at every batch size (sharded decode = unsharded).
+// Roles: owners (h = 0) store, the loader waves (w >= 4: never owners) wait
+// on their own DMA with a counted vmcnt before the barrier.
+// Measured per tile (tools/rg_trace.py, s_memtime): the MFMAs alone 3.1 us
+// at the ~2.1 GHz the chip holds under this load (6144 MFMA cycles per
+// SIMD), the DMA alone 1.9 us (25 GB/s per CU).
+// diagnostic build (-DHPA_RG_TRACE, tools/rg_trace.py): stamps per workgroup
+// -- [0] start, [1] prologue done, [2..15] iteration starts (after the
+// barrier), [16] loop end, [17] end -- as s_memrealtime (10 ns) and
+// s_memtime (shader clock); sums over the iterations (10 ns ticks): [18]
+// wave 4 (a loader) in its vmcnt wait, [19] wave 0 in the barrier, [20]
+// wave 0 and [21] wave 4 from the barrier to their fold write; never in the
+// product library
+#ifdef HPA_RG_TRACE
+__device__ unsigned long long g_rg_trace[2][256][24];
+#define RG_MARK(k)                                                                                     \
+    do {                                                                                               \
+        if (threadIdx.x == 0 && blockIdx.x < 256) {                                                    \
+            g_rg_trace[0][blockIdx.x][k] = (unsigned long long)__builtin_amdgcn_s_memrealtime();       \
+            g_rg_trace[1][blockIdx.x][k] = (unsigned long long)__builtin_amdgcn_s_memtime();           \
+        }                                                                                              \
+    } while (0)
+#else
+#define RG_MARK(k) \
+    do {           \
+    } while (0)
+#endif
+constexpr int kRgNW = 8;
+constexpr int kRgK16 = 48;               // K = 768
+constexpr int kRgPart = 12;              // k16-steps per K part (4 parts)
+constexpr int kRgTileF = kRgK16 * 256;   // floats per 16-column wte tile (48 KiB)
+constexpr int kRgLoaders = kRgNW / 2;    // waves kRgNW/2 .. kRgNW-1 load the ring
+constexpr int kRgDma = kRgK16 / kRgLoaders;  // LDS-DMA wave-instructions per loader per tile (12)
+constexpr int kRgFoldF = 1536;           // floats per fold buffer (max over MT)
+constexpr int kRgStages = 3;
+constexpr int kRgLdsF = kRgStages * kRgTileF + 2 * kRgFoldF + 10 * 64;
+static_assert(kRgLdsF * 4 <= 160 * 1024, "LDS");
+static_assert(kRgDma == kRgPart, "one DMA per k-step");
+
+template <int MT>
+struct RgShape {
+    static constexpr int MTS = MT == 3 ? 4 : MT;  // row-block slots
+    static constexpr int NPW = MTS == 4 ? 2 : 1;  // K parts per wave
+    static constexpr int NWC = MTS * 4 / NPW;     // computing waves: 4 (MT 1) or 8
+    static constexpr int NSLOT = 4 / NPW - 1;     // published partials per row block
+    static_assert(MTS * NSLOT * 256 <= kRgFoldF, "fold buffer");
+    static_assert(MTS <= kRgLoaders, "owners are never loaders");
+};
+
+// LDS-DMA of 1 KiB (16 B per lane to lds_addr + 16 * lane), non-temporal.
+// Inline asm, so hipcc does not see it: with the builtin it waits vmcnt(0)
+// before every ds_read of the ring (it cannot tell the stages apart), which
+// drains the prefetch; the kernel counts these loads itself.
+__device__ __forceinline__ void rg_dma(const float* src, unsigned lds_addr) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_addr)
+                 : "memory");
+}
+
+// (max, lowest index) step of the per-row butterfly, branch-free
+template <int CTRL>
+__device__ __forceinline__ void rg_argmax(float& bv, int& bi) {
+    const float v2 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(bv), CTRL, 0xF, 0xF, false));
+    const int i2 = __builtin_amdgcn_mov_dpp(bi, CTRL, 0xF, 0xF, false);
+    const bool take = (v2 > bv) | ((v2 == bv) & (i2 < bi));
+    bv = take ? v2 : bv;
+    bi = take ? i2 : bi;
+}
+
+template <int MT>
+__global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
+    using S = RgShape<MT>;
+    constexpr int NPW = S::NPW;
+    constexpr int R = MT * 16;
+    __shared__ __attribute__((aligned(16))) float smem[kRgLdsF];
+    float* ring = smem;                          // [3][48 k16][64 lanes][4]
+    float* fold = smem + kRgStages * kRgTileF;   // [2][row block][slot][64 lanes][4]
+    float* lnst = fold + 2 * kRgFoldF;           // [R][2] mean, rstd
+    float* lnscr = lnst + 2 * 64;                // [4R][2]
+    float* lngb = ring + 2 * kRgTileF;           // prologue only: LNf gamma, beta (stage 2 is idle)
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = w % S::MTS;                  // row block
+    const int h = (w / S::MTS) % (4 / NPW);    // part group
+    const bool rvalid = w < S::NWC && r < MT;
+    const bool owner = rvalid && h == 0;
+    const bool loader = w >= kRgNW - kRgLoaders;
+    const int G = gridDim.x;
+    const int ntn = p.ntn;
+    int t = blockIdx.x;
+
+    const float* wl = p.w + lane * 4 + (w - (kRgNW - kRgLoaders)) * 256;  // loaders: their 1 KiB chunks
+    const unsigned ring_lds = __builtin_amdgcn_readfirstlane(
+        (unsigned)(size_t)(__attribute__((address_space(3))) float*)ring);
+    // loader chunk j of a tile = k16-step (w - 4) + 4 j
+    auto dma_src = [&](int tile) __attribute__((always_inline)) {
+        return wl + (size_t)min(tile, ntn - 1) * kRgTileF;  // past the end: a harmless repeat
+    };
+    auto dma_dst = [&](int stage) __attribute__((always_inline)) {
+        return ring_lds + (unsigned)(stage * kRgTileF + (w - (kRgNW - kRgLoaders)) * 256) * 4;
+    };
+    RG_MARK(0);
+    if (loader) {  // tile 0 lands during the LN prologue; tile 1 is issued after it
+        const float* src = dma_src(t);
+        const unsigned dst = dma_dst(0);
+#pragma unroll
+        for (int j = 0; j < kRgDma; ++j) rg_dma(src + kRgLoaders * j * 256, dst + kRgLoaders * j * 1024);
+    }
+
+    // prologue loads, all in flight together: LNf statistics partials, the
+    // wave's raw activations, LNf gamma / beta (into LDS)
+    if (threadIdx.x < 4 * R) {
+        // the same partial-sum order as gemm16_body: thread (row, q) sums
+        // tiles q, q + 4, ..., q + 44 in order (K = 768: 48 tiles)
+        const int rr = threadIdx.x >> 2, q = threadIdx.x & 3;
+        float s1 = 0.f, s2 = 0.f;
+        if (rr < p.M) {
+            float2 xs[kRgK16 / 4];
+            const float2* ls = reinterpret_cast<const float2*>(p.ln_stats) + rr;
+#pragma unroll
+            for (int j = 0; j < kRgK16 / 4; ++j) xs[j] = ls[(size_t)(q + 4 * j) * p.Mp];
+#pragma unroll
+            for (int j = 0; j < kRgK16 / 4; ++j) {
+                s1 += xs[j].x;
+                s2 += xs[j].y;
+            }
+        }
+        lnscr[2 * threadIdx.x] = s1;
+        lnscr[2 * threadIdx.x + 1] = s2;
+    }
+    if (threadIdx.x < 2 * kRgK16 * 4) {  // 192 float4 of gamma, then 192 of beta
+        const float4* src = reinterpret_cast<const float4*>(threadIdx.x < kRgK16 * 4 ? p.ln_w : p.ln_b);
+        reinterpret_cast<float4*>(lngb)[threadIdx.x] = src[threadIdx.x % (kRgK16 * 4)];
+    }
+    float4 a[NPW][kRgPart];
+    {
+        const float4* xf = reinterpret_cast<const float4*>(p.x) + (size_t)r * kRgK16 * 64 + lane;
+        if (rvalid) {
+#pragma unroll
+            for (int j = 0; j < NPW; ++j)
+#pragma unroll
+                for (int i = 0; i < kRgPart; ++i) a[j][i] = xf[((h * NPW + j) * kRgPart + i) * 64];
+        } else {
+#pragma unroll
+            for (int j = 0; j < NPW; ++j)
+#pragma unroll
+                for (int i = 0; i < kRgPart; ++i) a[j][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < R) {
+        const float* tt = lnscr + 8 * threadIdx.x;
+        const float s1 = (tt[0] + tt[2]) + (tt[4] + tt[6]);
+        const float s2 = (tt[1] + tt[3]) + (tt[5] + tt[7]);
+        const float m = s1 / p.K;
+        const float v = fmaxf(s2 / p.K - m * m, 0.f);
+        lnst[2 * threadIdx.x] = m;
+        lnst[2 * threadIdx.x + 1] = 1.0f / sqrtf(v + 1e-5f);
+    }
+    __syncthreads();
+    if (rvalid) {
+        const float4* gw = reinterpret_cast<const float4*>(lngb);
+        const float4* gb = gw + kRgK16 * 4;
+        const int q4 = lane >> 4;
+        const float mu = lnst[2 * (16 * r + (lane & 15))], rs = lnst[2 * (16 * r + (lane & 15)) + 1];
+#pragma unroll
+        for (int j = 0; j < NPW; ++j)
+#pragma unroll
+            for (int i = 0; i < kRgPart; ++i) {
+                const int k16 = (h * NPW + j) * kRgPart + i;
+                a[j][i] = ln4(a[j][i], mu, rs, gw[4 * k16 + q4], gb[4 * k16 + q4]);
+            }
+    }
+    // every prologue load and tile 0 landed (tile 0 was issued first); then
+    // tile 1, whose wait is iteration 1's counted one.  Stage 2 (gamma, beta)
+    // is first overwritten by iteration 0's DMA, after its barrier.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (loader) {
+        const float* src = dma_src(t + G);
+        const unsigned dst = dma_dst(1);
+#pragma unroll
+        for (int j = 0; j < kRgDma; ++j) rg_dma(src + kRgLoaders * j * 256, dst + kRgLoaders * j * 1024);
+    }
+    RG_MARK(1);
+
+    const __amdgpu_buffer_rsrc_t out_rs =
+        __builtin_amdgcn_make_buffer_rsrc(p.out, 0, (int)((size_t)p.M * p.N * 4), 0x00020000);
+    constexpr int kDrop = 0x7fffff00;
+    const int rbase = 16 * r + 4 * (lane >> 4);  // rows of this lane's 4 accumulator registers
+    float run_v[4];  // per lane: running (max, column) of rows rbase + g over this workgroup's tiles
+    int run_i[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        run_v[g] = -INFINITY;
+        run_i[g] = 0x7fffffff;
+    }
+    f32x4 pend = f32x4{0.f, 0.f, 0.f, 0.f};  // this owner's (p0 + p1) of the previous tile
+    const float* myfold = fold + (r * S::NSLOT) * 256 + lane * 4;
+
+    // owners: epilogue of tile tp (fold buffer fb) -- the fixed-order sum,
+    // the store, the per-lane running (max, column)
+    auto epilogue = [&](int tp, int fb) __attribute__((always_inline)) {
+        const int col = tp * 16 + (lane & 15);
+        const float* fs = myfold + fb * kRgFoldF;
+        f32x4 v;
+        if constexpr (NPW == 2) {
+            v = pend + *reinterpret_cast<const f32x4*>(fs);
+        } else {
+            const f32x4 o1 = *reinterpret_cast<const f32x4*>(fs);
+            const f32x4 o2 = *reinterpret_cast<const f32x4*>(fs + 256);
+            const f32x4 o3 = *reinterpret_cast<const f32x4*>(fs + 512);
+            v = (pend + o1) + (o2 + o3);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int row = rbase + g;
+            const bool live = row < p.M && col < p.N;
+            int off = live ? (row * p.N + col) * 4 : kDrop;  // dropped past num_records
+            asm volatile("" : "+v"(off));                     // a select, not a branch around the store
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[g]), out_rs, off, 0, 0);
+            const bool up = live && v[g] > run_v[g];  // tiles in increasing column order: first max stays
+            run_v[g] = up ? v[g] : run_v[g];
+            run_i[g] = up ? col : run_i[g];
+        }
+    };
+
+    int stage = 0;  // ring stage of tile t
+    int it = 0;
+#ifdef HPA_RG_TRACE
+    unsigned long long tr_vm = 0, tr_bar = 0, tr_mf[2] = {0, 0};
+#endif
+    for (; t < ntn; t += G, ++it) {
+        // loaders: their DMA of tile t landed (issued two iterations ago;
+        // after it, the previous iteration's kRgDma); the barrier makes every
+        // loader's landed and frees the stage read in the previous iteration
+#ifdef HPA_RG_TRACE
+        const unsigned long long tr_w0 = __builtin_amdgcn_s_memrealtime();
+#endif
+        if (loader) {
+            __builtin_amdgcn_s_waitcnt((kRgDma & 15) | ((kRgDma >> 4) << 14) | (7 << 4));  // vmcnt(12) lgkmcnt(0)
+#ifdef HPA_RG_TRACE
+            if (w == 4) tr_vm += __builtin_amdgcn_s_memrealtime() - tr_w0;
+#endif
+        } else {
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
+        }
+        asm volatile("" ::: "memory");
+#ifdef HPA_RG_TRACE
+        const unsigned long long tr_b0 = __builtin_amdgcn_s_memrealtime();
+#endif
+        __builtin_amdgcn_s_barrier();
+#ifdef HPA_RG_TRACE
+        if (it < 14) RG_MARK(2 + it);
+        const unsigned long long tr_b1 = __builtin_amdgcn_s_memrealtime();
+        if (w == 0) tr_bar += tr_b1 - tr_b0;
+#endif
+        // every B fragment of the tile read up front: one LDS latency per tile
+        const float* rb = ring + stage * kRgTileF + lane * 4 + h * NPW * kRgPart * 256;
+        float4 b[NPW][kRgPart];
+#pragma unroll
+        for (int j = 0; j < NPW; ++j)
+#pragma unroll
+            for (int i = 0; i < kRgPart; ++i) b[j][i] = *reinterpret_cast<const float4*>(rb + (j * kRgPart + i) * 256);
+        if (owner && it > 0) epilogue(t - G, (it + 1) & 1);
+        // loaders: tile t + 2G into the stage freed by the barrier, one DMA per k-step
+        const int st2 = stage == 0 ? 2 : stage - 1;
+        const float* dsrc = dma_src(t + 2 * G);
+        const unsigned ddst = dma_dst(st2);
+        // (waves of a missing row block compute on zeros; the loop is
+        // branch-free per k-step, one copy with the DMAs and one without)
+        f32x4 acc[NPW];
+#pragma unroll
+        for (int j = 0; j < NPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        auto ksteps = [&](auto with_dma) __attribute__((always_inline)) {
+#pragma unroll
+            for (int i = 0; i < kRgPart; ++i) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int j = 0; j < NPW; ++j) {
+                        const float xs = q == 0 ? a[j][i].x : q == 1 ? a[j][i].y : q == 2 ? a[j][i].z : a[j][i].w;
+                        const float ws = q == 0 ? b[j][i].x : q == 1 ? b[j][i].y : q == 2 ? b[j][i].z : b[j][i].w;
+                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(xs, ws, acc[j], 0, 0, 0);
+                    }
+                if constexpr (decltype(with_dma)::value) rg_dma(dsrc + kRgLoaders * i * 256, ddst + kRgLoaders * i * 1024);
+            }
+        };
+        if (loader)
+            ksteps(std::true_type{});
+        else
+            ksteps(std::false_type{});
+        f32x4 s = acc[0];
+        if constexpr (NPW == 2) s = acc[0] + acc[1];
+        if (owner) {
+            pend = s;
+        } else if (rvalid) {
+            *reinterpret_cast<f32x4*>(fold + (it & 1) * kRgFoldF + (r * S::NSLOT + h - 1) * 256 + lane * 4) = s;
+        }
+        stage = stage == kRgStages - 1 ? 0 : stage + 1;
+#ifdef HPA_RG_TRACE
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (w == 0 || w == 4) tr_mf[w >> 2] += __builtin_amdgcn_s_memrealtime() - tr_b1;
+#endif
+    }
+    RG_MARK(16);
+#ifdef HPA_RG_TRACE
+    if (lane == 0 && w == 4) {
+        g_rg_trace[0][blockIdx.x][18] = tr_vm;
+        g_rg_trace[0][blockIdx.x][21] = tr_mf[1];
+    }
+    if (lane == 0 && w == 0) {
+        g_rg_trace[0][blockIdx.x][19] = tr_bar;
+        g_rg_trace[0][blockIdx.x][20] = tr_mf[0];
+    }
+#endif
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (owner && it > 0) epilogue(t - G, (it + 1) & 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
+    RG_MARK(17);
+    // one partial per row: slot blockIdx.x of part_out ([G][Mp][2]); the
+    // 16 columns' running maxima of a row sit in 16 adjacent lanes
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        rg_argmax<0x140>(run_v[g], run_i[g]);  // row_mirror
+        rg_argmax<0x141>(run_v[g], run_i[g]);  // row_half_mirror
+        rg_argmax<0x4E>(run_v[g], run_i[g]);   // quad_perm [2,3,0,1]
+        rg_argmax<0xB1>(run_v[g], run_i[g]);   // quad_perm [1,0,3,2]
+    }
+    if (owner && (lane & 15) == 0) {
+        const __amdgpu_buffer_rsrc_t part_rs =
+            __builtin_amdgcn_make_buffer_rsrc(p.part_out, 0, (int)((size_t)G * p.Mp * 8), 0x00020000);
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const u32x2 pv = {__float_as_uint(run_v[g]), (unsigned int)run_i[g]};
+            __builtin_amdgcn_raw_buffer_store_b64(pv, part_rs, ((int)blockIdx.x * p.Mp + rbase + g) * 8, 0, 0);
+        }
+    }
+}
+
 int g_num_cus = 0;
+
+// HPA_LOGITS_FORM=ring: the ring form (A/B knob; measured no faster yet,
+// tools/rg_trace.py); default the 16-wave K-split form
+int logits_form() {
+    static const int f = [] {
+        const char* e = getenv("HPA_LOGITS_FORM");
+        return (e && e[0] == 'r') ? 0 : 16;
+    }();
+    return f;
+}
+
 
 template <int MT>
 int launch_resident_mt(const FG& p) {
-    logits_resident_kernel<MT><<<(unsigned)logits_resident_grid(p), kResNW * 64, 0, hpa_stream()>>>(p);
+    if (logits_form() == 16)
+        logits_resident_kernel<MT><<<(unsigned)logits_resident_grid(p), kResNW * 64, 0, hpa_stream()>>>(p);
+    else
+        logits_ring_kernel<MT><<<(unsigned)logits_resident_grid(p), kRgNW * 64, 0, hpa_stream()>>>(p);
     HPA_LAUNCH_CHECK();
     return 0;
 }
@@ -275,7 +655,8 @@ int logits_resident_grid(const FG& p) {
 }
 
 bool logits_resident_eligible(const FG& p, int epi) {
-    return epi == HPA_FEPI_LOGITS && p.ln_stats && p.K16 == kResNW * kResS && p.Mp <= 64 && p.M <= p.Mp;
+    return epi == HPA_FEPI_LOGITS && p.ln_stats && p.K16 == kResNW * kResS && p.Mp <= 64 && p.M <= p.Mp &&
+           (logits_form() == 16 || p.ln_ntiles == kRgK16);
 }
 
 int launch_logits_resident(const FG& p) {
@@ -286,6 +667,19 @@ int launch_logits_resident(const FG& p) {
         case 4: return launch_resident_mt<4>(p);
         default: return hpa_fail(__FILE__, __LINE__, "logits: rows must be <= 64");
     }
+}
+
+// trace build only: the ring logits kernel's per-workgroup stamps of the
+// last launch ([2][256][24] u64: s_memrealtime 10 ns ticks, s_memtime).  Returns 1 in
+// the product build.
+extern "C" int hpa_logits_trace(unsigned long long* host) {
+#ifdef HPA_RG_TRACE
+    HPA_CHECK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rg_trace), sizeof(g_rg_trace)));
+    return 0;
+#else
+    (void)host;
+    return 1;
+#endif
 }
 
 }  // namespace hpa_gemm

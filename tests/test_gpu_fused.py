@@ -335,6 +335,35 @@ def test_logits_resident_kernel(hip, M):
     assert np.array_equal(nxt.download(M, np.int32), got1.argmax(-1))
 
 
+def test_logits_resident_rows_independent_of_batch(hip):
+    """variant 4 (ring form: rows split over waves, 1 or 2 K parts per wave):
+    a row's logits and argmax are bit-identical at 64, 48, 32, 16 and 5 rows
+    -- the same (p0 + p1) + (p2 + p3) sum at every row count, which is what
+    keeps a sharded decode equal to the unsharded one"""
+    L = hip.lib()
+    rng = np.random.default_rng(23)
+    K, N = 768, 50257
+    fixed = dict(x=rng.uniform(-1, 1, (64, K)).astype(np.float32),
+                 W=rng.uniform(-0.05, 0.05, (N, K)).astype(np.float32),
+                 bias=np.zeros(N, np.float32),
+                 lw=rng.uniform(0.8, 1.2, K).astype(np.float32), lb=rng.uniform(-0.1, 0.1, K).astype(np.float32))
+    outs, ids = [], []
+    for M in (64, 48, 32, 16, 5):
+        out, acc, bound, keep = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, 0, ln=True, rng=np.random.default_rng(0),
+                                     fixed=fixed, variant=4)
+        got = out.download((M, N))
+        assert np.all(np.abs(got - acc) <= bound)
+        npart = L.hpa_logits_partials(ctypes.byref(keep[-1]))
+        nxt = hip.DeviceBuffer(M * 4)
+        hip.check(L.hpa_argmax_final(keep[-3].ptr, npart, (M + 15) // 16 * 16, M, nxt.ptr, None, None, None))
+        outs.append(got)
+        ids.append(nxt.download(M, np.int32))
+        assert np.array_equal(ids[-1], got.argmax(-1))
+    for o, i in zip(outs[1:], ids[1:]):
+        assert np.array_equal(o, outs[0][:o.shape[0]])
+        assert np.array_equal(i, ids[0][:i.shape[0]])
+
+
 def test_logits_resident_argmax_ties_first_index(hip):
     """equal maxima in several column tiles and workgroups: the lowest column
     wins, as the reference's strict-> scan (paged_infer.c:937-951)"""
