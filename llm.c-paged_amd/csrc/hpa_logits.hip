@@ -251,19 +251,22 @@ __global__ __launch_bounds__(kResNW * 64) void logits_resident_kernel(FG p) {
     }
 }
 
-// ---- ring form (round 3): rows split over waves, wte through an LDS ring ----
+// ---- ring form (round 3, the default): rows split over waves, wte through
+// an LDS ring filled by dedicated loader waves ----
 // The 16-wave form above splits K over 16 waves, so every 16x16 output tile
 // is folded from 16 partial tiles through LDS behind a barrier that all
-// waves reach together: the matrix pipes idle through each fold (MFMA busy
-// 50 %, profiles/r3/mfma_c2.txt).  Here the ROWS are split instead:
-//   * 8 waves (2 per SIMD); at 64 rows wave w owns row block w & 3 and K
-//     parts {2h, 2h+1} (h = w >> 2) of the 4 parts of 192, i.e. 96 VGPRs of
-//     LNf(x), with one accumulator per part (two independent MFMA chains);
-//   * the column tile's 48 KiB of wte is streamed ONCE per workgroup into a
-//     3-stage LDS ring by LDS-DMA (global_load_lds_dwordx4, non-temporal),
-//     two tiles ahead, by the upper four waves (12 wave-instructions each
-//     per tile, one per k-step); every wave reads its B fragments of the
-//     tile from the ring with ds_read_b128 right after the tile's barrier;
+// waves reach together, and every wave also streams its own wte fragments:
+// the matrix pipes idle through each fold (MFMA busy 50 %,
+// profiles/r3/mfma_c2.txt).  Here:
+//   * 8 computing waves (2 per SIMD) split the ROWS: at 64 rows wave w owns
+//     row block w & 3 and K parts {2h, 2h+1} (h = w >> 2) of the 4 parts of
+//     192, i.e. 96 VGPRs of LNf(x), one accumulator per part (two MFMA chains);
+//   * 4 loader waves stream each 48 KiB column tile of wte ONCE per workgroup
+//     into a 3-stage LDS ring by LDS-DMA (global_load_lds_dwordx4, non-
+//     temporal), two tiles ahead, and do nothing else: a wave issuing into
+//     the saturated per-CU memory queue stalls at issue (~0.25 us per 1 KiB
+//     instruction, tools/rg_trace.py), so no computing wave issues a load;
+//   * the computing waves read their B fragments from the ring (ds_read_b128);
 //   * a tile's result is (p0 + p1) + (p2 + p3) over the 4 K parts: the wave
 //     of h = 1 publishes (p2 + p3) (1 KiB) into a double-buffered fold slot;
 //     the owner (h = 0) adds it in the NEXT iteration, after that
@@ -273,11 +276,10 @@ __global__ __launch_bounds__(kResNW * 64) void logits_resident_kernel(FG p) {
 // Fewer rows (16 / 32) keep the same per-row arithmetic: one part per wave
 // and three published partials, summed in the same order, so a row's logits
 // are bit-identical at every batch size (sharded decode = unsharded).
-// Roles: owners (h = 0) store, the loader waves (w >= 4: never owners) wait
-// on their own DMA with a counted vmcnt before the barrier.
-// Measured per tile (tools/rg_trace.py, s_memtime): the MFMAs alone 3.1 us
-// at the ~2.1 GHz the chip holds under this load (6144 MFMA cycles per
-// SIMD), the DMA alone 1.9 us (25 GB/s per CU).
+// Measured (tools/rg_trace.py, s_memtime): per tile the computing waves take
+// 3.35 us (6144 MFMA cycles per SIMD = 2.98 us at the 2.06 GHz the chip holds
+// under this load), the loaders' 48 KiB DMA 3.15 us (15 GB/s per CU beside
+// the MFMAs, 25 alone): 3.64 us per iteration, 57.5 us per launch.
 // diagnostic build (-DHPA_RG_TRACE, tools/rg_trace.py): stamps per workgroup
 // -- [0] start, [1] prologue done, [2..15] iteration starts (after the
 // barrier), [16] loop end, [17] end -- as s_memrealtime (10 ns) and
@@ -299,26 +301,28 @@ __device__ unsigned long long g_rg_trace[2][256][24];
     do {           \
     } while (0)
 #endif
-constexpr int kRgNW = 8;
+constexpr int kRgNC = 8;                 // computing waves (2 per SIMD)
+constexpr int kRgNW = 12;                // + 4 loader waves
 constexpr int kRgK16 = 48;               // K = 768
 constexpr int kRgPart = 12;              // k16-steps per K part (4 parts)
 constexpr int kRgTileF = kRgK16 * 256;   // floats per 16-column wte tile (48 KiB)
-constexpr int kRgLoaders = kRgNW / 2;    // waves kRgNW/2 .. kRgNW-1 load the ring
-constexpr int kRgDma = kRgK16 / kRgLoaders;  // LDS-DMA wave-instructions per loader per tile (12)
+constexpr int kRgLoaders = kRgNW - kRgNC;    // waves kRgNC .. kRgNW-1 load the ring
+constexpr int kRgDma = kRgK16 / kRgLoaders;  // LDS-DMA wave-instructions per loader per tile
 constexpr int kRgFoldF = 1536;           // floats per fold buffer (max over MT)
 constexpr int kRgStages = 3;
 constexpr int kRgLdsF = kRgStages * kRgTileF + 2 * kRgFoldF + 10 * 64;
 static_assert(kRgLdsF * 4 <= 160 * 1024, "LDS");
-static_assert(kRgDma == kRgPart, "one DMA per k-step");
+static_assert(kRgPart % kRgDma == 0, "DMAs spread evenly over the k-steps");
 
 template <int MT>
 struct RgShape {
     static constexpr int MTS = MT == 3 ? 4 : MT;  // row-block slots
     static constexpr int NPW = MTS == 4 ? 2 : 1;  // K parts per wave
     static constexpr int NWC = MTS * 4 / NPW;     // computing waves: 4 (MT 1) or 8
+    static_assert(NWC <= kRgNC, "compute waves");
     static constexpr int NSLOT = 4 / NPW - 1;     // published partials per row block
     static_assert(MTS * NSLOT * 256 <= kRgFoldF, "fold buffer");
-    static_assert(MTS <= kRgLoaders, "owners are never loaders");
+
 };
 
 // LDS-DMA of 1 KiB (16 B per lane to lds_addr + 16 * lane), non-temporal.
@@ -475,7 +479,7 @@ __global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
 
     // owners: epilogue of tile tp (fold buffer fb) -- the fixed-order sum,
     // the store, the per-lane running (max, column)
-    auto epilogue = [&](int tp, int fb) __attribute__((always_inline)) {
+    auto epilogue = [&](int tp, int fb, bool any) __attribute__((always_inline)) {
         const int col = tp * 16 + (lane & 15);
         const float* fs = myfold + fb * kRgFoldF;
         f32x4 v;
@@ -490,8 +494,8 @@ __global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int row = rbase + g;
-            const bool live = row < p.M && col < p.N;
-            int off = live ? (row * p.N + col) * 4 : kDrop;  // dropped past num_records
+            const bool live = any && row < p.M && col < p.N;
+            int off = live ? (row * p.N + col) * 4 : kDrop + 16 * g;  // dropped past num_records
             asm volatile("" : "+v"(off));                     // a select, not a branch around the store
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[g]), out_rs, off, 0, 0);
             const bool up = live && v[g] > run_v[g];  // tiles in increasing column order: first max stays
@@ -513,9 +517,9 @@ __global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
         const unsigned long long tr_w0 = __builtin_amdgcn_s_memrealtime();
 #endif
         if (loader) {
-            __builtin_amdgcn_s_waitcnt((kRgDma & 15) | ((kRgDma >> 4) << 14) | (7 << 4));  // vmcnt(12) lgkmcnt(0)
+            __builtin_amdgcn_s_waitcnt((kRgDma & 15) | ((kRgDma >> 4) << 14) | (7 << 4));  // vmcnt(kRgDma) lgkmcnt(0)
 #ifdef HPA_RG_TRACE
-            if (w == 4) tr_vm += __builtin_amdgcn_s_memrealtime() - tr_w0;
+            if (w == kRgNC) tr_vm += __builtin_amdgcn_s_memrealtime() - tr_w0;
 #endif
         } else {
             __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
@@ -530,57 +534,53 @@ __global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
         const unsigned long long tr_b1 = __builtin_amdgcn_s_memrealtime();
         if (w == 0) tr_bar += tr_b1 - tr_b0;
 #endif
-        // every B fragment of the tile read up front: one LDS latency per tile
-        const float* rb = ring + stage * kRgTileF + lane * 4 + h * NPW * kRgPart * 256;
-        float4 b[NPW][kRgPart];
+        if (loader) {
+            // tile t + 2G into the stage freed by the barrier: the loader
+            // waves do nothing else, so the stalls of a saturated per-CU
+            // memory queue never hold up an MFMA
+            const int st2 = stage == 0 ? 2 : stage - 1;
+            const float* dsrc = dma_src(t + 2 * G);
+            const unsigned ddst = dma_dst(st2);
 #pragma unroll
-        for (int j = 0; j < NPW; ++j)
+            for (int j = 0; j < kRgDma; ++j) rg_dma(dsrc + kRgLoaders * j * 256, ddst + kRgLoaders * j * 1024);
+        } else {
+            // (waves of a missing row block compute on zeros)
+            const float* rb = ring + stage * kRgTileF + lane * 4 + h * NPW * kRgPart * 256;
+            if (owner) epilogue(t - G, (it + 1) & 1, it > 0);
+            f32x4 acc[NPW];
 #pragma unroll
-            for (int i = 0; i < kRgPart; ++i) b[j][i] = *reinterpret_cast<const float4*>(rb + (j * kRgPart + i) * 256);
-        if (owner && it > 0) epilogue(t - G, (it + 1) & 1);
-        // loaders: tile t + 2G into the stage freed by the barrier, one DMA per k-step
-        const int st2 = stage == 0 ? 2 : stage - 1;
-        const float* dsrc = dma_src(t + 2 * G);
-        const unsigned ddst = dma_dst(st2);
-        // (waves of a missing row block compute on zeros; the loop is
-        // branch-free per k-step, one copy with the DMAs and one without)
-        f32x4 acc[NPW];
-#pragma unroll
-        for (int j = 0; j < NPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        auto ksteps = [&](auto with_dma) __attribute__((always_inline)) {
+            for (int j = 0; j < NPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int i = 0; i < kRgPart; ++i) {
+                float4 b[NPW];
+#pragma unroll
+                for (int j = 0; j < NPW; ++j) b[j] = *reinterpret_cast<const float4*>(rb + (j * kRgPart + i) * 256);
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
 #pragma unroll
                     for (int j = 0; j < NPW; ++j) {
                         const float xs = q == 0 ? a[j][i].x : q == 1 ? a[j][i].y : q == 2 ? a[j][i].z : a[j][i].w;
-                        const float ws = q == 0 ? b[j][i].x : q == 1 ? b[j][i].y : q == 2 ? b[j][i].z : b[j][i].w;
+                        const float ws = q == 0 ? b[j].x : q == 1 ? b[j].y : q == 2 ? b[j].z : b[j].w;
                         acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(xs, ws, acc[j], 0, 0, 0);
                     }
-                if constexpr (decltype(with_dma)::value) rg_dma(dsrc + kRgLoaders * i * 256, ddst + kRgLoaders * i * 1024);
             }
-        };
-        if (loader)
-            ksteps(std::true_type{});
-        else
-            ksteps(std::false_type{});
-        f32x4 s = acc[0];
-        if constexpr (NPW == 2) s = acc[0] + acc[1];
-        if (owner) {
-            pend = s;
-        } else if (rvalid) {
-            *reinterpret_cast<f32x4*>(fold + (it & 1) * kRgFoldF + (r * S::NSLOT + h - 1) * 256 + lane * 4) = s;
+            f32x4 s = acc[0];
+            if constexpr (NPW == 2) s = acc[0] + acc[1];
+            if (owner) {
+                pend = s;
+            } else if (rvalid) {
+                *reinterpret_cast<f32x4*>(fold + (it & 1) * kRgFoldF + (r * S::NSLOT + h - 1) * 256 + lane * 4) = s;
+            }
         }
         stage = stage == kRgStages - 1 ? 0 : stage + 1;
 #ifdef HPA_RG_TRACE
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (w == 0 || w == 4) tr_mf[w >> 2] += __builtin_amdgcn_s_memrealtime() - tr_b1;
+        if (w == 0 || w == kRgNC) tr_mf[w == kRgNC] += __builtin_amdgcn_s_memrealtime() - tr_b1;
 #endif
     }
     RG_MARK(16);
 #ifdef HPA_RG_TRACE
-    if (lane == 0 && w == 4) {
+    if (lane == 0 && w == kRgNC) {
         g_rg_trace[0][blockIdx.x][18] = tr_vm;
         g_rg_trace[0][blockIdx.x][21] = tr_mf[1];
     }
@@ -591,7 +591,7 @@ __global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
 #endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (owner && it > 0) epilogue(t - G, (it + 1) & 1);
+    if (owner) epilogue(t - G, (it + 1) & 1, it > 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
     RG_MARK(17);
     // one partial per row: slot blockIdx.x of part_out ([G][Mp][2]); the
@@ -617,12 +617,12 @@ __global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
 
 int g_num_cus = 0;
 
-// HPA_LOGITS_FORM=ring: the ring form (A/B knob; measured no faster yet,
-// tools/rg_trace.py); default the 16-wave K-split form
+// HPA_LOGITS_FORM=16: the 16-wave K-split form (A/B knob); default the ring
+// form (57.5 vs 58.7-59.8 us per launch, gpurun_out rg8 / profiles/r3)
 int logits_form() {
     static const int f = [] {
         const char* e = getenv("HPA_LOGITS_FORM");
-        return (e && e[0] == 'r') ? 0 : 16;
+        return (e && e[0] == '1' && e[1] == '6') ? 16 : 0;
     }();
     return f;
 }

@@ -46,6 +46,6 @@ print(f"iteration length (iters 1..11): med {np.median(d):.3f} us, mean {d.mean(
       f"shader clock {np.median(dc / d):.0f} MHz (median)")
 nit = np.where(t[:, 2:16] > 0, 1, 0).sum(1)  # iterations stamped (<= 14) -- use the loop count instead
 n_iter = np.where(us[:, 16] > 0, 0, 0) + 12.27
-for k, nm in [(18, "loader vmcnt wait"), (19, "wave0 barrier wait"), (20, "wave0 compute"), (21, "loader compute")]:
+for k, nm in [(18, "loader vmcnt wait"), (19, "wave0 barrier wait"), (20, "wave0 compute"), (21, "loader DMA issue")]:
     v = t[:, k] / 100.0 / n_iter
     print(f"{nm:20s} per iteration: med {np.median(v):.3f} us")
