@@ -380,11 +380,14 @@ __global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
         return ring_lds + (unsigned)(stage * kRgTileF + (w - (kRgNW - kRgLoaders)) * 256) * 4;
     };
     RG_MARK(0);
-    if (loader) {  // tile 0 lands during the LN prologue; tile 1 is issued after it
-        const float* src = dma_src(t);
-        const unsigned dst = dma_dst(0);
+    if (loader) {  // tiles 0 and 1 land during the LN prologue (the loaders take no part in it)
 #pragma unroll
-        for (int j = 0; j < kRgDma; ++j) rg_dma(src + kRgLoaders * j * 256, dst + kRgLoaders * j * 1024);
+        for (int d = 0; d < 2; ++d) {
+            const float* src = dma_src(t + d * G);
+            const unsigned dst = dma_dst(d);
+#pragma unroll
+            for (int j = 0; j < kRgDma; ++j) rg_dma(src + kRgLoaders * j * 256, dst + kRgLoaders * j * 1024);
+        }
     }
 
     // prologue loads, all in flight together: LNf statistics partials, the
@@ -451,16 +454,9 @@ __global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
                 a[j][i] = ln4(a[j][i], mu, rs, gw[4 * k16 + q4], gb[4 * k16 + q4]);
             }
     }
-    // every prologue load and tile 0 landed (tile 0 was issued first); then
-    // tile 1, whose wait is iteration 1's counted one.  Stage 2 (gamma, beta)
-    // is first overwritten by iteration 0's DMA, after its barrier.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (loader) {
-        const float* src = dma_src(t + G);
-        const unsigned dst = dma_dst(1);
-#pragma unroll
-        for (int j = 0; j < kRgDma; ++j) rg_dma(src + kRgLoaders * j * 256, dst + kRgLoaders * j * 1024);
-    }
+    // the loaders' tile 0 is waited for by iteration 0's counted vmcnt (tile
+    // 1's 12 DMAs still in flight), tile 1 by iteration 1's.  Stage 2 (gamma,
+    // beta) is first overwritten by iteration 0's DMA, after its barrier.
     RG_MARK(1);
 
     const __amdgpu_buffer_rsrc_t out_rs =
