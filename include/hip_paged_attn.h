@@ -209,7 +209,11 @@ typedef struct {
     const int* block_table;
     int bt_stride;
     const int* pos;
-    int waves;            /* waves per workgroup sharing the K range: 4, 8 or 16; 0 = by shape */
+    int waves;            /* waves per workgroup sharing the K range: 4, 8 or 16; 0 = by shape.
+                             Variant 4 on the resident logits kernel: 16 = its 16-wave
+                             K-split form, 12 = its ring form, else by M (the two sum a
+                             row's K in different orders: give sharded callers the
+                             global batch's form) */
     int row_blocks;       /* 16-row blocks per workgroup: 1, 2 or 4; 0 = by shape */
     int variant;          /* 0 = by shape; 1 = looped (two trips in flight);
                              2 = one-shot (every operand load issued up front; one
@@ -354,6 +358,10 @@ int hpa_logits_trace(unsigned long long* host);
 /* residual = wte[tok] + wpe[pos] in frag layout [Mp][C], stats (1 tile) */
 int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const float* wpe,
                    float* res_frag, float* stats, int B, int C);
+/* the same, also zeroing zero[0 .. zero_bytes) (16-byte granules): the
+ * decode step's hand-off counters without a memset node of their own */
+int hpa_embed_frag_zero(const int* tokens, const int* pos, const float* wte, const float* wpe,
+                        float* res_frag, float* stats, int B, int C, void* zero, size_t zero_bytes);
 /* greedy id from the logits GEMM's per-tile (max, argmax) partials:
  * lowest index wins ties; next[b], tokens[b] = next[b], pos[b] += 1.
  * active (nullable, [B]): rows with active[b] <= 0 are left untouched */

@@ -99,9 +99,12 @@ __global__ __launch_bounds__(256) void embed_frag_kernel(const int* __restrict__
                                                          const float* __restrict__ wte,
                                                          const float* __restrict__ wpe,
                                                          float* __restrict__ res, float* __restrict__ stats,
-                                                         int C) {
+                                                         int C, int4* __restrict__ zero, int zero_n4) {
     __shared__ float sc[8];
     const int b = blockIdx.x;
+    // the step's counter block (persistent layer hand-offs), zeroed here
+    // instead of by a memset node of its own
+    for (int i = b * 256 + threadIdx.x; i < zero_n4; i += gridDim.x * 256) zero[i] = make_int4(0, 0, 0, 0);
     const float* te = wte + (size_t)tokens[b] * C;
     const float* pe = wpe + (size_t)pos[b] * C;
     float s1 = 0.f, s2 = 0.f;
@@ -837,7 +840,8 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
                 "gemm_fused: row_blocks must be 1, 2 or 4");
     looped_shape(g, p.Mp, &nw, &mt, &ntw);
     HPA_REQUIRE(g->variant >= 0 && g->variant <= 4 && g->variant != 3, "gemm_fused: variant must be 0, 1, 2 or 4");
-    if (g->variant == 4 && logits_resident_eligible(p, g->epilogue)) return launch_logits_resident(p);
+    // (waves 16 / 12: the resident kernel's 16-wave or ring form; else by M)
+    if (g->variant == 4 && logits_resident_eligible(p, g->epilogue)) return launch_logits_resident(p, g->waves);
     // variant 4 elsewhere (GPT-2 XL logits, K = 1600): stream-K when the caller
     // gave its workspace (120 vs 143 us at M = 64, profiles/r2/sk_tune_xl.txt)
     if (g->variant == 4 && g->epilogue == HPA_FEPI_LOGITS && p.sk_slab && p.sk_cnt && sk_eligible(p.Mp, p.ntn, p.K16))
@@ -887,7 +891,18 @@ int hpa_logits_partials(const HpaFusedGemm* g) {
 int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const float* wpe,
                    float* res_frag, float* stats, int B, int C) {
     HPA_REQUIRE(B > 0 && C > 0 && C % 16 == 0, "embed_frag: bad shape");
-    embed_frag_kernel<<<B, 256, 0, hpa_stream()>>>(tokens, pos, wte, wpe, res_frag, stats, C);
+    embed_frag_kernel<<<B, 256, 0, hpa_stream()>>>(tokens, pos, wte, wpe, res_frag, stats, C, nullptr, 0);
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+int hpa_embed_frag_zero(const int* tokens, const int* pos, const float* wte, const float* wpe, float* res_frag,
+                        float* stats, int B, int C, void* zero, size_t zero_bytes) {
+    HPA_REQUIRE(B > 0 && C > 0 && C % 16 == 0, "embed_frag_zero: bad shape");
+    HPA_REQUIRE(zero_bytes % 16 == 0 && zero_bytes / 16 <= 0x7fffffff && ((size_t)zero & 15) == 0,
+                "embed_frag_zero: the zeroed block must be whole 16-byte granules");
+    embed_frag_kernel<<<B, 256, 0, hpa_stream()>>>(tokens, pos, wte, wpe, res_frag, stats, C,
+                                                   reinterpret_cast<int4*>(zero), (int)(zero_bytes / 16));
     HPA_LAUNCH_CHECK();
     return 0;
 }

@@ -620,7 +620,7 @@ __global__ __launch_bounds__(NW * 64) void gemm16_os_kernel(FG p) {
 // set by the launcher); nonzero (with hpa_last_error) on a bad description
 // the activation-resident logits kernel (hpa_logits.hip, variant 4)
 bool logits_resident_eligible(const FG& p, int epi);
-int launch_logits_resident(const FG& p);
+int launch_logits_resident(const FG& p, int form);  // form: 16 / 12 (ring) / 0 by rows
 int logits_resident_grid(const FG& p);  // workgroups = argmax partials per row it writes
 
 // bf16-weight GEMM launch (hpa_gemm_bf16.hip): waves 4/8, (row_blocks,

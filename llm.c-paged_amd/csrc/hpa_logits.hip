@@ -613,20 +613,19 @@ __global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
 
 int g_num_cus = 0;
 
-// HPA_LOGITS_FORM=16: the 16-wave K-split form (A/B knob); default the ring
-// form (57.5 vs 58.7-59.8 us per launch, gpurun_out rg8 / profiles/r3)
+// HPA_LOGITS_FORM=16 / ring: force a form (A/B knob); else 0 = the caller's
 int logits_form() {
     static const int f = [] {
         const char* e = getenv("HPA_LOGITS_FORM");
-        return (e && e[0] == '1' && e[1] == '6') ? 16 : 0;
+        return (e && e[0] == '1' && e[1] == '6') ? 16 : (e && e[0] == 'r') ? 12 : 0;
     }();
     return f;
 }
 
 
 template <int MT>
-int launch_resident_mt(const FG& p) {
-    if (logits_form() == 16)
+int launch_resident_mt(const FG& p, int form) {
+    if (form == 16)
         logits_resident_kernel<MT><<<(unsigned)logits_resident_grid(p), kResNW * 64, 0, hpa_stream()>>>(p);
     else
         logits_ring_kernel<MT><<<(unsigned)logits_resident_grid(p), kRgNW * 64, 0, hpa_stream()>>>(p);
@@ -655,12 +654,20 @@ bool logits_resident_eligible(const FG& p, int epi) {
            (logits_form() == 16 || p.ln_ntiles == kRgK16);
 }
 
-int launch_logits_resident(const FG& p) {
+// form: 16 = the 16-wave K-split form, 12 = the ring form, else by the rows
+// (the ring at 48-64 rows, 57.5 vs 58.7-59.8 us at 64; the 16-wave form at
+// 8-32 rows: 28.0 vs 35.3 us at 8, where the kernel streams wte with one
+// computing wave per SIMD).  The two forms sum a row's K in different orders:
+// callers that must match another batch size bit for bit (sharded decode)
+// pass the form of the GLOBAL batch.  HPA_LOGITS_FORM=16 / ring overrides.
+int launch_logits_resident(const FG& p, int form) {
+    if (logits_form() == 16 || logits_form() == 12) form = logits_form();
+    if (form != 16 && form != 12) form = p.Mp >= 48 ? 12 : 16;
     switch (p.Mp / 16) {
-        case 1: return launch_resident_mt<1>(p);
-        case 2: return launch_resident_mt<2>(p);
-        case 3: return launch_resident_mt<3>(p);
-        case 4: return launch_resident_mt<4>(p);
+        case 1: return launch_resident_mt<1>(p, form);
+        case 2: return launch_resident_mt<2>(p, form);
+        case 3: return launch_resident_mt<3>(p, form);
+        case 4: return launch_resident_mt<4>(p, form);
         default: return hpa_fail(__FILE__, __LINE__, "logits: rows must be <= 64");
     }
 }

@@ -1253,6 +1253,10 @@ static void dec_gemm_desc(GPT2* model, int l, int which, HpaFusedGemm* g) {
             g->out = d->d_logits; g->part_out = d->part; g->layer = 0;
             g->variant = 4; /* activation-resident kernel where the shape allows (hpa_logits.hip), */
             g->sk_slab = d->sk_slab; g->sk_count = d->sk_cnt; /* else stream-K with this workspace */
+            if (!d->w_bf16 && hpa_logits_kernel(d->B, V, C) == 4) { /* its form by the GLOBAL batch: a */
+                const int Bg = d->pl_global_B > 0 ? d->pl_global_B : d->B; /* row's sum order (sharded = */
+                g->waves = Bg > 32 ? 12 : 16;                             /* unsharded bit for bit) */
+            }
             break;
     }
 }
@@ -1299,13 +1303,16 @@ static int dec_launch(GPT2* model) {
     const ParameterTensors* w = &model->params;
     const int L = model->config.num_layers;
     const int C = model->config.channels;
-    int rc = hpa_embed_frag(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C);
+    const int pl = d->pl_on && !d->profiling;
+    /* persistent layers: the embed kernel also zeroes their hand-off counters */
+    int rc = pl ? hpa_embed_frag_zero(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C, d->pl_ctr,
+                                      (size_t)L * d->pl_ctr_ints * sizeof(int))
+                : hpa_embed_frag(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C);
 #define DEC_TRACE(i) \
     if (d->trace_x) rc |= hpa_unpack_frag(d->res, d->B, C, d->trace_x + (size_t)(i) * d->B * C, C)
     DEC_TRACE(0);
-    if (d->pl_on && !d->profiling) { /* qkv(0), then one persistent launch per layer */
+    if (pl) { /* qkv(0), then one persistent launch per layer */
         rc |= dec_gemm(model, 0, G_QKV);
-        rc |= hpa_memset_async(d->pl_ctr, 0, (size_t)L * d->pl_ctr_ints * sizeof(int));
         for (int l = 0; l < L && !rc; l++) {
             if (d->pl_on == 2) rc |= dec_attention(model, l); /* chain form: the attention's own launch */
             rc |= dec_layer(model, l);

@@ -263,6 +263,7 @@ def lib():
     _sig(L, "hpa_fused_pick_bf16", None, [i, i, i, _I])
     _sig(L, "hpa_fused_pick_bf16_ares", i, [i, i, i, _I])
     _sig(L, "hpa_embed_frag", i, [v, v, v, v, v, v, i, i])
+    _sig(L, "hpa_embed_frag_zero", i, [v, v, v, v, v, v, i, i, v, ctypes.c_size_t])
     _sig(L, "hpa_argmax_final", i, [v, i, i, i, v, v, v, v])
     _sig(L, "hpa_sample_final", i, [v, i, i, v, v, v, v, v])
     _sig(L, "hpa_sample_final_serial", i, [v, i, i, v, v, v, v, v])

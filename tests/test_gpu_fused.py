@@ -306,15 +306,17 @@ def test_fused_logits_argmax(hip, M, waves, rb, ct):
     assert np.array_equal(ids, got.argmax(-1))
 
 
+@pytest.mark.parametrize("form", [0, 12, 16])
 @pytest.mark.parametrize("M", [64, 37, 16, 1])
-def test_logits_resident_kernel(hip, M):
-    """variant 4 (activation-resident, 16 waves, hpa_logits.hip): logits
-    within the fp32 bound of the float64 reference, argmax partials consistent,
-    and within rounding of the looped kernel"""
+def test_logits_resident_kernel(hip, M, form):
+    """variant 4 (activation-resident, hpa_logits.hip; form 12 = ring, 16 =
+    16-wave K split, 0 = by M): logits within the fp32 bound of the float64
+    reference, argmax partials consistent, and within rounding of the looped
+    kernel"""
     L = hip.lib()
     rng = np.random.default_rng(11)
     K, N = 768, 50257
-    out, acc, bound, keep = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, 0, ln=True, rng=rng, variant=4)
+    out, acc, bound, keep = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, form, ln=True, rng=rng, variant=4)
     got = out.download((M, N))
     assert np.all(np.abs(got - acc) <= bound)
     part, g = keep[-3], keep[-1]
@@ -335,11 +337,14 @@ def test_logits_resident_kernel(hip, M):
     assert np.array_equal(nxt.download(M, np.int32), got1.argmax(-1))
 
 
-def test_logits_resident_rows_independent_of_batch(hip):
-    """variant 4 (ring form: rows split over waves, 1 or 2 K parts per wave):
-    a row's logits and argmax are bit-identical at 64, 48, 32, 16 and 5 rows
-    -- the same (p0 + p1) + (p2 + p3) sum at every row count, which is what
-    keeps a sharded decode equal to the unsharded one"""
+@pytest.mark.parametrize("form", [12, 16])
+def test_logits_resident_rows_independent_of_batch(hip, form):
+    """variant 4, each form of the resident kernel (waves 12: the ring form,
+    rows split over waves, 1 or 2 K parts per wave; waves 16: K split over 16
+    waves): a row's logits and argmax are bit-identical at 64, 48, 32, 16 and
+    5 rows -- the same sum at every row count, which is what keeps a sharded
+    decode equal to the unsharded one (the engine picks the form by the
+    global batch)"""
     L = hip.lib()
     rng = np.random.default_rng(23)
     K, N = 768, 50257
@@ -349,7 +354,7 @@ def test_logits_resident_rows_independent_of_batch(hip):
                  lw=rng.uniform(0.8, 1.2, K).astype(np.float32), lb=rng.uniform(-0.1, 0.1, K).astype(np.float32))
     outs, ids = [], []
     for M in (64, 48, 32, 16, 5):
-        out, acc, bound, keep = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, 0, ln=True, rng=np.random.default_rng(0),
+        out, acc, bound, keep = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, form, ln=True, rng=np.random.default_rng(0),
                                      fixed=fixed, variant=4)
         got = out.download((M, N))
         assert np.all(np.abs(got - acc) <= bound)
