@@ -47,6 +47,9 @@ int   hpa_host_free(void* p);
 int   hpa_memcpy(void* dst, const void* src, size_t bytes);       /* hipMemcpyDefault, sync */
 int   hpa_memcpy_async(void* dst, const void* src, size_t bytes); /* on the current stream */
 int   hpa_memset_async(void* dst, int value, size_t bytes);
+/* read [p, p + bytes) on the current stream and drop it, so a later kernel
+ * finds those lines in the 256 MiB Infinity Cache (grid: workgroups of 256) */
+int   hpa_l3_prefetch(const void* p, size_t bytes, int grid);
 int   hpa_is_device_accessible(const void* p); /* 1 if a kernel may dereference p */
 void* hpa_event_create(void);
 int   hpa_event_record(void* ev);

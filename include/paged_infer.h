@@ -248,6 +248,11 @@ int    gpt2_decode_gemm_config(GPT2* model, int* waves5, int* row_blocks5, int* 
  * launch (bench.py roofline) */
 int    gpt2_decode_time_attention(GPT2* model, int iters, double* ms_per_launch,
                                   double* bytes_per_launch);
+/* Infinity-Cache probe: the first `frac` of layer l's pool slab read by
+ * hpa_l3_prefetch (pf_grid workgroups), then layer l's attention; average ms
+ * of each part (per-iteration events) */
+int    gpt2_decode_time_attention_pf(GPT2* model, int iters, double frac, int pf_grid, double* ms_attn,
+                                     double* ms_pf);
 /* token choice: 0 = greedy argmax (default); 1 = multinomial sampling as the
  * reference driver (softmax_forward + sample_mult with random_f32 coins),
  * sequence b seeded with seed + b; the coins stay on the device */

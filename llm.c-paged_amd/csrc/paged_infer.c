@@ -1861,6 +1861,56 @@ int gpt2_decode_time_attention(GPT2* model, int iters, double* ms_per_launch, do
     return rc;
 }
 
+/* Infinity-Cache probe (tools/l3_probe.py): per iteration, the first `frac`
+ * of layer l's pool slab is read by hpa_l3_prefetch (grid pf_grid), then the
+ * attention of layer l runs; HIP events around each part, synchronised per
+ * iteration.  frac = 0 times the attention alone in the same form. */
+int gpt2_decode_time_attention_pf(GPT2* model, int iters, double frac, int pf_grid, double* ms_attn,
+                                  double* ms_pf) {
+    GPT2Decode* d = model->decode;
+    if (!d || iters <= 0 || frac < 0.0 || frac > 1.0) return 1;
+    const int B = d->B, C = model->config.channels, L = model->config.num_layers;
+    for (int b = 0; b < B; b++)
+        if (d->h_pos[b] < 1) return 1;
+    int* d_p = (int*)hpa_malloc(B * sizeof(int));
+    int* h_p = (int*)malloc(B * sizeof(int));
+    float* out = (float*)hpa_malloc(hpa_frag_elems(B, C) * sizeof(float));
+    void* e[3] = {hpa_event_create(), hpa_event_create(), hpa_event_create()};
+    int rc = !d_p || !h_p || !out || !e[0] || !e[1] || !e[2];
+    double ta = 0.0, tp = 0.0;
+    const size_t slab = d->pool.layer_elems * d->pool.elem_bytes;
+    const size_t nb = ((size_t)(frac * (double)slab)) & ~(size_t)4095;
+    if (!rc) {
+        for (int b = 0; b < B; b++) h_p[b] = d->h_pos[b] - 1;
+        rc |= hpa_memcpy(d_p, h_p, B * sizeof(int));
+        for (int i = -1; i < iters && !rc; i++) { /* i = -1: warm-up */
+            const int l = (i + L) % L;
+            rc |= hpa_event_record(e[0]);
+            if (nb) rc |= hpa_l3_prefetch((const char*)d->pool.base + (size_t)l * slab, nb, pf_grid);
+            rc |= hpa_event_record(e[1]);
+            rc |= hpa_paged_attention_decode_split_w(d->d_q, &d->pool, l, d->d_bt, d->bt_stride, d_p, out, B,
+                                                     d->attn_splits, d->d_attn_ws, 1, d->attn_waves);
+            rc |= hpa_event_record(e[2]);
+            if (rc) break;
+            const float a = hpa_event_elapsed_ms(e[1], e[2]), p = hpa_event_elapsed_ms(e[0], e[1]);
+            if (a < 0 || p < 0) rc = 1;
+            if (i >= 0) {
+                ta += a;
+                tp += p;
+            }
+        }
+    }
+    if (!rc) {
+        if (ms_attn) *ms_attn = ta / iters;
+        if (ms_pf) *ms_pf = tp / iters;
+    }
+    for (int k = 0; k < 3; k++) hpa_event_destroy(e[k]);
+    hpa_free(out);
+    hpa_free(d_p);
+    free(h_p);
+    return rc;
+}
+
 /* weights + wpe rows + KV read (ctx = pos+1) + KV append + logits */
 double gpt2_decode_step_bytes(GPT2* model, double* attn_bytes) {
     GPT2Decode* d = model->decode;

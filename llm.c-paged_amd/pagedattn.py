@@ -275,6 +275,9 @@ def lib():
     _sig(L, "gpt2_decode_gemm_config", i, [v, _I, _I, _I, i])
     _sig(L, "gpt2_decode_time_attention", i, [v, i, ctypes.POINTER(ctypes.c_double),
                                               ctypes.POINTER(ctypes.c_double)])
+    _sig(L, "gpt2_decode_time_attention_pf", i, [v, i, ctypes.c_double, i, ctypes.POINTER(ctypes.c_double),
+                                                 ctypes.POINTER(ctypes.c_double)])
+    _sig(L, "hpa_l3_prefetch", i, [v, sz, i])
     _sig(L, "gpt2_decode_step_bytes", ctypes.c_double, [v, ctypes.POINTER(ctypes.c_double)])
     _sig(L, "random_u32", ctypes.c_uint, [ctypes.POINTER(ctypes.c_ulonglong)])
     _sig(L, "random_f32", f, [ctypes.POINTER(ctypes.c_ulonglong)])
@@ -666,6 +669,14 @@ class Model:
         check(lib().gpt2_decode_time_attention(self.h, int(iters), ctypes.byref(ms), ctypes.byref(by)),
               "time_attention")
         return ms.value, by.value
+
+    def time_attention_pf(self, frac, iters=24, grid=1024):
+        """(attention ms, prefetch ms) per iteration: the first `frac` of the
+        layer's pool slab read into the Infinity Cache, then its attention"""
+        a, p = ctypes.c_double(), ctypes.c_double()
+        check(lib().gpt2_decode_time_attention_pf(self.h, int(iters), float(frac), int(grid), ctypes.byref(a),
+                                                  ctypes.byref(p)), "time_attention_pf")
+        return a.value, p.value
 
     def prefill(self, tokens):
         """tokens (B, T): all T tokens of every sequence in one pass; returns

@@ -172,7 +172,9 @@ def test_rccl_single_process_init_all_barrier_and_max(hip):
 # identical K/V (the fill hashes the global sequence index) to ~1000 tokens,
 # 8 steps; every row's logits and greedy id equal the unsharded B = 64 engine
 # bit for bit.  Both sides use five launches per layer with the global batch's
-# attention split count (what gpt2_decode_shard picks), so the arithmetic is
+# attention split count and logits form (what gpt2_decode_shard picks: the
+# ring logits form at a global batch of 64, HPA_LOGITS_FORM in the shard
+# processes, which have no communicator to tell them), so the arithmetic is
 # the same; the shards hand their rows over by file (the RCCL gather of this
 # path is tested above on a 1-rank communicator).
 GPT2_124M = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
@@ -194,6 +196,7 @@ def _c4_tokens():
 
 
 def _c4_worker(lo, hi, out_path):
+    os.environ["HPA_LOGITS_FORM"] = "ring"  # the global batch's form (launch_logits_resident)
     import pagedattn as hip
     hip.init(0)
     m = _c4_engine(hip, hi - lo, lo)
