@@ -221,6 +221,9 @@ typedef struct {
     int variant;          /* 0 = by shape; 1 = looped (two trips in flight);
                              2 = one-shot (every operand load issued up front; one
                              row block; (waves, K/16) in {(4,48),(8,48),(16,48),(8,192),(16,192),(10,100)});
+                             3 = loader / MFMA-wave ring (hpa_gemm_ring.hip): <= 64 padded rows,
+                             LN folded (ln_fold_c1) or absent, QKV / GELU / RESID; one
+                             12-wave workgroup per 32 columns, waves/row_blocks/col_tiles ignored;
                              4 = LOGITS only: activation-resident persistent kernel
                              (K = 768, rows <= 64; 16 waves); else stream-K (6) when
                              sk_slab / sk_count are given and rows <= 64; else as 1;

@@ -1,0 +1,252 @@
+// hpa_gemm_ring.hip -- the 64-row fp32 layer GEMM with a loader / MFMA-wave
+// split over an LDS ring (variant 3 of hpa_gemm_fused; GPT-2 XL's decode
+// qkv and fc, matmul_forward paged_infer.c:92-114 / matmul_cached :117-160).
+//
+// Why (DESIGN.md "Where an XL layer GEMM's time goes"):
+// in the looped kernel every wave both loads its operands and runs the
+// MFMAs, and the two barely overlap (XL fc: loads alone 10.9 us, MFMAs alone
+// 14.1, both 21.8).  Here one workgroup of 12 waves takes 64 rows x 32
+// columns over the whole K (rows past Mp: a repeated row block, never stored):
+//   * 4 loader waves move each 8-deep k16 stage -- the 4 row blocks' A
+//     fragments (16 KiB, default cache policy: every workgroup re-reads A
+//     from its XCD's L2) and the 2 column tiles' W fragments (8 KiB,
+//     non-temporal: read once) -- into a 3-stage LDS ring by LDS-DMA
+//     (global_load_lds_dwordx4), two stages ahead, and do nothing else;
+//   * 8 MFMA waves (2 per SIMD): wave w owns row block w & 3 and half h =
+//     w >> 2 of every stage's steps (4h .. 4h + 3) for BOTH column tiles --
+//     two independent accumulator chains, each A fragment read once for two
+//     W fragments (ds_read_b128 from the ring); the two halves are added in
+//     the epilogue (h = 0 + h = 1);
+//   * one workgroup barrier per stage (the loaders' counted vmcnt makes the
+//     stage's bytes visible; the barrier also frees the stage read before).
+// Measured (tools/ring_tune.py, profiles/r3/experiments/xl_ring_gemm.txt,
+// B = 64): XL qkv 21.7 vs 23.8 us, fc 22.4 vs 24.7 (the engine's default
+// for them; XL step 10.23 vs 10.38 ms).  The ring traffic alone takes 12.6 /
+// 13.8 us, the MFMA waves alone 19.1 / 19.7 (against 12.4 at the fp32 issue
+// rate): the MFMA side bounds it.  attproj (50 workgroups) and fcproj (K =
+// 6400 on 50 workgroups) stay on the looped kernel.
+// The row statistics of a folded LayerNorm come from the A fragments the
+// waves read (each half's partial sums in its own slot); the epilogue is the shared
+// Epi::apply (QKV with the K/V append, GELU, RESID with LN partial sums).
+// A row's summation order depends only on K (two fixed chains per tile),
+// never on M or the grid: bit-identical rows across launch shapes.
+#include "hpa_gemm_body.h"
+
+namespace hpa_gemm {
+namespace {
+
+constexpr int kRnNW = 12;                   // waves per workgroup
+constexpr int kRnNC = 8;                    // MFMA waves (row block w & 3, stage half w >> 2)
+constexpr int kRnLd = kRnNW - kRnNC;        // loader waves
+constexpr int kRnKS = 8;                    // k16 steps per stage
+constexpr int kRnChunks = (4 + 2) * kRnKS;  // 1 KiB fragments per stage: A[4][KS], W[2][KS]
+constexpr int kRnPerLd = kRnChunks / kRnLd; // LDS-DMA wave-instructions per loader per stage
+constexpr int kRnStageF = kRnChunks * 256;  // floats per stage (48 KiB)
+constexpr int kRnStages = 3;
+constexpr int kRnLdsF = kRnStages * kRnStageF;
+static_assert(kRnLdsF * 4 <= 160 * 1024, "LDS");
+static_assert(kRnChunks % kRnLd == 0, "chunks per loader");
+// epilogue scratch over the ring (dead after the loop)
+constexpr int kRnRedF = 2 * 2 * 4 * 256;    // [2 halves][2 tiles][4 row blocks][4 regs][64 lanes]
+constexpr int kRnTileF = 2 * 64 * 17;       // Epi::apply's row-statistics tile
+constexpr int kRnWsumF = kRnNW * 64 * 2;    // [NW][64 rows][2] LN row partials (slots 0, 1 used)
+static_assert(kRnRedF + kRnTileF + kRnWsumF <= kRnLdsF, "epilogue scratch");
+
+// LDS-DMA of one 1 KiB fragment (16 B per lane to lds_addr + 16 * lane).
+// Inline asm (as hpa_logits.hip's ring): the compiler does not count these
+// loads, the loader waves wait for them themselves.
+template <bool NT>
+__device__ __forceinline__ void rn_dma(const float* src, unsigned lds_addr) {
+    unsigned keep;
+    if constexpr (NT)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(src), "s"(lds_addr)
+                     : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(src), "s"(lds_addr)
+                     : "memory");
+}
+
+// MODE (diagnostics, tools/ring_tune.py): 0 the product; 1 no MFMAs (the
+// ring runs, the MFMA waves only read it); 2 no LDS-DMA (MFMAs on whatever
+// the ring holds)
+// ROT: workgroup b walks the K stages starting at stage b % nst (every
+// workgroup reads the same A: this spreads the concurrent A requests over
+// the L2 channels instead of all workgroups asking for the same lines); a
+// tile's summation order then depends on its column pair, never on M
+template <int EPI, int MODE, bool ROT>
+__global__ __launch_bounds__(kRnNW * 64) void gemm_ring_kernel(FG p) {
+    __shared__ __attribute__((aligned(16))) float ring[kRnLdsF];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool loader = w >= kRnNC;
+    const int r = w & 3, h = (w >> 2) & 1;
+    const int nt0 = blockIdx.x * 2;
+    const int K16 = p.K16;
+    const int nst = (K16 + kRnKS - 1) / kRnKS;
+    const int rot = ROT ? (int)(blockIdx.x % (unsigned)nst) : 0;
+    auto phys = [&](int st) __attribute__((always_inline)) {  // logical stage -> k stage
+        return st < nst ? (st + rot >= nst ? st + rot - nst : st + rot) : st;
+    };
+    const bool fold = p.fold_c1 != nullptr;
+
+    Epi<kRnNW, EPI, 4, 2> epi;
+    epi.prefetch(p, nt0, 0);  // bias / residual / c1 of the owned elements, landing during the loop
+
+    const unsigned ring_lds =
+        __builtin_amdgcn_readfirstlane((unsigned)(size_t)(__attribute__((address_space(3))) float*)ring);
+    // loader wave L = w - 8 moves chunks q = L + 4 i of every stage: q < 32 ->
+    // A (row block q >> 3, step q & 7), else W (tile (q - 32) >> 3, step q & 7)
+    const int L = w - kRnNC;
+    const int nrb = p.Mp >> 4;
+    const float* xa = p.x + (size_t)lane * 4;
+    const float* wa0 = p.w + (size_t)min(nt0, p.ntn - 1) * K16 * 256 + lane * 4;
+    const float* wa1 = p.w + (size_t)min(nt0 + 1, p.ntn - 1) * K16 * 256 + lane * 4;
+    auto issue = [&](int st) __attribute__((always_inline)) {
+        const unsigned base = ring_lds + (unsigned)((st % kRnStages) * kRnStageF) * 4;
+#pragma unroll
+        for (int i = 0; i < kRnPerLd; ++i) {
+            const int q = L + kRnLd * i;
+            const int s = q & 7;
+            const int k = min(phys(st) * kRnKS + s, K16 - 1);  // past the end: a harmless re-read
+            const unsigned dst = base + (unsigned)q * 1024;
+            if (i < 32 / kRnLd) {  // A chunk (compile-time: q < 32 for every loader); row
+                // blocks past Mp re-read the last one (their rows are never stored)
+                rn_dma<false>(xa + ((size_t)min(q >> 3, nrb - 1) * K16 + k) * 256, dst);
+            } else {
+                rn_dma<true>((((q - 32) >> 3) ? wa1 : wa0) + (size_t)k * 256, dst);
+            }
+        }
+    };
+    if (loader && MODE != 2) {
+        issue(0);
+        issue(1);
+    }
+
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    float fs1 = 0.f, fs2 = 0.f;
+    constexpr int KH = kRnKS / 2;  // steps per half-stage
+    const float* ra = ring + (r * kRnKS + h * KH) * 256 + lane * 4;   // A[r][s] of a stage
+    const float* rw = ring + (32 + h * KH) * 256 + lane * 4;          // W[0][s]; W[1][s] at + KS
+    // iteration st: the loaders' stage st has landed -> barrier -> loaders
+    // issue stage st + 2 into the slot read in iteration st - 1; the MFMA
+    // waves multiply stage st.  The two roles run separate loops with the
+    // same nst barriers (the loaders' address registers and the MFMA waves'
+    // fragments never share a live range).  (A software-pipelined form --
+    // stage st read while stage st - 1's MFMAs run, two register sets --
+    // measured slower: XL qkv 23.7 vs 23.0 us, profiles/r3/experiments/.)
+    if (loader) {
+        for (int st = 0; st < nst; ++st) {
+            if (MODE != 2)
+                __builtin_amdgcn_s_waitcnt((kRnPerLd & 15) | ((kRnPerLd >> 4) << 14) | (7 << 4));  // vmcnt(PerLd) lgkmcnt(0)
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (MODE != 2) issue(st + 2);
+        }
+    } else {
+        for (int st = 0; st < nst; ++st) {
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            const int so = (st % kRnStages) * kRnStageF;
+            const int ns = min(KH, K16 - phys(st) * kRnKS - h * KH);  // may be <= 0 in the last stage
+#pragma unroll
+            for (int s = 0; s < KH; ++s) {
+                if (s < ns) {
+                    const float4 xv = *reinterpret_cast<const float4*>(ra + so + s * 256);
+                    const float4 w0 = *reinterpret_cast<const float4*>(rw + so + s * 256);
+                    const float4 w1 = *reinterpret_cast<const float4*>(rw + so + (kRnKS + s) * 256);
+                    if (fold) row_sums_add(xv, fs1, fs2);
+                    if (MODE == 1) {
+                        acc0[0] += (xv.x + w0.x) + (xv.y + w0.y);
+                        acc1[1] += (xv.z + w1.z) + (xv.w + w1.w);
+                    } else {
+                        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.x, w0.x, acc0, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.x, w1.x, acc1, 0, 0, 0);
+                        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.y, w0.y, acc0, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.y, w1.y, acc1, 0, 0, 0);
+                        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.z, w0.z, acc0, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.z, w1.z, acc1, 0, 0, 0);
+                        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.w, w0.w, acc0, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.w, w1.w, acc1, 0, 0, 0);
+                    }
+                }
+            }
+        }
+    }
+    // no LDS-DMA outlives the loop: the scratch below overlays the ring
+    if (loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+    float* red = ring;                       // [2 halves][2 tiles][4][4][64]
+    float* tile = ring + kRnRedF;            // Epi::apply row statistics
+    float* wsum = tile + kRnTileF;           // [NW][64][2]: slots 0, 1 = the halves' row sums, the rest 0
+    if (!loader) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            red[h * 2048 + r * 256 + g * 64 + lane] = acc0[g];
+            red[h * 2048 + 1024 + r * 256 + g * 64 + lane] = acc1[g];
+        }
+        if (fold) row_sums_publish(fs1, fs2, wsum + h * 128 + 32 * r);
+    } else if (fold) {
+        for (int i = (w - kRnNC) * 64 + lane; i < kRnWsumF - 256; i += kRnLd * 64) wsum[256 + i] = 0.f;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    constexpr int EPT = (2 * 1024 + kRnNW * 64 - 1) / (kRnNW * 64);
+    float vals[EPT];
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+        const int e = threadIdx.x + i * kRnNW * 64;
+        vals[i] = e < 2 * 1024 ? red[e] + red[2048 + e] : 0.f;  // half 0 + half 1
+    }
+    epi.apply(p, vals, tile, nt0, 0, wsum);
+}
+
+template <int EPI, bool ROT>
+int launch_ring_rot(const FG& p, int mode) {
+    const unsigned grid = (unsigned)((p.ntn + 1) / 2);
+    switch (mode) {
+        case 0: gemm_ring_kernel<EPI, 0, ROT><<<grid, kRnNW * 64, 0, hpa_stream()>>>(p); break;
+        case 1: gemm_ring_kernel<EPI, 1, ROT><<<grid, kRnNW * 64, 0, hpa_stream()>>>(p); break;
+        default: gemm_ring_kernel<EPI, 2, ROT><<<grid, kRnNW * 64, 0, hpa_stream()>>>(p); break;
+    }
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int EPI>
+int launch_ring_epi(const FG& p, int mode, bool rot) {
+    return rot ? launch_ring_rot<EPI, true>(p, mode) : launch_ring_rot<EPI, false>(p, mode);
+}
+
+}  // namespace
+
+// at most 64 padded rows (4 row blocks; fewer compute on a repeated block
+// and store nothing), an even or odd tile count, LN folded or absent (no LN
+// applied on load), an epilogue other than LOGITS
+bool ring_eligible(const FG& p, int epi) {
+    return p.Mp <= 64 && p.M <= 64 && p.K16 >= 1 && (!p.ln_stats || p.fold_c1) &&
+           (epi == HPA_FEPI_QKV || epi == HPA_FEPI_GELU || epi == HPA_FEPI_RESID);
+}
+
+// HPA_RING_MODE=1 / 2: the diagnostic forms (no MFMAs / no LDS-DMA);
+// HPA_RING_ROT=1: the rotated stage order
+int launch_ring(const FG& p, int epi) {
+    HPA_REQUIRE(ring_eligible(p, epi), "gemm_fused ring (variant 3): <= 64 padded rows, LN folded or none, "
+                                       "QKV / GELU / RESID");
+    static const int mode = [] {
+        const char* e = getenv("HPA_RING_MODE");
+        return e ? atoi(e) : 0;
+    }();
+    static const bool rot = [] {  // HPA_RING_ROT=1: rotated stage order (A/B knob)
+        const char* e = getenv("HPA_RING_ROT");
+        return e && e[0] == '1';
+    }();
+    switch (epi) {
+        case HPA_FEPI_QKV: return launch_ring_epi<HPA_FEPI_QKV>(p, mode, rot);
+        case HPA_FEPI_GELU: return launch_ring_epi<HPA_FEPI_GELU>(p, mode, rot);
+        default: return launch_ring_epi<HPA_FEPI_RESID>(p, mode, rot);
+    }
+}
+
+}  // namespace hpa_gemm

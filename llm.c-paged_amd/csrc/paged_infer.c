@@ -1261,9 +1261,29 @@ static void dec_gemm_desc(GPT2* model, int l, int which, HpaFusedGemm* g) {
     }
 }
 
+/* HPA_GEMM_RING=0: GPT-2 XL's qkv / fc on the looped kernel instead of the
+ * ring kernel (A/B knob; XL step 10.23 vs 10.38 ms) */
+static int dec_ring_allowed(void) {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("HPA_GEMM_RING");
+        v = !(e && e[0] == '0');
+    }
+    return v;
+}
+
 static int dec_gemm(GPT2* model, int l, int which) {
     HpaFusedGemm g;
     dec_gemm_desc(model, l, which, &g);
+    {   /* wide layers (C >= 1024: GPT-2 XL) at 49-64 rows of the GLOBAL batch: qkv and fc on the loader / MFMA-wave ring kernel
+         * (hpa_gemm_ring.hip, variant 3; a row's sums never depend on M, so
+         * shards of that batch take it too and stay bit-identical) */
+        GPT2Decode* d = model->decode;
+        const int Bg = d->pl_global_B > 0 ? d->pl_global_B : d->B;
+        if ((which == G_QKV || which == G_FC) && !d->w_bf16 && d->d_fold && model->config.channels >= 1024 &&
+            Bg > 48 && d->B <= 64 && dec_ring_allowed())
+            g.variant = 3;
+    }
     return hpa_gemm_fused(&g);
 }
 

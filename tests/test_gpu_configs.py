@@ -152,6 +152,15 @@ def test_config3_xl_end_to_end_full_depth(hip):
     _identical_cache_run(hip, CFG_XL, params, B=2, P=32, ctx0=1000, steps=6, seed=33)
 
 
+def test_config3_xl_full_batch_end_to_end(hip):
+    """the full batch of config 3 (B=64: the layer GEMMs that run at it --
+    qkv / fc on the ring kernel, hpa_gemm_ring.hip) against the oracle, all
+    48 layers and V=50257; a short context (the K/V the oracle is handed is
+    40 GB at ctx 1000, and the GEMMs do not depend on it)"""
+    params = _params(hip, CFG_XL, 35)
+    _identical_cache_run(hip, CFG_XL, params, B=64, P=32, ctx0=40, steps=2, seed=35)
+
+
 # ---------------------------------------------------------------- config 5: bf16, B=256, ctx 2048, page 8
 def test_config5_attention_full_size(hip):
     """bf16 KV, B=256, ctx 2048, page 8 (identical stored values on both sides)"""

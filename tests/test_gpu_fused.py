@@ -625,3 +625,79 @@ def test_logits_variant4_takes_stream_k_with_workspace(hip):
         outs.append(got)
     assert np.array_equal(outs[0], outs[1])
 
+
+
+@pytest.mark.parametrize("epi,K,N,fold", [("GELU", 1600, 6400, True), ("QKV", 1600, 4800, True),
+                                          ("RESID", 6400, 1600, False), ("RESID", 1600, 1600, False),
+                                          ("GELU", 768, 3072, True), ("GELU", 256, 80, False),
+                                          ("RESID", 48, 1616, False), ("QKV", 768, 2304, False)])
+@pytest.mark.parametrize("M", [64, 49, 20, 5])
+def test_fused_ring(hip, epi, K, N, fold, M):
+    """loader / MFMA-wave ring kernel (variant 3, hpa_gemm_ring.hip): every
+    epilogue within the f64 bound at 16-64 padded rows; LN folded or absent;
+    K not a multiple of the 8-step stage (K16 = 100, 3); an odd column-tile
+    count (N = 80, 1616: the last workgroup's second tile past N); the RESID
+    epilogue's 16-column LN partial sums; a relaunch is bit identical"""
+    e = getattr(hip, "HPA_FEPI_" + epi)
+    rng = np.random.default_rng(K + N + M + 3)
+    res = rng.uniform(-1, 1, (M, N)).astype(np.float32) if epi == "RESID" else None
+    pool_args = None
+    if epi == "QKV":
+        pool = hip.Pool(1, N // 3 // 64, 16, 4 * M)
+        bt = np.arange(4 * M, dtype=np.int32).reshape(M, 4)
+        pos = (np.arange(M, dtype=np.int32) * 7) % 64
+        pool_args = (pool, bt, pos)
+    out, acc, bound, keep = _run(hip, e, M, K, N, 8, ln=fold, rng=rng, res=res, pool_args=pool_args,
+                                 variant=3, fold=fold)
+    Mp = (M + 15) // 16 * 16
+    if epi == "QKV":
+        C = N // 3
+        got = out.download((M, C))
+        assert np.all(np.abs(got - acc[:, :C]) <= bound[:, :C])
+        for b in (0, M // 2, M - 1):
+            k, v = pool.read_tokens(0, bt[b], pos[b] + 1)
+            assert np.all(np.abs(k[pos[b]] - acc[b, C:2 * C]) <= bound[b, C:2 * C])
+            assert np.all(np.abs(v[pos[b]] - acc[b, 2 * C:]) <= bound[b, 2 * C:])
+    else:
+        full = out.download(Mp * N)
+        got = hip.from_frag(full, M, N)
+        if epi == "GELU":
+            ref = 0.5 * acc * (1 + np.tanh(np.sqrt(2 / np.pi) * (acc + 0.044715 * acc ** 3)))
+            assert np.all(np.abs(got - ref) <= bound + 1e-6)
+        else:
+            assert np.all(np.abs(got - (acc + res)) <= bound + 1e-6)
+            assert not hip.from_frag(full, Mp, N)[M:].any()  # padded rows stay zero
+            st = [k for k in keep if isinstance(k, hip.DeviceBuffer)][-2].download((N // 16, Mp, 2))
+            g16 = got.astype(np.float64).reshape(M, N // 16, 16)
+            assert np.allclose(st[:, :M, 0].T, g16.sum(-1), rtol=1e-5, atol=1e-4)
+            assert np.allclose(st[:, :M, 1].T, (g16 ** 2).sum(-1), rtol=1e-5, atol=1e-4)
+    g = [k for k in keep if isinstance(k, hip.HpaFusedGemm)][0]
+    hip.check(hip.lib().hpa_gemm_fused(ctypes.byref(g)), "relaunch")
+    hip.check(hip.lib().hpa_synchronize())
+    again = out.download((M, N // 3)) if epi == "QKV" else hip.from_frag(out.download(Mp * N), M, N)
+    assert np.array_equal(again, got)
+
+
+def test_fused_ring_rows_independent_of_batch(hip):
+    """a row's result depends only on K (the ring's two fixed chains), never
+    on M: the rows of a 20-row launch equal the same rows of a 64-row one"""
+    rng = np.random.default_rng(12)
+    K, N = 1600, 4800
+    fixed = dict(x=rng.uniform(-1, 1, (64, K)).astype(np.float32),
+                 W=rng.uniform(-0.05, 0.05, (N, K)).astype(np.float32),
+                 bias=rng.uniform(-0.1, 0.1, N).astype(np.float32),
+                 lw=rng.uniform(0.8, 1.2, K).astype(np.float32), lb=rng.uniform(-0.1, 0.1, K).astype(np.float32))
+    outs = []
+    for M in (64, 20):
+        out, _, _, keep = _run(hip, hip.HPA_FEPI_GELU, M, K, N, 8, ln=True, rng=rng, fixed=fixed, variant=3,
+                               fold=True)
+        outs.append(hip.from_frag(out.download((M + 15) // 16 * 16 * N), M, N))
+    assert np.array_equal(outs[0][:20], outs[1])
+
+
+def test_fused_ring_rejects_unsupported_shape(hip):
+    """variant 3 needs <= 64 padded rows and no LayerNorm applied on load"""
+    with pytest.raises(RuntimeError):
+        _run(hip, hip.HPA_FEPI_GELU, 65, 768, 256, 8, ln=False, rng=np.random.default_rng(1), variant=3)
+    with pytest.raises(RuntimeError):
+        _run(hip, hip.HPA_FEPI_GELU, 64, 768, 256, 8, ln=True, rng=np.random.default_rng(1), variant=3)
