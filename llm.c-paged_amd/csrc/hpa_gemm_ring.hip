@@ -72,7 +72,8 @@ __device__ __forceinline__ void rn_dma(const float* src, unsigned lds_addr) {
 
 // MODE (diagnostics, tools/ring_tune.py): 0 the product; 1 no MFMAs (the
 // ring runs, the MFMA waves only read it); 2 no LDS-DMA (MFMAs on whatever
-// the ring holds)
+// the ring holds); 3 as 2 without the per-stage barriers; 4 as 3 on
+// register operands (no LDS reads)
 // ROT: workgroup b walks the K stages starting at stage b % nst (every
 // workgroup reads the same A: this spreads the concurrent A requests over
 // the L2 channels instead of all workgroups asking for the same lines); a
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(kRnNW * 64) void gemm_ring_kernel(FG p) {
             }
         }
     };
-    if (loader && MODE != 2) {
+    if (loader && MODE < 2) {
         issue(0);
         issue(1);
     }
@@ -140,22 +141,30 @@ __global__ __launch_bounds__(kRnNW * 64) void gemm_ring_kernel(FG p) {
     // measured slower: XL qkv 23.7 vs 23.0 us, profiles/r3/experiments/.)
     if (loader) {
         for (int st = 0; st < nst; ++st) {
-            if (MODE != 2)
+            if (MODE < 2)
                 __builtin_amdgcn_s_waitcnt((kRnPerLd & 15) | ((kRnPerLd >> 4) << 14) | (7 << 4));  // vmcnt(PerLd) lgkmcnt(0)
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            if (MODE != 2) issue(st + 2);
+            if (MODE < 3) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (MODE < 2) issue(st + 2);
         }
     } else {
         for (int st = 0; st < nst; ++st) {
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (MODE < 3) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
             const int so = (st % kRnStages) * kRnStageF;
             const int ns = min(KH, K16 - phys(st) * kRnKS - h * KH);  // may be <= 0 in the last stage
 #pragma unroll
             for (int s = 0; s < KH; ++s) {
                 if (s < ns) {
-                    const float4 xv = *reinterpret_cast<const float4*>(ra + so + s * 256);
-                    const float4 w0 = *reinterpret_cast<const float4*>(rw + so + s * 256);
-                    const float4 w1 = *reinterpret_cast<const float4*>(rw + so + (kRnKS + s) * 256);
+                    float4 xv, w0, w1;
+                    if (MODE == 4) {  // register operands only
+                        const float f = (float)(lane + s + st);
+                        xv = make_float4(f, f + 1.f, f + 2.f, f + 3.f);
+                        w0 = make_float4(f * 0.5f, f, f, f);
+                        w1 = make_float4(f, f * 0.25f, f, f);
+                    } else {
+                        xv = *reinterpret_cast<const float4*>(ra + so + s * 256);
+                        w0 = *reinterpret_cast<const float4*>(rw + so + s * 256);
+                        w1 = *reinterpret_cast<const float4*>(rw + so + (kRnKS + s) * 256);
+                    }
                     if (fold) row_sums_add(xv, fs1, fs2);
                     if (MODE == 1) {
                         acc0[0] += (xv.x + w0.x) + (xv.y + w0.y);
@@ -208,7 +217,9 @@ int launch_ring_rot(const FG& p, int mode) {
     switch (mode) {
         case 0: gemm_ring_kernel<EPI, 0, ROT><<<grid, kRnNW * 64, 0, hpa_stream()>>>(p); break;
         case 1: gemm_ring_kernel<EPI, 1, ROT><<<grid, kRnNW * 64, 0, hpa_stream()>>>(p); break;
-        default: gemm_ring_kernel<EPI, 2, ROT><<<grid, kRnNW * 64, 0, hpa_stream()>>>(p); break;
+        case 2: gemm_ring_kernel<EPI, 2, ROT><<<grid, kRnNW * 64, 0, hpa_stream()>>>(p); break;
+        case 3: gemm_ring_kernel<EPI, 3, ROT><<<grid, kRnNW * 64, 0, hpa_stream()>>>(p); break;
+        default: gemm_ring_kernel<EPI, 4, ROT><<<grid, kRnNW * 64, 0, hpa_stream()>>>(p); break;
     }
     HPA_LAUNCH_CHECK();
     return 0;
