@@ -223,7 +223,10 @@ typedef struct {
                              row block; (waves, K/16) in {(4,48),(8,48),(16,48),(8,192),(16,192),(10,100)});
                              3 = loader / MFMA-wave ring (hpa_gemm_ring.hip): <= 64 padded rows,
                              LN folded (ln_fold_c1) or absent, QKV / GELU / RESID; one
-                             12-wave workgroup per 32 columns, waves/row_blocks/col_tiles ignored;
+                             12-wave workgroup per 32 columns and K part; waves = K parts
+                             (0/1 = none; 2..4 need sk_slab / sk_count sized by
+                             hpa_gemm_ring_workspace: the last part of a column pair sums
+                             the parts in part order); row_blocks / col_tiles ignored;
                              4 = LOGITS only: activation-resident persistent kernel
                              (K = 768, rows <= 64; 16 waves); else stream-K (6) when
                              sk_slab / sk_count are given and rows <= 64; else as 1;
@@ -266,6 +269,10 @@ typedef struct {
 int hpa_ln_fold_pack(const float* W, int N, int K, const float* ln_w, const float* ln_b, const float* bias,
                      float* dst_frag, float* c1, float* c2);
 int hpa_gemm_fused(const HpaFusedGemm* g);
+/* variant 3 K-split workspace for an (N) GEMM in `parts` K parts: slab
+ * floats and counters (zero before the first launch; every launch leaves them
+ * zero); nonzero on bad arguments */
+int hpa_gemm_ring_workspace(int N, int parts, size_t* slab_floats, size_t* counters);
 /* variant 6 workspace: slab floats and counters for an (N) GEMM on this
  * device's CU count (enough for any K and M <= 64) */
 int hpa_gemm_sk_workspace(int N, size_t* slab_floats, size_t* counters);

@@ -840,7 +840,8 @@ int hpa_gemm_fused(const HpaFusedGemm* g) {
                 "gemm_fused: row_blocks must be 1, 2 or 4");
     looped_shape(g, p.Mp, &nw, &mt, &ntw);
     HPA_REQUIRE(g->variant >= 0 && g->variant <= 4, "gemm_fused: variant must be 0, 1, 2, 3 or 4");
-    if (g->variant == 3) return launch_ring(p, g->epilogue);  // loader / MFMA-wave ring (hpa_gemm_ring.hip)
+    if (g->variant == 3)  // loader / MFMA-wave ring (hpa_gemm_ring.hip); waves = K parts
+        return launch_ring(p, g->epilogue, g->waves > 0 ? g->waves : 1);
     // (waves 16 / 12: the resident kernel's 16-wave or ring form; else by M)
     if (g->variant == 4 && logits_resident_eligible(p, g->epilogue)) return launch_logits_resident(p, g->waves);
     // variant 4 elsewhere (GPT-2 XL logits, K = 1600): stream-K when the caller

@@ -629,10 +629,11 @@ int launch_b16(const FG& p, int epi, int nw, int mt, int ntw);
 // A-resident bf16 variant (variant 5): waves 4/8, row_blocks (mt) 1/2/4 with
 // mt*K <= 3200; each workgroup takes waves*rounds column tiles
 int launch_b16_ares(const FG& p, int epi, int nw, int mt, int rounds);
-// loader / MFMA-wave ring kernel (hpa_gemm_ring.hip, variant 3): 64 padded
-// rows, LN folded or absent, QKV / GELU / RESID
+// loader / MFMA-wave ring kernel (hpa_gemm_ring.hip, variant 3): <= 64
+// padded rows, LN folded or absent, QKV / GELU / RESID; parts = K parts
+// (> 1: sk_slab / sk_cnt workspace, hpa_gemm_ring_workspace)
 bool ring_eligible(const FG& p, int epi);
-int launch_ring(const FG& p, int epi);
+int launch_ring(const FG& p, int epi, int parts);
 // stream-K fp32 kernel (hpa_gemm_sk.hip, variant 6): M <= 64
 int launch_sk(const FG& p, int epi);
 bool sk_eligible(int Mp, int ntn, int K16);

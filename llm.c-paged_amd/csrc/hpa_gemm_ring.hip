@@ -38,19 +38,25 @@ namespace {
 constexpr int kRnNW = 12;                   // waves per workgroup
 constexpr int kRnNC = 8;                    // MFMA waves (row block w & 3, stage half w >> 2)
 constexpr int kRnLd = kRnNW - kRnNC;        // loader waves
-constexpr int kRnKS = 8;                    // k16 steps per stage
-constexpr int kRnChunks = (4 + 2) * kRnKS;  // 1 KiB fragments per stage: A[4][KS], W[2][KS]
-constexpr int kRnPerLd = kRnChunks / kRnLd; // LDS-DMA wave-instructions per loader per stage
-constexpr int kRnStageF = kRnChunks * 256;  // floats per stage (48 KiB)
 constexpr int kRnStages = 3;
-constexpr int kRnLdsF = kRnStages * kRnStageF;
-static_assert(kRnLdsF * 4 <= 160 * 1024, "LDS");
-static_assert(kRnChunks % kRnLd == 0, "chunks per loader");
+// per stage of KS k16 steps: 1 KiB fragments A[4][KS], W[2][KS]
+template <int KS>
+struct RnShape {
+    static constexpr int Chunks = 6 * KS;
+    static constexpr int PerLd = Chunks / kRnLd;  // LDS-DMA wave-instructions per loader per stage
+    static constexpr int StageF = Chunks * 256;   // floats per stage
+    static constexpr int LdsF = kRnStages * StageF;
+    static_assert(LdsF * 4 <= 160 * 1024, "LDS");
+    static_assert(Chunks % kRnLd == 0 && KS % 2 == 0, "chunks per loader, stage halves");
+};
 // epilogue scratch over the ring (dead after the loop)
 constexpr int kRnRedF = 2 * 2 * 4 * 256;    // [2 halves][2 tiles][4 row blocks][4 regs][64 lanes]
 constexpr int kRnTileF = 2 * 64 * 17;       // Epi::apply's row-statistics tile
 constexpr int kRnWsumF = kRnNW * 64 * 2;    // [NW][64 rows][2] LN row partials (slots 0, 1 used)
-static_assert(kRnRedF + kRnTileF + kRnWsumF <= kRnLdsF, "epilogue scratch");
+static_assert(kRnRedF + kRnTileF + kRnWsumF <= RnShape<4>::LdsF, "epilogue scratch");
+// K-split workspace per (column pair, K part): the folded 64 x 32 tile, then
+// the rows' (sum, sum of squares)
+constexpr int kRnPartF = 2048 + 128;
 
 // LDS-DMA of one 1 KiB fragment (16 B per lane to lds_addr + 16 * lane).
 // Inline asm (as hpa_logits.hip's ring): the compiler does not count these
@@ -74,23 +80,31 @@ __device__ __forceinline__ void rn_dma(const float* src, unsigned lds_addr) {
 // ring runs, the MFMA waves only read it); 2 no LDS-DMA (MFMAs on whatever
 // the ring holds); 3 as 2 without the per-stage barriers; 4 as 3 on
 // register operands (no LDS reads)
-// ROT: workgroup b walks the K stages starting at stage b % nst (every
-// workgroup reads the same A: this spreads the concurrent A requests over
-// the L2 channels instead of all workgroups asking for the same lines); a
-// tile's summation order then depends on its column pair, never on M
-template <int EPI, int MODE, bool ROT>
-__global__ __launch_bounds__(kRnNW * 64) void gemm_ring_kernel(FG p) {
-    __shared__ __attribute__((aligned(16))) float ring[kRnLdsF];
+// KS: k16 steps per stage (8: one 12-wave workgroup per CU, 144 KiB of ring;
+// 4: two per CU, 72 KiB).  SPLIT: the grid is column pairs x p.gy K parts
+// (contiguous stage ranges); each part publishes its folded tile and row
+// sums to p.sk_slab (write-through), draws a ticket on p.sk_cnt[pair], and
+// the last of the pair sums the parts in part order (results independent of
+// arrival order and of M), rewinds the counter and runs the epilogue.
+template <int EPI, int MODE, int KS, bool SPLIT>
+__global__ __launch_bounds__(kRnNW * 64, KS == 4 ? 2 : 1) void gemm_ring_kernel(FG p) {
+    using S = RnShape<KS>;
+    __shared__ __attribute__((aligned(16))) float ring[S::LdsF];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool loader = w >= kRnNC;
     const int r = w & 3, h = (w >> 2) & 1;
-    const int nt0 = blockIdx.x * 2;
+    const int npairs = (p.ntn + 1) / 2;
+    const int nparts = SPLIT ? p.gy : 1;
+    const int pair = SPLIT ? (int)(blockIdx.x % (unsigned)npairs) : (int)blockIdx.x;
+    const int part = SPLIT ? (int)(blockIdx.x / (unsigned)npairs) : 0;
+    const int nt0 = pair * 2;
     const int K16 = p.K16;
-    const int nst = (K16 + kRnKS - 1) / kRnKS;
-    const int rot = ROT ? (int)(blockIdx.x % (unsigned)nst) : 0;
-    auto phys = [&](int st) __attribute__((always_inline)) {  // logical stage -> k stage
-        return st < nst ? (st + rot >= nst ? st + rot - nst : st + rot) : st;
+    const int nst_all = (K16 + KS - 1) / KS;
+    const int st_b = part * nst_all / nparts;
+    const int nst = (part + 1) * nst_all / nparts - st_b;  // this part's stages
+    auto phys = [&](int st) __attribute__((always_inline)) {  // the part's stage st -> k stage
+        return st_b + st;
     };
     const bool fold = p.fold_c1 != nullptr;
 
@@ -99,26 +113,27 @@ __global__ __launch_bounds__(kRnNW * 64) void gemm_ring_kernel(FG p) {
 
     const unsigned ring_lds =
         __builtin_amdgcn_readfirstlane((unsigned)(size_t)(__attribute__((address_space(3))) float*)ring);
-    // loader wave L = w - 8 moves chunks q = L + 4 i of every stage: q < 32 ->
-    // A (row block q >> 3, step q & 7), else W (tile (q - 32) >> 3, step q & 7)
+    // loader wave L = w - 8 moves chunks q = L + 4 i of every stage: q < 4 KS
+    // -> A (row block q / KS, step q % KS), else W (tile (q - 4 KS) / KS)
     const int L = w - kRnNC;
     const int nrb = p.Mp >> 4;
     const float* xa = p.x + (size_t)lane * 4;
     const float* wa0 = p.w + (size_t)min(nt0, p.ntn - 1) * K16 * 256 + lane * 4;
     const float* wa1 = p.w + (size_t)min(nt0 + 1, p.ntn - 1) * K16 * 256 + lane * 4;
     auto issue = [&](int st) __attribute__((always_inline)) {
-        const unsigned base = ring_lds + (unsigned)((st % kRnStages) * kRnStageF) * 4;
+        const unsigned base = ring_lds + (unsigned)((st % kRnStages) * S::StageF) * 4;
+        const int kst = st < nst ? phys(st) : phys(nst - 1);  // past the part's end: a harmless re-read
 #pragma unroll
-        for (int i = 0; i < kRnPerLd; ++i) {
+        for (int i = 0; i < S::PerLd; ++i) {
             const int q = L + kRnLd * i;
-            const int s = q & 7;
-            const int k = min(phys(st) * kRnKS + s, K16 - 1);  // past the end: a harmless re-read
+            const int s = q % KS;
+            const int k = min(kst * KS + s, K16 - 1);
             const unsigned dst = base + (unsigned)q * 1024;
-            if (i < 32 / kRnLd) {  // A chunk (compile-time: q < 32 for every loader); row
+            if (i < KS) {  // A chunk (compile-time: q < 4 KS for every loader); row
                 // blocks past Mp re-read the last one (their rows are never stored)
-                rn_dma<false>(xa + ((size_t)min(q >> 3, nrb - 1) * K16 + k) * 256, dst);
+                rn_dma<false>(xa + ((size_t)min(q / KS, nrb - 1) * K16 + k) * 256, dst);
             } else {
-                rn_dma<true>((((q - 32) >> 3) ? wa1 : wa0) + (size_t)k * 256, dst);
+                rn_dma<true>((((q - 4 * KS) / KS) ? wa1 : wa0) + (size_t)k * 256, dst);
             }
         }
     };
@@ -129,9 +144,9 @@ __global__ __launch_bounds__(kRnNW * 64) void gemm_ring_kernel(FG p) {
 
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     float fs1 = 0.f, fs2 = 0.f;
-    constexpr int KH = kRnKS / 2;  // steps per half-stage
-    const float* ra = ring + (r * kRnKS + h * KH) * 256 + lane * 4;   // A[r][s] of a stage
-    const float* rw = ring + (32 + h * KH) * 256 + lane * 4;          // W[0][s]; W[1][s] at + KS
+    constexpr int KH = KS / 2;  // steps per half-stage
+    const float* ra = ring + (r * KS + h * KH) * 256 + lane * 4;   // A[r][s] of a stage
+    const float* rw = ring + (4 * KS + h * KH) * 256 + lane * 4;   // W[0][s]; W[1][s] at + KS
     // iteration st: the loaders' stage st has landed -> barrier -> loaders
     // issue stage st + 2 into the slot read in iteration st - 1; the MFMA
     // waves multiply stage st.  The two roles run separate loops with the
@@ -142,15 +157,15 @@ __global__ __launch_bounds__(kRnNW * 64) void gemm_ring_kernel(FG p) {
     if (loader) {
         for (int st = 0; st < nst; ++st) {
             if (MODE < 2)
-                __builtin_amdgcn_s_waitcnt((kRnPerLd & 15) | ((kRnPerLd >> 4) << 14) | (7 << 4));  // vmcnt(PerLd) lgkmcnt(0)
+                __builtin_amdgcn_s_waitcnt((S::PerLd & 15) | ((S::PerLd >> 4) << 14) | (7 << 4));  // vmcnt(PerLd) lgkmcnt(0)
             if (MODE < 3) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
             if (MODE < 2) issue(st + 2);
         }
     } else {
         for (int st = 0; st < nst; ++st) {
             if (MODE < 3) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            const int so = (st % kRnStages) * kRnStageF;
-            const int ns = min(KH, K16 - phys(st) * kRnKS - h * KH);  // may be <= 0 in the last stage
+            const int so = (st % kRnStages) * S::StageF;
+            const int ns = min(KH, K16 - phys(st) * KS - h * KH);  // may be <= 0 in the last stage
 #pragma unroll
             for (int s = 0; s < KH; ++s) {
                 if (s < ns) {
@@ -163,7 +178,7 @@ __global__ __launch_bounds__(kRnNW * 64) void gemm_ring_kernel(FG p) {
                     } else {
                         xv = *reinterpret_cast<const float4*>(ra + so + s * 256);
                         w0 = *reinterpret_cast<const float4*>(rw + so + s * 256);
-                        w1 = *reinterpret_cast<const float4*>(rw + so + (kRnKS + s) * 256);
+                        w1 = *reinterpret_cast<const float4*>(rw + so + (KS + s) * 256);
                     }
                     if (fold) row_sums_add(xv, fs1, fs2);
                     if (MODE == 1) {
@@ -208,26 +223,67 @@ __global__ __launch_bounds__(kRnNW * 64) void gemm_ring_kernel(FG p) {
         const int e = threadIdx.x + i * kRnNW * 64;
         vals[i] = e < 2 * 1024 ? red[e] + red[2048 + e] : 0.f;  // half 0 + half 1
     }
+    if constexpr (SPLIT) {
+        float* slab = p.sk_slab;
+        const int own = (pair * nparts + part) * kRnPartF;
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+            const int e = threadIdx.x + i * kRnNW * 64;
+            if (e < 2048) hpa::store_wt4(slab, (own + e) * 4, vals[i]);
+        }
+        float rsum = 0.f;  // thread t < 128: row t / 2's sum (t even) or sum of squares
+        if (fold && threadIdx.x < 128) {
+            rsum = wsum[threadIdx.x] + wsum[128 + threadIdx.x];
+            hpa::store_wt4(slab, (own + 2048 + threadIdx.x) * 4, rsum);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drained
+        __shared__ int s_last;
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (threadIdx.x == 0) {
+            const int t = __hip_atomic_fetch_add(p.sk_cnt + pair, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = t == nparts - 1;
+            if (t == nparts - 1) __hip_atomic_store(p.sk_cnt + pair, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (!s_last) return;
+        // the last part: every part's value in part order (own from registers)
+        const int pb = pair * nparts * kRnPartF;
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+            const int e = threadIdx.x + i * kRnNW * 64;
+            if (e < 2048) {
+                float v = 0.f;
+                for (int q = 0; q < nparts; ++q) v += q == part ? vals[i] : hpa::load_wt4(slab, (pb + q * kRnPartF + e) * 4);
+                vals[i] = v;
+            }
+        }
+        if (fold && threadIdx.x < 128) {
+            float v = 0.f;
+            for (int q = 0; q < nparts; ++q) v += q == part ? rsum : hpa::load_wt4(slab, (pb + q * kRnPartF + 2048 + threadIdx.x) * 4);
+            wsum[threadIdx.x] = v;  // slot 0: the whole K; slot 1 emptied
+            wsum[128 + threadIdx.x] = 0.f;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
     epi.apply(p, vals, tile, nt0, 0, wsum);
 }
 
-template <int EPI, bool ROT>
-int launch_ring_rot(const FG& p, int mode) {
-    const unsigned grid = (unsigned)((p.ntn + 1) / 2);
-    switch (mode) {
-        case 0: gemm_ring_kernel<EPI, 0, ROT><<<grid, kRnNW * 64, 0, hpa_stream()>>>(p); break;
-        case 1: gemm_ring_kernel<EPI, 1, ROT><<<grid, kRnNW * 64, 0, hpa_stream()>>>(p); break;
-        case 2: gemm_ring_kernel<EPI, 2, ROT><<<grid, kRnNW * 64, 0, hpa_stream()>>>(p); break;
-        case 3: gemm_ring_kernel<EPI, 3, ROT><<<grid, kRnNW * 64, 0, hpa_stream()>>>(p); break;
-        default: gemm_ring_kernel<EPI, 4, ROT><<<grid, kRnNW * 64, 0, hpa_stream()>>>(p); break;
+template <int EPI>
+int launch_ring_epi(const FG& p, int mode, int parts) {
+    const unsigned npairs = (unsigned)((p.ntn + 1) / 2);
+    if (parts > 1) {
+        gemm_ring_kernel<EPI, 0, 4, true><<<npairs * (unsigned)parts, kRnNW * 64, 0, hpa_stream()>>>(p);
+    } else {
+        switch (mode) {
+            case 0: gemm_ring_kernel<EPI, 0, 8, false><<<npairs, kRnNW * 64, 0, hpa_stream()>>>(p); break;
+            case 1: gemm_ring_kernel<EPI, 1, 8, false><<<npairs, kRnNW * 64, 0, hpa_stream()>>>(p); break;
+            case 2: gemm_ring_kernel<EPI, 2, 8, false><<<npairs, kRnNW * 64, 0, hpa_stream()>>>(p); break;
+            case 3: gemm_ring_kernel<EPI, 3, 8, false><<<npairs, kRnNW * 64, 0, hpa_stream()>>>(p); break;
+            default: gemm_ring_kernel<EPI, 4, 8, false><<<npairs, kRnNW * 64, 0, hpa_stream()>>>(p); break;
+        }
     }
     HPA_LAUNCH_CHECK();
     return 0;
-}
-
-template <int EPI>
-int launch_ring_epi(const FG& p, int mode, bool rot) {
-    return rot ? launch_ring_rot<EPI, true>(p, mode) : launch_ring_rot<EPI, false>(p, mode);
 }
 
 }  // namespace
@@ -240,24 +296,37 @@ bool ring_eligible(const FG& p, int epi) {
            (epi == HPA_FEPI_QKV || epi == HPA_FEPI_GELU || epi == HPA_FEPI_RESID);
 }
 
-// HPA_RING_MODE=1 / 2: the diagnostic forms (no MFMAs / no LDS-DMA);
-// HPA_RING_ROT=1: the rotated stage order
-int launch_ring(const FG& p, int epi) {
-    HPA_REQUIRE(ring_eligible(p, epi), "gemm_fused ring (variant 3): <= 64 padded rows, LN folded or none, "
-                                       "QKV / GELU / RESID");
+// parts: K parts (1 = no split; 2..4 with p.sk_slab / p.sk_cnt from
+// hpa_gemm_ring_workspace).  HPA_RING_MODE=1..4: the unsplit kernel's
+// diagnostic forms (no MFMAs / no LDS-DMA / no barriers / register operands)
+int launch_ring(const FG& p_in, int epi, int parts) {
+    HPA_REQUIRE(ring_eligible(p_in, epi), "gemm_fused ring (variant 3): <= 64 padded rows, LN folded or none, "
+                                          "QKV / GELU / RESID");
+    HPA_REQUIRE(parts >= 1 && parts <= 4, "gemm_fused ring: K parts 1..4");
+    HPA_REQUIRE(parts == 1 || (p_in.sk_slab && p_in.sk_cnt), "gemm_fused ring: K split needs sk_slab / sk_count");
+    HPA_REQUIRE(parts == 1 || (p_in.K16 + 3) / 4 >= parts, "gemm_fused ring: fewer 4-step stages than K parts");
     static const int mode = [] {
         const char* e = getenv("HPA_RING_MODE");
         return e ? atoi(e) : 0;
     }();
-    static const bool rot = [] {  // HPA_RING_ROT=1: rotated stage order (A/B knob)
-        const char* e = getenv("HPA_RING_ROT");
-        return e && e[0] == '1';
-    }();
+    FG p = p_in;
+    p.gy = parts;
     switch (epi) {
-        case HPA_FEPI_QKV: return launch_ring_epi<HPA_FEPI_QKV>(p, mode, rot);
-        case HPA_FEPI_GELU: return launch_ring_epi<HPA_FEPI_GELU>(p, mode, rot);
-        default: return launch_ring_epi<HPA_FEPI_RESID>(p, mode, rot);
+        case HPA_FEPI_QKV: return launch_ring_epi<HPA_FEPI_QKV>(p, mode, parts);
+        case HPA_FEPI_GELU: return launch_ring_epi<HPA_FEPI_GELU>(p, mode, parts);
+        default: return launch_ring_epi<HPA_FEPI_RESID>(p, mode, parts);
     }
 }
 
 }  // namespace hpa_gemm
+
+// K-split workspace of the ring kernel (variant 3, waves = K parts) for an
+// (N) GEMM: slab floats and counters (zero before the first launch; every
+// launch leaves them zero)
+extern "C" int hpa_gemm_ring_workspace(int N, int parts, size_t* slab_floats, size_t* counters) {
+    if (N <= 0 || parts < 1 || parts > 4 || !slab_floats || !counters) return 1;
+    const size_t npairs = (size_t)((N + 15) / 16 + 1) / 2;
+    *slab_floats = npairs * (size_t)parts * hpa_gemm::kRnPartF;
+    *counters = npairs;
+    return 0;
+}

@@ -21,6 +21,11 @@
 #include "block_manager.h"
 #include "hip_paged_attn.h"
 
+/* K parts of the ring qkv / fc at C >= 1024 (dec_gemm, hpa_gemm_ring.hip) */
+#define DEC_RING_QKV_PARTS 3
+#define DEC_RING_FC_PARTS 2
+static int dec_ring_allowed(void);
+
 #define PI_FATAL(...)                                         \
     do {                                                      \
         fprintf(stderr, "[paged_infer] " __VA_ARGS__);        \
@@ -625,6 +630,9 @@ struct GPT2Decode {
     float* sk_slab;   /* stream-K logits workspace (hpa_logits_kernel == 6), else NULL */
     int* sk_cnt;
     size_t sk_cnt_n;
+    float* ring_slab; /* K-split workspace of the ring qkv / fc (C >= 1024, fp32), else NULL */
+    int* ring_cnt;
+    size_t ring_cnt_n;
     float* d_wpack;   /* packed qkvw, attprojw, fcw, fcprojw of every layer, then wte */
     int w_bf16;       /* weights packed bf16 (hpa_pack_frag_bf16; offsets in elements) */
     size_t wpack_off[5]; /* per-layer offsets (0..3) and wte offset (4) */
@@ -762,6 +770,7 @@ static void dec_free(GPT2Decode* d) {
     hpa_free(d->res); hpa_free(d->res2); hpa_free(d->att); hpa_free(d->fch);
     hpa_free(d->st1); hpa_free(d->st2); hpa_free(d->part);
     hpa_free(d->sk_slab); hpa_free(d->sk_cnt);
+    hpa_free(d->ring_slab); hpa_free(d->ring_cnt);
     hpa_free(d->d_wpack);
     hpa_free(d->d_fold);
     hpa_free(d->d_attn_ws);
@@ -954,14 +963,15 @@ static int dec_layer(GPT2* model, int l) {
     return hpa_decode_layer(&a);
 }
 
-/* the in-launch arrival counters of the attention's split merge and of the
- * stream-K logits back to zero: every completed launch leaves them zero, a
+/* the in-launch arrival counters of the attention's split merge, of the
+ * stream-K logits and of the K-split ring GEMMs back to zero: every completed launch leaves them zero, a
  * launch that failed part-way may not.  Called before a graph is
  * recaptured and after a reported failure. */
 static int dec_rezero(GPT2Decode* d) {
     int rc = 0;
     if (d->d_attn_ws) rc |= hpa_memset_async(d->d_attn_ws, 0, d->attn_ws_bytes);
     if (d->sk_cnt && d->sk_cnt_n) rc |= hpa_memset_async(d->sk_cnt, 0, d->sk_cnt_n * sizeof(int));
+    if (d->ring_cnt && d->ring_cnt_n) rc |= hpa_memset_async(d->ring_cnt, 0, d->ring_cnt_n * sizeof(int));
     return rc;
 }
 
@@ -1079,6 +1089,20 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
             d->sk_cnt = (int*)hpa_malloc(nc * sizeof(int));
             d->sk_cnt_n = nc;
             ok = d->sk_slab && d->sk_cnt && hpa_memset_async(d->sk_cnt, 0, nc * sizeof(int)) == 0;
+        }
+    }
+    /* the ring qkv / fc of wide layers (dec_gemm): K split in DEC_RING_QKV_PARTS /
+     * DEC_RING_FC_PARTS parts over workgroups, one slab + counters for both */
+    if (ok && w_dtype != HPA_BF16 && C >= 1024 && dec_ring_allowed() == 2) {
+        size_t f1 = 0, c1 = 0, f2 = 0, c2 = 0;
+        ok = hpa_gemm_ring_workspace(3 * C, DEC_RING_QKV_PARTS, &f1, &c1) == 0 &&
+             hpa_gemm_ring_workspace(4 * C, DEC_RING_FC_PARTS, &f2, &c2) == 0;
+        if (ok) {
+            const size_t nf = f1 > f2 ? f1 : f2, nc = c1 > c2 ? c1 : c2;
+            d->ring_slab = (float*)hpa_malloc(nf * sizeof(float));
+            d->ring_cnt = (int*)hpa_malloc(nc * sizeof(int));
+            d->ring_cnt_n = nc;
+            ok = d->ring_slab && d->ring_cnt && hpa_memset_async(d->ring_cnt, 0, nc * sizeof(int)) == 0;
         }
     }
     for (int k = 0; k < 2 && ok; k++) {
@@ -1261,13 +1285,14 @@ static void dec_gemm_desc(GPT2* model, int l, int which, HpaFusedGemm* g) {
     }
 }
 
-/* HPA_GEMM_RING=0: GPT-2 XL's qkv / fc on the looped kernel instead of the
- * ring kernel (A/B knob; XL step 10.23 vs 10.38 ms) */
+/* GPT-2 XL's qkv / fc: 1 (default) the ring kernel; HPA_GEMM_RING=0 the
+ * looped kernel, =2 the ring with its K split over workgroups (A/B knobs; XL
+ * step 10.31 / 10.41 / 10.43 ms) */
 static int dec_ring_allowed(void) {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("HPA_GEMM_RING");
-        v = !(e && e[0] == '0');
+        v = e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
     }
     return v;
 }
@@ -1280,9 +1305,17 @@ static int dec_gemm(GPT2* model, int l, int which) {
          * shards of that batch take it too and stay bit-identical) */
         GPT2Decode* d = model->decode;
         const int Bg = d->pl_global_B > 0 ? d->pl_global_B : d->B;
+        const int ring = dec_ring_allowed();
         if ((which == G_QKV || which == G_FC) && !d->w_bf16 && d->d_fold && model->config.channels >= 1024 &&
-            Bg > 48 && d->B <= 64 && dec_ring_allowed())
+            Bg > 48 && d->B <= 64 && ring) {
             g.variant = 3;
+            /* HPA_GEMM_RING=2: K split over workgroups so all CUs compute (qkv
+             * 150 column pairs x 3, fc 200 x 2): measured slower (qkv 22.1 vs
+             * 21.9 us, fc 26.6 vs 22.9), kept as a tested option */
+            g.waves = ring == 1 || !d->ring_slab ? 1 : which == G_QKV ? DEC_RING_QKV_PARTS : DEC_RING_FC_PARTS;
+            g.sk_slab = d->ring_slab;
+            g.sk_count = d->ring_cnt;
+        }
     }
     return hpa_gemm_fused(&g);
 }

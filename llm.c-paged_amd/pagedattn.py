@@ -278,6 +278,7 @@ def lib():
     _sig(L, "gpt2_decode_time_attention_pf", i, [v, i, ctypes.c_double, i, ctypes.POINTER(ctypes.c_double),
                                                  ctypes.POINTER(ctypes.c_double)])
     _sig(L, "hpa_l3_prefetch", i, [v, sz, i])
+    _sig(L, "hpa_gemm_ring_workspace", i, [i, i, ctypes.POINTER(sz), ctypes.POINTER(sz)])
     _sig(L, "gpt2_decode_step_bytes", ctypes.c_double, [v, ctypes.POINTER(ctypes.c_double)])
     _sig(L, "random_u32", ctypes.c_uint, [ctypes.POINTER(ctypes.c_ulonglong)])
     _sig(L, "random_f32", f, [ctypes.POINTER(ctypes.c_ulonglong)])

@@ -246,6 +246,13 @@ def _run(hip, epi, M, K, N, waves, ln, rng, res=None, pool_args=None, rb=0, fixe
         g.block_table, g.bt_stride, g.pos = dev(bt), bt.shape[1], dev(pos)
     keep.append(out)
     keep.append(g)  # the descriptor (LOGITS: hpa_logits_partials)
+    if variant == 3 and waves > 1:  # K-split ring: slab + counters (zeroed once; every launch leaves them zero)
+        nf, nc = ctypes.c_size_t(), ctypes.c_size_t()
+        hip.check(L.hpa_gemm_ring_workspace(N, waves, ctypes.byref(nf), ctypes.byref(nc)), "ring workspace")
+        slab = hip.DeviceBuffer(nf.value * 4)
+        cnt = hip.DeviceBuffer.from_array(np.zeros(nc.value, np.int32))
+        keep.extend([slab, cnt])
+        g.sk_slab, g.sk_count = slab.ptr, cnt.ptr
     if variant == 6 or sk_ws:  # stream-K: slab + counters (zeroed once; every launch leaves them zero)
         nf, nc = ctypes.c_size_t(), ctypes.c_size_t()
         hip.check(L.hpa_gemm_sk_workspace(N, ctypes.byref(nf), ctypes.byref(nc)), "sk workspace")
@@ -632,12 +639,17 @@ def test_logits_variant4_takes_stream_k_with_workspace(hip):
                                           ("GELU", 768, 3072, True), ("GELU", 256, 80, False),
                                           ("RESID", 48, 1616, False), ("QKV", 768, 2304, False)])
 @pytest.mark.parametrize("M", [64, 49, 20, 5])
-def test_fused_ring(hip, epi, K, N, fold, M):
+@pytest.mark.parametrize("parts", [1, 3])
+def test_fused_ring(hip, epi, K, N, fold, M, parts):
     """loader / MFMA-wave ring kernel (variant 3, hpa_gemm_ring.hip): every
     epilogue within the f64 bound at 16-64 padded rows; LN folded or absent;
     K not a multiple of the 8-step stage (K16 = 100, 3); an odd column-tile
     count (N = 80, 1616: the last workgroup's second tile past N); the RESID
-    epilogue's 16-column LN partial sums; a relaunch is bit identical"""
+    epilogue's 16-column LN partial sums; a relaunch is bit identical; K split
+    in 3 parts over workgroups (the last part of a column pair sums them and
+    rewinds its counter)"""
+    if parts > 1 and K < 48 * parts:
+        pytest.skip("fewer 4-step stages than K parts")
     e = getattr(hip, "HPA_FEPI_" + epi)
     rng = np.random.default_rng(K + N + M + 3)
     res = rng.uniform(-1, 1, (M, N)).astype(np.float32) if epi == "RESID" else None
@@ -647,7 +659,7 @@ def test_fused_ring(hip, epi, K, N, fold, M):
         bt = np.arange(4 * M, dtype=np.int32).reshape(M, 4)
         pos = (np.arange(M, dtype=np.int32) * 7) % 64
         pool_args = (pool, bt, pos)
-    out, acc, bound, keep = _run(hip, e, M, K, N, 8, ln=fold, rng=rng, res=res, pool_args=pool_args,
+    out, acc, bound, keep = _run(hip, e, M, K, N, parts, ln=fold, rng=rng, res=res, pool_args=pool_args,
                                  variant=3, fold=fold)
     Mp = (M + 15) // 16 * 16
     if epi == "QKV":
@@ -667,7 +679,8 @@ def test_fused_ring(hip, epi, K, N, fold, M):
         else:
             assert np.all(np.abs(got - (acc + res)) <= bound + 1e-6)
             assert not hip.from_frag(full, Mp, N)[M:].any()  # padded rows stay zero
-            st = [k for k in keep if isinstance(k, hip.DeviceBuffer)][-2].download((N // 16, Mp, 2))
+            st = [k for k in keep if isinstance(k, hip.DeviceBuffer) and k.nbytes == N // 16 * Mp * 2 * 4][0]
+            st = st.download((N // 16, Mp, 2))
             g16 = got.astype(np.float64).reshape(M, N // 16, 16)
             assert np.allclose(st[:, :M, 0].T, g16.sum(-1), rtol=1e-5, atol=1e-4)
             assert np.allclose(st[:, :M, 1].T, (g16 ** 2).sum(-1), rtol=1e-5, atol=1e-4)
@@ -676,6 +689,9 @@ def test_fused_ring(hip, epi, K, N, fold, M):
     hip.check(hip.lib().hpa_synchronize())
     again = out.download((M, N // 3)) if epi == "QKV" else hip.from_frag(out.download(Mp * N), M, N)
     assert np.array_equal(again, got)
+    if parts > 1:
+        cnt = [k for k in keep if isinstance(k, hip.DeviceBuffer)][-1]
+        assert not cnt.download((cnt.nbytes // 4,), np.int32).any()
 
 
 def test_fused_ring_rows_independent_of_batch(hip):
@@ -687,17 +703,20 @@ def test_fused_ring_rows_independent_of_batch(hip):
                  W=rng.uniform(-0.05, 0.05, (N, K)).astype(np.float32),
                  bias=rng.uniform(-0.1, 0.1, N).astype(np.float32),
                  lw=rng.uniform(0.8, 1.2, K).astype(np.float32), lb=rng.uniform(-0.1, 0.1, K).astype(np.float32))
-    outs = []
-    for M in (64, 20):
-        out, _, _, keep = _run(hip, hip.HPA_FEPI_GELU, M, K, N, 8, ln=True, rng=rng, fixed=fixed, variant=3,
-                               fold=True)
-        outs.append(hip.from_frag(out.download((M + 15) // 16 * 16 * N), M, N))
-    assert np.array_equal(outs[0][:20], outs[1])
+    for parts in (1, 3):
+        outs = []
+        for M in (64, 20):
+            out, _, _, keep = _run(hip, hip.HPA_FEPI_GELU, M, K, N, parts, ln=True, rng=rng, fixed=fixed, variant=3,
+                                   fold=True)
+            outs.append(hip.from_frag(out.download((M + 15) // 16 * 16 * N), M, N))
+        assert np.array_equal(outs[0][:20], outs[1])
 
 
 def test_fused_ring_rejects_unsupported_shape(hip):
     """variant 3 needs <= 64 padded rows and no LayerNorm applied on load"""
     with pytest.raises(RuntimeError):
-        _run(hip, hip.HPA_FEPI_GELU, 65, 768, 256, 8, ln=False, rng=np.random.default_rng(1), variant=3)
+        _run(hip, hip.HPA_FEPI_GELU, 65, 768, 256, 1, ln=False, rng=np.random.default_rng(1), variant=3)
     with pytest.raises(RuntimeError):
-        _run(hip, hip.HPA_FEPI_GELU, 64, 768, 256, 8, ln=True, rng=np.random.default_rng(1), variant=3)
+        _run(hip, hip.HPA_FEPI_GELU, 64, 768, 256, 1, ln=True, rng=np.random.default_rng(1), variant=3)
+    with pytest.raises(RuntimeError):  # 5 K parts
+        _run(hip, hip.HPA_FEPI_GELU, 64, 768, 256, 5, ln=False, rng=np.random.default_rng(1), variant=3)

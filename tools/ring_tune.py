@@ -3,7 +3,8 @@
 engine's launch shape against the loader / MFMA-wave ring kernel (variant 3,
 hpa_gemm_ring.hip).  qkv / fc with LayerNorm folded (hpa_ln_fold_pack), as in
 the engine; HIP-event timing of back-to-back launches; max |diff| between the
-two kernels' outputs.  HPA_RING_MODE=1 / 2 (set before the run) times the
+two kernels' outputs; the ring at K parts S = 1..4 (S > 1: two
+workgroups per CU, the last part of a column pair sums the parts).  HPA_RING_MODE=1 / 2 (set before the run) times the
 ring's no-MFMA / no-DMA diagnostic forms.  usage: ring_tune.py [B] [C]"""
 import ctypes
 import os
@@ -81,12 +82,25 @@ for name, K, N, epi, fold in (("qkv", C, 3 * C, pa.HPA_FEPI_GELU, True), ("attpr
     a = np.empty(n, np.float32)
     pa.check(pa.lib().hpa_memcpy(a.ctypes.data, g.out, a.nbytes))
     g.variant = 3
-    t_ring = run(g)
-    b = np.empty(n, np.float32)
-    pa.check(pa.lib().hpa_memcpy(b.ctypes.data, g.out, b.nbytes))
+    line = f"{name:8s} K={K:5d} N={N:5d}  looped {tuple(pk)} {t_loop:7.2f} us  ring"
+    best = None
+    for parts in (1, 2, 3, 4):
+        if parts > 1:
+            if (K // 16 + 3) // 4 < parts:
+                continue
+            nf, nc = ctypes.c_size_t(), ctypes.c_size_t()
+            pa.check(pa.lib().hpa_gemm_ring_workspace(N, parts, ctypes.byref(nf), ctypes.byref(nc)), "ws")
+            slab = pa.DeviceBuffer(nf.value * 4)
+            cnt = pa.DeviceBuffer.from_array(np.zeros(nc.value, np.int32))
+            keep.extend([slab, cnt])
+            g.sk_slab, g.sk_count = slab.ptr, cnt.ptr
+        g.waves = parts
+        t = run(g)
+        b = np.empty(n, np.float32)
+        pa.check(pa.lib().hpa_memcpy(b.ctypes.data, g.out, b.nbytes))
+        line += f"  S={parts} {t:6.2f} ({float(np.abs(a - b).max()):.1e})"
+        best = t if best is None else min(best, t)
     tot[0] += t_loop
-    tot[1] += t_ring
-    fl = 2.0 * B * K * N
-    print(f"{name:8s} K={K:5d} N={N:5d}  looped {tuple(pk)} {t_loop:7.2f} us  ring {t_ring:7.2f} us "
-          f"({fl / t_ring / 1e6:5.1f} TF/s)  max|diff| {float(np.abs(a - b).max()):.2e}", flush=True)
-print(f"layer GEMMs: looped {tot[0]:.1f} us, ring {tot[1]:.1f} us")
+    tot[1] += best
+    print(line, flush=True)
+print(f"layer GEMMs: looped {tot[0]:.1f} us, ring (best S) {tot[1]:.1f} us")
