@@ -379,7 +379,9 @@ def main():
                        "layer_loop": {0: "five launches per layer",
                                       1: "one persistent launch per layer (hpa_decode_layer)",
                                       2: "attention launch + one persistent launch of the GEMM chain "
-                                         "(hpa_decode_layer chain_only)"}[model.layer_form()],
+                                         "(hpa_decode_layer chain_only)",
+                                      3: "attention launch + one persistent launch of the GEMM chain, wide "
+                                         "units (hpa_decode_layer chain_only 2)"}[model.layer_form()],
                        "token_choice": "multinomial (reference sample_mult)" if args.sample else "greedy",
                        "gemm_waves": [int(x) for x in model.gemm_config()[0]],
                        "gemm_row_blocks": [int(x) for x in model.gemm_config()[1]],

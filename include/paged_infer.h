@@ -208,15 +208,17 @@ int  gpt2_decode_attn_splits(GPT2* model);
 /* the layer loop's form: 0 five launches per layer; 2 one persistent launch
  * per layer (hpa_decode_layer: attention -> attproj -> fc -> fcproj -> next
  * qkv); 3 the decode attention's own launch + one persistent launch of the
- * GEMM chain (attproj -> fc -> fcproj -> next qkv); 1 (default, "auto") the
- * form measured fastest for the batch (profiles/r3).  The persistent forms
- * need fp32 weights, C = 128 / 768 and B <= 64 (else five launches).
- * HPA_LAYER_KERNEL=0..3 in the environment sets the default.  A persistent
+ * GEMM chain (attproj -> fc -> fcproj -> next qkv); 4 the same chain with
+ * wide units (one unit per 12-wave workgroup; B <= 16, C = 768; else 3);
+ * 1 (default, "auto") the form measured fastest for the batch (profiles/r3;
+ * the wide chain at a global batch <= 16 unless HPA_PL_WIDE=0).  The
+ * persistent forms need fp32 weights, C = 128 / 768 and B <= 64 (else five
+ * launches).  HPA_LAYER_KERNEL=0..4 in the environment sets the default.  A persistent
  * launch needs every CU for its 12-wave workgroups: a GPU shared with
  * another process's persistent kernels should use 0. */
 int  gpt2_decode_set_layer_kernel(GPT2* model, int enable);
 /* the form in use: 0 five launches, 1 full persistent layer, 2 attention
- * launch + persistent chain */
+ * launch + persistent chain, 3 the chain with wide units */
 int  gpt2_decode_layer_kernel(GPT2* model);
 /* waits for the queued work; 0, or the code of a timed-out in-launch wait of
  * the persistent layer (the step's outputs are then invalid), which it clears */

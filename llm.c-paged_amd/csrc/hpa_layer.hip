@@ -405,13 +405,23 @@ __device__ __forceinline__ float fold4(const float* red, int slot, int e) {
     return v;
 }
 
-// LayerNorm-folded value: rstd*(acc - mean*c1) + c2 (Epi::apply's order)
+// wide units (one unit per 12-wave workgroup): the 12 waves in wave order
+__device__ __forceinline__ float fold12(const float* red, int e) {
+    float v = red[e];
+#pragma unroll
+    for (int w = 1; w < 12; ++w) v += red[w * 256 + e];
+    return v;
+}
+
+// LayerNorm-folded value: rstd*(acc - mean*c1) + c2 (Epi::apply's order);
+// the row partial sums of the unit's NWU waves from wave slot * 4
+template <int NWU = 4>
 __device__ __forceinline__ float ln_fold_val(const float* wsum, int slot, int lrow, int K, float val, float c1,
                                              float c2) {
     const float* ws = wsum + slot * 4 * 32;
     float S1 = ws[2 * lrow], S2 = ws[2 * lrow + 1];
 #pragma unroll
-    for (int ww = 1; ww < 4; ++ww) {
+    for (int ww = 1; ww < NWU; ++ww) {
         S1 += ws[ww * 32 + 2 * lrow];
         S2 += ws[ww * 32 + 2 * lrow + 1];
     }
@@ -437,11 +447,19 @@ __device__ __forceinline__ void publish(const KA& a, int which, int nslots) {
 // ------------------------------------------------------------------ the kernel
 // ATTN = false: the chain only (attproj -> fc -> fcproj -> next qkv); the
 // attention ran as its own launch just before (hpa_paged_attention_decode_split
-// writing `att` in frag layout), so phase B needs no in-launch wait
-template <int NH, int P, bool BF, bool ATTN>
+// writing `att` in frag layout), so phase B needs no in-launch wait.
+// WIDE (chain only, one row block, C = 768): a unit is a whole workgroup --
+// unit v on workgroup v, its K range over all 12 waves (SW / 3 k16 steps
+// each, folded in wave order) -- instead of a 4-wave slot: at 16 rows every
+// phase has <= 192 units for 256 workgroups, so the 4-wave form leaves two of
+// the three slots idle and runs 3x longer MFMA chains per wave
+template <int NH, int P, bool BF, bool ATTN, bool WIDE>
 __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
     using D = LD<NH>;
     constexpr int C = D::C, SW = D::SW, NCT = D::NCT;
+    static_assert(!WIDE || (!ATTN && SW % 3 == 0), "wide units: chain form, SW divisible by 3");
+    constexpr int NWU = WIDE ? 12 : 4;  // waves per unit
+    constexpr int SWU = SW * 4 / NWU;   // k16 steps per wave
     // fields read where used from the kernarg segment (not all hoisted into
     // SGPRs at entry: the attention keeps q in 64 SGPRs)
     const KA& a = *(const KA*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -452,7 +470,9 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
     const int lane = threadIdx.x & 63;
     const int bid = blockIdx.x;
     const int R = a.R, G = a.G;
-    const int v = bid + slot * G;          // this slot's unit index in every phase
+    const int v = WIDE ? bid : bid + slot * G;  // this slot's (wide: workgroup's) unit in every phase
+    const int wu = WIDE ? wv : wq;              // wave index within the unit
+    const bool fin = !WIDE || slot == 0;        // waves that finish the unit's elements (e, lrow)
     const int e = wq * 64 + lane;           // the tile element this thread finishes
     const int lrow = 4 * (lane >> 4) + wq, lcol = lane & 15;
     const bool nt = R == 1;                 // one row block: every weight tile read once
@@ -473,12 +493,12 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         PL_STORE(1, t_issued);
     }
     PL_STORE(0, t_start);
-    float4 wr[SW];
+    float4 wr[SWU];
     float fs1, fs2;
     // B: attproj(l): res2 = res + att . Wap^T + b
     {
         const Unit u = unit_of(v, NCT * R, NCT, R);
-        if (u.has) load_w<SW>(a.w_ap, D::K16, u.j, 0, wq, nt, wr);
+        if (u.has) load_w<SWU>(a.w_ap, D::K16, u.j, 0, wu, nt, wr);
         lds_barrier();
         PL_MARK(3);
         if (ATTN && !wait_ctr<NH>(a, CT_ATT, a.B * NH, 1, sm)) return;
@@ -488,25 +508,27 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
         float bv = 0.f, rv = 0.f;
         if (u.has) {
-            bv = a.b_ap[col];
-            rv = hpa::load_wt4(a.res, fi);
-            acc = unit_mfma<SW, false>(a.att, D::K16, u.rb, 0, wq, wr, fs1, fs2);
+            if (fin) {
+                bv = a.b_ap[col];
+                rv = hpa::load_wt4(a.res, fi);
+            }
+            acc = unit_mfma<SWU, false>(a.att, D::K16, u.rb, 0, wu, wr, fs1, fs2);
         }
         put_red(sm.red, wv, acc);
         lds_barrier();
-        if (u.has) {
-            float val = fold4(sm.red, slot, e);
+        if (u.has && fin) {
+            float val = WIDE ? fold12(sm.red, e) : fold4(sm.red, slot, e);
             val += bv;
             val = row < a.B ? rv + val : 0.f;  // residual_forward(out, res, proj)
             hpa::store_wt4(a.res2, fi, val);
         }
-        publish(a, CT_X1, slots_with(bid, G, NCT * R));
+        publish(a, CT_X1, WIDE ? (int)(bid < NCT * R) : slots_with(bid, G, NCT * R));
     }
     PL_MARK(5);
     // C: fc(l): fch = gelu(LN2(res2) . Wfc^T + b), LN folded
     {
         const Unit u = unit_of(v, 4 * NCT * R, 4 * NCT, R);
-        if (u.has) load_w<SW>(a.w_fc, D::K16, u.j, 0, wq, nt, wr);
+        if (u.has) load_w<SWU>(a.w_fc, D::K16, u.j, 0, wu, nt, wr);
         if (!wait_ctr<NH>(a, CT_X1, NCT * R, 2, sm)) return;
         PL_MARK(6);
         const int row = u.rb * 16 + lrow, col = u.j * 16 + lcol;
@@ -514,48 +536,50 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         float c1 = 0.f, c2 = 0.f;
         fs1 = fs2 = 0.f;
         if (u.has) {
-            c1 = a.fc_c1[col];
-            c2 = a.fc_c2[col];
-            acc = unit_mfma<SW, true>(a.res2, D::K16, u.rb, 0, wq, wr, fs1, fs2);
+            if (fin) {
+                c1 = a.fc_c1[col];
+                c2 = a.fc_c2[col];
+            }
+            acc = unit_mfma<SWU, true>(a.res2, D::K16, u.rb, 0, wu, wr, fs1, fs2);
         }
         hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + wv * 32);
         put_red(sm.red, wv, acc);
         lds_barrier();
-        if (u.has) {
-            float val = fold4(sm.red, slot, e);
-            val = ln_fold_val(sm.wsum, slot, lrow, C, val, c1, c2);
+        if (u.has && fin) {
+            float val = WIDE ? fold12(sm.red, e) : fold4(sm.red, slot, e);
+            val = ln_fold_val<NWU>(sm.wsum, slot, lrow, C, val, c1, c2);
             hpa::store_wt4(a.fch, (int)(hpa::frag_index(row, col, 4 * C) * 4), row < a.B ? hpa::gelu_ref(val) : 0.f);
         }
-        publish(a, CT_H, slots_with(bid, G, 4 * NCT * R));
+        publish(a, CT_H, WIDE ? (int)(bid < 4 * NCT * R) : slots_with(bid, G, 4 * NCT * R));
         PL_MARK(7);
     }
     // D: fcproj(l), K part p of 4: partial tiles -> slab; the last part of
     // (rb, j) adds the parts in order + bias + res2 -> res
     {
         const Unit u = unit_of(v, NCT * R * D::FP, NCT, R);
-        if (u.has) load_w<SW>(a.w_fp, 4 * D::K16, u.j, u.p * D::K16, wq, nt, wr);
+        if (u.has) load_w<SWU>(a.w_fp, 4 * D::K16, u.j, u.p * D::K16, wu, nt, wr);
         if (!wait_ctr<NH>(a, CT_H, 4 * NCT * R, 3, sm)) return;
         PL_MARK(8);
         const int row = u.rb * 16 + lrow, col = u.j * 16 + lcol;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        if (u.has) acc = unit_mfma<SW, false>(a.fch, 4 * D::K16, u.rb, u.p * D::K16, wq, wr, fs1, fs2);
+        if (u.has) acc = unit_mfma<SWU, false>(a.fch, 4 * D::K16, u.rb, u.p * D::K16, wu, wr, fs1, fs2);
         put_red(sm.red, wv, acc);
         lds_barrier();
         float val = 0.f;
         const int sofs = ((u.p * R + u.rb) * NCT + u.j) * 256 + e;
-        if (u.has) {
-            val = fold4(sm.red, slot, e);
+        if (u.has && fin) {
+            val = WIDE ? fold12(sm.red, e) : fold4(sm.red, slot, e);
             hpa::store_wt4(a.slab_fp, sofs * 4, val);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
-        if (u.has && wq == 0 && lane == 0) {
+        if (u.has && fin && wq == 0 && lane == 0) {
             const int t = __hip_atomic_fetch_add(a.ctr + kCtrInts + R * NCT + u.rb * NCT + u.j, 1, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
             sm.s_last[slot] = t == D::FP - 1;
         }
         lds_barrier();
-        const bool last = u.has && sm.s_last[slot] != 0;
+        const bool last = u.has && fin && sm.s_last[slot] != 0;
         if (last) {
             float pv[D::FP];
 #pragma unroll
@@ -587,7 +611,10 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         }
         if (threadIdx.x == 0) {
             int nd = 0;
-            for (int s2 = 0; s2 < 3; ++s2) nd += sm.s_last[s2] != 0 && bid + s2 * G < NCT * R * D::FP;
+            if (WIDE)
+                nd = bid < NCT * R * D::FP && sm.s_last[0] != 0;
+            else
+                for (int s2 = 0; s2 < 3; ++s2) nd += sm.s_last[s2] != 0 && bid + s2 * G < NCT * R * D::FP;
             if (nd) arrive(a, CT_X2, nd);
         }
         PL_MARK(9);
@@ -595,7 +622,7 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
     // E: qkv(l+1): LN1 folded, q + K/V appended into layer l+1's pages
     if (!a.last) {
         const Unit u = unit_of(v, 3 * NCT * R, 3 * NCT, R);
-        if (u.has) load_w<SW>(a.w_qkv, D::K16, u.j, 0, wq, nt, wr);
+        if (u.has) load_w<SWU>(a.w_qkv, D::K16, u.j, 0, wu, nt, wr);
         if (!wait_ctr<NH>(a, CT_X2, NCT * R, 4, sm)) return;
         PL_MARK(10);
         const int row = u.rb * 16 + lrow, col = u.j * 16 + lcol;
@@ -603,16 +630,18 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         float c1 = 0.f, c2 = 0.f;
         fs1 = fs2 = 0.f;
         if (u.has) {
-            c1 = a.qkv_c1[col];
-            c2 = a.qkv_c2[col];
-            acc = unit_mfma<SW, true>(a.res, D::K16, u.rb, 0, wq, wr, fs1, fs2);
+            if (fin) {
+                c1 = a.qkv_c1[col];
+                c2 = a.qkv_c2[col];
+            }
+            acc = unit_mfma<SWU, true>(a.res, D::K16, u.rb, 0, wu, wr, fs1, fs2);
         }
         hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + wv * 32);
         put_red(sm.red, wv, acc);
         lds_barrier();
-        if (u.has && row < a.B) {
-            float val = fold4(sm.red, slot, e);
-            val = ln_fold_val(sm.wsum, slot, lrow, C, val, c1, c2);
+        if (u.has && fin && row < a.B) {
+            float val = WIDE ? fold12(sm.red, e) : fold4(sm.red, slot, e);
+            val = ln_fold_val<NWU>(sm.wsum, slot, lrow, C, val, c1, c2);
             if (col < C) {
                 a.q_out[(size_t)row * C + col] = val;
             } else {  // K/V of this token into the sequence's page of layer l+1 (add_to_cache)
@@ -663,12 +692,12 @@ bool shape_ok(int B, int S, int G) {
            4L * LD<NH>::NCT * R <= 3L * G;
 }
 
-template <int NH, int P, bool BF, bool ATTN>
+template <int NH, int P, bool BF, bool ATTN, bool WIDE = false>
 int launch(const HpaLayerArgs* h, int G) {
     static int resident = -1;  // blocks per CU of this instantiation (occupancy API)
     if (resident < 0) {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, decode_layer_kernel<NH, P, BF, ATTN>, 768, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, decode_layer_kernel<NH, P, BF, ATTN, WIDE>, 768, 0) !=
             hipSuccess)
             nb = 0;
         resident = nb;
@@ -713,25 +742,33 @@ int launch(const HpaLayerArgs* h, int G) {
     a.slab_fp = h->slab;
     a.ctr = h->counters;
     a.err = h->err;
-    decode_layer_kernel<NH, P, BF, ATTN><<<G, 768, 0, hpa_stream()>>>(a);
+    decode_layer_kernel<NH, P, BF, ATTN, WIDE><<<G, 768, 0, hpa_stream()>>>(a);
     HPA_LAUNCH_CHECK();
     return 0;
 }
 
-template <int NH, bool ATTN>
+template <int NH, bool ATTN, bool WIDE = false>
 int dispatch_p(const HpaLayerArgs* h, int G) {
     const bool bf = h->pool->dtype == HPA_BF16;
     switch (h->pool->page_size) {
-        case 8: return bf ? launch<NH, 8, true, ATTN>(h, G) : launch<NH, 8, false, ATTN>(h, G);
-        case 16: return bf ? launch<NH, 16, true, ATTN>(h, G) : launch<NH, 16, false, ATTN>(h, G);
-        case 32: return bf ? launch<NH, 32, true, ATTN>(h, G) : launch<NH, 32, false, ATTN>(h, G);
-        case 64: return bf ? launch<NH, 64, true, ATTN>(h, G) : launch<NH, 64, false, ATTN>(h, G);
+        case 8: return bf ? launch<NH, 8, true, ATTN, WIDE>(h, G) : launch<NH, 8, false, ATTN, WIDE>(h, G);
+        case 16: return bf ? launch<NH, 16, true, ATTN, WIDE>(h, G) : launch<NH, 16, false, ATTN, WIDE>(h, G);
+        case 32: return bf ? launch<NH, 32, true, ATTN, WIDE>(h, G) : launch<NH, 32, false, ATTN, WIDE>(h, G);
+        case 64: return bf ? launch<NH, 64, true, ATTN, WIDE>(h, G) : launch<NH, 64, false, ATTN, WIDE>(h, G);
         default: return hpa_fail(__FILE__, __LINE__, "decode layer: page size must be 8, 16, 32 or 64");
     }
 }
 
 template <int NH>
 int dispatch(const HpaLayerArgs* h, int G) {
+    if (h->chain_only == 2) {  // wide units (one row block, C = 768)
+        if constexpr (LD<NH>::SW % 3 == 0) {
+            HPA_REQUIRE(h->B <= 16 && 4 * LD<NH>::NCT <= G, "decode layer: wide units need B <= 16 and 4C/16 <= CUs");
+            return dispatch_p<NH, false, true>(h, G);
+        } else {
+            return hpa_fail(__FILE__, __LINE__, "decode layer: wide units need C = 768");
+        }
+    }
     return h->chain_only ? dispatch_p<NH, false>(h, G) : dispatch_p<NH, true>(h, G);
 }
 

@@ -659,8 +659,9 @@ struct GPT2Decode {
     long prof_launches;
     DecShard* shard;
     /* persistent layer (hpa_decode_layer): one launch per layer */
-    int pl_want;      /* gpt2_decode_set_layer_kernel: 0 off, 1 auto, 2 full, 3 chain */
-    int pl_on;        /* in use: 0 five launches, 1 full persistent layer, 2 attention launch + chain */
+    int pl_want;      /* gpt2_decode_set_layer_kernel: 0 off, 1 auto, 2 full, 3 chain, 4 chain with wide units */
+    int pl_on;        /* in use: 0 five launches, 1 full persistent layer, 2 attention launch + chain,
+                         3 attention launch + chain of wide units (hpa_layer.hip WIDE) */
     int pl_splits;
     int pl_global_B;  /* sharded: the whole batch's size (picks follow it); else 0 */
     float* pl_rec;
@@ -893,11 +894,17 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
      * supports (B 64 / 32 / 16 / 8: -2.3 / -0.9 / -4.9 / -4.0 % per step
      * against five launches; the full persistent layer -0.1 / +0.2 / -2.3 /
      * -1.7 %) */
-    const int mode = d->pl_want == 2 ? 1 : 2;
+    /* the chain's wide units (one unit per 12-wave workgroup) where a global
+     * batch of <= 16 rows leaves two of each workgroup's three 4-wave slots
+     * idle (C = 768): auto and form 4; HPA_PL_WIDE=0 turns the auto pick off */
+    const char* wenv = getenv("HPA_PL_WIDE");
+    const int wide_ok = Bg <= 16 && d->B <= 16 && c.num_heads == 12;
+    const int mode = d->pl_want == 2 ? 1
+                   : wide_ok && (d->pl_want == 4 || (d->pl_want == 1 && !(wenv && wenv[0] == '0'))) ? 3 : 2;
     int splits = hpa_decode_layer_pick_splits(Bg, c.num_heads, d->max_ctx);
     const char* env = getenv("HPA_LAYER_SPLITS");
     if (env && atoi(env) > 0) splits = atoi(env);
-    if (mode == 2) splits = 1; /* no attention phase: no split records */
+    if (mode >= 2) splits = 1; /* no attention phase: no split records */
     if (!hpa_decode_layer_eligible(d->B, c.channels, c.num_heads, splits)) return 0;
     size_t sz[3];
     if (hpa_decode_layer_sizes(d->B, c.channels, c.num_heads, splits, sz)) return 1;
@@ -931,7 +938,7 @@ static int dec_layer(GPT2* model, int l) {
     a.num_heads = c.num_heads;
     a.splits = d->pl_splits;
     a.last = l + 1 == L;
-    a.chain_only = d->pl_on == 2;
+    a.chain_only = d->pl_on == 3 ? 2 : d->pl_on == 2;
     a.pool = &d->pool;
     a.layer = l;
     a.block_table = d->d_bt;
@@ -1129,7 +1136,7 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
     }
     {
         const char* env = getenv("HPA_LAYER_KERNEL");
-        d->pl_want = env && env[0] >= '0' && env[0] <= '3' ? env[0] - '0' : 1;
+        d->pl_want = env && env[0] >= '0' && env[0] <= '4' ? env[0] - '0' : 1;
     }
     if (dec_layer_setup(model, d)) {
         dec_free(d);
@@ -1367,7 +1374,7 @@ static int dec_launch(GPT2* model) {
     if (pl) { /* qkv(0), then one persistent launch per layer */
         rc |= dec_gemm(model, 0, G_QKV);
         for (int l = 0; l < L && !rc; l++) {
-            if (d->pl_on == 2) rc |= dec_attention(model, l); /* chain form: the attention's own launch */
+            if (d->pl_on >= 2) rc |= dec_attention(model, l); /* chain form: the attention's own launch */
             rc |= dec_layer(model, l);
             DEC_TRACE(l + 1);
         }
@@ -1719,7 +1726,7 @@ int gpt2_decode_set_layer_kernel(GPT2* model, int enable) {
     GPT2Decode* d = model->decode;
     if (!d) return 1;
     if (hpa_synchronize()) return 1;
-    d->pl_want = enable < 0 ? 0 : enable > 3 ? 3 : enable;
+    d->pl_want = enable < 0 ? 0 : enable > 4 ? 4 : enable;
     if (dec_layer_setup(model, d)) return 1;
     if (d->graph) { /* recapture with the other step */
         hpa_graph_destroy(d->graph);

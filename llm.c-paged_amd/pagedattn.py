@@ -608,7 +608,8 @@ class Model:
 
     def set_layer_kernel(self, on):
         """layer loop: 0 five launches, 2 full persistent layer, 3 attention
-        launch + persistent chain, 1 the form measured fastest for the batch;
+        launch + persistent chain, 4 the chain with wide units (B <= 16,
+        C = 768), 1 the form measured fastest for the batch;
         returns whether a persistent form is now in use"""
         check(lib().gpt2_decode_set_layer_kernel(self.h, int(on)), "set_layer_kernel")
         return bool(lib().gpt2_decode_layer_kernel(self.h))
@@ -617,7 +618,8 @@ class Model:
         return bool(lib().gpt2_decode_layer_kernel(self.h))
 
     def layer_form(self):
-        """0 five launches per layer, 1 full persistent layer, 2 attention launch + persistent chain"""
+        """0 five launches per layer, 1 full persistent layer, 2 attention launch + persistent chain,
+        3 the chain with wide units"""
         return int(lib().gpt2_decode_layer_kernel(self.h))
 
     def status(self):

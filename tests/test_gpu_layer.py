@@ -13,6 +13,9 @@ the oracle.
   waves, so logits differ by fp32 reassociation only: <= 2e-5 max-abs.
 * Rows never depend on the batch: engines of B = 6 and of its two halves give
   bit-identical logits at the same split count (the sharded-decode property).
+* The chain's wide units (form 4: a unit per 12-wave workgroup, its K over
+  12 waves) at B = 16 / 8 / 5: within the same bound of the launch path, rows
+  independent of the batch, eager = graph.
 * Every step reports status 0 (no in-launch wait timed out).
 """
 import os
@@ -38,13 +41,17 @@ def _model(hip, cfgd, params, B, P, layer, kv_dtype=0, splits_env=None, mode=2):
     finally:
         os.environ.pop("HPA_LAYER_SPLITS", None)
     # mode 2: the full persistent layer at every batch it supports; 3: the
-    # attention's own launch + the persistent GEMM chain
+    # attention's own launch + the persistent GEMM chain; 4: that chain with
+    # wide units (one unit per 12-wave workgroup, B <= 16, C = 768)
     assert m.set_layer_kernel(mode if layer else 0) == bool(layer)
+    if layer and mode == 4:
+        assert m.layer_form() == 3
     m.set_graph(True)
     return m
 
 
-@pytest.mark.parametrize("B,mode", [(64, 2), (32, 2), (16, 2), (8, 2), (64, 3), (40, 3), (8, 3)])
+@pytest.mark.parametrize("B,mode", [(64, 2), (32, 2), (16, 2), (8, 2), (64, 3), (40, 3), (8, 3), (16, 4), (8, 4),
+                                    (5, 4)])
 def test_persistent_layer_matches_launch_path_124m(hip, B, mode):
     params = synth.params(GPT2_124M, seed=31)
     ctx = 990
@@ -176,3 +183,34 @@ def test_persistent_layer_eager_equals_graph(hip):
         m.close()
         outs.append(np.stack(lg))
     assert np.array_equal(outs[0], outs[1])
+
+
+def test_persistent_chain_wide_rows_independent_of_batch_and_graph(hip):
+    """wide units at GPT-2 124M shapes: B = 12 vs its halves 5 + 7 give
+    bit-identical logits (attention split count and waves fixed, as a sharded
+    engine takes them from the global batch), and eager equals graph"""
+    params = synth.params(GPT2_124M, seed=93)
+    steps = 4
+    toks = np.random.default_rng(93).integers(0, GPT2_124M["V"], (steps, 12)).astype(np.int32)
+
+    def run(lo, hi, graph=True):
+        m = _model(hip, GPT2_124M, params, hi - lo, 16, 1, mode=4)
+        m.set_graph(graph)
+        m.set_attn_splits(2)
+        m.fill_random(300, seed=9, seq_offset=lo)
+        lg = []
+        for t in range(steps):
+            m.step(toks[t, lo:hi])
+            lg.append(m.logits())
+        m.status()
+        m.close()
+        return np.stack(lg)
+
+    hip.check(hip.lib().hpa_set_attention_waves(8), "waves")
+    try:
+        full = run(0, 12)
+        assert np.array_equal(full[:, :5], run(0, 5))
+        assert np.array_equal(full[:, 5:], run(5, 12))
+        assert np.array_equal(full, run(0, 12, graph=False))
+    finally:
+        hip.check(hip.lib().hpa_set_attention_waves(0), "waves")
