@@ -325,9 +325,9 @@ typedef struct {
     int last;                     /* 1: no qkv(l+1) phase (last layer) */
     int chain_only;               /* 1: no attention phase -- the caller launched the decode
                                      attention (frag output into att) before: the launch is
-                                     attproj -> fc -> fcproj -> qkv(l+1); 2: the same with wide
-                                     units (one unit per 12-wave workgroup, its K over all 12
-                                     waves; B <= 16, C = 768) */
+                                     attproj -> fc -> fcproj -> qkv(l+1); 2 / 3: the same with wide
+                                     units of 12 waves (one per workgroup; B <= 16) / 6 waves
+                                     (two per workgroup; B <= 32), C = 768 */
     const HpaKVPool* pool;
     int layer;
     const int* block_table;

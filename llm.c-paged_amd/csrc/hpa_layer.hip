@@ -405,20 +405,22 @@ __device__ __forceinline__ float fold4(const float* red, int slot, int e) {
     return v;
 }
 
-// wide units (one unit per 12-wave workgroup): the 12 waves in wave order
-__device__ __forceinline__ float fold12(const float* red, int e) {
-    float v = red[e];
+// units of NWU waves (unit slot us of the workgroup): the waves in wave order
+template <int NWU>
+__device__ __forceinline__ float foldn(const float* red, int us, int e) {
+    const float* r = red + us * NWU * 256 + e;
+    float v = r[0];
 #pragma unroll
-    for (int w = 1; w < 12; ++w) v += red[w * 256 + e];
+    for (int w = 1; w < NWU; ++w) v += r[w * 256];
     return v;
 }
 
 // LayerNorm-folded value: rstd*(acc - mean*c1) + c2 (Epi::apply's order);
-// the row partial sums of the unit's NWU waves from wave slot * 4
+// the row partial sums of the NWU waves of unit slot us
 template <int NWU = 4>
-__device__ __forceinline__ float ln_fold_val(const float* wsum, int slot, int lrow, int K, float val, float c1,
+__device__ __forceinline__ float ln_fold_val(const float* wsum, int us, int lrow, int K, float val, float c1,
                                              float c2) {
-    const float* ws = wsum + slot * 4 * 32;
+    const float* ws = wsum + us * NWU * 32;
     float S1 = ws[2 * lrow], S2 = ws[2 * lrow + 1];
 #pragma unroll
     for (int ww = 1; ww < NWU; ++ww) {
@@ -432,9 +434,13 @@ __device__ __forceinline__ float ln_fold_val(const float* wsum, int slot, int lr
     return val;
 }
 
-// slots of workgroup bid that hold one of n units
-__device__ __forceinline__ int slots_with(int bid, int G, int n) {
-    return (bid < n) + (bid + G < n) + (bid + 2 * G < n);
+// unit slots of workgroup bid (UPW per workgroup) that hold one of n units
+template <int UPW>
+__device__ __forceinline__ int units_with(int bid, int G, int n) {
+    int k = 0;
+#pragma unroll
+    for (int s2 = 0; s2 < UPW; ++s2) k += bid + s2 * G < n;
+    return k;
 }
 
 // every storing wave drained, then one lane counts the slots that stored
@@ -448,17 +454,19 @@ __device__ __forceinline__ void publish(const KA& a, int which, int nslots) {
 // ATTN = false: the chain only (attproj -> fc -> fcproj -> next qkv); the
 // attention ran as its own launch just before (hpa_paged_attention_decode_split
 // writing `att` in frag layout), so phase B needs no in-launch wait.
-// WIDE (chain only, one row block, C = 768): a unit is a whole workgroup --
-// unit v on workgroup v, its K range over all 12 waves (SW / 3 k16 steps
-// each, folded in wave order) -- instead of a 4-wave slot: at 16 rows every
-// phase has <= 192 units for 256 workgroups, so the 4-wave form leaves two of
-// the three slots idle and runs 3x longer MFMA chains per wave
-template <int NH, int P, bool BF, bool ATTN, bool WIDE>
+// NWU = waves per GEMM unit: 4 (three 4-wave slots per workgroup), or wide
+// units in the chain form (C = 768): 12 (one unit per workgroup, <= 16 rows:
+// every phase has <= 192 units for 256 workgroups) or 6 (two per workgroup,
+// <= 32 rows: <= 384 units).  A unit's K range is split over its NWU waves
+// (4 * SW / NWU k16 steps each, folded in wave order): with fewer units than
+// 4-wave slots the 4-wave form leaves slots idle and runs longer MFMA chains
+// per wave
+template <int NH, int P, bool BF, bool ATTN, int NWU>
 __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
     using D = LD<NH>;
     constexpr int C = D::C, SW = D::SW, NCT = D::NCT;
-    static_assert(!WIDE || (!ATTN && SW % 3 == 0), "wide units: chain form, SW divisible by 3");
-    constexpr int NWU = WIDE ? 12 : 4;  // waves per unit
+    static_assert(NWU == 4 || (!ATTN && (NWU == 6 || NWU == 12) && (SW * 4) % NWU == 0), "wide units");
+    constexpr int UPW = 12 / NWU;       // units per workgroup
     constexpr int SWU = SW * 4 / NWU;   // k16 steps per wave
     // fields read where used from the kernarg segment (not all hoisted into
     // SGPRs at entry: the attention keeps q in 64 SGPRs)
@@ -470,11 +478,11 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
     const int lane = threadIdx.x & 63;
     const int bid = blockIdx.x;
     const int R = a.R, G = a.G;
-    const int v = WIDE ? bid : bid + slot * G;  // this slot's (wide: workgroup's) unit in every phase
-    const int wu = WIDE ? wv : wq;              // wave index within the unit
-    const bool fin = !WIDE || slot == 0;        // waves that finish the unit's elements (e, lrow)
-    const int e = wq * 64 + lane;           // the tile element this thread finishes
-    const int lrow = 4 * (lane >> 4) + wq, lcol = lane & 15;
+    const int us = wv / NWU, wu = wv - us * NWU;  // unit slot of the workgroup, wave within the unit
+    const int v = bid + us * G;                   // this unit slot's unit in every phase
+    const bool fin = wu < 4;                      // waves that finish the unit's elements (e, lrow)
+    const int e = (NWU == 4 ? wq : wu) * 64 + lane;  // the tile element this thread finishes (fin waves)
+    const int lrow = 4 * (lane >> 4) + (NWU == 4 ? wq : wu), lcol = lane & 15;
     const bool nt = R == 1;                 // one row block: every weight tile read once
     PL_STAMP(t_start);
     if (threadIdx.x < 3) sm.s_cnt[threadIdx.x] = 0;
@@ -517,12 +525,12 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         put_red(sm.red, wv, acc);
         lds_barrier();
         if (u.has && fin) {
-            float val = WIDE ? fold12(sm.red, e) : fold4(sm.red, slot, e);
+            float val = foldn<NWU>(sm.red, us, e);
             val += bv;
             val = row < a.B ? rv + val : 0.f;  // residual_forward(out, res, proj)
             hpa::store_wt4(a.res2, fi, val);
         }
-        publish(a, CT_X1, WIDE ? (int)(bid < NCT * R) : slots_with(bid, G, NCT * R));
+        publish(a, CT_X1, units_with<UPW>(bid, G, NCT * R));
     }
     PL_MARK(5);
     // C: fc(l): fch = gelu(LN2(res2) . Wfc^T + b), LN folded
@@ -546,11 +554,11 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         put_red(sm.red, wv, acc);
         lds_barrier();
         if (u.has && fin) {
-            float val = WIDE ? fold12(sm.red, e) : fold4(sm.red, slot, e);
-            val = ln_fold_val<NWU>(sm.wsum, slot, lrow, C, val, c1, c2);
+            float val = foldn<NWU>(sm.red, us, e);
+            val = ln_fold_val<NWU>(sm.wsum, us, lrow, C, val, c1, c2);
             hpa::store_wt4(a.fch, (int)(hpa::frag_index(row, col, 4 * C) * 4), row < a.B ? hpa::gelu_ref(val) : 0.f);
         }
-        publish(a, CT_H, WIDE ? (int)(bid < 4 * NCT * R) : slots_with(bid, G, 4 * NCT * R));
+        publish(a, CT_H, units_with<UPW>(bid, G, 4 * NCT * R));
         PL_MARK(7);
     }
     // D: fcproj(l), K part p of 4: partial tiles -> slab; the last part of
@@ -568,18 +576,18 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         float val = 0.f;
         const int sofs = ((u.p * R + u.rb) * NCT + u.j) * 256 + e;
         if (u.has && fin) {
-            val = WIDE ? fold12(sm.red, e) : fold4(sm.red, slot, e);
+            val = foldn<NWU>(sm.red, us, e);
             hpa::store_wt4(a.slab_fp, sofs * 4, val);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
-        if (u.has && fin && wq == 0 && lane == 0) {
+        if (u.has && fin && wu == 0 && lane == 0) {
             const int t = __hip_atomic_fetch_add(a.ctr + kCtrInts + R * NCT + u.rb * NCT + u.j, 1, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
-            sm.s_last[slot] = t == D::FP - 1;
+            sm.s_last[us] = t == D::FP - 1;
         }
         lds_barrier();
-        const bool last = u.has && fin && sm.s_last[slot] != 0;
+        const bool last = u.has && fin && sm.s_last[us] != 0;
         if (last) {
             float pv[D::FP];
 #pragma unroll
@@ -593,12 +601,12 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
             tot += a.b_fp[col];
             tot = row < a.B ? rv + tot : 0.f;
             hpa::store_wt4(a.res, fi, tot);
-            if (a.stats_out) sm.tile[(slot * 16 + lrow) * 17 + lcol] = tot;
+            if (a.stats_out) sm.tile[(us * 16 + lrow) * 17 + lcol] = tot;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
-        if (a.stats_out && wq == 0 && lane < 16 && last) {  // 16-column LNf partial sums of the tile's rows
-            const float* tr = sm.tile + (slot * 16 + lane) * 17;
+        if (a.stats_out && wu == 0 && lane < 16 && last) {  // 16-column LNf partial sums of the tile's rows
+            const float* tr = sm.tile + (us * 16 + lane) * 17;
             float s1 = 0.f, s2 = 0.f;
 #pragma unroll
             for (int c = 0; c < 16; ++c) {
@@ -611,10 +619,7 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         }
         if (threadIdx.x == 0) {
             int nd = 0;
-            if (WIDE)
-                nd = bid < NCT * R * D::FP && sm.s_last[0] != 0;
-            else
-                for (int s2 = 0; s2 < 3; ++s2) nd += sm.s_last[s2] != 0 && bid + s2 * G < NCT * R * D::FP;
+            for (int s2 = 0; s2 < UPW; ++s2) nd += sm.s_last[s2] != 0 && bid + s2 * G < NCT * R * D::FP;
             if (nd) arrive(a, CT_X2, nd);
         }
         PL_MARK(9);
@@ -640,8 +645,8 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         put_red(sm.red, wv, acc);
         lds_barrier();
         if (u.has && fin && row < a.B) {
-            float val = WIDE ? fold12(sm.red, e) : fold4(sm.red, slot, e);
-            val = ln_fold_val<NWU>(sm.wsum, slot, lrow, C, val, c1, c2);
+            float val = foldn<NWU>(sm.red, us, e);
+            val = ln_fold_val<NWU>(sm.wsum, us, lrow, C, val, c1, c2);
             if (col < C) {
                 a.q_out[(size_t)row * C + col] = val;
             } else {  // K/V of this token into the sequence's page of layer l+1 (add_to_cache)
@@ -692,12 +697,12 @@ bool shape_ok(int B, int S, int G) {
            4L * LD<NH>::NCT * R <= 3L * G;
 }
 
-template <int NH, int P, bool BF, bool ATTN, bool WIDE = false>
+template <int NH, int P, bool BF, bool ATTN, int NWU = 4>
 int launch(const HpaLayerArgs* h, int G) {
     static int resident = -1;  // blocks per CU of this instantiation (occupancy API)
     if (resident < 0) {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, decode_layer_kernel<NH, P, BF, ATTN, WIDE>, 768, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, decode_layer_kernel<NH, P, BF, ATTN, NWU>, 768, 0) !=
             hipSuccess)
             nb = 0;
         resident = nb;
@@ -742,29 +747,34 @@ int launch(const HpaLayerArgs* h, int G) {
     a.slab_fp = h->slab;
     a.ctr = h->counters;
     a.err = h->err;
-    decode_layer_kernel<NH, P, BF, ATTN, WIDE><<<G, 768, 0, hpa_stream()>>>(a);
+    decode_layer_kernel<NH, P, BF, ATTN, NWU><<<G, 768, 0, hpa_stream()>>>(a);
     HPA_LAUNCH_CHECK();
     return 0;
 }
 
-template <int NH, bool ATTN, bool WIDE = false>
+template <int NH, bool ATTN, int NWU = 4>
 int dispatch_p(const HpaLayerArgs* h, int G) {
     const bool bf = h->pool->dtype == HPA_BF16;
     switch (h->pool->page_size) {
-        case 8: return bf ? launch<NH, 8, true, ATTN, WIDE>(h, G) : launch<NH, 8, false, ATTN, WIDE>(h, G);
-        case 16: return bf ? launch<NH, 16, true, ATTN, WIDE>(h, G) : launch<NH, 16, false, ATTN, WIDE>(h, G);
-        case 32: return bf ? launch<NH, 32, true, ATTN, WIDE>(h, G) : launch<NH, 32, false, ATTN, WIDE>(h, G);
-        case 64: return bf ? launch<NH, 64, true, ATTN, WIDE>(h, G) : launch<NH, 64, false, ATTN, WIDE>(h, G);
+        case 8: return bf ? launch<NH, 8, true, ATTN, NWU>(h, G) : launch<NH, 8, false, ATTN, NWU>(h, G);
+        case 16: return bf ? launch<NH, 16, true, ATTN, NWU>(h, G) : launch<NH, 16, false, ATTN, NWU>(h, G);
+        case 32: return bf ? launch<NH, 32, true, ATTN, NWU>(h, G) : launch<NH, 32, false, ATTN, NWU>(h, G);
+        case 64: return bf ? launch<NH, 64, true, ATTN, NWU>(h, G) : launch<NH, 64, false, ATTN, NWU>(h, G);
         default: return hpa_fail(__FILE__, __LINE__, "decode layer: page size must be 8, 16, 32 or 64");
     }
 }
 
 template <int NH>
 int dispatch(const HpaLayerArgs* h, int G) {
-    if (h->chain_only == 2) {  // wide units (one row block, C = 768)
+    if (h->chain_only == 2 || h->chain_only == 3) {  // wide units (C = 768): 12 waves (<= 16 rows) / 6 (<= 32)
         if constexpr (LD<NH>::SW % 3 == 0) {
-            HPA_REQUIRE(h->B <= 16 && 4 * LD<NH>::NCT <= G, "decode layer: wide units need B <= 16 and 4C/16 <= CUs");
-            return dispatch_p<NH, false, true>(h, G);
+            const int R = (h->B + 15) / 16;
+            if (h->chain_only == 2) {
+                HPA_REQUIRE(R == 1 && 4 * LD<NH>::NCT <= G, "decode layer: 12-wave units need B <= 16, 4C/16 <= CUs");
+                return dispatch_p<NH, false, 12>(h, G);
+            }
+            HPA_REQUIRE(R <= 2 && 4 * LD<NH>::NCT * R <= 2 * G, "decode layer: 6-wave units need B <= 32");
+            return dispatch_p<NH, false, 6>(h, G);
         } else {
             return hpa_fail(__FILE__, __LINE__, "decode layer: wide units need C = 768");
         }

@@ -13,9 +13,11 @@ the oracle.
   waves, so logits differ by fp32 reassociation only: <= 2e-5 max-abs.
 * Rows never depend on the batch: engines of B = 6 and of its two halves give
   bit-identical logits at the same split count (the sharded-decode property).
-* The chain's wide units (form 4: a unit per 12-wave workgroup, its K over
-  12 waves) at B = 16 / 8 / 5: within the same bound of the launch path, rows
-  independent of the batch, eager = graph.
+* The chain's wide units (form 4: 12-wave units, one per workgroup, at
+  B <= 16; 6-wave units, two per workgroup, at B <= 32; a unit's K over its
+  waves) at B = 32 / 20 / 16 / 8 / 5: within the same bound of the launch
+  path, rows independent of the batch (12 vs 5 + 7; 28 vs 20), eager =
+  graph.
 * Every step reports status 0 (no in-launch wait timed out).
 """
 import os
@@ -42,7 +44,7 @@ def _model(hip, cfgd, params, B, P, layer, kv_dtype=0, splits_env=None, mode=2):
         os.environ.pop("HPA_LAYER_SPLITS", None)
     # mode 2: the full persistent layer at every batch it supports; 3: the
     # attention's own launch + the persistent GEMM chain; 4: that chain with
-    # wide units (one unit per 12-wave workgroup, B <= 16, C = 768)
+    # wide units (12-wave units at B <= 16, 6-wave at B <= 32; C = 768)
     assert m.set_layer_kernel(mode if layer else 0) == bool(layer)
     if layer and mode == 4:
         assert m.layer_form() == 3
@@ -51,7 +53,7 @@ def _model(hip, cfgd, params, B, P, layer, kv_dtype=0, splits_env=None, mode=2):
 
 
 @pytest.mark.parametrize("B,mode", [(64, 2), (32, 2), (16, 2), (8, 2), (64, 3), (40, 3), (8, 3), (16, 4), (8, 4),
-                                    (5, 4)])
+                                    (5, 4), (32, 4), (20, 4)])
 def test_persistent_layer_matches_launch_path_124m(hip, B, mode):
     params = synth.params(GPT2_124M, seed=31)
     ctx = 990
@@ -191,7 +193,7 @@ def test_persistent_chain_wide_rows_independent_of_batch_and_graph(hip):
     engine takes them from the global batch), and eager equals graph"""
     params = synth.params(GPT2_124M, seed=93)
     steps = 4
-    toks = np.random.default_rng(93).integers(0, GPT2_124M["V"], (steps, 12)).astype(np.int32)
+    toks = np.random.default_rng(93).integers(0, GPT2_124M["V"], (steps, 28)).astype(np.int32)
 
     def run(lo, hi, graph=True):
         m = _model(hip, GPT2_124M, params, hi - lo, 16, 1, mode=4)
@@ -212,5 +214,7 @@ def test_persistent_chain_wide_rows_independent_of_batch_and_graph(hip):
         assert np.array_equal(full[:, :5], run(0, 5))
         assert np.array_equal(full[:, 5:], run(5, 12))
         assert np.array_equal(full, run(0, 12, graph=False))
+        full = run(0, 28)  # 6-wave units (17-32 rows): the first 20 rows of 28 = a 20-row engine
+        assert np.array_equal(full[:, :20], run(0, 20))
     finally:
         hip.check(hip.lib().hpa_set_attention_waves(0), "waves")
