@@ -325,9 +325,10 @@ typedef struct {
     int last;                     /* 1: no qkv(l+1) phase (last layer) */
     int chain_only;               /* 1: no attention phase -- the caller launched the decode
                                      attention (frag output into att) before: the launch is
-                                     attproj -> fc -> fcproj -> qkv(l+1); 2 / 3: the same with wide
-                                     units of 12 waves (one per workgroup; B <= 16) / 6 waves
-                                     (two per workgroup; B <= 32), C = 768 */
+                                     attproj -> fc -> fcproj -> qkv(l+1); 2..5: the same with wide
+                                     units (C = 768), waves per unit of (attproj, fc / fcproj,
+                                     qkv): 2 (12, 12, 12) B <= 16; 3 (12, 6, 6) B <= 32;
+                                     4 (12, 4, 6) B <= 48; 5 (12, 4, 4) B <= 64 */
     const HpaKVPool* pool;
     int layer;
     const int* block_table;

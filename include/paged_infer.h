@@ -209,10 +209,10 @@ int  gpt2_decode_attn_splits(GPT2* model);
  * per layer (hpa_decode_layer: attention -> attproj -> fc -> fcproj -> next
  * qkv); 3 the decode attention's own launch + one persistent launch of the
  * GEMM chain (attproj -> fc -> fcproj -> next qkv); 4 the same chain with
- * wide units (12-wave units, one per workgroup, at B <= 16; 6-wave units at
- * B <= 32; C = 768; else 3); 1 (default, "auto") the form measured fastest
- * for the batch (profiles/r3; the wide chain at a global batch <= 32 unless
- * HPA_PL_WIDE=0, or <= 16 with HPA_PL_WIDE=12).  The
+ * wide units where a phase has fewer units than 4-wave slots (C = 768; the
+ * widths follow the global batch; else 3); 1 (default, "auto") the form
+ * measured fastest for the batch (profiles/r3; the wide chain unless
+ * HPA_PL_WIDE=0, or only at <= 16 rows with HPA_PL_WIDE=12).  The
  * persistent forms need fp32 weights, C = 128 / 768 and B <= 64 (else five
  * launches).  HPA_LAYER_KERNEL=0..4 in the environment sets the default.  A persistent
  * launch needs every CU for its 12-wave workgroups: a GPU shared with

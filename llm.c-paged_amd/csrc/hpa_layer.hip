@@ -454,20 +454,34 @@ __device__ __forceinline__ void publish(const KA& a, int which, int nslots) {
 // ATTN = false: the chain only (attproj -> fc -> fcproj -> next qkv); the
 // attention ran as its own launch just before (hpa_paged_attention_decode_split
 // writing `att` in frag layout), so phase B needs no in-launch wait.
-// NWU = waves per GEMM unit: 4 (three 4-wave slots per workgroup), or wide
-// units in the chain form (C = 768): 12 (one unit per workgroup, <= 16 rows:
-// every phase has <= 192 units for 256 workgroups) or 6 (two per workgroup,
-// <= 32 rows: <= 384 units).  A unit's K range is split over its NWU waves
+// Waves per GEMM unit, per phase (NB attproj, NCD fc and fcproj, NE qkv): 4
+// (three 4-wave slots per workgroup), or wide units in the chain form
+// (C = 768): 12 (one unit per workgroup, a phase of <= 256 units) or 6 (two
+// per workgroup, <= 512 units).  A unit's K range is split over its waves
 // (4 * SW / NWU k16 steps each, folded in wave order): with fewer units than
 // 4-wave slots the 4-wave form leaves slots idle and runs longer MFMA chains
 // per wave
-template <int NH, int P, bool BF, bool ATTN, int NWU>
+template <int NWU>
+struct UW {  // a wave's place in its phase's unit
+    int us, wu, v, e, lrow;
+    bool fin;
+    __device__ __forceinline__ UW(int wv, int bid, int G, int lane) {
+        us = wv / NWU;       // unit slot of the workgroup
+        wu = wv - us * NWU;  // wave within the unit
+        v = bid + us * G;    // the unit slot's unit
+        fin = wu < 4;        // the waves that finish the unit's elements
+        e = (wu & 3) * 64 + lane;
+        lrow = 4 * (lane >> 4) + (wu & 3);
+    }
+};
+
+template <int NH, int P, bool BF, bool ATTN, int NB, int NCD, int NE>
 __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
     using D = LD<NH>;
     constexpr int C = D::C, SW = D::SW, NCT = D::NCT;
-    static_assert(NWU == 4 || (!ATTN && (NWU == 6 || NWU == 12) && (SW * 4) % NWU == 0), "wide units");
-    constexpr int UPW = 12 / NWU;       // units per workgroup
-    constexpr int SWU = SW * 4 / NWU;   // k16 steps per wave
+    static_assert((NB == 4 && NCD == 4 && NE == 4) ||
+                      (!ATTN && (SW * 4) % NB == 0 && (SW * 4) % NCD == 0 && (SW * 4) % NE == 0),
+                  "wide units: chain form, K split evenly");
     // fields read where used from the kernarg segment (not all hoisted into
     // SGPRs at entry: the attention keeps q in 64 SGPRs)
     const KA& a = *(const KA*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -478,11 +492,8 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
     const int lane = threadIdx.x & 63;
     const int bid = blockIdx.x;
     const int R = a.R, G = a.G;
-    const int us = wv / NWU, wu = wv - us * NWU;  // unit slot of the workgroup, wave within the unit
-    const int v = bid + us * G;                   // this unit slot's unit in every phase
-    const bool fin = wu < 4;                      // waves that finish the unit's elements (e, lrow)
-    const int e = (NWU == 4 ? wq : wu) * 64 + lane;  // the tile element this thread finishes (fin waves)
-    const int lrow = 4 * (lane >> 4) + (NWU == 4 ? wq : wu), lcol = lane & 15;
+    const int v = bid + slot * G;           // this slot's attention unit (phase A)
+    const int lcol = lane & 15;
     const bool nt = R == 1;                 // one row block: every weight tile read once
     PL_STAMP(t_start);
     if (threadIdx.x < 3) sm.s_cnt[threadIdx.x] = 0;
@@ -501,11 +512,15 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         PL_STORE(1, t_issued);
     }
     PL_STORE(0, t_start);
-    float4 wr[SWU];
     float fs1, fs2;
     // B: attproj(l): res2 = res + att . Wap^T + b
     {
-        const Unit u = unit_of(v, NCT * R, NCT, R);
+        constexpr int SWU = SW * 4 / NB;
+        const UW<NB> uw(wv, bid, G, lane);
+        const int us = uw.us, wu = uw.wu, e = uw.e, lrow = uw.lrow;
+        const bool fin = uw.fin;
+        float4 wr[SWU];
+        const Unit u = unit_of(uw.v, NCT * R, NCT, R);
         if (u.has) load_w<SWU>(a.w_ap, D::K16, u.j, 0, wu, nt, wr);
         lds_barrier();
         PL_MARK(3);
@@ -525,17 +540,22 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         put_red(sm.red, wv, acc);
         lds_barrier();
         if (u.has && fin) {
-            float val = foldn<NWU>(sm.red, us, e);
+            float val = foldn<NB>(sm.red, us, e);
             val += bv;
             val = row < a.B ? rv + val : 0.f;  // residual_forward(out, res, proj)
             hpa::store_wt4(a.res2, fi, val);
         }
-        publish(a, CT_X1, units_with<UPW>(bid, G, NCT * R));
+        publish(a, CT_X1, units_with<12 / NB>(bid, G, NCT * R));
     }
     PL_MARK(5);
     // C: fc(l): fch = gelu(LN2(res2) . Wfc^T + b), LN folded
     {
-        const Unit u = unit_of(v, 4 * NCT * R, 4 * NCT, R);
+        constexpr int SWU = SW * 4 / NCD;
+        const UW<NCD> uw(wv, bid, G, lane);
+        const int us = uw.us, wu = uw.wu, e = uw.e, lrow = uw.lrow;
+        const bool fin = uw.fin;
+        float4 wr[SWU];
+        const Unit u = unit_of(uw.v, 4 * NCT * R, 4 * NCT, R);
         if (u.has) load_w<SWU>(a.w_fc, D::K16, u.j, 0, wu, nt, wr);
         if (!wait_ctr<NH>(a, CT_X1, NCT * R, 2, sm)) return;
         PL_MARK(6);
@@ -554,17 +574,22 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         put_red(sm.red, wv, acc);
         lds_barrier();
         if (u.has && fin) {
-            float val = foldn<NWU>(sm.red, us, e);
-            val = ln_fold_val<NWU>(sm.wsum, us, lrow, C, val, c1, c2);
+            float val = foldn<NCD>(sm.red, us, e);
+            val = ln_fold_val<NCD>(sm.wsum, us, lrow, C, val, c1, c2);
             hpa::store_wt4(a.fch, (int)(hpa::frag_index(row, col, 4 * C) * 4), row < a.B ? hpa::gelu_ref(val) : 0.f);
         }
-        publish(a, CT_H, units_with<UPW>(bid, G, 4 * NCT * R));
+        publish(a, CT_H, units_with<12 / NCD>(bid, G, 4 * NCT * R));
         PL_MARK(7);
     }
     // D: fcproj(l), K part p of 4: partial tiles -> slab; the last part of
     // (rb, j) adds the parts in order + bias + res2 -> res
     {
-        const Unit u = unit_of(v, NCT * R * D::FP, NCT, R);
+        constexpr int SWU = SW * 4 / NCD;
+        const UW<NCD> uw(wv, bid, G, lane);
+        const int us = uw.us, wu = uw.wu, e = uw.e, lrow = uw.lrow;
+        const bool fin = uw.fin;
+        float4 wr[SWU];
+        const Unit u = unit_of(uw.v, NCT * R * D::FP, NCT, R);
         if (u.has) load_w<SWU>(a.w_fp, 4 * D::K16, u.j, u.p * D::K16, wu, nt, wr);
         if (!wait_ctr<NH>(a, CT_H, 4 * NCT * R, 3, sm)) return;
         PL_MARK(8);
@@ -576,7 +601,7 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         float val = 0.f;
         const int sofs = ((u.p * R + u.rb) * NCT + u.j) * 256 + e;
         if (u.has && fin) {
-            val = foldn<NWU>(sm.red, us, e);
+            val = foldn<NCD>(sm.red, us, e);
             hpa::store_wt4(a.slab_fp, sofs * 4, val);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -619,14 +644,19 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         }
         if (threadIdx.x == 0) {
             int nd = 0;
-            for (int s2 = 0; s2 < UPW; ++s2) nd += sm.s_last[s2] != 0 && bid + s2 * G < NCT * R * D::FP;
+            for (int s2 = 0; s2 < 12 / NCD; ++s2) nd += sm.s_last[s2] != 0 && bid + s2 * G < NCT * R * D::FP;
             if (nd) arrive(a, CT_X2, nd);
         }
         PL_MARK(9);
     }
     // E: qkv(l+1): LN1 folded, q + K/V appended into layer l+1's pages
     if (!a.last) {
-        const Unit u = unit_of(v, 3 * NCT * R, 3 * NCT, R);
+        constexpr int SWU = SW * 4 / NE;
+        const UW<NE> uw(wv, bid, G, lane);
+        const int us = uw.us, wu = uw.wu, e = uw.e, lrow = uw.lrow;
+        const bool fin = uw.fin;
+        float4 wr[SWU];
+        const Unit u = unit_of(uw.v, 3 * NCT * R, 3 * NCT, R);
         if (u.has) load_w<SWU>(a.w_qkv, D::K16, u.j, 0, wu, nt, wr);
         if (!wait_ctr<NH>(a, CT_X2, NCT * R, 4, sm)) return;
         PL_MARK(10);
@@ -645,8 +675,8 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
         put_red(sm.red, wv, acc);
         lds_barrier();
         if (u.has && fin && row < a.B) {
-            float val = foldn<NWU>(sm.red, us, e);
-            val = ln_fold_val<NWU>(sm.wsum, us, lrow, C, val, c1, c2);
+            float val = foldn<NE>(sm.red, us, e);
+            val = ln_fold_val<NE>(sm.wsum, us, lrow, C, val, c1, c2);
             if (col < C) {
                 a.q_out[(size_t)row * C + col] = val;
             } else {  // K/V of this token into the sequence's page of layer l+1 (add_to_cache)
@@ -697,12 +727,12 @@ bool shape_ok(int B, int S, int G) {
            4L * LD<NH>::NCT * R <= 3L * G;
 }
 
-template <int NH, int P, bool BF, bool ATTN, int NWU = 4>
+template <int NH, int P, bool BF, bool ATTN, int NB = 4, int NCD = 4, int NE = 4>
 int launch(const HpaLayerArgs* h, int G) {
     static int resident = -1;  // blocks per CU of this instantiation (occupancy API)
     if (resident < 0) {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, decode_layer_kernel<NH, P, BF, ATTN, NWU>, 768, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, decode_layer_kernel<NH, P, BF, ATTN, NB, NCD, NE>, 768, 0) !=
             hipSuccess)
             nb = 0;
         resident = nb;
@@ -747,34 +777,48 @@ int launch(const HpaLayerArgs* h, int G) {
     a.slab_fp = h->slab;
     a.ctr = h->counters;
     a.err = h->err;
-    decode_layer_kernel<NH, P, BF, ATTN, NWU><<<G, 768, 0, hpa_stream()>>>(a);
+    decode_layer_kernel<NH, P, BF, ATTN, NB, NCD, NE><<<G, 768, 0, hpa_stream()>>>(a);
     HPA_LAUNCH_CHECK();
     return 0;
 }
 
-template <int NH, bool ATTN, int NWU = 4>
+template <int NH, bool ATTN, int NB = 4, int NCD = 4, int NE = 4>
 int dispatch_p(const HpaLayerArgs* h, int G) {
     const bool bf = h->pool->dtype == HPA_BF16;
     switch (h->pool->page_size) {
-        case 8: return bf ? launch<NH, 8, true, ATTN, NWU>(h, G) : launch<NH, 8, false, ATTN, NWU>(h, G);
-        case 16: return bf ? launch<NH, 16, true, ATTN, NWU>(h, G) : launch<NH, 16, false, ATTN, NWU>(h, G);
-        case 32: return bf ? launch<NH, 32, true, ATTN, NWU>(h, G) : launch<NH, 32, false, ATTN, NWU>(h, G);
-        case 64: return bf ? launch<NH, 64, true, ATTN, NWU>(h, G) : launch<NH, 64, false, ATTN, NWU>(h, G);
+        case 8: return bf ? launch<NH, 8, true, ATTN, NB, NCD, NE>(h, G) : launch<NH, 8, false, ATTN, NB, NCD, NE>(h, G);
+        case 16: return bf ? launch<NH, 16, true, ATTN, NB, NCD, NE>(h, G) : launch<NH, 16, false, ATTN, NB, NCD, NE>(h, G);
+        case 32: return bf ? launch<NH, 32, true, ATTN, NB, NCD, NE>(h, G) : launch<NH, 32, false, ATTN, NB, NCD, NE>(h, G);
+        case 64: return bf ? launch<NH, 64, true, ATTN, NB, NCD, NE>(h, G) : launch<NH, 64, false, ATTN, NB, NCD, NE>(h, G);
         default: return hpa_fail(__FILE__, __LINE__, "decode layer: page size must be 8, 16, 32 or 64");
     }
 }
 
 template <int NH>
 int dispatch(const HpaLayerArgs* h, int G) {
-    if (h->chain_only == 2 || h->chain_only == 3) {  // wide units (C = 768): 12 waves (<= 16 rows) / 6 (<= 32)
+    if (h->chain_only >= 2) {  // wide units (C = 768), widths (attproj, fc / fcproj, qkv) by chain_only
         if constexpr (LD<NH>::SW % 3 == 0) {
-            const int R = (h->B + 15) / 16;
-            if (h->chain_only == 2) {
-                HPA_REQUIRE(R == 1 && 4 * LD<NH>::NCT <= G, "decode layer: 12-wave units need B <= 16, 4C/16 <= CUs");
-                return dispatch_p<NH, false, 12>(h, G);
+            const int R = (h->B + 15) / 16, nct = LD<NH>::NCT;
+            // every phase's units fit its unit slots: attproj R*nct, fc / fcproj 4*R*nct, qkv 3*R*nct
+            auto fits = [&](int nb, int ncd, int ne) {
+                return R * nct <= 12 / nb * G && 4 * R * nct <= 12 / ncd * G && 3 * R * nct <= 12 / ne * G;
+            };
+            switch (h->chain_only) {
+                case 2:
+                    HPA_REQUIRE(fits(12, 12, 12), "decode layer: chain form 2 (12/12/12-wave units) needs B <= 16");
+                    return dispatch_p<NH, false, 12, 12, 12>(h, G);
+                case 3:
+                    HPA_REQUIRE(fits(12, 6, 6), "decode layer: chain form 3 (12/6/6-wave units) needs B <= 32");
+                    return dispatch_p<NH, false, 12, 6, 6>(h, G);
+                case 4:
+                    HPA_REQUIRE(fits(12, 4, 6), "decode layer: chain form 4 (12/4/6-wave units) needs B <= 48");
+                    return dispatch_p<NH, false, 12, 4, 6>(h, G);
+                case 5:
+                    HPA_REQUIRE(fits(12, 4, 4), "decode layer: chain form 5 (12/4/4-wave units) needs B <= 64");
+                    return dispatch_p<NH, false, 12, 4, 4>(h, G);
+                default:
+                    return hpa_fail(__FILE__, __LINE__, "decode layer: chain_only must be 0..5");
             }
-            HPA_REQUIRE(R <= 2 && 4 * LD<NH>::NCT * R <= 2 * G, "decode layer: 6-wave units need B <= 32");
-            return dispatch_p<NH, false, 6>(h, G);
         } else {
             return hpa_fail(__FILE__, __LINE__, "decode layer: wide units need C = 768");
         }

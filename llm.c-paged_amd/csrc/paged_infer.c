@@ -662,7 +662,7 @@ struct GPT2Decode {
     int pl_want;      /* gpt2_decode_set_layer_kernel: 0 off, 1 auto, 2 full, 3 chain, 4 chain with wide units */
     int pl_on;        /* in use: 0 five launches, 1 full persistent layer, 2 attention launch + chain,
                          3 attention launch + chain of wide units (hpa_layer.hip NWU = pl_nwu) */
-    int pl_nwu;       /* waves per GEMM unit of the chain: 4, or 12 / 6 (wide units) */
+    int pl_wform;     /* wide-unit form of the chain (HpaLayerArgs.chain_only 2..5), else 1 */
     int pl_splits;
     int pl_global_B;  /* sharded: the whole batch's size (picks follow it); else 0 */
     float* pl_rec;
@@ -895,17 +895,18 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
      * supports (B 64 / 32 / 16 / 8: -2.3 / -0.9 / -4.9 / -4.0 % per step
      * against five launches; the full persistent layer -0.1 / +0.2 / -2.3 /
      * -1.7 %) */
-    /* the chain's wide units where a small global batch leaves 4-wave slots
-     * idle (C = 768): 12 waves per unit at <= 16 rows (one per workgroup), 6
-     * at <= 32 (two per workgroup); auto and form 4.  HPA_PL_WIDE=0 turns
-     * the auto pick off, =12 keeps it to the 12-wave form */
+    /* the chain's wide units where a phase has fewer units than 4-wave slots
+     * (C = 768), by the global batch's row blocks Rg: attproj always 12
+     * waves per unit, fc / fcproj and qkv 12 at Rg = 1, 6 at Rg = 2, qkv 6 at
+     * Rg = 3 (hpa_layer.hip); auto and form 4.  HPA_PL_WIDE=0 turns the auto
+     * pick off, =12 keeps it to Rg = 1 */
     const char* wenv = getenv("HPA_PL_WIDE");
-    const int wide12 = Bg <= 16 && d->B <= 16 && c.num_heads == 12;
-    const int wide6 = !wide12 && Bg <= 32 && d->B <= 32 && c.num_heads == 12 &&
-                      !(d->pl_want == 1 && wenv && wenv[0] == '1' && wenv[1] == '2');
+    const int Rg = (Bg + 15) / 16;
+    const int wide_ok = c.num_heads == 12 && Rg >= 1 && Rg <= 4 &&
+                        !(d->pl_want == 1 && wenv && wenv[0] == '1' && wenv[1] == '2' && Rg > 1);
     const int want_wide = d->pl_want == 4 || (d->pl_want == 1 && !(wenv && wenv[0] == '0'));
-    const int mode = d->pl_want == 2 ? 1 : want_wide && (wide12 || wide6) ? 3 : 2;
-    d->pl_nwu = mode == 3 ? (wide12 ? 12 : 6) : 4;
+    const int mode = d->pl_want == 2 ? 1 : want_wide && wide_ok ? 3 : 2;
+    d->pl_wform = mode == 3 ? 1 + Rg : 1;
     int splits = hpa_decode_layer_pick_splits(Bg, c.num_heads, d->max_ctx);
     const char* env = getenv("HPA_LAYER_SPLITS");
     if (env && atoi(env) > 0) splits = atoi(env);
@@ -943,7 +944,7 @@ static int dec_layer(GPT2* model, int l) {
     a.num_heads = c.num_heads;
     a.splits = d->pl_splits;
     a.last = l + 1 == L;
-    a.chain_only = d->pl_on == 3 ? (d->pl_nwu == 12 ? 2 : 3) : d->pl_on == 2;
+    a.chain_only = d->pl_on == 3 ? d->pl_wform : d->pl_on == 2;
     a.pool = &d->pool;
     a.layer = l;
     a.block_table = d->d_bt;

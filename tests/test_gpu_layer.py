@@ -13,9 +13,10 @@ the oracle.
   waves, so logits differ by fp32 reassociation only: <= 2e-5 max-abs.
 * Rows never depend on the batch: engines of B = 6 and of its two halves give
   bit-identical logits at the same split count (the sharded-decode property).
-* The chain's wide units (form 4: 12-wave units, one per workgroup, at
-  B <= 16; 6-wave units, two per workgroup, at B <= 32; a unit's K over its
-  waves) at B = 32 / 20 / 16 / 8 / 5: within the same bound of the launch
+* The chain's wide units (form 4: per phase 12-wave units, one per
+  workgroup, or 6-wave, two per workgroup, where the phase has fewer units
+  than 4-wave slots; a unit's K over its waves) at B = 64 / 40 / 32 / 20 /
+  16 / 8 / 5: within the same bound of the launch
   path, rows independent of the batch (12 vs 5 + 7; 28 vs 20), eager =
   graph.
 * Every step reports status 0 (no in-launch wait timed out).
@@ -44,7 +45,7 @@ def _model(hip, cfgd, params, B, P, layer, kv_dtype=0, splits_env=None, mode=2):
         os.environ.pop("HPA_LAYER_SPLITS", None)
     # mode 2: the full persistent layer at every batch it supports; 3: the
     # attention's own launch + the persistent GEMM chain; 4: that chain with
-    # wide units (12-wave units at B <= 16, 6-wave at B <= 32; C = 768)
+    # wide units (per-phase widths by the batch's row blocks; C = 768)
     assert m.set_layer_kernel(mode if layer else 0) == bool(layer)
     if layer and mode == 4:
         assert m.layer_form() == 3
@@ -53,7 +54,7 @@ def _model(hip, cfgd, params, B, P, layer, kv_dtype=0, splits_env=None, mode=2):
 
 
 @pytest.mark.parametrize("B,mode", [(64, 2), (32, 2), (16, 2), (8, 2), (64, 3), (40, 3), (8, 3), (16, 4), (8, 4),
-                                    (5, 4), (32, 4), (20, 4)])
+                                    (5, 4), (32, 4), (20, 4), (40, 4), (64, 4)])
 def test_persistent_layer_matches_launch_path_124m(hip, B, mode):
     params = synth.params(GPT2_124M, seed=31)
     ctx = 990
