@@ -134,13 +134,25 @@ def parse():
     ap.add_argument("--prof-steps", type=int, default=4,
                     help="attention roofline timing: prof_steps x L back-to-back launches (0 = off)")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="per CPU build (strict and -Ofast)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="per CPU run (-Ofast all cores, -Ofast at OMP_NUM_THREADS, strict all cores)")
     ap.add_argument("--attn-waves", type=int, default=0,
                     help="waves per attention workgroup for every launch (0 = the engine's pick by batch)")
     ap.add_argument("--attn-splits", type=int, default=0, help="attention context ranges (0 = by shape)")
-    ap.add_argument("--layer-kernel", type=int, default=-1, choices=[-1, 0, 1, 2],
-                    help="layer loop: 0 five launches per layer, 1 persistent where it measured faster (B <= 32), "
-                         "2 persistent wherever it applies; -1 the engine's default (HPA_LAYER_KERNEL or 1)")
+    ap.add_argument("--layer-kernel", type=int, default=-1, choices=[-1, 0, 1, 2, 3, 4],
+                    help="gpt2_decode_set_layer_kernel: 0 five launches per layer; 1 auto (the form measured "
+                         "fastest for the batch: the attention launch + the persistent chain with wide units); "
+                         "2 the full persistent layer (attention inside); 3 the attention launch + the chain "
+                         "(4-wave units); 4 the chain with wide units; -1 the engine's default "
+                         "(HPA_LAYER_KERNEL or 1)")
+    ap.add_argument("--picks", default="local", choices=["local", "global"],
+                    help="N>1 / --emulate-rank: shape picks by the rank's own batch (default: a rank computes "
+                         "what a single-GPU engine of its rows computes) or by the global batch "
+                         "(gpt2_decode_set_global_batch: rows bit-identical to the unsharded engine)")
+    ap.add_argument("--emulate-rank", type=int, default=0,
+                    help="N: on one GPU, time rank 0's engine of an N-GPU run (B/N rows for --scaling strong, "
+                         "B for weak, with --picks), and report the per-rank step and the N-GPU projection; "
+                         "no collective (the gather overlaps the next step)")
     ap.add_argument("--sample", action="store_true",
                     help="multinomial sampling as the reference driver (default: greedy argmax)")
     ap.add_argument("--gemm-waves", default="", help="fused GEMM waves qkv,attproj,fc,fcproj,logits (0 = auto)")
@@ -150,16 +162,18 @@ def parse():
 
 
 def cpu_baseline(cfgd, B, P, start_ctx, end_ctx, budget_s, kv_bf16=False, w_bf16=False):
-    """The oracle's OpenMP C restatement of the same paged decode, timed on
-    every host core this process may use, at the GPU's positions: once per
-    build (-O2 -fno-fast-math strict, -O3 -Ofast), each a bounded sample.
-    Rank 0, N=1.  Test infrastructure only (never the measured product)."""
+    """The oracle's OpenMP C restatement of the same paged decode, timed at
+    the GPU's positions on EVERY core this process may use (the
+    affinity mask, not the job's OMP_NUM_THREADS share), with the OMP_NUM_THREADS
+    figure beside it (the box sets 16, its CPU share): the -Ofast build at all
+    cores (the value), the -Ofast build at OMP_NUM_THREADS, the strict build at
+    all cores; each a bounded sample.  Rank 0, N=1.  Test infrastructure only
+    (never the measured product)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle_ctypes as oc
     import pagedattn
     affinity = len(os.sched_getaffinity(0))
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or affinity
-    os.environ["OMP_NUM_THREADS"] = str(threads)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     params = pagedattn.synthetic_params(cfgd, seed=1337)
     c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
     cpu_model = ""
@@ -171,9 +185,14 @@ def cpu_baseline(cfgd, B, P, start_ctx, end_ctx, budget_s, kv_bf16=False, w_bf16
                     break
     except OSError:
         pass
+    plan = [(True, affinity), (False, affinity)]
+    if share and share != affinity:
+        plan.insert(1, (True, share))
     runs = []
-    for fast, build in ((False, "-O2 -fno-fast-math -ffp-contract=off (liboracle.so)"),
-                        (True, "-O3 -Ofast -march=x86-64-v3 (liboracle_fast.so)")):
+    for fast, threads in plan:
+        build = "-O3 -Ofast -march=x86-64-v3 (liboracle_fast.so)" if fast else \
+            "-O2 -fno-fast-math -ffp-contract=off (liboracle.so)"
+        used = oc.lib(fast).oracle_set_threads(threads)
         dec = oc.PagedDecoder(params, c, B, P, cfgd["maxT"], page_seed=3, fast=fast, kv_bf16=kv_bf16,
                               w_bf16=w_bf16)
         dec.fill_random(start_ctx, seed=5)
@@ -186,15 +205,20 @@ def cpu_baseline(cfgd, B, P, start_ctx, end_ctx, budget_s, kv_bf16=False, w_bf16
             if el >= budget_s:
                 break
         dec.close()
-        runs.append({"build": build, "value": round(B * steps / el, 2), "steps": steps,
+        runs.append({"build": build, "threads": used, "value": round(B * steps / el, 2), "steps": steps,
                      "positions": f"{start_ctx}..{start_ctx + steps - 1}", "seconds": round(el, 2)})
-    return {"value": runs[1]["value"], "unit": "tokens/s", "cores": threads, "kind": "port",
+    share_run = next((r for r in runs[1:] if r["threads"] == share and "Ofast" in r["build"]), None)
+    return {"value": runs[0]["value"], "unit": "tokens/s", "cores": runs[0]["threads"], "kind": "port",
             "nproc": os.cpu_count(), "affinity_cores": affinity,
-            "sample": f"oracle/ C restatement of the same paged decode (OpenMP, {threads} threads = the cores "
-                      f"this process may use; nproc {os.cpu_count()}), GPT-2 {'XL' if cfgd['C'] == 1600 else '124M'}"
+            "value_at_omp_num_threads": None if share_run is None else
+            {"threads": share, "value": share_run["value"]},
+            "sample": f"oracle/ C restatement of the same paged decode (OpenMP on all {runs[0]['threads']} cores "
+                      f"of this process's affinity mask; nproc {os.cpu_count()}), GPT-2 "
+                      f"{'XL' if cfgd['C'] == 1600 else '124M'}"
                       f"{' bf16-rounded weights and GEMM inputs' if w_bf16 else ' fp32'}"
                       f"{' (bf16 KV)' if kv_bf16 else ''}, B={B}, page {P}, decode steps at the GPU's positions "
-                      f"after a synthetic K/V fill, <= {budget_s:.0f} s per build; value = the -Ofast build; "
+                      f"after a synthetic K/V fill, <= {budget_s:.0f} s per run; value = the -Ofast build on all "
+                      f"cores (beside it: the OMP_NUM_THREADS={share or 'unset'} share and the strict build); "
                       f"cpu: {cpu_model}",
             "builds": runs}
 
@@ -219,9 +243,11 @@ def main():
         cfgd["maxT"] = args.ctx
     kv_bf16 = args.kv_dtype == "bf16"
     w_bf16 = args.w_dtype == "bf16"
-    B, lo, hi = shard.batch_layout(args.batch, world, rank, args.scaling)
+    emulate = args.emulate_rank if world == 1 and args.emulate_rank > 1 else 0
+    layout_world = emulate or world  # --emulate-rank N: rank 0's share of an N-GPU run, on this one GPU
+    B, lo, hi = shard.batch_layout(args.batch, layout_world, rank, args.scaling)
     B_local = hi - lo
-    counts = [shard.batch_layout(args.batch, world, r, args.scaling) for r in range(world)]
+    counts = [shard.batch_layout(args.batch, layout_world, r, args.scaling) for r in range(layout_world)]
     counts = [h - l for _, l, h in counts]
     P = args.page_size
     ctx = min(args.ctx, cfgd["maxT"])
@@ -234,6 +260,8 @@ def main():
                       w_dtype=pagedattn.HPA_BF16 if w_bf16 else pagedattn.HPA_F32)
     if args.attn_splits:
         model.set_attn_splits(args.attn_splits)
+    if args.picks == "global" and layout_world > 1:
+        model.set_global_batch(B)  # every row as the unsharded engine of B computes it
     if args.layer_kernel >= 0:
         model.set_layer_kernel(args.layer_kernel)
     if args.sample:
@@ -282,10 +310,20 @@ def main():
     def sync():  # every stream of the device: the decode stream and the comm stream
         pagedattn.check(L.hpa_device_synchronize(), "device sync")
 
+    def status_gate(where):
+        """a timed-out in-launch wait of the persistent layer invalidates the
+        steps (their outputs are garbage and they end early): no value then"""
+        try:
+            model.status()
+        except RuntimeError as e:
+            print(f"[bench] rank {rank}: {e} after the {where}; no value reported", file=sys.stderr, flush=True)
+            sys.exit(5)
+
     one_step(first)
     for _ in range(args.warmup - 1 if args.warmup > 0 else 0):
         one_step(None)
     sync()
+    status_gate("warm-up steps")
     if world > 1:
         pagedattn.check(L.hpa_comm_barrier(), "comm barrier")  # RCCL all-reduce + wait
     sync()
@@ -298,13 +336,15 @@ def main():
         pagedattn.check(L.hpa_comm_barrier(), "comm barrier")
     t1 = time.perf_counter()
     bytes_after, _ = model.step_bytes()
+    status_gate("timed steps")
     elapsed = t1 - t0
     if world > 1:  # max over ranks, through the library's RCCL communicator
         el = ctypes.c_double(elapsed)
         pagedattn.check(L.hpa_comm_allreduce_max(ctypes.byref(el)), "comm max")
         elapsed = el.value
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
-    tokens_per_s = B * args.steps / elapsed  # whole job: every rank's sequences
+    # whole job: every rank's sequences (--emulate-rank: this one GPU's rows)
+    tokens_per_s = (B_local if emulate else B) * args.steps / elapsed
 
     # ---- live attention-kernel timing: HIP events on the launch stream around
     # back-to-back launches of the step's attention kernel over the layers, on
@@ -347,7 +387,7 @@ def main():
                     "bytes_per_launch": int(attn["per_launch_bytes"]), "launches_timed": attn["launches"]}
         step_bytes = 0.5 * (bytes_before + bytes_after)
         which = ("configs[4]" if kv_bf16 else "configs[2]" if args.model == "XL" else
-                 "configs[1]" if world == 1 or args.scaling == "strong" else "configs[3]: per-seq sharded pool")
+                 "configs[1]" if layout_world == 1 or args.scaling == "strong" else "configs[3]: per-seq sharded pool")
         result = {
             "metric": METRIC,
             "value": round(tokens_per_s, 1),
@@ -375,13 +415,13 @@ def main():
                                                                if gather else
                                                                f" (gather: {args.gather})" if world > 1 else ""),
                        "hip_graph": not args.no_graph, "attn_splits": splits,
-                       "attn_waves": args.attn_waves or int(L.hpa_attn_pick_waves(B, cfgd["NH"], splits, cus)),
+                       "attn_waves": args.attn_waves or int(L.gpt2_decode_attn_waves(model.h)),
                        "layer_loop": {0: "five launches per layer",
                                       1: "one persistent launch per layer (hpa_decode_layer)",
                                       2: "attention launch + one persistent launch of the GEMM chain "
                                          "(hpa_decode_layer chain_only)",
                                       3: "attention launch + one persistent launch of the GEMM chain, wide "
-                                         "units (hpa_decode_layer chain_only 2)"}[model.layer_form()],
+                                         "units (hpa_decode_layer chain_only 2..5)"}[model.layer_form()],
                        "token_choice": "multinomial (reference sample_mult)" if args.sample else "greedy",
                        "gemm_waves": [int(x) for x in model.gemm_config()[0]],
                        "gemm_row_blocks": [int(x) for x in model.gemm_config()[1]],
@@ -392,6 +432,20 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        result["config"]["picks"] = (f"global (gpt2_decode_set_global_batch({B}))" if args.picks == "global"
+                                     and layout_world > 1 else "local (the rank's own batch)")
+        # every HPA_* knob in this process's environment (none in the default run)
+        result["config"]["env_knobs"] = {k: v for k, v in sorted(os.environ.items()) if k.startswith("HPA_")}
+        result["status"] = 0  # gpt2_decode_status after the warm-up and after the timed steps
+        if emulate:
+            result["emulated_rank"] = {
+                "n_gpus": emulate, "rank": 0, "rows": B_local, "global_batch": B, "scaling": args.scaling,
+                "ms_per_step": round(ms_per_step, 4),
+                "projected_n_gpu_tokens_per_s": round(sum(counts) * args.steps / elapsed, 1),
+                "note": "one GPU running rank 0's engine of an N-GPU decode; value = this GPU's tokens/s; "
+                        "the projection assumes every rank steps as fast and the logits gather stays hidden "
+                        "behind the next step (it overlaps on its own stream); not a multi-GPU measurement"}
+            result["n_gpus"] = 1
         if prefill_stats:
             result["prefill"] = prefill_stats
         print(json.dumps(result), flush=True)

@@ -354,7 +354,11 @@ typedef struct {
     float* rec;                   /* attention split records (hpa_decode_layer_sizes) */
     float* slab;                  /* K-part partial sums */
     int* counters;                /* this layer's counter block, zero before the launch */
-    int* err;                     /* 0, or the code of the first timed-out wait */
+    int* err;                     /* this step's: 0, or the code of the first timed-out wait; zeroed
+                                     with the counters before every step (the launch's waits bail
+                                     out at once when it is set) */
+    int* err_sticky;              /* nullable: the first code also lands here, never zeroed by a
+                                     step (gpt2_decode_status reads and clears it) */
 } HpaLayerArgs;
 /* 1 if the persistent layer applies (shape, CU count, residency), else 0 */
 int hpa_decode_layer_eligible(int B, int C, int num_heads, int splits);

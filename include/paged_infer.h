@@ -205,6 +205,8 @@ int  gpt2_decode_set_graph(GPT2* model, int enable);
  * GPT-2 124M 1 at B >= 64 and 16, 2 at 32 and 8), else 1..16 */
 int  gpt2_decode_set_attn_splits(GPT2* model, int splits);
 int  gpt2_decode_attn_splits(GPT2* model);
+/* waves per attention workgroup the engine picked for its batch (hpa_attn_pick_waves) */
+int  gpt2_decode_attn_waves(GPT2* model);
 /* the layer loop's form: 0 five launches per layer; 2 one persistent launch
  * per layer (hpa_decode_layer: attention -> attproj -> fc -> fcproj -> next
  * qkv); 3 the decode attention's own launch + one persistent launch of the
@@ -273,6 +275,15 @@ double gpt2_decode_step_bytes(GPT2* model, double* attention_bytes);
  * the logits (what = 0) or greedy ids (what = 1) on a communication stream
  * (double-buffered: it overlaps the next step).  gpt2_decode_gathered (root)
  * returns the device rows of the last gather after gpt2_decode_gather_wait. */
+/* the batch the shape picks follow (attention splits / waves, layer-loop
+ * form, logits form): 0 (default) the engine's own B -- a shard computes what
+ * a single-GPU engine of its rows computes; total > 0 (<= 64 applies, above
+ * that the own B) -- what the unsharded engine of `total` rows computes, bit
+ * for bit.  No communicator needed.  Replaces the global-batch picks
+ * gpt2_decode_shard forced until round 3. */
+int    gpt2_decode_set_global_batch(GPT2* model, int total);
+/* the value set by gpt2_decode_set_global_batch (0: own B), -1 without an engine */
+int    gpt2_decode_global_batch(GPT2* model);
 int    gpt2_decode_shard(GPT2* model, const int* rows_per_rank, int root);
 int    gpt2_decode_gather(GPT2* model, int what);
 int    gpt2_decode_gather_wait(GPT2* model);

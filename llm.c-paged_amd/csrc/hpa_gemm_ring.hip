@@ -274,6 +274,7 @@ int launch_ring_epi(const FG& p, int mode, int parts) {
     if (parts > 1) {
         gemm_ring_kernel<EPI, 0, 4, true><<<npairs * (unsigned)parts, kRnNW * 64, 0, hpa_stream()>>>(p);
     } else {
+#ifdef HPA_RING_DIAG  // diagnostic build only (tools/ring_modes.sh): never in the product library
         switch (mode) {
             case 0: gemm_ring_kernel<EPI, 0, 8, false><<<npairs, kRnNW * 64, 0, hpa_stream()>>>(p); break;
             case 1: gemm_ring_kernel<EPI, 1, 8, false><<<npairs, kRnNW * 64, 0, hpa_stream()>>>(p); break;
@@ -281,6 +282,10 @@ int launch_ring_epi(const FG& p, int mode, int parts) {
             case 3: gemm_ring_kernel<EPI, 3, 8, false><<<npairs, kRnNW * 64, 0, hpa_stream()>>>(p); break;
             default: gemm_ring_kernel<EPI, 4, 8, false><<<npairs, kRnNW * 64, 0, hpa_stream()>>>(p); break;
         }
+#else
+        (void)mode;
+        gemm_ring_kernel<EPI, 0, 8, false><<<npairs, kRnNW * 64, 0, hpa_stream()>>>(p);
+#endif
     }
     HPA_LAUNCH_CHECK();
     return 0;
@@ -297,18 +302,23 @@ bool ring_eligible(const FG& p, int epi) {
 }
 
 // parts: K parts (1 = no split; 2..4 with p.sk_slab / p.sk_cnt from
-// hpa_gemm_ring_workspace).  HPA_RING_MODE=1..4: the unsplit kernel's
-// diagnostic forms (no MFMAs / no LDS-DMA / no barriers / register operands)
+// hpa_gemm_ring_workspace).  HPA_RING_MODE=1..4 in a -DHPA_RING_DIAG build
+// only: the unsplit kernel's diagnostic forms (no MFMAs / no LDS-DMA / no
+// barriers / register operands); the product library has none of them
 int launch_ring(const FG& p_in, int epi, int parts) {
     HPA_REQUIRE(ring_eligible(p_in, epi), "gemm_fused ring (variant 3): <= 64 padded rows, LN folded or none, "
                                           "QKV / GELU / RESID");
     HPA_REQUIRE(parts >= 1 && parts <= 4, "gemm_fused ring: K parts 1..4");
     HPA_REQUIRE(parts == 1 || (p_in.sk_slab && p_in.sk_cnt), "gemm_fused ring: K split needs sk_slab / sk_count");
     HPA_REQUIRE(parts == 1 || (p_in.K16 + 3) / 4 >= parts, "gemm_fused ring: fewer 4-step stages than K parts");
+#ifdef HPA_RING_DIAG
     static const int mode = [] {
         const char* e = getenv("HPA_RING_MODE");
         return e ? atoi(e) : 0;
     }();
+#else
+    constexpr int mode = 0;
+#endif
     FG p = p_in;
     p.gy = parts;
     switch (epi) {

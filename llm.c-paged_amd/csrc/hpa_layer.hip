@@ -93,6 +93,7 @@ struct KA {
     float* slab_fp;
     int* ctr;
     int* err;
+    int* err_sticky;
 };
 
 // diagnostic build (-DHPA_LAYER_TRACE, tools/pl_trace.py): s_memrealtime of
@@ -168,7 +169,10 @@ __device__ __forceinline__ bool wait_ctr(const KA& a, int which, int expected, i
                     __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
                 if (e) break;  // another workgroup gave up: follow at once
                 if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
-                    if (lane == 0) atomicCAS(a.err, 0, code);
+                    if (lane == 0) {
+                        atomicCAS(a.err, 0, code);
+                        if (a.err_sticky) atomicCAS(a.err_sticky, 0, code);
+                    }
                     break;
                 }
             }
@@ -777,6 +781,7 @@ int launch(const HpaLayerArgs* h, int G) {
     a.slab_fp = h->slab;
     a.ctr = h->counters;
     a.err = h->err;
+    a.err_sticky = h->err_sticky;
     decode_layer_kernel<NH, P, BF, ATTN, NB, NCD, NE><<<G, 768, 0, hpa_stream()>>>(a);
     HPA_LAUNCH_CHECK();
     return 0;

@@ -664,10 +664,10 @@ struct GPT2Decode {
                          3 attention launch + chain of wide units (hpa_layer.hip NWU = pl_nwu) */
     int pl_wform;     /* wide-unit form of the chain (HpaLayerArgs.chain_only 2..5), else 1 */
     int pl_splits;
-    int pl_global_B;  /* sharded: the whole batch's size (picks follow it); else 0 */
+    int pl_global_B;  /* gpt2_decode_set_global_batch: the batch the picks follow (<= 64); else 0 */
     float* pl_rec;
     float* pl_slab;
-    int* pl_ctr;      /* [L][pl_ctr_ints], zeroed at the start of every step */
+    int* pl_ctr;      /* [L][pl_ctr_ints] + the step's error word (DEC_ERR_INTS), zeroed at the start of every step */
     size_t pl_ctr_ints;
     /* gpt2_forward: token at every cached position [B][max_ctx] and, when it
      * fits, the logits of every position [B][max_ctx][V] (managed) */
@@ -856,6 +856,21 @@ static int dec_init_weights(GPT2* model, GPT2Decode* d) {
     return 0;
 }
 
+/* the batch every shape pick follows: the global batch a shard was told
+ * (gpt2_decode_set_global_batch, so its rows equal the unsharded engine's
+ * bit for bit) where that is <= 64 -- above 64 the unsharded engine has no
+ * persistent forms and a shard's own B is the better guide --
+ * else the engine's own B (a shard then computes what a single-GPU engine of
+ * its rows computes) */
+static int dec_pick_B(const GPT2Decode* d) {
+    return d->pl_global_B > 0 && d->pl_global_B <= 64 ? d->pl_global_B : d->B;
+}
+
+/* ints after the per-layer counter blocks: the step's own error word (zeroed
+ * with the counters, so one timed-out wait cannot make later steps bail out;
+ * the first code of any step also sticks in d_next[B] for gpt2_decode_status) */
+#define DEC_ERR_INTS 32
+
 /* the attention's context ranges and their workspace (zeroed whenever the
  * split count changes: the counters sit after the records of that count) */
 static int dec_set_splits(GPT2Decode* d, int splits) {
@@ -870,7 +885,7 @@ static int dec_set_splits(GPT2Decode* d, int splits) {
     {   /* the waves follow the batch the picks follow (sharded: the global one) */
         int ncu = 0;
         hpa_device_info(NULL, 0, &ncu, NULL);
-        d->attn_waves = hpa_attn_pick_waves(d->pl_global_B > 0 ? d->pl_global_B : d->B, d->pool.num_heads, splits, ncu);
+        d->attn_waves = hpa_attn_pick_waves(dec_pick_B(d), d->pool.num_heads, splits, ncu);
     }
     if (d->graph) { /* recapture with the new grid */
         hpa_synchronize();
@@ -888,7 +903,7 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
     const GPT2Config c = model->config;
     d->pl_on = 0;
     if (!d->pl_want || d->w_bf16 || !d->d_fold) return 0;
-    const int Bg = d->pl_global_B > 0 ? d->pl_global_B : d->B; /* the batch the picks follow */
+    const int Bg = dec_pick_B(d); /* the batch the picks follow */
     if (Bg > 64) return 0;
     /* auto (1): the form measured fastest (profiles/r3/pl_ab.txt): the
      * attention's own launch + the persistent chain, at every batch it
@@ -921,7 +936,7 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
     if (!d->pl_slab) d->pl_slab = (float*)hpa_malloc(sz[1] * sizeof(float));
     if (!d->pl_ctr) {
         d->pl_ctr_ints = sz[2];
-        d->pl_ctr = (int*)hpa_malloc((size_t)c.num_layers * sz[2] * sizeof(int));
+        d->pl_ctr = (int*)hpa_malloc(((size_t)c.num_layers * sz[2] + DEC_ERR_INTS) * sizeof(int));
     }
     if (!d->pl_rec || !d->pl_slab || !d->pl_ctr) return 1;
     d->pl_splits = splits;
@@ -972,7 +987,8 @@ static int dec_layer(GPT2* model, int l) {
     a.rec = d->pl_rec;
     a.slab = d->pl_slab;
     a.counters = d->pl_ctr + (size_t)l * d->pl_ctr_ints;
-    a.err = d->d_next + d->B;
+    a.err = d->pl_ctr + (size_t)L * d->pl_ctr_ints; /* this step's (zeroed with the counters) */
+    a.err_sticky = d->d_next + d->B;                /* first code of any step, until gpt2_decode_status */
     return hpa_decode_layer(&a);
 }
 
@@ -1291,7 +1307,7 @@ static void dec_gemm_desc(GPT2* model, int l, int which, HpaFusedGemm* g) {
             g->variant = 4; /* activation-resident kernel where the shape allows (hpa_logits.hip), */
             g->sk_slab = d->sk_slab; g->sk_count = d->sk_cnt; /* else stream-K with this workspace */
             if (!d->w_bf16 && hpa_logits_kernel(d->B, V, C) == 4) { /* its form by the GLOBAL batch: a */
-                const int Bg = d->pl_global_B > 0 ? d->pl_global_B : d->B; /* row's sum order (sharded = */
+                const int Bg = dec_pick_B(d); /* row's sum order (global picks: sharded = */
                 g->waves = Bg > 32 ? 12 : 16;                             /* unsharded bit for bit) */
             }
             break;
@@ -1317,7 +1333,7 @@ static int dec_gemm(GPT2* model, int l, int which) {
          * (hpa_gemm_ring.hip, variant 3; a row's sums never depend on M, so
          * shards of that batch take it too and stay bit-identical) */
         GPT2Decode* d = model->decode;
-        const int Bg = d->pl_global_B > 0 ? d->pl_global_B : d->B;
+        const int Bg = dec_pick_B(d);
         const int ring = dec_ring_allowed();
         if ((which == G_QKV || which == G_FC) && !d->w_bf16 && d->d_fold && model->config.channels >= 1024 &&
             Bg > 48 && d->B <= 64 && ring) {
@@ -1372,7 +1388,7 @@ static int dec_launch(GPT2* model) {
     const int pl = d->pl_on && !d->profiling;
     /* persistent layers: the embed kernel also zeroes their hand-off counters */
     int rc = pl ? hpa_embed_frag_zero(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C, d->pl_ctr,
-                                      (size_t)L * d->pl_ctr_ints * sizeof(int))
+                                      ((size_t)L * d->pl_ctr_ints + DEC_ERR_INTS) * sizeof(int))
                 : hpa_embed_frag(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C);
 #define DEC_TRACE(i) \
     if (d->trace_x) rc |= hpa_unpack_frag(d->res, d->B, C, d->trace_x + (size_t)(i) * d->B * C, C)
@@ -1448,13 +1464,16 @@ int gpt2_decode_set_attn_splits(GPT2* model, int splits) {
     if (splits == 0) {
         int ncu = 0;
         hpa_device_info(NULL, 0, &ncu, NULL);
-        splits = hpa_attn_pick_splits(d->B, d->pool.num_heads, d->max_ctx, ncu);
+        splits = hpa_attn_pick_splits(dec_pick_B(d), d->pool.num_heads, d->max_ctx, ncu);
     }
     if (hpa_synchronize()) return 1;
     return dec_set_splits(d, splits);
 }
 
 int gpt2_decode_attn_splits(GPT2* model) { return model->decode ? model->decode->attn_splits : 0; }
+
+/* waves per attention workgroup the engine picked (hpa_set_attention_waves may override it) */
+int gpt2_decode_attn_waves(GPT2* model) { return model->decode ? model->decode->attn_waves : 0; }
 
 static int dec_enqueue(GPT2* model, const int* tokens) {
     GPT2Decode* d = model->decode;
@@ -1997,9 +2016,45 @@ double gpt2_decode_step_bytes(GPT2* model, double* attn_bytes) {
 /* ------------------------------------------------------------------------ */
 /* sequence-sharded decode: one process per GPU, RCCL gather  */
 /* ------------------------------------------------------------------------ */
+/* The batch the engine's shape picks follow (attention split count and
+ * waves, layer-loop form and unit widths, logits form, ring GEMM): total = 0
+ * (the default) picks by the engine's own B, so a shard computes exactly what
+ * a single-GPU engine of its rows computes (the small-batch forms: what the
+ * metric's 2/4/8-GPU points time); total > 0 picks as the unsharded engine of
+ * `total` sequences does where total <= 64, so each of a shard's rows equals
+ * that engine's row bit for bit (row results depend on M only through these
+ * picks); above 64 the unsharded engine has no persistent forms and the
+ * engine's own B is used.  Needs no communicator (tests emulate a rank of an
+ * N-GPU decode on one GPU with it).  Replaces the global-batch picks that
+ * gpt2_decode_shard used to force. */
+int gpt2_decode_set_global_batch(GPT2* model, int total) {
+    GPT2Decode* d = model ? model->decode : NULL;
+    if (!d) { fprintf(stderr, "[paged_infer] gpt2_decode_init first\n"); return 1; }
+    if (total < 0 || (total > 0 && total < d->B)) {
+        fprintf(stderr, "[paged_infer] gpt2_decode_set_global_batch: total %d < this engine's %d rows\n", total, d->B);
+        return 1;
+    }
+    int ncu = 0;
+    hpa_device_info(NULL, 0, &ncu, NULL);
+    d->pl_global_B = total;
+    if (hpa_synchronize() ||
+        dec_set_splits(d, hpa_attn_pick_splits(dec_pick_B(d), model->config.num_heads, d->max_ctx, ncu)) ||
+        dec_layer_setup(model, d))
+        return 1;
+    if (d->graph) {
+        hpa_graph_destroy(d->graph);
+        d->graph = NULL;
+    }
+    return dec_rezero(d);
+}
+
+int gpt2_decode_global_batch(GPT2* model) { return model && model->decode ? model->decode->pl_global_B : -1; }
+
 /* This rank's engine decodes rows_per_rank[rank] sequences (its slice of the
  * global batch, in rank order); hpa_comm_init must have bound the
- * communicator.  The gather runs on a communication stream of its own. */
+ * communicator.  The gather runs on a communication stream of its own.  The
+ * shape picks stay the engine's own (its B); gpt2_decode_set_global_batch
+ * makes them follow the whole batch instead. */
 int gpt2_decode_shard(GPT2* model, const int* rows_per_rank, int root) {
     GPT2Decode* d = model->decode;
     if (!d) { fprintf(stderr, "[paged_infer] gpt2_decode_init first\n"); return 1; }
@@ -2014,25 +2069,6 @@ int gpt2_decode_shard(GPT2* model, const int* rows_per_rank, int root) {
         return 1;
     }
     dec_shard_free(d);
-    {   /* the arithmetic follows the GLOBAL batch, so a sharded decode equals
-         * the unsharded one bit for bit: the attention split
-         * count and the layer loop's form are what the unsharded engine of
-         * sum(rows) sequences picks (row results never depend on M beyond
-         * those two choices) */
-        long tot = 0;
-        for (int r = 0; r < n; r++) tot += rows_per_rank[r];
-        const GPT2Config c = model->config;
-        int ncu = 0;
-        hpa_device_info(NULL, 0, &ncu, NULL);
-        d->pl_global_B = (int)tot;
-        if (hpa_synchronize() || dec_set_splits(d, hpa_attn_pick_splits((int)tot, c.num_heads, d->max_ctx, ncu)))
-            return 1;
-        if (dec_layer_setup(model, d)) return 1;
-        if (d->graph) {
-            hpa_graph_destroy(d->graph);
-            d->graph = NULL;
-        }
-    }
     DecShard* s = (DecShard*)calloc(1, sizeof(DecShard));
     if (!s) return 1;
     d->shard = s;

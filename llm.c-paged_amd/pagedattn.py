@@ -232,6 +232,9 @@ def lib():
     _sig(L, "gpt2_decode_free", None, [v])
     _sig(L, "gpt2_decode_set_attn_splits", i, [v, i])
     _sig(L, "gpt2_decode_attn_splits", i, [v])
+    _sig(L, "gpt2_decode_attn_waves", i, [v])
+    _sig(L, "gpt2_decode_set_global_batch", i, [v, i])
+    _sig(L, "gpt2_decode_global_batch", i, [v])
     _sig(L, "gpt2_decode_set_layer_kernel", i, [v, i])
     _sig(L, "gpt2_decode_fill_random_ex", i, [v, i, ctypes.c_uint64, i])
     _sig(L, "hpa_pool_fill_random_ex", i, [P, v, i, i, i, ctypes.c_uint64, i])
@@ -605,6 +608,14 @@ class Model:
 
     def attn_splits(self):
         return lib().gpt2_decode_attn_splits(self.h)
+
+    def attn_waves(self):
+        return lib().gpt2_decode_attn_waves(self.h)
+
+    def set_global_batch(self, total):
+        """shape picks of the unsharded engine of `total` rows (<= 64; 0 = this
+        engine's own B): a shard's rows then equal that engine's bit for bit"""
+        check(lib().gpt2_decode_set_global_batch(self.h, int(total)), "set_global_batch")
 
     def set_layer_kernel(self, on):
         """layer loop: 0 five launches, 2 full persistent layer, 3 attention

@@ -43,6 +43,8 @@ def lib(fast=False):
         build(fast)
     L = ctypes.CDLL(path)
     L.oracle_num_params.restype = ctypes.c_size_t
+    L.oracle_set_threads.argtypes = [ctypes.c_int]
+    L.oracle_set_threads.restype = ctypes.c_int
     L.oracle_num_params.argtypes = [OracleConfig]
     L.oracle_param_offsets.argtypes = [OracleConfig, ctypes.POINTER(ctypes.c_size_t)]
     L.oracle_attention_paged.argtypes = [_F, _F, _F, _F, _PF, _PF] + [ctypes.c_int] * 6

@@ -17,6 +17,18 @@
 #include <omp.h>
 #endif
 
+/* threads of the OpenMP regions from now on (n <= 0: leave as is); returns
+ * the count in effect.  The timed CPU baseline sets it per run (bench.py). */
+int oracle_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+    return omp_get_max_threads();
+#else
+    (void)n;
+    return 1;
+#endif
+}
+
 size_t oracle_num_params(OracleConfig c) {
     size_t off[16];
     oracle_param_offsets(c, off);

@@ -38,6 +38,7 @@ typedef struct {
 } OracleConfig;
 
 /* ParameterTensors sizes/offsets in the checkpoint order, paged_infer.c:308-326,461-476 */
+int oracle_set_threads(int n);
 size_t oracle_num_params(OracleConfig c);
 void oracle_param_offsets(OracleConfig c, size_t off[16]);
 

@@ -182,20 +182,22 @@ def test_config5_end_to_end_full_context(hip):
 
 # ---------------------------------------------------------------- per-layer pinning
 def _layer_pinned_run(hip, cfgd, params, B, P, ctx0, steps, seed, kv_bf16=False, w_bf16=False, layer_rtol=1e-5,
-                      tol=LOGIT_TOL, max_exempt_frac=0.02):
+                      tol=LOGIT_TOL, max_exempt_frac=0.02, max_ctx=None):
     """Each layer on the GPU's own input: gpt2_decode_step_traced returns the
     residual stream entering every layer (and LNf), the oracle runs layer l
     from the GPU's stream[l] (oracle_paged_step_ex) and its output is compared
     with the GPU's stream[l+1]; logits and ids from the GPU's final stream.
     Rounding differences then do not compound over the 12 layers, so the ids
     are held to the fp32 bar (<= 2 % near-tie rows) also for bf16 numerics.
+    max_ctx (default maxT) bounds both sides' pools (the wpe stays maxT rows).
     Returns the per-layer max |diff| / max |x| and the IdCheck."""
+    max_ctx = max_ctx or cfgd["maxT"]
     model = hip.Model(cfgd, params=params)
-    model.decode_init(B, P, cfgd["maxT"], kv_dtype=hip.HPA_BF16 if kv_bf16 else hip.HPA_F32,
+    model.decode_init(B, P, max_ctx, kv_dtype=hip.HPA_BF16 if kv_bf16 else hip.HPA_F32,
                       w_dtype=hip.HPA_BF16 if w_bf16 else hip.HPA_F32)
     model.fill_random(ctx0, seed=seed)
     c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
-    orc = oc.PagedDecoder(params, c, B, P, cfgd["maxT"], page_seed=seed, kv_bf16=kv_bf16, w_bf16=w_bf16)
+    orc = oc.PagedDecoder(params, c, B, P, max_ctx, page_seed=seed, kv_bf16=kv_bf16, w_bf16=w_bf16)
     for l in range(cfgd["L"]):
         for b in range(B):
             k, v = model.read_kv(l, b, ctx0)
@@ -243,6 +245,17 @@ def test_config5_layer_pinned_full_context(hip):
     params = _params(hip, CFG_124M_2K, 56)
     _layer_pinned_run(hip, CFG_124M_2K, params, B=32, P=8, ctx0=2048 - 10, steps=10, seed=56, kv_bf16=True,
                       w_bf16=True, layer_rtol=BF16_LAYER_RTOL, tol=BF16_PINNED_LOGIT_TOL)
+
+
+def test_config5_layer_pinned_full_batch(hip):
+    """config 5's real batch, B=256 (bf16 weights + bf16 KV, page 8, the
+    2048-row wpe): the GEMMs run the A-resident bf16 kernel (variant 5, M >
+    112) on the shape they serve, each layer on the GPU's own input against
+    the oracle; a short context (the GEMMs do not depend on it; the pools
+    bounded to 64 positions), ids at the 2 % near-tie bar"""
+    params = _params(hip, CFG_124M_2K, 58)
+    _layer_pinned_run(hip, CFG_124M_2K, params, B=256, P=8, ctx0=40, steps=4, seed=58, kv_bf16=True,
+                      w_bf16=True, layer_rtol=BF16_LAYER_RTOL, tol=BF16_PINNED_LOGIT_TOL, max_ctx=64)
 
 
 def test_config2_layer_pinned_full_context(hip):

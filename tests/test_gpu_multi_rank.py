@@ -18,9 +18,11 @@ import os
 import socket
 
 import numpy as np
+import oracle_ctypes as oc
 import pytest
 import shard
 import synth
+from test_gpu_decode import LOGIT_TOL, IdCheck
 
 pytestmark = pytest.mark.gpu
 
@@ -122,6 +124,11 @@ def test_rccl_gather_one_rank(hip):
     hip.check(L.hpa_comm_unique_id(uid, n), "unique id")
     hip.check(L.hpa_comm_init(1, 0, uid), "comm init")
     try:
+        from conftest import runtime_mapped
+        libs = runtime_mapped()
+        print(f"runtime libraries mapped: {libs}")
+        assert any("librccl" in x and x.startswith("/opt/rocm") for x in libs), libs
+        assert not any("/torch/" in x for x in libs), libs
         assert L.hpa_comm_size() == 1 and L.hpa_comm_rank() == 0
         B = 5
         m = _engine(hip, B)
@@ -167,64 +174,177 @@ def test_rccl_single_process_init_all_barrier_and_max(hip):
         hip.check(L.hpa_comm_destroy(), "comm destroy")
 
 
-# ---- BASELINE config 4's per-rank work at model size:
-# GPT-2 124M, B = 64 split 32 / 32 over two engine processes on the one GPU,
-# identical K/V (the fill hashes the global sequence index) to ~1000 tokens,
-# 8 steps; every row's logits and greedy id equal the unsharded B = 64 engine
-# bit for bit.  Both sides use five launches per layer with the global batch's
-# attention split count and logits form (what gpt2_decode_shard picks: the
-# ring logits form at a global batch of 64, HPA_LOGITS_FORM in the shard
-# processes, which have no communicator to tell them), so the arithmetic is
-# the same; the shards hand their rows over by file (the RCCL gather of this
-# path is tested above on a 1-rank communicator).
+# ---- BASELINE config 4's per-rank work at model size, on the product's
+# DEFAULT path: GPT-2 124M, ctx ~1000, page 16, the
+# engine's default layer form (the persistent chain), graph replay, no HPA_*
+# knob in any process (a worker refuses to run with one set).  Each rank is a
+# process of its own, spawned one after another (the persistent kernel needs
+# every CU), holding one shard: its own engine + page pool, K/V filled from the
+# GLOBAL sequence index (identical to the unsharded engine's), a 1-rank RCCL
+# communicator and the end-of-step gather every step (the N>1 bench's gather
+# beside the default layer form).  Per case:
+#   * picks "global" (gpt2_decode_set_global_batch(total), total <= 64): every
+#     row's logits and id equal the unsharded engine of `total` rows bit for bit;
+#   * picks "local" (the N>1 default): each shard equals a single-GPU engine of
+#     its rows bit for bit (what the bench's --emulate-rank times), the
+#     unsharded engine within the layer-form reassociation bound, and the
+#     oracle on identical K/V (<= 2e-4, ids outside near-ties).
+# Cases: weak 64 + 64 (config 4's per-rank batch; its global batch of 128 is
+# above 64, so both pick modes are the local one), strong 32 + 32 and 8 x 8.
+# Reference per-rank work: paged_infer.c:575-729.
 GPT2_124M = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
-C4_CTX, C4_STEPS, C4_B = 990, 8, 64
+C4_CTX, C4_STEPS, C4_SEED = 990, 8, 41
+FORM_TOL = 2e-5  # fcproj's K-part sum reassociates between layer forms (test_gpu_layer.py)
 
 
-def _c4_engine(hip, B, lo):
-    m = hip.Model(GPT2_124M, params=synth.params(GPT2_124M, seed=41))
-    m.decode_init(B, 16, GPT2_124M["maxT"])
-    m.set_layer_kernel(0)
-    m.set_attn_splits(hip.lib().hpa_attn_pick_splits(C4_B, GPT2_124M["NH"], GPT2_124M["maxT"], 0))
+def _c4_tokens(total):
+    return np.random.default_rng(44).integers(0, GPT2_124M["V"], (C4_STEPS, total)).astype(np.int32)
+
+
+def _c4_engine(hip, params, lo, hi):
+    m = hip.Model(GPT2_124M, params=params)
+    m.decode_init(hi - lo, 16, GPT2_124M["maxT"])
     m.set_graph(True)
     m.fill_random(C4_CTX, seed=7, seq_offset=lo)
     return m
 
 
-def _c4_tokens():
-    return np.random.default_rng(44).integers(0, GPT2_124M["V"], (C4_STEPS, C4_B)).astype(np.int32)
-
-
-def _c4_worker(lo, hi, out_path):
-    os.environ["HPA_LOGITS_FORM"] = "ring"  # the global batch's form (launch_logits_resident)
+def _c4_rank(lo, hi, total, picks, out_path):
+    """one rank of the sharded decode, in its own process"""
+    knobs = sorted(k for k in os.environ if k.startswith("HPA_"))
+    if knobs:
+        raise SystemExit(f"product env knobs set in a config-4 rank: {knobs}")
     import pagedattn as hip
     hip.init(0)
-    m = _c4_engine(hip, hi - lo, lo)
-    toks = _c4_tokens()
+    L = hip.lib()
+    params = hip.synthetic_params(GPT2_124M, seed=C4_SEED)
+    toks = _c4_tokens(total)
+    n = L.hpa_comm_id_bytes()
+    uid = ctypes.create_string_buffer(n)
+    hip.check(L.hpa_comm_unique_id(uid, n), "unique id")
+    hip.check(L.hpa_comm_init(1, 0, uid), "comm init")
+    try:
+        m = _c4_engine(hip, params, lo, hi)
+        if picks == "global":
+            m.set_global_batch(total)
+        m.shard([hi - lo], root=0)
+        ids, lg = [], []
+        for t in range(C4_STEPS):
+            ids.append(m.step(toks[t, lo:hi]))
+            m.gather(0)  # the RCCL end-of-step gather of this step's logits
+            g = m.gathered(hi - lo, 0)
+            assert np.array_equal(g, m.logits()), t
+            lg.append(g)
+        m.status()  # no in-launch wait timed out
+        info = np.array([m.layer_form(), m.attn_splits(), m.attn_waves()], np.int32)
+        m.close()
+    finally:
+        hip.check(L.hpa_comm_destroy(), "comm destroy")
+    np.savez(out_path, ids=np.stack(ids), logits=np.stack(lg), info=info)
+
+
+def _run_ranks(tmp_path, shards, total, picks):
+    ctx = multiprocessing.get_context("spawn")
+    got = []
+    for r, (lo, hi) in enumerate(shards):  # one after another: the persistent kernel needs every CU
+        out = str(tmp_path / f"rank{r}.npz")
+        p = ctx.Process(target=_c4_rank, args=(lo, hi, total, picks, out))
+        p.start()
+        p.join(240)
+        assert p.exitcode == 0, (r, p.exitcode)
+        got.append(np.load(out))
+        print(f"rank {r} ({lo}..{hi}, picks {picks}) done: form / splits / waves {tuple(got[-1]['info'])}",
+              flush=True)
+    return got
+
+
+def _single(hip, params, lo, hi, total):
+    """an unsharded engine of rows lo..hi (its own picks): ids, logits per step"""
+    m = _c4_engine(hip, params, lo, hi)
+    toks = _c4_tokens(total)
     ids, lg = [], []
     for t in range(C4_STEPS):
         ids.append(m.step(toks[t, lo:hi]))
         lg.append(m.logits())
+    info = (m.layer_form(), m.attn_splits(), m.attn_waves())
     m.close()
-    np.savez(out_path, ids=np.stack(ids), logits=np.stack(lg))
+    return np.stack(ids), np.stack(lg), info
 
 
-def test_config4_shards_at_model_size_equal_unsharded(hip, tmp_path):
-    ctx = multiprocessing.get_context("spawn")
-    halves = [(0, 32), (32, 64)]
-    outs = [str(tmp_path / f"shard{r}.npz") for r in range(2)]
-    procs = [ctx.Process(target=_c4_worker, args=(lo, hi, o)) for (lo, hi), o in zip(halves, outs)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(300)
-    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    got = [np.load(o) for o in outs]
-    m = _c4_engine(hip, C4_B, 0)
-    toks = _c4_tokens()
+def _oracle_check(hip, params, lo, hi, total, ids, logits):
+    """the oracle decoding rows lo..hi from the same K/V and tokens"""
+    m = _c4_engine(hip, params, lo, hi)
+    B = hi - lo
+    c = oc.cfg(GPT2_124M["maxT"], GPT2_124M["V"], GPT2_124M["L"], GPT2_124M["NH"], GPT2_124M["C"])
+    orc = oc.PagedDecoder(params, c, B, 16, GPT2_124M["maxT"], page_seed=9)
+    for l in range(GPT2_124M["L"]):
+        for b in range(B):
+            k, v = m.read_kv(l, b, C4_CTX)
+            orc.set_kv(l, b, k, v)
+    m.close()
+    toks = _c4_tokens(total)
+    chk = IdCheck()
     for t in range(C4_STEPS):
-        want_ids = m.step(toks[t])
-        want_lg = m.logits()
-        assert np.array_equal(np.concatenate([g["ids"][t] for g in got]), want_ids), t
-        assert np.array_equal(np.concatenate([g["logits"][t] for g in got]), want_lg), t
-    m.close()
+        o_next, o_logits = orc.step(toks[t, lo:hi])
+        chk.add(logits[t], o_logits, ids[t], o_next)
+    orc.close()
+    chk.verify(LOGIT_TOL)
+
+
+@pytest.fixture(scope="module")
+def c4_params(hip):
+    return hip.synthetic_params(GPT2_124M, seed=C4_SEED)
+
+
+@pytest.fixture(scope="module")
+def c4_unsharded64(hip, c4_params):
+    return _single(hip, c4_params, 0, 64, 64)
+
+
+def _cat(got, key):
+    return np.concatenate([g[key] for g in got], axis=1)
+
+
+@pytest.mark.parametrize("picks", ["global", "local"])
+@pytest.mark.parametrize("nranks", [2, 8])
+def test_config4_strong_shards_default_path(hip, tmp_path, c4_params, c4_unsharded64, nranks, picks):
+    """B = 64 over 2 (32 + 32) or 8 (8 x 8) ranks"""
+    per = 64 // nranks
+    shards = [(r * per, (r + 1) * per) for r in range(nranks)]
+    got = _run_ranks(tmp_path, shards, 64, picks)
+    want_ids, want_lg, want_info = c4_unsharded64
+    ids, lg = _cat(got, "ids"), _cat(got, "logits")
+    print(f"{nranks} ranks, picks {picks}: rank forms / splits / waves {[tuple(g['info']) for g in got]}, "
+          f"unsharded {want_info}")
+    if picks == "global":
+        assert all(tuple(g["info"]) == tuple(want_info) for g in got)
+        assert np.array_equal(ids, want_ids) and np.array_equal(lg, want_lg)
+        return
+    # local: each rank is the single-GPU engine of its rows ...
+    lo, hi = shards[-1]
+    s_ids, s_lg, s_info = _single(hip, c4_params, lo, hi, 64)
+    assert tuple(got[-1]["info"]) == tuple(s_info)
+    assert np.array_equal(got[-1]["ids"], s_ids) and np.array_equal(got[-1]["logits"], s_lg)
+    # ... within the layer forms' reassociation of the unsharded engine, and the oracle's
+    diff = float(np.abs(lg - want_lg).max())
+    print(f"max |sharded - unsharded| logits {diff:.2e}")
+    assert diff <= FORM_TOL
+    _oracle_check(hip, c4_params, lo, hi, 64, got[-1]["ids"], got[-1]["logits"])
+
+
+def test_config4_weak_64_per_rank_default_path(hip, tmp_path, c4_params):
+    """config 4's per-rank batch: 64 + 64 (global 128 > 64: both pick modes
+    are the rank's own); each rank equals the single-GPU B = 64 engine of its
+    rows bit for bit, the unsharded B = 128 engine within the layer forms'
+    reassociation (that engine has no persistent form above 64), the oracle"""
+    shards = [(0, 64), (64, 128)]
+    got = _run_ranks(tmp_path, shards, 128, "global")
+    for g, (lo, hi) in zip(got, shards):
+        s_ids, s_lg, s_info = _single(hip, c4_params, lo, hi, 128)
+        assert tuple(g["info"]) == tuple(s_info)
+        assert np.array_equal(g["ids"], s_ids) and np.array_equal(g["logits"], s_lg)
+    w_ids, w_lg, w_info = _single(hip, c4_params, 0, 128, 128)
+    diff = float(np.abs(_cat(got, "logits") - w_lg).max())
+    print(f"rank forms {[tuple(g['info']) for g in got]}, unsharded B=128 {w_info}; max |diff| {diff:.2e}")
+    assert diff <= FORM_TOL
+    _oracle_check(hip, c4_params, 64, 128, 128, got[1]["ids"], got[1]["logits"])

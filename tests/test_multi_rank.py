@@ -11,7 +11,6 @@ import socket
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
 
 import oracle_ctypes as oc
 import shard
@@ -91,10 +90,20 @@ def _unsharded(B, mode):
 def test_two_rank_sharded_decode_equals_unsharded(tmp_path, batch, scaling, mode, nbuf):
     """nbuf = 2: the double-buffered asynchronous gather bench.py overlaps
     with the next step"""
+    # stdlib spawn: torch is imported by the ranks only, never in the pytest
+    # process (a -m gpu session must not map torch's HIP runtime beside the
+    # library's, and two HIP runtimes in one process abort at exit)
+    import multiprocessing
     world = 2
     out = str(tmp_path / "rank0.npy")
-    mp.start_processes(_worker, args=(world, _free_port(), batch, scaling, mode, out, nbuf), nprocs=world,
-                       join=True, start_method="spawn")
+    ctx = multiprocessing.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, batch, scaling, mode, out, nbuf)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     got = np.load(out)
     B = batch * world if scaling == "weak" else batch
     want = _unsharded(B, mode)
