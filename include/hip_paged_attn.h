@@ -328,7 +328,11 @@ typedef struct {
                                      attproj -> fc -> fcproj -> qkv(l+1); 2..5: the same with wide
                                      units (C = 768), waves per unit of (attproj, fc / fcproj,
                                      qkv): 2 (12, 12, 12) B <= 16; 3 (12, 6, 6) B <= 32;
-                                     4 (12, 4, 6) B <= 48; 5 (12, 4, 4) B <= 64 */
+                                     4 (12, 4, 6) B <= 48; 5 (12, 4, 4) B <= 64; 6: every phase
+                                     in units of all 12 waves of a workgroup holding T 16-column
+                                     tiles (T by batch, one unit per workgroup, the 12-wave
+                                     summation order at every B <= 64), 16-byte epilogues,
+                                     waits per row block (C = 768) */
     const HpaKVPool* pool;
     int layer;
     const int* block_table;

@@ -709,6 +709,381 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
     PL_MARK(11);
 }
 
+// ------------------------------------------------------------------ the chain, multi-tile units (form 6)
+// The default chain form for C = 768.  Every phase runs
+// units of all 12 waves of a workgroup (one unit per workgroup): a unit is T
+// 16-column tiles of one 16-row block (and, for fcproj, one of its 4 K parts)
+// over its K range, wave w taking k16 steps 4w .. 4w+3 of every tile -- the
+// summation order of the 12-wave units of chain forms 2..5 (a row's result
+// depends on neither T nor the batch, so every batch size and every shard
+// computes the same rows).  Against the 4-wave units at B = 64:
+//   * a workgroup reads its row block's activation ONCE (48 KB) for its T
+//     tiles, where three 4-wave slots read three row blocks (144 KB) through
+//     the CU's L2 -> CU path;
+//   * the epilogue is 16-byte: a thread owns 4 consecutive columns of one
+//     row (one float4 of the next GEMM's frag layout, of q, of a K/V page
+//     row), so every hand-off store and residual / bias / LN-fold operand load
+//     is dwordx4 (was 4 B per lane);
+//   * waits are per row block (fcproj: per row block and K part): a unit
+//     waits only for the producers of the rows it reads.
+// T per phase (host, chain6_tiles): the fewest tiles with units <= workgroups.
+namespace c6 {
+constexpr int NW = 12;  // waves per workgroup = waves per unit
+constexpr int SPW = 4;  // k16 steps per wave of a K = 768 range (48 / 12)
+// wait counters: X1 per row block, H per (row block, K part), X2 per row block
+enum { X1 = 0, H = 4, X2 = 20, NCTR = 24 };
+constexpr int kCtr = NCTR * 8 * kPad;  // ints of the sharded counters
+
+struct Smem6 {
+    float red[NW * 3 * 256];  // [wave][tile][256] accumulators
+    float wsum[NW * 32];      // [wave][16 rows][2] LN row partial sums
+    float tile[3 * 16 * 17];  // last layer: [tile][16 rows][17] for the LNf statistics
+    int s_ok;
+    int s_last;
+};
+
+__device__ __forceinline__ void arrive6(const KA& a, int ctr, int n) {
+    __hip_atomic_fetch_add(a.ctr + ctr * 8 * kPad + (blockIdx.x & 7) * kPad, n, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// wave 0 polls the 8 shards of counter ctr until they sum to `expected`
+// (bounded; the other waves wait at the barrier), as wait_ctr
+__device__ __forceinline__ bool wait6(const KA& a, int ctr, int expected, int code, Smem6& sm) {
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wv == 0) {
+        const int lane = threadIdx.x & 63;
+        const int* c = a.ctr + ctr * 8 * kPad;
+        int ok = 0;
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        for (unsigned it = 0;; ++it) {
+            int v = lane < 8 ? __hip_atomic_load(c + lane * kPad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+            v = __builtin_amdgcn_readfirstlane(wave_sum_int(v));
+            if (v >= expected) {
+                ok = 1;
+                break;
+            }
+            if ((it & 7) == 7) {
+                const int e = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if (e) break;
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+                    if (lane == 0) {
+                        atomicCAS(a.err, 0, code);
+                        if (a.err_sticky) atomicCAS(a.err_sticky, 0, code);
+                    }
+                    break;
+                }
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (lane == 0) sm.s_ok = ok;
+    }
+    lds_barrier();
+    const bool ok = sm.s_ok != 0;
+    lds_barrier();
+    return ok;
+}
+
+// the wave's weight fragments of tiles j0 .. j0+T-1, k16 steps kb + 4w ..
+template <int T>
+__device__ __forceinline__ void load_wt(const float* W, int K16W, int j0, int kb, int w, bool nt, float4 (&wr)[T][SPW]) {
+    const float4* wf = reinterpret_cast<const float4*>(W) + ((size_t)j0 * K16W + kb + w * SPW) * 64 + (threadIdx.x & 63);
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int s = 0; s < SPW; ++s) wr[t][s] = nt ? ld_nt(wf + ((size_t)t * K16W + s) * 64) : wf[((size_t)t * K16W + s) * 64];
+}
+
+// the wave's 4 A fragments (sc1: written in this launch or the previous
+// one), the T tiles' accumulator chains (each in the one-shot order: steps in
+// order, components x, y, z, w), and (STATS) the LN row partial sums
+template <int T, bool STATS>
+__device__ __forceinline__ void mfma_t(const float* A, int K16A, int rb, int kb, int w, const float4 (&wr)[T][SPW],
+                                       f32x4 (&acc)[T], float& fs1, float& fs2) {
+    float4 xv[SPW];
+    const int off = ((rb * K16A + kb + w * SPW) * 64 + (int)(threadIdx.x & 63)) * 16;
+#pragma unroll
+    for (int s = 0; s < SPW; ++s) xv[s] = hpa::load_wt16(A, off + s * 1024);
+#pragma unroll
+    for (int t = 0; t < T; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < SPW; ++s)
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s].x, wr[t][s].x, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s].y, wr[t][s].y, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s].z, wr[t][s].z, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s].w, wr[t][s].w, acc[t], 0, 0, 0);
+        }
+    if (STATS)
+#pragma unroll
+        for (int s = 0; s < SPW; ++s) hpa_gemm::row_sums_add(xv[s], fs1, fs2);
+}
+
+template <int T>
+__device__ __forceinline__ void put_red_t(float* red, int w, const f32x4 (&acc)[T]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) red[(w * T + t) * 256 + g * 64 + lane] = acc[t][g];
+}
+
+// epilogue thread tid < T*64: tile t = tid / 64, row r = (tid % 64) / 4,
+// columns 4q .. 4q+3 (q = tid % 4) of that tile; its 4 values summed over the
+// 12 waves in wave order (foldn<12>)
+template <int T>
+__device__ __forceinline__ float4 fold_t(const float* red, int t, int r, int q) {
+    const float* p = red + t * 256 + (r & 3) * 64 + 16 * (r >> 2) + 4 * q;
+    float4 v = *reinterpret_cast<const float4*>(p);
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+        const float4 x = *reinterpret_cast<const float4*>(p + w * T * 256);
+        v.x += x.x;
+        v.y += x.y;
+        v.z += x.z;
+        v.w += x.w;
+    }
+    return v;
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// LN fold of 4 values of row r (ln_fold_val<12>, elementwise)
+__device__ __forceinline__ float4 ln_fold4(const float* wsum, int r, float4 v, float4 c1, float4 c2) {
+    v.x = ln_fold_val<NW>(wsum, 0, r, 64 * 12, v.x, c1.x, c2.x);
+    v.y = ln_fold_val<NW>(wsum, 0, r, 64 * 12, v.y, c1.y, c2.y);
+    v.z = ln_fold_val<NW>(wsum, 0, r, 64 * 12, v.z, c1.z, c2.z);
+    v.w = ln_fold_val<NW>(wsum, 0, r, 64 * 12, v.w, c1.w, c2.w);
+    return v;
+}
+
+__device__ __forceinline__ void publish6(const KA& a, int ctr, bool did) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    if (threadIdx.x == 0 && did) arrive6(a, ctr, 1);
+}
+}  // namespace c6
+
+// TB, TC, TD, TE: tiles per unit of attproj, fc, fcproj, qkv (NH = 12)
+template <int P, bool BF, int TC, int TD, int TE>
+__global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
+    using namespace c6;
+    constexpr int NH = 12, C = 768, K16 = 48, NCT = 48;
+    const KA& a = *(const KA*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
+    (void)args;
+    __shared__ Smem6 sm;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tid = threadIdx.x;
+    const int bid = blockIdx.x;
+    const int R = a.R;
+    const bool nt = R == 1;
+    // epilogue thread's place: tile et, row er, column quad eq
+    const int et = tid >> 6, er = (tid & 63) >> 2, eq = tid & 3;
+    int* tick = a.ctr + kCtr;  // fcproj K-part tickets [R][NCT / TD]
+    PL_STAMP(t_start);
+    PL_STORE(0, t_start);
+    float fs1 = 0.f, fs2 = 0.f;
+    // B: attproj(l), 1 tile per unit: res2 = res + att . Wap^T + b
+    {
+        constexpr int T = 1, NG = NCT;
+        const int n = R * NG;
+        const bool has = bid < n;
+        const int g = bid % NG, rb = bid / NG;
+        float4 wr[T][SPW];
+        if (has) load_wt<T>(a.w_ap, K16, g * T, 0, w, nt, wr);
+        const bool ep = has && tid < T * 64;
+        const int row = rb * 16 + er, col = (g * T + et) * 16 + 4 * eq;
+        const int fi = (int)(hpa::frag_index(row, col, C) * 4);
+        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f), rv = bv;
+        if (ep) {
+            bv = ld4(a.b_ap + col);
+            rv = hpa::load_wt16(a.res, fi);
+        }
+        PL_MARK(4);
+        if (has) {
+            f32x4 acc[T];
+            mfma_t<T, false>(a.att, K16, rb, 0, w, wr, acc, fs1, fs2);
+            put_red_t<T>(sm.red, w, acc);
+        }
+        lds_barrier();
+        if (ep) {
+            float4 v = fold_t<T>(sm.red, et, er, eq);
+            v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
+            const bool live = row < a.B;  // residual_forward(out, res, proj); padded rows stay 0
+            v = live ? make_float4(rv.x + v.x, rv.y + v.y, rv.z + v.z, rv.w + v.w) : make_float4(0.f, 0.f, 0.f, 0.f);
+            hpa::store_wt16(a.res2, fi, v);
+        }
+        publish6(a, X1 + rb, has);
+    }
+    PL_MARK(5);
+    // C: fc(l): fch = gelu(LN2(res2) . Wfc^T + b), LN folded; T = TC tiles
+    {
+        constexpr int T = TC, NG = 4 * NCT / TC;
+        const int n = R * NG;
+        const bool has = bid < n;
+        const int g = bid % NG, rb = bid / NG;
+        float4 wr[T][SPW];
+        if (has) load_wt<T>(a.w_fc, K16, g * T, 0, w, nt, wr);
+        const bool ep = has && tid < T * 64;
+        const int row = rb * 16 + er, col = (g * T + et) * 16 + 4 * eq;
+        float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f), c2 = c1;
+        if (ep) {
+            c1 = ld4(a.fc_c1 + col);
+            c2 = ld4(a.fc_c2 + col);
+        }
+        if (!wait6(a, X1 + (has ? rb : 0), has ? NCT : 0, 2, sm)) return;
+        PL_MARK(6);
+        fs1 = fs2 = 0.f;
+        if (has) {
+            f32x4 acc[T];
+            mfma_t<T, true>(a.res2, K16, rb, 0, w, wr, acc, fs1, fs2);
+            put_red_t<T>(sm.red, w, acc);
+        }
+        hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + w * 32);
+        lds_barrier();
+        if (ep) {
+            float4 v = ln_fold4(sm.wsum, er, fold_t<T>(sm.red, et, er, eq), c1, c2);
+            const bool live = row < a.B;
+            v = live ? make_float4(hpa::gelu_ref(v.x), hpa::gelu_ref(v.y), hpa::gelu_ref(v.z), hpa::gelu_ref(v.w))
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+            hpa::store_wt16(a.fch, (int)(hpa::frag_index(row, col, 4 * C) * 4), v);
+        }
+        publish6(a, H + rb * 4 + (g * T) / NCT, has);  // the K part of fcproj these columns feed
+        PL_MARK(7);
+    }
+    // D: fcproj(l), K part p of 4, T = TD tiles: partial tiles -> slab; the
+    // last part of (row block, tile group) adds the parts in order + bias + res2
+    {
+        constexpr int T = TD, NG = NCT / TD;
+        const int n = 4 * R * NG;
+        const bool has = bid < n;
+        const int g = bid % NG, q1 = bid / NG, rb = q1 % R, p = q1 / R;
+        float4 wr[T][SPW];
+        if (has) load_wt<T>(a.w_fp, 4 * K16, g * T, p * K16, w, nt, wr);
+        const bool ep = has && tid < T * 64;
+        const int row = rb * 16 + er, col = (g * T + et) * 16 + 4 * eq;
+        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ep) bv = ld4(a.b_fp + col);
+        if (!wait6(a, H + (has ? rb * 4 + p : 0), has ? 4 * NCT / TC / 4 : 0, 3, sm)) return;
+        PL_MARK(8);
+        if (has) {
+            f32x4 acc[T];
+            mfma_t<T, false>(a.fch, 4 * K16, rb, p * K16, w, wr, acc, fs1, fs2);
+            put_red_t<T>(sm.red, w, acc);
+        }
+        lds_barrier();
+        float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int sl = (((p * R + rb) * NG + g) * T * 64 + tid) * 16;  // this part's float4 in the slab
+        if (ep) {
+            val = fold_t<T>(sm.red, et, er, eq);
+            hpa::store_wt16(a.slab_fp, sl, val);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        if (has && tid == 0) {
+            const int tk = __hip_atomic_fetch_add(tick + rb * NG + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sm.s_last = tk == 3;
+        }
+        lds_barrier();
+        const bool last = has && sm.s_last != 0;
+        if (last && ep) {
+            float4 pv[4];
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq)
+                pv[qq] = qq == p ? val : hpa::load_wt16(a.slab_fp, (((qq * R + rb) * NG + g) * T * 64 + tid) * 16);
+            const int fi = (int)(hpa::frag_index(row, col, C) * 4);
+            const float4 rv = hpa::load_wt16(a.res2, fi);
+            float4 tot = pv[0];
+#pragma unroll
+            for (int qq = 1; qq < 4; ++qq) {
+                tot.x += pv[qq].x; tot.y += pv[qq].y; tot.z += pv[qq].z; tot.w += pv[qq].w;
+            }
+            tot.x += bv.x; tot.y += bv.y; tot.z += bv.z; tot.w += bv.w;
+            const bool live = row < a.B;
+            tot = live ? make_float4(rv.x + tot.x, rv.y + tot.y, rv.z + tot.z, rv.w + tot.w)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+            hpa::store_wt16(a.res, fi, tot);
+            if (a.stats_out) {
+                float* tr = sm.tile + (et * 16 + er) * 17 + 4 * eq;
+                tr[0] = tot.x; tr[1] = tot.y; tr[2] = tot.z; tr[3] = tot.w;
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        if (a.stats_out && last && tid < T * 16) {  // 16-column LNf partial sums of the tiles' rows
+            const int t = tid >> 4, r = tid & 15;
+            const float* tr = sm.tile + (t * 16 + r) * 17;
+            float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+                s1 += tr[c];
+                s2 += tr[c] * tr[c];
+            }
+            const int j = g * T + t, rr = rb * 16 + r;
+            a.stats_out[((size_t)j * a.Mp + rr) * 2] = s1;
+            a.stats_out[((size_t)j * a.Mp + rr) * 2 + 1] = s2;
+        }
+        if (tid == 0 && last) arrive6(a, X2 + rb, 1);
+        PL_MARK(9);
+    }
+    // E: qkv(l+1), T = TE tiles: LN1 folded, q + K/V appended into layer l+1's pages
+    if (!a.last) {
+        constexpr int T = TE, NG = 3 * NCT / TE;
+        const int n = R * NG;
+        const bool has = bid < n;
+        const int g = bid % NG, rb = bid / NG;
+        float4 wr[T][SPW];
+        if (has) load_wt<T>(a.w_qkv, K16, g * T, 0, w, nt, wr);
+        const bool ep = has && tid < T * 64;
+        const int row = rb * 16 + er, col = (g * T + et) * 16 + 4 * eq;
+        float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f), c2 = c1;
+        if (ep) {
+            c1 = ld4(a.qkv_c1 + col);
+            c2 = ld4(a.qkv_c2 + col);
+        }
+        if (!wait6(a, X2 + (has ? rb : 0), has ? NCT / TD : 0, 4, sm)) return;
+        PL_MARK(10);
+        fs1 = fs2 = 0.f;
+        if (has) {
+            f32x4 acc[T];
+            mfma_t<T, true>(a.res, K16, rb, 0, w, wr, acc, fs1, fs2);
+            put_red_t<T>(sm.red, w, acc);
+        }
+        hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + w * 32);
+        lds_barrier();
+        if (ep && row < a.B) {
+            const float4 v = ln_fold4(sm.wsum, er, fold_t<T>(sm.red, et, er, eq), c1, c2);
+            if (col < C) {
+                *reinterpret_cast<float4*>(a.q_out + (size_t)row * C + col) = v;
+            } else {  // K/V of this token into the sequence's page of layer l+1 (add_to_cache)
+                const int kv = col >= 2 * C;
+                const int c = col - (kv ? 2 * C : C);
+                const int hh = c >> 6, d = c & 63;
+                const int ps = a.pos[row];
+                const int page = a.bt[(size_t)row * a.bt_stride + ps / P];
+                if (page >= 0) {
+                    const int pslot = ps % P;
+                    const size_t toff = (size_t)page * a.page_elems + ((size_t)kv * NH + hh) * P * 64;
+                    if constexpr (BF) {
+                        unsigned short* kvt = reinterpret_cast<unsigned short*>(a.kv_next) + toff +
+                                              (kv == 0 ? ((d >> 3) * P + pslot) * 8 + (d & 7) : pslot * 64 + d);
+                        const unsigned lo = hpa::f32_to_bf16(v.x) | ((unsigned)hpa::f32_to_bf16(v.y) << 16);
+                        const unsigned hi = hpa::f32_to_bf16(v.z) | ((unsigned)hpa::f32_to_bf16(v.w) << 16);
+                        *reinterpret_cast<uint2*>(kvt) = make_uint2(lo, hi);
+                    } else {
+                        float* kvt = reinterpret_cast<float*>(a.kv_next) + toff +
+                                     (kv == 0 ? ((d >> 2) * P + pslot) * 4 : pslot * 64 + d);
+                        *reinterpret_cast<float4*>(kvt) = v;
+                    }
+                }
+            }
+        }
+    }
+    PL_MARK(11);
+}
+
 int g_ncu = 0;
 
 int num_cus() {
@@ -731,19 +1106,9 @@ bool shape_ok(int B, int S, int G) {
            4L * LD<NH>::NCT * R <= 3L * G;
 }
 
-template <int NH, int P, bool BF, bool ATTN, int NB = 4, int NCD = 4, int NE = 4>
-int launch(const HpaLayerArgs* h, int G) {
-    static int resident = -1;  // blocks per CU of this instantiation (occupancy API)
-    if (resident < 0) {
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, decode_layer_kernel<NH, P, BF, ATTN, NB, NCD, NE>, 768, 0) !=
-            hipSuccess)
-            nb = 0;
-        resident = nb;
-    }
-    HPA_REQUIRE(resident >= 1, "decode layer: the persistent workgroup does not fit a CU");
+// kernel arguments of one layer launch (every form)
+void fill_ka(const HpaLayerArgs* h, int G, KA& a) {
     const HpaKVPool* pool = h->pool;
-    KA a;
     a.B = h->B;
     a.Mp = (h->B + 15) / 16 * 16;
     a.R = a.Mp / 16;
@@ -782,9 +1147,67 @@ int launch(const HpaLayerArgs* h, int G) {
     a.ctr = h->counters;
     a.err = h->err;
     a.err_sticky = h->err_sticky;
+}
+
+// blocks per CU of a 768-thread instantiation (occupancy API), cached per kernel
+template <typename K>
+int resident_blocks(K kernel) {
+    static int resident = -1;
+    if (resident < 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, 768, 0) != hipSuccess) nb = 0;
+        resident = nb;
+    }
+    return resident;
+}
+
+template <int NH, int P, bool BF, bool ATTN, int NB = 4, int NCD = 4, int NE = 4>
+int launch(const HpaLayerArgs* h, int G) {
+    HPA_REQUIRE(resident_blocks(decode_layer_kernel<NH, P, BF, ATTN, NB, NCD, NE>) >= 1,
+                "decode layer: the persistent workgroup does not fit a CU");
+    KA a;
+    fill_ka(h, G, a);
     decode_layer_kernel<NH, P, BF, ATTN, NB, NCD, NE><<<G, 768, 0, hpa_stream()>>>(a);
     HPA_LAUNCH_CHECK();
     return 0;
+}
+
+template <int P, bool BF, int TC, int TD, int TE>
+int launch6(const HpaLayerArgs* h, int G) {
+    HPA_REQUIRE(resident_blocks(decode_chain6_kernel<P, BF, TC, TD, TE>) >= 1,
+                "decode layer: the chain-6 workgroup does not fit a CU");
+    const int R = (h->B + 15) / 16;
+    HPA_REQUIRE(R * 48 <= G && R * 192 / TC <= G && 4 * R * 48 / TD <= G && R * 144 / TE <= G,
+                "decode layer: chain form 6 needs a unit per workgroup in every phase");
+    KA a;
+    fill_ka(h, G, a);
+    decode_chain6_kernel<P, BF, TC, TD, TE><<<G, 768, 0, hpa_stream()>>>(a);
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+// tiles per unit of fc, fcproj, qkv by row blocks R: the fewest with every
+// phase's units <= 256 workgroups (attproj: 1)
+template <int P, bool BF>
+int dispatch6_t(const HpaLayerArgs* h, int G) {
+    switch ((h->B + 15) / 16) {
+        case 1: return launch6<P, BF, 1, 1, 1>(h, G);
+        case 2: return launch6<P, BF, 2, 2, 2>(h, G);
+        case 3: return launch6<P, BF, 3, 3, 2>(h, G);
+        case 4: return launch6<P, BF, 3, 3, 3>(h, G);
+        default: return hpa_fail(__FILE__, __LINE__, "decode layer: chain form 6 needs B <= 64");
+    }
+}
+
+int dispatch6(const HpaLayerArgs* h, int G) {
+    const bool bf = h->pool->dtype == HPA_BF16;
+    switch (h->pool->page_size) {
+        case 8: return bf ? dispatch6_t<8, true>(h, G) : dispatch6_t<8, false>(h, G);
+        case 16: return bf ? dispatch6_t<16, true>(h, G) : dispatch6_t<16, false>(h, G);
+        case 32: return bf ? dispatch6_t<32, true>(h, G) : dispatch6_t<32, false>(h, G);
+        case 64: return bf ? dispatch6_t<64, true>(h, G) : dispatch6_t<64, false>(h, G);
+        default: return hpa_fail(__FILE__, __LINE__, "decode layer: page size must be 8, 16, 32 or 64");
+    }
 }
 
 template <int NH, bool ATTN, int NB = 4, int NCD = 4, int NE = 4>
@@ -801,6 +1224,10 @@ int dispatch_p(const HpaLayerArgs* h, int G) {
 
 template <int NH>
 int dispatch(const HpaLayerArgs* h, int G) {
+    if (h->chain_only == 6) {
+        if constexpr (NH == 12) return dispatch6(h, G);
+        return hpa_fail(__FILE__, __LINE__, "decode layer: chain form 6 needs C = 768");
+    }
     if (h->chain_only >= 2) {  // wide units (C = 768), widths (attproj, fc / fcproj, qkv) by chain_only
         if constexpr (LD<NH>::SW % 3 == 0) {
             const int R = (h->B + 15) / 16, nct = LD<NH>::NCT;
@@ -822,7 +1249,7 @@ int dispatch(const HpaLayerArgs* h, int G) {
                     HPA_REQUIRE(fits(12, 4, 4), "decode layer: chain form 5 (12/4/4-wave units) needs B <= 64");
                     return dispatch_p<NH, false, 12, 4, 4>(h, G);
                 default:
-                    return hpa_fail(__FILE__, __LINE__, "decode layer: chain_only must be 0..5");
+                    return hpa_fail(__FILE__, __LINE__, "decode layer: chain_only must be 0..6");
             }
         } else {
             return hpa_fail(__FILE__, __LINE__, "decode layer: wide units need C = 768");
@@ -859,7 +1286,9 @@ int hpa_decode_layer_sizes(int B, int C, int num_heads, int splits, size_t* out3
     const int R = (B + 15) / 16, nct = C / 16;
     out3[0] = (size_t)B * num_heads * splits * kRec;
     out3[1] = (size_t)4 * R * nct * 256;  // fcproj K-part partial tiles
-    const size_t ints = (size_t)kCtrInts + 2 * (size_t)R * nct + (size_t)B * num_heads;
+    const size_t ints5 = (size_t)kCtrInts + 2 * (size_t)R * nct + (size_t)B * num_heads;
+    const size_t ints6 = (size_t)c6::kCtr + (size_t)R * nct;  // chain form 6: per-row-block counters + tickets
+    const size_t ints = ints5 > ints6 ? ints5 : ints6;
     out3[2] = (ints + 31) / 32 * 32;  // whole 128-B lines (memset in multiples of 16 B)
     return 0;
 }

@@ -659,10 +659,11 @@ struct GPT2Decode {
     long prof_launches;
     DecShard* shard;
     /* persistent layer (hpa_decode_layer): one launch per layer */
-    int pl_want;      /* gpt2_decode_set_layer_kernel: 0 off, 1 auto, 2 full, 3 chain, 4 chain with wide units */
+    int pl_want;      /* gpt2_decode_set_layer_kernel: 0 off, 1 auto, 2 full, 3 chain, 4 chain with wide units,
+                         5 chain form 6 (12-wave multi-tile units) */
     int pl_on;        /* in use: 0 five launches, 1 full persistent layer, 2 attention launch + chain,
                          3 attention launch + chain of wide units (hpa_layer.hip NWU = pl_nwu) */
-    int pl_wform;     /* wide-unit form of the chain (HpaLayerArgs.chain_only 2..5), else 1 */
+    int pl_wform;     /* wide-unit form of the chain (HpaLayerArgs.chain_only 2..6), else 1 */
     int pl_splits;
     int pl_global_B;  /* gpt2_decode_set_global_batch: the batch the picks follow (<= 64); else 0 */
     float* pl_rec;
@@ -920,8 +921,12 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
     const int wide_ok = c.num_heads == 12 && Rg >= 1 && Rg <= 4 &&
                         !(d->pl_want == 1 && wenv && wenv[0] == '1' && wenv[1] == '2' && Rg > 1);
     const int want_wide = d->pl_want == 4 || (d->pl_want == 1 && !(wenv && wenv[0] == '0'));
-    const int mode = d->pl_want == 2 ? 1 : want_wide && wide_ok ? 3 : 2;
+    int mode = d->pl_want == 2 ? 1 : want_wide && wide_ok ? 3 : 2;
     d->pl_wform = mode == 3 ? 1 + Rg : 1;
+    if (d->pl_want == 5 && c.num_heads == 12 && Rg >= 1 && Rg <= 4) { /* chain form 6: 12-wave multi-tile units */
+        mode = 3;
+        d->pl_wform = 6;
+    }
     int splits = hpa_decode_layer_pick_splits(Bg, c.num_heads, d->max_ctx);
     const char* env = getenv("HPA_LAYER_SPLITS");
     if (env && atoi(env) > 0) splits = atoi(env);
@@ -1158,7 +1163,7 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
     }
     {
         const char* env = getenv("HPA_LAYER_KERNEL");
-        d->pl_want = env && env[0] >= '0' && env[0] <= '4' ? env[0] - '0' : 1;
+        d->pl_want = env && env[0] >= '0' && env[0] <= '5' ? env[0] - '0' : 1;
     }
     if (dec_layer_setup(model, d)) {
         dec_free(d);
@@ -1751,7 +1756,7 @@ int gpt2_decode_set_layer_kernel(GPT2* model, int enable) {
     GPT2Decode* d = model->decode;
     if (!d) return 1;
     if (hpa_synchronize()) return 1;
-    d->pl_want = enable < 0 ? 0 : enable > 4 ? 4 : enable;
+    d->pl_want = enable < 0 ? 0 : enable > 5 ? 5 : enable;
     if (dec_layer_setup(model, d)) return 1;
     if (d->graph) { /* recapture with the other step */
         hpa_graph_destroy(d->graph);

@@ -45,16 +45,18 @@ def _model(hip, cfgd, params, B, P, layer, kv_dtype=0, splits_env=None, mode=2):
         os.environ.pop("HPA_LAYER_SPLITS", None)
     # mode 2: the full persistent layer at every batch it supports; 3: the
     # attention's own launch + the persistent GEMM chain; 4: that chain with
-    # wide units (per-phase widths by the batch's row blocks; C = 768)
+    # wide units (per-phase widths by the batch's row blocks; C = 768); 5:
+    # chain form 6 (12-wave units of T tiles, one per workgroup; C = 768)
     assert m.set_layer_kernel(mode if layer else 0) == bool(layer)
-    if layer and mode == 4:
+    if layer and mode in (4, 5):
         assert m.layer_form() == 3
     m.set_graph(True)
     return m
 
 
 @pytest.mark.parametrize("B,mode", [(64, 2), (32, 2), (16, 2), (8, 2), (64, 3), (40, 3), (8, 3), (16, 4), (8, 4),
-                                    (5, 4), (32, 4), (20, 4), (40, 4), (64, 4)])
+                                    (5, 4), (32, 4), (20, 4), (40, 4), (64, 4), (64, 5), (48, 5), (33, 5), (32, 5),
+                                    (20, 5), (16, 5), (8, 5), (5, 5)])
 def test_persistent_layer_matches_launch_path_124m(hip, B, mode):
     params = synth.params(GPT2_124M, seed=31)
     ctx = 990
@@ -217,5 +219,43 @@ def test_persistent_chain_wide_rows_independent_of_batch_and_graph(hip):
         assert np.array_equal(full, run(0, 12, graph=False))
         full = run(0, 28)  # 6-wave units (17-32 rows): the first 20 rows of 28 = a 20-row engine
         assert np.array_equal(full[:, :20], run(0, 20))
+    finally:
+        hip.check(hip.lib().hpa_set_attention_waves(0), "waves")
+
+
+def test_chain6_rows_independent_of_batch_and_form4(hip):
+    """chain form 6 keeps the 12-wave units' summation order at every batch:
+    with the attention's split count and waves pinned, rows of B = 64 (4 row
+    blocks, 3 tiles per unit) equal those of B = 8 / 24 / 40 engines bit for
+    bit, and at one row block form 6 equals form 4's 12-wave units; eager =
+    graph"""
+    params = synth.params(GPT2_124M, seed=94)
+    steps = 3
+    toks = np.random.default_rng(94).integers(0, GPT2_124M["V"], (steps, 64)).astype(np.int32)
+
+    def run(lo, hi, mode=5, graph=True):
+        m = _model(hip, GPT2_124M, params, hi - lo, 16, 1, mode=mode)
+        m.set_graph(graph)
+        m.set_attn_splits(1)
+        m.fill_random(300, seed=11, seq_offset=lo)
+        lg, ids = [], []
+        for t in range(steps):
+            ids.append(m.step(toks[t, lo:hi]))
+            lg.append(m.logits())
+        m.status()
+        m.close()
+        return np.stack(lg), np.stack(ids)
+
+    hip.check(hip.lib().hpa_set_attention_waves(4), "waves")
+    try:
+        full, fid = run(0, 64)
+        for lo, hi in ((0, 8), (40, 64), (8, 48)):
+            lg, ids = run(lo, hi)
+            assert np.array_equal(full[:, lo:hi], lg), (lo, hi)
+            assert np.array_equal(fid[:, lo:hi], ids), (lo, hi)
+        lg8, _ = run(0, 8, mode=4)
+        assert np.array_equal(full[:, :8], lg8)
+        lge, _ = run(0, 64, graph=False)
+        assert np.array_equal(full, lge)
     finally:
         hip.check(hip.lib().hpa_set_attention_waves(0), "waves")
