@@ -915,6 +915,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             v = live ? make_float4(rv.x + v.x, rv.y + v.y, rv.z + v.z, rv.w + v.w) : make_float4(0.f, 0.f, 0.f, 0.f);
             hpa::store_wt16(a.res2, fi, v);
         }
+        PL_MARK(12);
         publish6(a, X1 + rb, has);
     }
     PL_MARK(5);
@@ -950,6 +951,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
                      : make_float4(0.f, 0.f, 0.f, 0.f);
             hpa::store_wt16(a.fch, (int)(hpa::frag_index(row, col, 4 * C) * 4), v);
         }
+        PL_MARK(13);
         publish6(a, H + rb * 4 + (g * T) / NCT, has);  // the K part of fcproj these columns feed
         PL_MARK(7);
     }
@@ -980,6 +982,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             val = fold_t<T>(sm.red, et, er, eq);
             hpa::store_wt16(a.slab_fp, sl, val);
         }
+        PL_MARK(14);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
         if (has && tid == 0) {
@@ -1053,6 +1056,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         }
         hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + w * 32);
         lds_barrier();
+        PL_MARK(15);
         if (ep && row < a.B) {
             const float4 v = ln_fold4(sm.wsum, er, fold_t<T>(sm.red, et, er, eq), c1, c2);
             if (col < C) {

@@ -20,7 +20,9 @@ import pagedattn as hip  # noqa: E402
 import synth  # noqa: E402
 
 EVENTS = ["start", "A issued", "A unit done", "A barrier", "B wait done", "B done", "C wait done", "C done",
-          "D wait done", "D done", "E wait done", "end"]
+          "D wait done", "D done", "E wait done", "end",
+          # chain form 6 only: stores issued (before the drain) / E folded
+          "B stored", "C stored", "D part stored", "E folded"]
 
 
 def main():
@@ -42,7 +44,7 @@ def main():
         raise SystemExit("not a trace build (make XFLAGS=-DHPA_LAYER_TRACE)")
     m.step(toks)
     m.status()
-    buf = np.zeros((cfg["L"], 256, 16), np.uint64)
+    buf = np.zeros((cfg["L"], 256, 16), np.uint64)  # 16 event slots per (layer, workgroup)
     hip.check(L.hpa_decode_layer_trace(buf.ctypes.data_as(ctypes.c_void_p), cfg["L"]), "trace")
     rows = {k: [] for k in range(len(EVENTS))}
     spans = []
