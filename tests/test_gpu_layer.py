@@ -48,7 +48,7 @@ def _model(hip, cfgd, params, B, P, layer, kv_dtype=0, splits_env=None, mode=2):
     # wide units (per-phase widths by the batch's row blocks; C = 768); 5:
     # chain form 6 (12-wave units of T tiles, one per workgroup; C = 768)
     assert m.set_layer_kernel(mode if layer else 0) == bool(layer)
-    if layer and mode in (4, 5):
+    if layer and mode in (4, 5, 6):
         assert m.layer_form() == 3
     m.set_graph(True)
     return m
@@ -56,7 +56,8 @@ def _model(hip, cfgd, params, B, P, layer, kv_dtype=0, splits_env=None, mode=2):
 
 @pytest.mark.parametrize("B,mode", [(64, 2), (32, 2), (16, 2), (8, 2), (64, 3), (40, 3), (8, 3), (16, 4), (8, 4),
                                     (5, 4), (32, 4), (20, 4), (40, 4), (64, 4), (64, 5), (48, 5), (33, 5), (32, 5),
-                                    (20, 5), (16, 5), (8, 5), (5, 5)])
+                                    (20, 5), (16, 5), (8, 5), (5, 5), (64, 6), (48, 6), (40, 6), (32, 6), (17, 6),
+                                    (8, 6), (1, 6)])
 def test_persistent_layer_matches_launch_path_124m(hip, B, mode):
     params = synth.params(GPT2_124M, seed=31)
     ctx = 990
@@ -257,6 +258,9 @@ def test_chain6_rows_independent_of_batch_and_form4(hip):
         for lo, hi in ((0, 8), (40, 64), (8, 48)):
             assert np.array_equal(full[:, :, lo:hi], run(lo, hi)), (lo, hi)
         assert np.array_equal(run(0, 8, traced=False), run(0, 8, mode=4, traced=False))
+        # granule hand-offs change no arithmetic: form 7 = form 6 bit for bit
+        assert np.array_equal(full, run(0, 64, mode=6))
+        assert np.array_equal(run(0, 40, mode=6, traced=False), run(0, 40, mode=5, traced=False))
         g64 = run(0, 64, traced=False)  # graph replay: its last step's residual feeds these logits
         assert np.isfinite(g64).all()
     finally:
