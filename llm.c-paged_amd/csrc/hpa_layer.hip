@@ -98,6 +98,9 @@ struct KA {
     // res2 / fch / res / fcproj's K-part partials, tagged per (step, layer)
     unsigned *res2g, *fchg, *resg, *slabg;
     const unsigned* epoch;
+    // chain form 8 (wide layers, GPT-2 XL): tiles per unit and tile groups
+    // (padded to a multiple of 8) of attproj, fc, fcproj, qkv
+    int xt[4], xng[4];
 };
 
 // diagnostic build (-DHPA_LAYER_TRACE, tools/pl_trace.py): s_memrealtime of
@@ -753,7 +756,8 @@ __device__ __forceinline__ void arrive6(const KA& a, int ctr, int n) {
 
 // wave 0 polls the 8 shards of counter ctr until they sum to `expected`
 // (bounded; the other waves wait at the barrier), as wait_ctr
-__device__ __forceinline__ bool wait6(const KA& a, int ctr, int expected, int code, Smem6& sm) {
+template <typename SM>
+__device__ __forceinline__ bool wait6(const KA& a, int ctr, int expected, int code, SM& sm) {
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wv == 0) {
         const int lane = threadIdx.x & 63;
@@ -1232,6 +1236,318 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
     PL_MARK(11);
 }
 
+
+// ------------------------------------------------------------------ the chain for wide layers (form 8)
+// GPT-2 XL (C = 1600, NH = 25): the same persistent
+// chain attproj -> fc -> fcproj -> qkv(l+1) as form 6, sized for GEMMs that
+// are MFMA-bound (3.9 GFLOP per layer at B = 64, 25 us at the fp32 rate):
+//   * one unit of all 12 waves per workgroup = (row block, up to XT_MAX
+//     16-column tiles[, fcproj K part]), T per phase chosen on the host so
+//     the units fill the CUs (B = 64: attproj 2, fc 7, fcproj 7, qkv 5 tiles);
+//     tile groups are padded to a multiple of 8 so the row blocks of a weight
+//     tile land on one XCD and re-read it from that L2;
+//   * a wave holds its K range of the A rows (K16 / 12 steps, 8 or 9 at XL)
+//     once per phase and streams its weight fragments tile by tile, double
+//     buffered: the phase's first tile is loaded before its wait;
+//   * every tile's accumulators stay in registers until one LDS fold of all
+//     T tiles; epilogues are 16-byte as in form 6;
+//   * waits per row block; fcproj's 4 K parts (of C each) are combined by the
+//     last part to draw its ticket, in part order.
+// A wave's K range depends only on K, so a row's sums never depend on B.
+namespace cx {
+constexpr int NW = 12;
+constexpr int XT_MAX = 7;
+
+template <int MAXS>
+__device__ __forceinline__ void ld_tile(const float* W, int K16W, int j, int kb, int s0, int ns, bool nt,
+                                        float4 (&wr)[MAXS]) {
+    const float4* wf = reinterpret_cast<const float4*>(W) + ((size_t)j * K16W + kb + s0) * 64 + (threadIdx.x & 63);
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s)
+        if (s < ns) wr[s] = nt ? ld_nt(wf + (size_t)s * 64) : wf[(size_t)s * 64];
+}
+
+template <int MAXS>
+__device__ __forceinline__ f32x4 chain_tile(const float4 (&xv)[MAXS], const float4 (&wr)[MAXS], int ns) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s)
+        if (s < ns) {
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s].x, wr[s].x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s].y, wr[s].y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s].z, wr[s].z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s].w, wr[s].w, acc, 0, 0, 0);
+        }
+    return acc;
+}
+
+struct SmemX {
+    float red[NW * XT_MAX * 256];
+    float wsum[NW * 32];
+    float tile[XT_MAX * 16 * 17];
+    int s_ok;
+    int s_last;
+};
+
+// the unit body up to the LDS fold: A (its K range of row block rb, sc1),
+// row sums (STATS), the nt tiles j0.. streamed double-buffered (wr0 holds
+// tile 0, loaded before the caller's wait), accumulators -> red[w][t]
+template <int MAXS, bool STATS>
+__device__ __forceinline__ void unit_body(const float* A, int K16A, const float* W, int K16W, int rb, int kb, int j0,
+                                          int ntl, int s0, int ns, bool nt, float4 (&wr0)[MAXS], float* red,
+                                          float& fs1, float& fs2) {
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    float4 xv[MAXS];
+    const int off = ((rb * K16A + kb + s0) * 64 + lane) * 16;
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s)
+        if (s < ns) xv[s] = hpa::load_wt16(A, off + s * 1024);
+    if (STATS)
+#pragma unroll
+        for (int s = 0; s < MAXS; ++s)
+            if (s < ns) hpa_gemm::row_sums_add(xv[s], fs1, fs2);
+    float4 wr1[MAXS];
+#pragma unroll
+    for (int t = 0; t < XT_MAX; ++t) {
+        if (t >= ntl) break;
+        if (t + 1 < ntl) {  // the next tile's fragments into the other buffer
+            if (t & 1)
+                ld_tile<MAXS>(W, K16W, j0 + t + 1, kb, s0, ns, nt, wr0);
+            else
+                ld_tile<MAXS>(W, K16W, j0 + t + 1, kb, s0, ns, nt, wr1);
+        }
+        const f32x4 acc = (t & 1) ? chain_tile<MAXS>(xv, wr1, ns) : chain_tile<MAXS>(xv, wr0, ns);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) red[(w * XT_MAX + t) * 256 + g * 64 + lane] = acc[g];
+    }
+}
+
+// epilogue element of thread tid: tile et = tid / 64 of the unit, row er,
+// columns 4 eq .. +3; summed over the 12 waves in wave order
+__device__ __forceinline__ float4 fold_x(const float* red, int t, int r, int q) {
+    const float* p = red + t * 256 + (r & 3) * 64 + 16 * (r >> 2) + 4 * q;
+    float4 v = *reinterpret_cast<const float4*>(p);
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+        const float4 x = *reinterpret_cast<const float4*>(p + w * XT_MAX * 256);
+        v.x += x.x; v.y += x.y; v.z += x.z; v.w += x.w;
+    }
+    return v;
+}
+
+__device__ __forceinline__ float4 ln_fold4x(const float* wsum, int r, int K, float4 v, float4 c1, float4 c2) {
+    v.x = ln_fold_val<NW>(wsum, 0, r, K, v.x, c1.x, c2.x);
+    v.y = ln_fold_val<NW>(wsum, 0, r, K, v.y, c1.y, c2.y);
+    v.z = ln_fold_val<NW>(wsum, 0, r, K, v.z, c1.z, c2.z);
+    v.w = ln_fold_val<NW>(wsum, 0, r, K, v.w, c1.w, c2.w);
+    return v;
+}
+
+__device__ __forceinline__ bool waitx(const KA& a, int ctr, int expected, int code, SmemX& sm) {
+    return c6::wait6<SmemX>(a, ctr, expected, code, sm);
+}
+}  // namespace cx
+
+template <int NH, int P, bool BF>
+__global__ __launch_bounds__(768) void decode_chainx_kernel(KA args) {
+    using namespace cx;
+    constexpr int C = 64 * NH, K16 = C / 16, NCT = C / 16;
+    constexpr int MAXS = (K16 + NW - 1) / NW;
+    const KA& a = *(const KA*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
+    (void)args;
+    __shared__ SmemX sm;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tid = threadIdx.x;
+    const int bid = blockIdx.x;
+    const int R = a.R;
+    const bool nt = R == 1;
+    const int s0 = w * K16 / NW, ns = (w + 1) * K16 / NW - s0;  // this wave's k16 steps of a K = C range
+    const int et = tid >> 6, er = (tid & 63) >> 2, eq = tid & 3;
+    int* tick = a.ctr + c6::kCtr;
+    PL_STAMP(t_start);
+    PL_STORE(0, t_start);
+    float fs1 = 0.f, fs2 = 0.f;
+    float4 wr0[MAXS];
+    // B: attproj(l): res2 = res + att . Wap^T + b
+    {
+        const int T = a.xt[0], NG = a.xng[0];
+        const int g = bid % NG, rb = bid / NG, j0 = g * T;
+        const bool has = rb < R && j0 < NCT;
+        const int ntl = has ? min(T, NCT - j0) : 0;
+        if (has) cx::ld_tile<MAXS>(a.w_ap, K16, j0, 0, s0, ns, nt, wr0);
+        const bool ep = tid < ntl * 64;
+        const int row = rb * 16 + er, col = (j0 + et) * 16 + 4 * eq;
+        const int fi = ep ? (int)(hpa::frag_index(row, col, C) * 4) : 0;
+        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f), rv = bv;
+        if (ep) {
+            bv = c6::ld4(a.b_ap + col);
+            rv = hpa::load_wt16(a.res, fi);
+        }
+        if (has) unit_body<MAXS, false>(a.att, K16, a.w_ap, K16, rb, 0, j0, ntl, s0, ns, nt, wr0, sm.red, fs1, fs2);
+        lds_barrier();
+        if (ep) {
+            float4 v = fold_x(sm.red, et, er, eq);
+            v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
+            v = row < a.B ? make_float4(rv.x + v.x, rv.y + v.y, rv.z + v.z, rv.w + v.w) : make_float4(0.f, 0.f, 0.f, 0.f);
+            hpa::store_wt16(a.res2, fi, v);
+        }
+        c6::publish6(a, c6::X1 + rb, has);
+    }
+    PL_MARK(5);
+    // C: fc(l): fch = gelu(LN2(res2) . Wfc^T + b), LN folded
+    {
+        constexpr int NJ = 4 * NCT;
+        const int T = a.xt[1], NG = a.xng[1];
+        const int g = bid % NG, rb = bid / NG, j0 = g * T;
+        const bool has = rb < R && j0 < NJ;
+        const int ntl = has ? min(T, NJ - j0) : 0;
+        if (has) cx::ld_tile<MAXS>(a.w_fc, K16, j0, 0, s0, ns, nt, wr0);
+        const bool ep = tid < ntl * 64;
+        const int row = rb * 16 + er, col = (j0 + et) * 16 + 4 * eq;
+        float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f), c2 = c1;
+        if (ep) {
+            c1 = c6::ld4(a.fc_c1 + col);
+            c2 = c6::ld4(a.fc_c2 + col);
+        }
+        const int n_b = (NCT + a.xt[0] - 1) / a.xt[0];  // attproj units of a row block
+        if (!waitx(a, c6::X1 + (has ? rb : 0), has ? n_b : 0, 2, sm)) return;
+        PL_MARK(6);
+        fs1 = fs2 = 0.f;
+        if (has) unit_body<MAXS, true>(a.res2, K16, a.w_fc, K16, rb, 0, j0, ntl, s0, ns, nt, wr0, sm.red, fs1, fs2);
+        hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + w * 32);
+        lds_barrier();
+        if (ep) {
+            float4 v = ln_fold4x(sm.wsum, er, C, fold_x(sm.red, et, er, eq), c1, c2);
+            v = row < a.B ? make_float4(hpa::gelu_ref(v.x), hpa::gelu_ref(v.y), hpa::gelu_ref(v.z), hpa::gelu_ref(v.w))
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+            hpa::store_wt16(a.fch, (int)(hpa::frag_index(row, col, 4 * C) * 4), v);
+        }
+        c6::publish6(a, c6::H + rb * 4, has);
+        PL_MARK(7);
+    }
+    // D: fcproj(l), K part p of 4 (C each): partials -> slab; the last part of
+    // (row block, tile group) adds the parts in order + bias + res2 -> res
+    {
+        const int T = a.xt[2], NG = a.xng[2];
+        const int g = bid % NG, q1 = bid / NG, rb = q1 % R, p = q1 / R, j0 = g * T;
+        const bool has = p < 4 && j0 < NCT;
+        const int ntl = has ? min(T, NCT - j0) : 0;
+        if (has) cx::ld_tile<MAXS>(a.w_fp, 4 * K16, j0, p * K16, s0, ns, nt, wr0);
+        const bool ep = tid < ntl * 64;
+        const int row = rb * 16 + er, col = (j0 + et) * 16 + 4 * eq;
+        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ep) bv = c6::ld4(a.b_fp + col);
+        const int n_c = (4 * NCT + a.xt[1] - 1) / a.xt[1];  // fc units of a row block
+        if (!waitx(a, c6::H + (has ? rb * 4 : 0), has ? n_c : 0, 3, sm)) return;
+        PL_MARK(8);
+        if (has) unit_body<MAXS, false>(a.fch, 4 * K16, a.w_fp, 4 * K16, rb, p * K16, j0, ntl, s0, ns, nt, wr0, sm.red, fs1, fs2);
+        lds_barrier();
+        float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+        auto slab_at = [&](int pp) { return (((pp * R + rb) * NCT + j0 + et) * 256 + (tid & 63) * 4) * 4; };
+        if (ep) {
+            val = fold_x(sm.red, et, er, eq);
+            hpa::store_wt16(a.slab_fp, slab_at(p), val);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        if (has && tid == 0) {
+            const int tk = __hip_atomic_fetch_add(tick + rb * NG + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sm.s_last = tk == 3;
+        }
+        lds_barrier();
+        const bool last = has && sm.s_last != 0;
+        if (last && ep) {
+            float4 pv[4];
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) pv[qq] = qq == p ? val : hpa::load_wt16(a.slab_fp, slab_at(qq));
+            const int fi = (int)(hpa::frag_index(row, col, C) * 4);
+            const float4 rv = hpa::load_wt16(a.res2, fi);
+            float4 tot = pv[0];
+#pragma unroll
+            for (int qq = 1; qq < 4; ++qq) {
+                tot.x += pv[qq].x; tot.y += pv[qq].y; tot.z += pv[qq].z; tot.w += pv[qq].w;
+            }
+            tot.x += bv.x; tot.y += bv.y; tot.z += bv.z; tot.w += bv.w;
+            tot = row < a.B ? make_float4(rv.x + tot.x, rv.y + tot.y, rv.z + tot.z, rv.w + tot.w)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+            hpa::store_wt16(a.res, fi, tot);
+            if (a.stats_out) {
+                float* tr = sm.tile + (et * 16 + er) * 17 + 4 * eq;
+                tr[0] = tot.x; tr[1] = tot.y; tr[2] = tot.z; tr[3] = tot.w;
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        if (a.stats_out && last && tid < ntl * 16) {  // 16-column LNf partial sums of the tiles' rows
+            const int t = tid >> 4, r = tid & 15;
+            const float* tr = sm.tile + (t * 16 + r) * 17;
+            float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+                s1 += tr[c];
+                s2 += tr[c] * tr[c];
+            }
+            const int j = j0 + t, rr = rb * 16 + r;
+            a.stats_out[((size_t)j * a.Mp + rr) * 2] = s1;
+            a.stats_out[((size_t)j * a.Mp + rr) * 2 + 1] = s2;
+        }
+        if (tid == 0 && last) c6::arrive6(a, c6::X2 + rb, 1);
+        PL_MARK(9);
+    }
+    // E: qkv(l+1): LN1 folded, q + K/V appended into layer l+1's pages
+    if (!a.last) {
+        constexpr int NJ = 3 * NCT;
+        const int T = a.xt[3], NG = a.xng[3];
+        const int g = bid % NG, rb = bid / NG, j0 = g * T;
+        const bool has = rb < R && j0 < NJ;
+        const int ntl = has ? min(T, NJ - j0) : 0;
+        if (has) cx::ld_tile<MAXS>(a.w_qkv, K16, j0, 0, s0, ns, nt, wr0);
+        const bool ep = tid < ntl * 64;
+        const int row = rb * 16 + er, col = (j0 + et) * 16 + 4 * eq;
+        float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f), c2 = c1;
+        if (ep) {
+            c1 = c6::ld4(a.qkv_c1 + col);
+            c2 = c6::ld4(a.qkv_c2 + col);
+        }
+        const int n_d = (NCT + a.xt[2] - 1) / a.xt[2];  // fcproj tile groups of a row block
+        if (!waitx(a, c6::X2 + (has ? rb : 0), has ? n_d : 0, 4, sm)) return;
+        PL_MARK(10);
+        fs1 = fs2 = 0.f;
+        if (has) unit_body<MAXS, true>(a.res, K16, a.w_qkv, K16, rb, 0, j0, ntl, s0, ns, nt, wr0, sm.red, fs1, fs2);
+        hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + w * 32);
+        lds_barrier();
+        if (ep && row < a.B) {
+            const float4 v = ln_fold4x(sm.wsum, er, C, fold_x(sm.red, et, er, eq), c1, c2);
+            if (col < C) {
+                *reinterpret_cast<float4*>(a.q_out + (size_t)row * C + col) = v;
+            } else {  // K/V of this token into the sequence's page of layer l+1 (add_to_cache)
+                const int kv = col >= 2 * C;
+                const int c = col - (kv ? 2 * C : C);
+                const int hh = c >> 6, d = c & 63;
+                const int ps = a.pos[row];
+                const int page = a.bt[(size_t)row * a.bt_stride + ps / P];
+                if (page >= 0) {
+                    const int pslot = ps % P;
+                    const size_t toff = (size_t)page * a.page_elems + ((size_t)kv * NH + hh) * P * 64;
+                    if constexpr (BF) {
+                        unsigned short* kvt = reinterpret_cast<unsigned short*>(a.kv_next) + toff +
+                                              (kv == 0 ? ((d >> 3) * P + pslot) * 8 + (d & 7) : pslot * 64 + d);
+                        const unsigned lo = hpa::f32_to_bf16(v.x) | ((unsigned)hpa::f32_to_bf16(v.y) << 16);
+                        const unsigned hi = hpa::f32_to_bf16(v.z) | ((unsigned)hpa::f32_to_bf16(v.w) << 16);
+                        *reinterpret_cast<uint2*>(kvt) = make_uint2(lo, hi);
+                    } else {
+                        float* kvt = reinterpret_cast<float*>(a.kv_next) + toff +
+                                     (kv == 0 ? ((d >> 2) * P + pslot) * 4 : pslot * 64 + d);
+                        *reinterpret_cast<float4*>(kvt) = v;
+                    }
+                }
+            }
+        }
+    }
+    PL_MARK(11);
+}
+
 int g_ncu = 0;
 
 int num_cus() {
@@ -1339,6 +1655,53 @@ int launch6(const HpaLayerArgs* h, int G) {
     decode_chain6_kernel<P, BF, TC, TD, TE, GR><<<G, 768, 0, hpa_stream()>>>(a);
     HPA_LAUNCH_CHECK();
     return 0;
+}
+
+// chain form 8: tiles per unit T (<= cx::XT_MAX) and tile groups NG (padded
+// to a multiple of 8 where that still fits) of a phase with NJ column tiles
+// and `parts` K parts: the fewest tiles with every unit on a workgroup
+int pick_xt(int R, int parts, int NJ, int G, int* T, int* NG) {
+    for (int pad = 8; pad >= 1; pad /= 8)
+        for (int t = (R * parts * NJ + G - 1) / G; t <= cx::XT_MAX; ++t) {
+            if (t < 1) continue;
+            const int ng = ((NJ + t - 1) / t + pad - 1) / pad * pad;
+            if (R * parts * ng <= G) {
+                *T = t;
+                *NG = ng;
+                return 0;
+            }
+        }
+    return 1;
+}
+
+int chainx_shape(int B, int NH, int G, int xt[4], int xng[4]) {
+    const int R = (B + 15) / 16, nct = 4 * NH;  // C / 16
+    return B < 1 || B > 64 || pick_xt(R, 1, nct, G, &xt[0], &xng[0]) || pick_xt(R, 1, 4 * nct, G, &xt[1], &xng[1]) ||
+           pick_xt(R, 4, nct, G, &xt[2], &xng[2]) || pick_xt(R, 1, 3 * nct, G, &xt[3], &xng[3]);
+}
+
+template <int NH, int P, bool BF>
+int launchx(const HpaLayerArgs* h, int G) {
+    HPA_REQUIRE(resident_blocks(decode_chainx_kernel<NH, P, BF>) >= 1,
+                "decode layer: the chain-8 workgroup does not fit a CU");
+    KA a;
+    fill_ka(h, G, a);
+    HPA_REQUIRE(chainx_shape(h->B, NH, G, a.xt, a.xng) == 0, "decode layer: chain form 8 shape (B <= 64)");
+    decode_chainx_kernel<NH, P, BF><<<G, 768, 0, hpa_stream()>>>(a);
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int NH>
+int dispatchx(const HpaLayerArgs* h, int G) {
+    const bool bf = h->pool->dtype == HPA_BF16;
+    switch (h->pool->page_size) {
+        case 8: return bf ? launchx<NH, 8, true>(h, G) : launchx<NH, 8, false>(h, G);
+        case 16: return bf ? launchx<NH, 16, true>(h, G) : launchx<NH, 16, false>(h, G);
+        case 32: return bf ? launchx<NH, 32, true>(h, G) : launchx<NH, 32, false>(h, G);
+        case 64: return bf ? launchx<NH, 64, true>(h, G) : launchx<NH, 64, false>(h, G);
+        default: return hpa_fail(__FILE__, __LINE__, "decode layer: page size must be 8, 16, 32 or 64");
+    }
 }
 
 // tiles per unit of fc, fcproj, qkv by row blocks R: the fewest with every
@@ -1473,6 +1836,24 @@ int hpa_decode_layer_trace(unsigned long long* host, int layers) {
 #endif
 }
 
+// the chain forms 6 / 7 (C = 768) and 8 (C = 768 or 1600): B <= 64, fp32 or
+// bf16 pool, a unit per workgroup in every phase
+int hpa_decode_chain_eligible(int B, int C, int num_heads, int form) {
+    const int G = num_cus();
+    if (G <= 0 || C != 64 * num_heads || B < 1 || B > 64) return 0;
+    if (form == 6 || form == 7) {
+        if (num_heads != 12) return 0;
+        const int R = (B + 15) / 16;
+        return R * 48 <= G && 4 * R * 48 / (R == 1 ? 1 : R == 2 ? 2 : 3) <= G ? 1 : 0;
+    }
+    if (form == 8) {
+        if (num_heads != 12 && num_heads != 25) return 0;
+        int xt[4], xng[4];
+        return chainx_shape(B, num_heads, G, xt, xng) == 0 ? 1 : 0;
+    }
+    return 0;
+}
+
 int hpa_decode_layer(const HpaLayerArgs* h) {
     HPA_REQUIRE(h && h->pool && h->pool->base, "decode layer: pool");
     const HpaKVPool* pool = h->pool;
@@ -1487,6 +1868,12 @@ int hpa_decode_layer(const HpaLayerArgs* h) {
     HPA_REQUIRE(h->last || (h->w_qkv && h->qkv_c1 && h->qkv_c2 && h->q_out), "decode layer: qkv(l+1) operands");
     HPA_REQUIRE(h->splits >= 1 && h->splits <= HPA_ATTN_MAX_SPLITS, "decode layer: splits 1..16");
     const int G = num_cus();
+    if (h->chain_only >= 6) {
+        HPA_REQUIRE(hpa_decode_chain_eligible(h->B, h->C, h->num_heads, h->chain_only),
+                    "decode layer: chain form not supported for this shape");
+        if (h->chain_only == 8) return h->num_heads == 25 ? dispatchx<25>(h, G) : dispatchx<12>(h, G);
+        return dispatch<12>(h, G);
+    }
     HPA_REQUIRE(hpa_decode_layer_eligible(h->B, h->C, h->num_heads, h->splits), "decode layer: shape not supported");
     if (h->num_heads == 12) return dispatch<12>(h, G);
     return dispatch<2>(h, G);

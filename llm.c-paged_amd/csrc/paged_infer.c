@@ -660,7 +660,8 @@ struct GPT2Decode {
     DecShard* shard;
     /* persistent layer (hpa_decode_layer): one launch per layer */
     int pl_want;      /* gpt2_decode_set_layer_kernel: 0 off, 1 auto, 2 full, 3 chain, 4 chain with wide units,
-                         5 chain form 6 (12-wave multi-tile units), 6 form 6 with granule hand-offs (7) */
+                         5 chain form 6 (12-wave multi-tile units), 6 form 6 with granule hand-offs (7),
+                         7 chain form 8 (streamed-weight units, C = 768 / 1600) */
     int pl_on;        /* in use: 0 five launches, 1 full persistent layer, 2 attention launch + chain,
                          3 attention launch + chain of wide units (hpa_layer.hip NWU = pl_nwu) */
     int pl_wform;     /* wide-unit form of the chain (HpaLayerArgs.chain_only 2..7), else 1 */
@@ -930,11 +931,17 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
         mode = 3; /* chain form 6: 12-wave multi-tile units; 7: the same with granule hand-offs */
         d->pl_wform = d->pl_want == 6 ? 7 : 6;
     }
+    if (d->pl_want == 7) { /* chain form 8: streamed-weight units for MFMA-bound wide layers (C = 768, 1600) */
+        mode = 3;
+        d->pl_wform = 8;
+    }
     int splits = hpa_decode_layer_pick_splits(Bg, c.num_heads, d->max_ctx);
     const char* env = getenv("HPA_LAYER_SPLITS");
     if (env && atoi(env) > 0) splits = atoi(env);
     if (mode >= 2) splits = 1; /* no attention phase: no split records */
-    if (!hpa_decode_layer_eligible(d->B, c.channels, c.num_heads, splits)) return 0;
+    if (d->pl_wform >= 6 ? !hpa_decode_chain_eligible(d->B, c.channels, c.num_heads, d->pl_wform)
+                         : !hpa_decode_layer_eligible(d->B, c.channels, c.num_heads, splits))
+        return 0;
     size_t sz[3];
     if (hpa_decode_layer_sizes(d->B, c.channels, c.num_heads, splits, sz)) return 1;
     if (!d->pl_rec || d->pl_splits != splits) { /* records depend on the split count */
@@ -1184,7 +1191,7 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
     }
     {
         const char* env = getenv("HPA_LAYER_KERNEL");
-        d->pl_want = env && env[0] >= '0' && env[0] <= '6' ? env[0] - '0' : 1;
+        d->pl_want = env && env[0] >= '0' && env[0] <= '7' ? env[0] - '0' : 1;
     }
     if (dec_layer_setup(model, d)) {
         dec_free(d);
@@ -1780,7 +1787,7 @@ int gpt2_decode_set_layer_kernel(GPT2* model, int enable) {
     GPT2Decode* d = model->decode;
     if (!d) return 1;
     if (hpa_synchronize()) return 1;
-    d->pl_want = enable < 0 ? 0 : enable > 6 ? 6 : enable;
+    d->pl_want = enable < 0 ? 0 : enable > 7 ? 7 : enable;
     if (dec_layer_setup(model, d)) return 1;
     if (d->graph) { /* recapture with the other step */
         hpa_graph_destroy(d->graph);

@@ -265,3 +265,66 @@ def test_chain6_rows_independent_of_batch_and_form4(hip):
         assert np.isfinite(g64).all()
     finally:
         hip.check(hip.lib().hpa_set_attention_waves(0), "waves")
+
+
+@pytest.mark.parametrize("B", [64, 40, 8])
+def test_chain8_equals_chain6_124m(hip, B):
+    """chain form 8 (streamed weights, host-picked tiles per unit) at GPT-2 124M
+    shapes picks the same units as form 6 and sums in the same order: every
+    layer's output and every logit bit-identical"""
+    params = synth.params(GPT2_124M, seed=95)
+    steps = 3
+    toks = np.random.default_rng(95).integers(0, GPT2_124M["V"], (steps, B)).astype(np.int32)
+
+    def run(mode, traced):
+        m = _model(hip, GPT2_124M, params, B, 16, 1, mode=mode)
+        assert m.layer_form() == 3
+        m.set_graph(not traced)
+        m.fill_random(500, seed=12)
+        out = []
+        for t in range(steps):
+            if traced:
+                out.append(m.step_traced(toks[t])[1])
+            else:
+                m.step(toks[t])
+                out.append(m.logits())
+        m.status()
+        m.close()
+        return np.stack(out)
+
+    assert np.array_equal(run(7, True), run(5, True))
+    assert np.array_equal(run(7, False), run(5, False))
+
+
+GPT2_XL = dict(maxT=1024, V=50257, L=48, NH=25, C=1600)
+
+
+@pytest.mark.parametrize("B", [64, 33, 5])
+def test_chain8_xl_matches_launch_path(hip, B):
+    """GPT-2 XL (C = 1600, 48 layers) on chain form 8 against the five-launch
+    layer (ring / looped GEMMs): logits within fp32 reassociation, ids equal
+    outside near-ties, status 0"""
+    params = hip.synthetic_params(GPT2_XL, seed=96)
+    ctx, steps = 200, 3
+    toks = np.random.default_rng(96).integers(0, GPT2_XL["V"], (steps, B)).astype(np.int32)
+    out = []
+    for mode in (7, 0):
+        m = hip.Model(GPT2_XL, params=params)
+        m.decode_init(B, 32, ctx + 8)
+        assert m.set_layer_kernel(mode) == (mode != 0)
+        m.set_graph(True)
+        m.fill_random(ctx, seed=13)
+        lg, ids = [], []
+        for t in range(steps):
+            ids.append(m.step(toks[t]))
+            lg.append(m.logits())
+        m.status()
+        m.close()
+        out.append((np.stack(lg), np.stack(ids)))
+    (l8, i8), (l0, i0) = out
+    diff = float(np.abs(l8 - l0).max())
+    s = np.sort(l0, axis=-1)
+    clear = (s[..., -1] - s[..., -2]) > 4 * diff
+    print(f"XL B={B}: max |logit diff| form 8 vs launches {diff:.3e}; near-ties {int((~clear).sum())}")
+    assert diff <= 5e-5, diff
+    assert np.array_equal(i8[clear], i0[clear])
