@@ -481,6 +481,10 @@ int    hpa_comm_allreduce_max(double* value);
  * calls above.  Exclusive with hpa_comm_init. */
 int    hpa_comm_init_all(int ndev, const int* devs);
 int    hpa_comm_use(int index);
+/* ncclGroupStart / ncclGroupEnd around the collectives posted between them
+ * (the single-process form: every device's gather from one thread) */
+int    hpa_comm_group_start(void);
+int    hpa_comm_group_end(void);
 
 /* ---------------- reference-layout kernels (drop-in compat) ----------------
  * Pages in the reference layout: token-major [block_size][C] per page

@@ -286,6 +286,9 @@ int    gpt2_decode_set_global_batch(GPT2* model, int total);
 int    gpt2_decode_global_batch(GPT2* model);
 int    gpt2_decode_shard(GPT2* model, const int* rows_per_rank, int root);
 int    gpt2_decode_gather(GPT2* model, int what);
+/* the single-process form (hpa_comm_init_all): models[i] on device i, every
+ * gather posted inside one NCCL group */
+int    gpt2_decode_gather_all(GPT2** models, int n, int what);
 int    gpt2_decode_gather_wait(GPT2* model);
 void*  gpt2_decode_gathered(GPT2* model, int what);
 void   gpt2_decode_free(GPT2* model);

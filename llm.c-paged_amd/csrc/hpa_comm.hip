@@ -169,6 +169,19 @@ int hpa_comm_init_all(int ndev, const int* devs) {
     return hpa_comm_use(0);
 }
 
+// an NCCL group around the calls between them (the single-process form: one
+// thread posting every device's gather, which RCCL needs grouped or it
+// blocks on the first device's send)
+int hpa_comm_group_start(void) {
+    HPA_NCCL(ncclGroupStart());
+    return 0;
+}
+
+int hpa_comm_group_end(void) {
+    HPA_NCCL(ncclGroupEnd());
+    return 0;
+}
+
 int hpa_comm_use(int index) {
     HPA_REQUIRE(g_all && index >= 0 && index < g_all_n, "comm_use: hpa_comm_init_all first / index");
     if (hpa_get_device() != g_all_dev[index]) HPA_REQUIRE(hpa_init(g_all_dev[index]) == 0, "comm_use: device");

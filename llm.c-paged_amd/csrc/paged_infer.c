@@ -2174,6 +2174,26 @@ int gpt2_decode_gather(GPT2* model, int what) {
     return rc;
 }
 
+/* the single-process form (hpa_comm_init_all): one thread
+ * drives the engines of n devices; models[i] runs on device i of the
+ * communicator set.  Every engine's gather is posted inside ONE NCCL group
+ * (an ungrouped ncclSend to the root would block the thread before the other
+ * devices' calls are posted); the current device returns to index 0. */
+int gpt2_decode_gather_all(GPT2** models, int n, int what) {
+    if (!models || n < 1 || n != hpa_comm_size()) {
+        fprintf(stderr, "[paged_infer] gpt2_decode_gather_all: one engine per device of hpa_comm_init_all\n");
+        return 1;
+    }
+    int rc = hpa_comm_group_start();
+    for (int i = 0; i < n && !rc; i++) {
+        rc |= hpa_comm_use(i);
+        rc |= gpt2_decode_gather(models[i], what);
+    }
+    rc |= hpa_comm_group_end();
+    rc |= hpa_comm_use(0);
+    return rc;
+}
+
 /* host waits for the last gather */
 int gpt2_decode_gather_wait(GPT2* model) {
     GPT2Decode* d = model->decode;

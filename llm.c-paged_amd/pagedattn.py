@@ -250,6 +250,9 @@ def lib():
     _sig(L, "gpt2_decode_batch", i, [v])
     _sig(L, "gpt2_decode_shard", i, [v, _I, i])
     _sig(L, "gpt2_decode_gather", i, [v, i])
+    _sig(L, "gpt2_decode_gather_all", i, [ctypes.POINTER(v), i, i])
+    _sig(L, "hpa_comm_group_start", i, [])
+    _sig(L, "hpa_comm_group_end", i, [])
     _sig(L, "gpt2_decode_gather_wait", i, [v])
     _sig(L, "gpt2_decode_gathered", v, [v, i])
     _sig(L, "gpt2_decode_profile", i, [v, i])

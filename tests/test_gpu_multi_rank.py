@@ -169,6 +169,12 @@ def test_rccl_single_process_init_all_barrier_and_max(hip):
             nxt = m.step(toks[t])
             m.gather(1)
             assert np.array_equal(m.gathered(B, 1), nxt)
+        # the grouped form one thread uses for every device's engine
+        handles = (ctypes.c_void_p * 1)(m.h)
+        for t in range(3, 5):
+            nxt = m.step(toks[t])
+            hip.check(L.gpt2_decode_gather_all(handles, 1, 1), "gather_all")
+            assert np.array_equal(m.gathered(B, 1), nxt)
         m.close()
     finally:
         hip.check(L.hpa_comm_destroy(), "comm destroy")
