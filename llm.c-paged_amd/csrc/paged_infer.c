@@ -910,30 +910,30 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
     if (!d->pl_want || d->w_bf16 || !d->d_fold) return 0;
     const int Bg = dec_pick_B(d); /* the batch the picks follow */
     if (Bg > 64) return 0;
-    /* auto (1): the form measured fastest (profiles/r3/pl_ab.txt): the
-     * attention's own launch + the persistent chain, at every batch it
-     * supports (B 64 / 32 / 16 / 8: -2.3 / -0.9 / -4.9 / -4.0 % per step
-     * against five launches; the full persistent layer -0.1 / +0.2 / -2.3 /
-     * -1.7 %) */
-    /* the chain's wide units where a phase has fewer units than 4-wave slots
-     * (C = 768), by the global batch's row blocks Rg: attproj always 12
-     * waves per unit, fc / fcproj and qkv 12 at Rg = 1, 6 at Rg = 2, qkv 6 at
-     * Rg = 3 (hpa_layer.hip); auto and form 4.  HPA_PL_WIDE=0 turns the auto
-     * pick off, =12 keeps it to Rg = 1 */
-    const char* wenv = getenv("HPA_PL_WIDE");
+    /* the loop's form (gpt2_decode_set_layer_kernel).  1 = auto, the form
+     * measured fastest (round 4, profiles/r4/forms.txt): chain form 6 at C =
+     * 768 (B = 64 / 8: 1.1106 / 0.4334 ms per step against the round-3 wide
+     * units' 1.1476 / 0.4510), chain form 8 at C >= 1024 (GPT-2 XL: 9.91 vs
+     * 10.29 ms for five launches), else the chain of 4-wave units.
+     * mode: 1 the full persistent layer, 2 the attention launch + the chain
+     * of 4-wave units, 3 the attention launch + the chain form pl_wform */
     const int Rg = (Bg + 15) / 16;
-    const int wide_ok = c.num_heads == 12 && Rg >= 1 && Rg <= 4 &&
-                        !(d->pl_want == 1 && wenv && wenv[0] == '1' && wenv[1] == '2' && Rg > 1);
-    const int want_wide = d->pl_want == 4 || (d->pl_want == 1 && !(wenv && wenv[0] == '0'));
-    int mode = d->pl_want == 2 ? 1 : want_wide && wide_ok ? 3 : 2;
-    d->pl_wform = mode == 3 ? 1 + Rg : 1;
-    if ((d->pl_want == 5 || d->pl_want == 6) && c.num_heads == 12 && Rg >= 1 && Rg <= 4) {
-        mode = 3; /* chain form 6: 12-wave multi-tile units; 7: the same with granule hand-offs */
-        d->pl_wform = d->pl_want == 6 ? 7 : 6;
-    }
-    if (d->pl_want == 7) { /* chain form 8: streamed-weight units for MFMA-bound wide layers (C = 768, 1600) */
-        mode = 3;
-        d->pl_wform = 8;
+    int mode = 2;
+    d->pl_wform = 1;
+    switch (d->pl_want) {
+        case 2: mode = 1; break;
+        case 3: break;
+        case 4: /* round 3's wide units, widths by row blocks: chain_only 2..5 */
+            if (c.num_heads == 12) { mode = 3; d->pl_wform = 1 + Rg; }
+            break;
+        case 5: case 6: /* form 6 (12-wave multi-tile units); 7: with granule hand-offs */
+            if (c.num_heads == 12) { mode = 3; d->pl_wform = d->pl_want == 6 ? 7 : 6; }
+            break;
+        case 7: mode = 3; d->pl_wform = 8; break; /* form 8: streamed-weight units (C = 768, 1600) */
+        default: /* auto */
+            if (c.num_heads == 12) { mode = 3; d->pl_wform = 6; }
+            else if (c.channels >= 1024) { mode = 3; d->pl_wform = 8; }
+            break;
     }
     int splits = hpa_decode_layer_pick_splits(Bg, c.num_heads, d->max_ctx);
     const char* env = getenv("HPA_LAYER_SPLITS");
