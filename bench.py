@@ -139,12 +139,12 @@ def parse():
     ap.add_argument("--attn-waves", type=int, default=0,
                     help="waves per attention workgroup for every launch (0 = the engine's pick by batch)")
     ap.add_argument("--attn-splits", type=int, default=0, help="attention context ranges (0 = by shape)")
-    ap.add_argument("--layer-kernel", type=int, default=-1, choices=[-1, 0, 1, 2, 3, 4, 5, 6, 7],
+    ap.add_argument("--layer-kernel", type=int, default=-1, choices=[-1, 0, 1, 2, 3, 4, 5, 6],
                     help="gpt2_decode_set_layer_kernel: 0 five launches per layer; 1 auto (the form measured "
                          "fastest for the batch: the attention launch + the persistent chain with wide units); "
                          "2 the full persistent layer (attention inside); 3 the attention launch + the chain "
                          "(4-wave units); 4 the chain with wide units; 5 chain form 6 (12-wave multi-tile units); "
-                         "6 form 6 with granule hand-offs; 7 chain form 8 (streamed weights, also GPT-2 XL); "
+                         "6 chain form 8 (streamed weights, also GPT-2 XL); "
                          "-1 the engine's default "
                          "(HPA_LAYER_KERNEL or 1)")
     ap.add_argument("--picks", default="local", choices=["local", "global"],

@@ -332,8 +332,7 @@ typedef struct {
                                      in units of all 12 waves of a workgroup holding T 16-column
                                      tiles (T by batch, one unit per workgroup, the 12-wave
                                      summation order at every B <= 64), 16-byte epilogues,
-                                     waits per row block (C = 768); 7: form 6 with granule
-                                     hand-offs (res2g .. epoch below); 8: the chain for
+                                     waits per row block (C = 768); 8: the chain for
                                      MFMA-bound wide layers (C = 768 or 1600, GPT-2 XL): units of
                                      12 waves x up to 7 tiles, weights streamed per tile */
     const HpaKVPool* pool;
@@ -366,13 +365,6 @@ typedef struct {
                                      out at once when it is set) */
     int* err_sticky;              /* nullable: the first code also lands here, never zeroed by a
                                      step (gpt2_decode_status reads and clears it) */
-    /* chain_only 7 (form 6 with granule hand-offs): tagged {value, tag}
-     * 8-byte granules of res2 [Mp][C], fch [Mp][4C], res [Mp][C] and of
-     * fcproj's K-part partials [4][R][C/16][256] (zeroed once at
-     * allocation); epoch: the step counter hpa_embed_frag_step advances,
-     * tag = epoch << 6 | layer */
-    unsigned *res2g, *fchg, *resg, *slabg;
-    const unsigned* epoch;
 } HpaLayerArgs;
 /* 1 if the persistent layer applies (shape, CU count, residency), else 0 */
 int hpa_decode_layer_eligible(int B, int C, int num_heads, int splits);
@@ -399,11 +391,6 @@ int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const fl
  * decode step's hand-off counters without a memset node of their own */
 int hpa_embed_frag_zero(const int* tokens, const int* pos, const float* wte, const float* wpe,
                         float* res_frag, float* stats, int B, int C, void* zero, size_t zero_bytes);
-/* hpa_embed_frag_zero that also advances the step counter *epoch by one
- * (chain form 7's granule tags) */
-int hpa_embed_frag_step(const int* tokens, const int* pos, const float* wte, const float* wpe,
-                        float* res_frag, float* stats, int B, int C, void* zero, size_t zero_bytes,
-                        unsigned* epoch);
 /* greedy id from the logits GEMM's per-tile (max, argmax) partials:
  * lowest index wins ties; next[b], tokens[b] = next[b], pos[b] += 1.
  * active (nullable, [B]): rows with active[b] <= 0 are left untouched */

@@ -213,18 +213,18 @@ int  gpt2_decode_attn_waves(GPT2* model);
  * GEMM chain (attproj -> fc -> fcproj -> next qkv) in 4-wave units; 4 the
  * chain in round 3's wide units (C = 768); 5 chain form 6: every phase in
  * 12-wave units of T tiles, one per workgroup, 16-byte epilogues, waits per
- * row block (C = 768); 6 form 6 with tagged-granule hand-offs; 7 chain form 8:
- * streamed-weight units for MFMA-bound wide layers (C = 768 / 1600, GPT-2
- * XL); 1 (default, "auto") the form measured fastest (profiles/r4: 5 at C =
- * 768, 7 at C >= 1024, else 3).  The persistent forms need fp32 weights and
- * B <= 64 (else five launches).  HPA_LAYER_KERNEL=0..7 in the environment
+ * row block (C = 768); 6 chain form 8: streamed-weight units for MFMA-bound
+ * wide layers (C = 768 / 1600, GPT-2 XL); 1 (default, "auto") the form
+ * measured fastest (profiles/r4: 5 at C = 768, 6 at C >= 1024, else 3).
+ * The persistent forms need fp32 weights and B <= 64 (else five launches).
+ * HPA_LAYER_KERNEL=0..6 in the environment
  * sets the default.  A persistent launch needs every CU for its 12-wave
  * workgroups: a GPU shared with another process's persistent kernels should
  * use 0. */
 int  gpt2_decode_set_layer_kernel(GPT2* model, int enable);
 /* the form in use: 0 five launches, 1 full persistent layer, 2 attention
  * launch + persistent chain of 4-wave units, 3 the chain in wide / multi-tile
- * units (forms 4..7 of gpt2_decode_set_layer_kernel) */
+ * units (forms 4..6 of gpt2_decode_set_layer_kernel) */
 int  gpt2_decode_layer_kernel(GPT2* model);
 /* waits for the queued work; 0, or the code of a timed-out in-launch wait of
  * the persistent layer (the step's outputs are then invalid), which it clears */

@@ -99,11 +99,9 @@ __global__ __launch_bounds__(256) void embed_frag_kernel(const int* __restrict__
                                                          const float* __restrict__ wte,
                                                          const float* __restrict__ wpe,
                                                          float* __restrict__ res, float* __restrict__ stats,
-                                                         int C, int4* __restrict__ zero, int zero_n4,
-                                                         unsigned* __restrict__ epoch) {
+                                                         int C, int4* __restrict__ zero, int zero_n4) {
     __shared__ float sc[8];
     const int b = blockIdx.x;
-    if (epoch && b == 0 && threadIdx.x == 0) epoch[0] += 1u;  // the step counter (granule tags of chain form 7)
     // the step's counter block (persistent layer hand-offs), zeroed here
     // instead of by a memset node of its own
     for (int i = b * 256 + threadIdx.x; i < zero_n4; i += gridDim.x * 256) zero[i] = make_int4(0, 0, 0, 0);
@@ -895,7 +893,7 @@ int hpa_logits_partials(const HpaFusedGemm* g) {
 int hpa_embed_frag(const int* tokens, const int* pos, const float* wte, const float* wpe,
                    float* res_frag, float* stats, int B, int C) {
     HPA_REQUIRE(B > 0 && C > 0 && C % 16 == 0, "embed_frag: bad shape");
-    embed_frag_kernel<<<B, 256, 0, hpa_stream()>>>(tokens, pos, wte, wpe, res_frag, stats, C, nullptr, 0, nullptr);
+    embed_frag_kernel<<<B, 256, 0, hpa_stream()>>>(tokens, pos, wte, wpe, res_frag, stats, C, nullptr, 0);
     HPA_LAUNCH_CHECK();
     return 0;
 }
@@ -906,18 +904,7 @@ int hpa_embed_frag_zero(const int* tokens, const int* pos, const float* wte, con
     HPA_REQUIRE(zero_bytes % 16 == 0 && zero_bytes / 16 <= 0x7fffffff && ((size_t)zero & 15) == 0,
                 "embed_frag_zero: the zeroed block must be whole 16-byte granules");
     embed_frag_kernel<<<B, 256, 0, hpa_stream()>>>(tokens, pos, wte, wpe, res_frag, stats, C,
-                                                   reinterpret_cast<int4*>(zero), (int)(zero_bytes / 16), nullptr);
-    HPA_LAUNCH_CHECK();
-    return 0;
-}
-
-int hpa_embed_frag_step(const int* tokens, const int* pos, const float* wte, const float* wpe, float* res_frag,
-                        float* stats, int B, int C, void* zero, size_t zero_bytes, unsigned* epoch) {
-    HPA_REQUIRE(B > 0 && C > 0 && C % 16 == 0 && epoch, "embed_frag_step: bad shape or no epoch");
-    HPA_REQUIRE(zero_bytes % 16 == 0 && zero_bytes / 16 <= 0x7fffffff && ((size_t)zero & 15) == 0,
-                "embed_frag_step: the zeroed block must be whole 16-byte granules");
-    embed_frag_kernel<<<B, 256, 0, hpa_stream()>>>(tokens, pos, wte, wpe, res_frag, stats, C,
-                                                   reinterpret_cast<int4*>(zero), (int)(zero_bytes / 16), epoch);
+                                                   reinterpret_cast<int4*>(zero), (int)(zero_bytes / 16));
     HPA_LAUNCH_CHECK();
     return 0;
 }

@@ -94,10 +94,6 @@ struct KA {
     int* ctr;
     int* err;
     int* err_sticky;
-    // chain form 6 with granule hand-offs: {value, tag} 8-byte granules of
-    // res2 / fch / res / fcproj's K-part partials, tagged per (step, layer)
-    unsigned *res2g, *fchg, *resg, *slabg;
-    const unsigned* epoch;
     // chain form 8 (wide layers, GPT-2 XL): tiles per unit and tile groups
     // (padded to a multiple of 8) of attproj, fc, fcproj, qkv
     int xt[4], xng[4];
@@ -873,101 +869,10 @@ __device__ __forceinline__ void publish6(const KA& a, int ctr, bool did) {
     if (threadIdx.x == 0 && did) arrive6(a, ctr, 1);
 }
 
-// ---- granule hand-offs (GR): every handed-over float travels with a 4-byte
-// tag in one 8-byte granule, (value, tag) of 4 consecutive frag-layout
-// floats = 32 B = two 16-byte sc1 stores (MI355X_MICROARCH.md "handoff-1to1":
-// a granule is observed untorn, no ordering needed).  The producer therefore
-// neither drains its stores before it counts itself in nor fences: the
-// counter only says "probably there", and the consumer re-loads any granule
-// whose tag is not this (step, layer)'s until all are.
-__device__ __forceinline__ void store_g4(unsigned* base, int fidx, float4 v, unsigned tag) {
-    const float t = __uint_as_float(tag);
-    hpa::store_wt16(base, fidx * 8, make_float4(v.x, t, v.y, t));
-    hpa::store_wt16(base, fidx * 8 + 16, make_float4(v.z, t, v.w, t));
-}
-__device__ __forceinline__ bool load_g4(const unsigned* base, int fidx, unsigned tag, float4& v) {
-    const float4 lo = hpa::load_wt16(base, fidx * 8), hi = hpa::load_wt16(base, fidx * 8 + 16);
-    v = make_float4(lo.x, lo.z, hi.x, hi.z);
-    const unsigned bad = (__float_as_uint(lo.y) ^ tag) | (__float_as_uint(lo.w) ^ tag) | (__float_as_uint(hi.y) ^ tag) |
-                         (__float_as_uint(hi.w) ^ tag);
-    return bad == 0;
-}
-// N granule-quads per lane (frag float indices fidx), re-loaded until every
-// lane of the wave holds this tag's values (bounded as wait6: false on a
-// timeout or when another workgroup gave up).  active = false: nothing to load.
-template <int N>
-__device__ __forceinline__ bool poll_g4(const KA& a, const unsigned* base, const int (&fidx)[N], unsigned tag,
-                                        float4 (&v)[N], bool active, int code) {
-    bool ok[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) ok[i] = active ? load_g4(base, fidx[i], tag, v[i]) : true;
-    bool mine = true;
-#pragma unroll
-    for (int i = 0; i < N; ++i) mine = mine && ok[i];
-    if (!__any(!mine)) return true;
-    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    for (unsigned it = 0;; ++it) {
-        __builtin_amdgcn_s_sleep(1);
-        asm volatile("" ::: "memory");  // the re-loads below are new loads
-#pragma unroll
-        for (int i = 0; i < N; ++i)
-            if (!ok[i]) ok[i] = load_g4(base, fidx[i], tag, v[i]);
-        mine = true;
-#pragma unroll
-        for (int i = 0; i < N; ++i) mine = mine && ok[i];
-        if (!__any(!mine)) return true;
-        if ((it & 7) == 7) {
-            const int e = __builtin_amdgcn_readfirstlane(__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            if (e) return false;
-            if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
-                if ((threadIdx.x & 63) == 0) {
-                    atomicCAS(a.err, 0, code);
-                    if (a.err_sticky) atomicCAS(a.err_sticky, 0, code);
-                }
-                return false;
-            }
-        }
-    }
-}
-
-// GR mfma_t: the wave's 4 A fragments as granules (polled), then the chains
-template <int T, bool STATS>
-__device__ __forceinline__ bool mfma_tg(const KA& a, const unsigned* Ag, int K16A, int rb, int kb, int w, unsigned tag,
-                                        const float4 (&wr)[T][SPW], f32x4 (&acc)[T], float& fs1, float& fs2, int code) {
-    float4 xv[SPW];
-    int fidx[SPW];
-#pragma unroll
-    for (int s = 0; s < SPW; ++s) fidx[s] = ((rb * K16A + kb + w * SPW + s) * 64 + (int)(threadIdx.x & 63)) * 4;
-    if (!poll_g4<SPW>(a, Ag, fidx, tag, xv, true, code)) return false;
-#pragma unroll
-    for (int t = 0; t < T; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < SPW; ++s)
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s].x, wr[t][s].x, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s].y, wr[t][s].y, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s].z, wr[t][s].z, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s].w, wr[t][s].w, acc[t], 0, 0, 0);
-        }
-    if (STATS)
-#pragma unroll
-        for (int s = 0; s < SPW; ++s) hpa_gemm::row_sums_add(xv[s], fs1, fs2);
-    return true;
-}
-
-// no drain: the barrier orders every wave's store issue before the count
-__device__ __forceinline__ void publish6g(const KA& a, int ctr, bool did) {
-    lds_barrier();
-    if (threadIdx.x == 0 && did) arrive6(a, ctr, 1);
-}
 }  // namespace c6
 
-// TC, TD, TE: tiles per unit of fc, fcproj, qkv (NH = 12; attproj 1).  GR:
-// granule hand-offs (chain_only 7): res2 / fch / res and fcproj's K-part
-// partials travel as tagged granules, producers never drain, part 0 of
-// fcproj combines the parts (polled) instead of a ticket's last arriver
-template <int P, bool BF, int TC, int TD, int TE, bool GR>
+// TC, TD, TE: tiles per unit of fc, fcproj, qkv (NH = 12; attproj 1)
+template <int P, bool BF, int TC, int TD, int TE>
 __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
     using namespace c6;
     constexpr int NH = 12, C = 768, K16 = 48, NCT = 48;
@@ -982,7 +887,6 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
     // epilogue thread's place: tile et, row er, column quad eq
     const int et = tid >> 6, er = (tid & 63) >> 2, eq = tid & 3;
     int* tick = a.ctr + kCtr;  // fcproj K-part tickets [R][NCT / TD]
-    const unsigned tag = GR ? (a.epoch[0] << 6) | (unsigned)a.layer : 0u;  // this (step, layer)'s granules
     PL_STAMP(t_start);
     PL_STORE(0, t_start);
     float fs1 = 0.f, fs2 = 0.f;
@@ -1014,16 +918,10 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
             const bool live = row < a.B;  // residual_forward(out, res, proj); padded rows stay 0
             v = live ? make_float4(rv.x + v.x, rv.y + v.y, rv.z + v.z, rv.w + v.w) : make_float4(0.f, 0.f, 0.f, 0.f);
-            if constexpr (GR)
-                store_g4(a.res2g, fx, v, tag);
-            else
-                hpa::store_wt16(a.res2, fi, v);
+            hpa::store_wt16(a.res2, fi, v);
         }
         PL_MARK(12);
-        if constexpr (GR)
-            publish6g(a, X1 + rb, has);
-        else
-            publish6(a, X1 + rb, has);
+        publish6(a, X1 + rb, has);
     }
     PL_MARK(5);
     // C: fc(l): fch = gelu(LN2(res2) . Wfc^T + b), LN folded; T = TC tiles
@@ -1046,10 +944,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         fs1 = fs2 = 0.f;
         if (has) {
             f32x4 acc[T];
-            if constexpr (GR)
-                mfma_tg<T, true>(a, a.res2g, K16, rb, 0, w, tag, wr, acc, fs1, fs2, 2);  // a timeout sets err
-            else
-                mfma_t<T, true>(a.res2, K16, rb, 0, w, wr, acc, fs1, fs2);
+            mfma_t<T, true>(a.res2, K16, rb, 0, w, wr, acc, fs1, fs2);
             put_red_t<T>(sm.red, w, acc);
         }
         hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + w * 32);
@@ -1059,17 +954,10 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             const bool live = row < a.B;
             v = live ? make_float4(hpa::gelu_ref(v.x), hpa::gelu_ref(v.y), hpa::gelu_ref(v.z), hpa::gelu_ref(v.w))
                      : make_float4(0.f, 0.f, 0.f, 0.f);
-            const int hx = (int)hpa::frag_index(row, col, 4 * C);
-            if constexpr (GR)
-                store_g4(a.fchg, hx, v, tag);
-            else
-                hpa::store_wt16(a.fch, hx * 4, v);
+            hpa::store_wt16(a.fch, (int)(hpa::frag_index(row, col, 4 * C) * 4), v);
         }
         PL_MARK(13);
-        if constexpr (GR)
-            publish6g(a, H + rb * 4 + (g * T) / NCT, has);
-        else
-            publish6(a, H + rb * 4 + (g * T) / NCT, has);  // the K part of fcproj these columns feed
+        publish6(a, H + rb * 4 + (g * T) / NCT, has);  // the K part of fcproj these columns feed
         PL_MARK(7);
     }
     // D: fcproj(l), K part p of 4, T = TD tiles: partial tiles -> slab; the
@@ -1089,59 +977,32 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         PL_MARK(8);
         if (has) {
             f32x4 acc[T];
-            if constexpr (GR)
-                mfma_tg<T, false>(a, a.fchg, 4 * K16, rb, p * K16, w, tag, wr, acc, fs1, fs2, 3);
-            else
-                mfma_t<T, false>(a.fch, 4 * K16, rb, p * K16, w, wr, acc, fs1, fs2);
+            mfma_t<T, false>(a.fch, 4 * K16, rb, p * K16, w, wr, acc, fs1, fs2);
             put_red_t<T>(sm.red, w, acc);
         }
         lds_barrier();
         float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
         const int sx = (((p * R + rb) * NG + g) * T * 64 + tid) * 4;  // this part's float4 in the slab (float index)
-        bool last;
-        if constexpr (GR) {  // parts 1..3 publish granules; part 0 polls them and combines
-            if (ep) val = fold_t<T>(sm.red, et, er, eq);
-            if (ep && p != 0) store_g4(a.slabg, sx, val, tag);
-            PL_MARK(14);
-            last = has && p == 0;
-        } else {
-            if (ep) {
-                val = fold_t<T>(sm.red, et, er, eq);
-                hpa::store_wt16(a.slab_fp, sx * 4, val);
-            }
-            PL_MARK(14);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            lds_barrier();
-            if (has && tid == 0) {
-                const int tk = __hip_atomic_fetch_add(tick + rb * NG + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                sm.s_last = tk == 3;
-            }
-            lds_barrier();
-            last = has && sm.s_last != 0;
+        if (ep) {
+            val = fold_t<T>(sm.red, et, er, eq);
+            hpa::store_wt16(a.slab_fp, sx * 4, val);
         }
+        PL_MARK(14);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        if (has && tid == 0) {
+            const int tk = __hip_atomic_fetch_add(tick + rb * NG + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sm.s_last = tk == 3;
+        }
+        lds_barrier();
+        const bool last = has && sm.s_last != 0;
         if (last && ep) {
             float4 pv[4];
             const int fx = (int)hpa::frag_index(row, col, C), fi = fx * 4;
-            float4 rv;
-            if constexpr (GR) {
-                int px[3];
-                float4 pq[3];
 #pragma unroll
-                for (int qq = 0; qq < 3; ++qq) px[qq] = ((((qq + 1) * R + rb) * NG + g) * T * 64 + tid) * 4;
-                poll_g4<3>(a, a.slabg, px, tag, pq, true, 3);
-                int rx[1] = {fx};
-                float4 rq[1];
-                poll_g4<1>(a, a.res2g, rx, tag, rq, true, 3);
-                rv = rq[0];
-                pv[0] = val;
-#pragma unroll
-                for (int qq = 1; qq < 4; ++qq) pv[qq] = pq[qq - 1];
-            } else {
-#pragma unroll
-                for (int qq = 0; qq < 4; ++qq)
-                    pv[qq] = qq == p ? val : hpa::load_wt16(a.slab_fp, ((((qq * R + rb) * NG + g) * T * 64 + tid) * 4) * 4);
-                rv = hpa::load_wt16(a.res2, fi);
-            }
+            for (int qq = 0; qq < 4; ++qq)
+                pv[qq] = qq == p ? val : hpa::load_wt16(a.slab_fp, ((((qq * R + rb) * NG + g) * T * 64 + tid) * 4) * 4);
+            const float4 rv = hpa::load_wt16(a.res2, fi);
             float4 tot = pv[0];
 #pragma unroll
             for (int qq = 1; qq < 4; ++qq) {
@@ -1151,14 +1012,13 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             const bool live = row < a.B;
             tot = live ? make_float4(rv.x + tot.x, rv.y + tot.y, rv.z + tot.z, rv.w + tot.w)
                        : make_float4(0.f, 0.f, 0.f, 0.f);
-            hpa::store_wt16(a.res, fi, tot);  // later launches (next attproj's residual, logits) read it plain
-            if constexpr (GR) store_g4(a.resg, fx, tot, tag);
+            hpa::store_wt16(a.res, fi, tot);
             if (a.stats_out) {
                 float* tr = sm.tile + (et * 16 + er) * 17 + 4 * eq;
                 tr[0] = tot.x; tr[1] = tot.y; tr[2] = tot.z; tr[3] = tot.w;
             }
         }
-        if constexpr (!GR) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
         if (a.stats_out && last && tid < T * 16) {  // 16-column LNf partial sums of the tiles' rows
             const int t = tid >> 4, r = tid & 15;
@@ -1196,10 +1056,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         fs1 = fs2 = 0.f;
         if (has) {
             f32x4 acc[T];
-            if constexpr (GR)
-                mfma_tg<T, true>(a, a.resg, K16, rb, 0, w, tag, wr, acc, fs1, fs2, 4);
-            else
-                mfma_t<T, true>(a.res, K16, rb, 0, w, wr, acc, fs1, fs2);
+            mfma_t<T, true>(a.res, K16, rb, 0, w, wr, acc, fs1, fs2);
             put_red_t<T>(sm.red, w, acc);
         }
         hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + w * 32);
@@ -1290,12 +1147,59 @@ struct SmemX {
 };
 
 // the unit body up to the LDS fold: A (its K range of row block rb, sc1),
-// row sums (STATS), the nt tiles j0.. streamed double-buffered (wr0 holds
-// tile 0, loaded before the caller's wait), accumulators -> red[w][t]
+// row sums (STATS), then the nt tiles j0.. streamed in half-tiles (HS k16
+// steps of the wave's range) through four register sets rotating by name,
+// three half-tiles ahead (wr01 holds tile 0, loaded before the caller's
+// wait); accumulators -> red[w][t].  One whole tile ahead left the XL fc
+// phase at 19 us for 11.7 us of MFMA issue (profiles/r4/traces): a tile's
+// 100 KB per CU did not land within one tile's MFMAs; two whole tiles ahead
+// need 168 VGPRs + spills.
+template <int MAXS>
+struct HalfT {
+    static constexpr int HS = (MAXS + 1) / 2;
+};
+
+template <int MAXS>
+__device__ __forceinline__ void ld_half(const float* W, int K16W, int j, int kb, int s0, int ns, int h, bool nt,
+                                        float4 (&wr)[HalfT<MAXS>::HS]) {
+    constexpr int HS = HalfT<MAXS>::HS;
+    const float4* wf = reinterpret_cast<const float4*>(W) + ((size_t)j * K16W + kb + s0 + h * HS) * 64 + (threadIdx.x & 63);
+#pragma unroll
+    for (int s = 0; s < HS; ++s)
+        if (h * HS + s < ns) wr[s] = nt ? ld_nt(wf + (size_t)s * 64) : wf[(size_t)s * 64];
+}
+
+template <int MAXS>
+__device__ __forceinline__ void chain_half(const float4 (&xv)[MAXS], const float4 (&wr)[HalfT<MAXS>::HS], int ns, int h,
+                                           f32x4& acc) {
+    constexpr int HS = HalfT<MAXS>::HS;
+#pragma unroll
+    for (int s = 0; s < HS; ++s)
+        if (h * HS + s < ns) {
+            const float4 x = xv[h * HS + s];
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, wr[s].x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, wr[s].y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, wr[s].z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, wr[s].w, acc, 0, 0, 0);
+        }
+}
+
+template <int MAXS>
+struct Tile0 {  // tile 0's two halves, loaded before the caller's wait
+    float4 h0[HalfT<MAXS>::HS], h1[HalfT<MAXS>::HS];
+};
+
+template <int MAXS>
+__device__ __forceinline__ void ld_tile0(const float* W, int K16W, int j, int kb, int s0, int ns, bool nt, Tile0<MAXS>& t0) {
+    ld_half<MAXS>(W, K16W, j, kb, s0, ns, 0, nt, t0.h0);
+    ld_half<MAXS>(W, K16W, j, kb, s0, ns, 1, nt, t0.h1);
+}
+
 template <int MAXS, bool STATS>
 __device__ __forceinline__ void unit_body(const float* A, int K16A, const float* W, int K16W, int rb, int kb, int j0,
-                                          int ntl, int s0, int ns, bool nt, float4 (&wr0)[MAXS], float* red,
+                                          int ntl, int s0, int ns, bool nt, Tile0<MAXS>& t0, float* red,
                                           float& fs1, float& fs2) {
+    constexpr int HS = HalfT<MAXS>::HS;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     float4 xv[MAXS];
@@ -1307,19 +1211,42 @@ __device__ __forceinline__ void unit_body(const float* A, int K16A, const float*
 #pragma unroll
         for (int s = 0; s < MAXS; ++s)
             if (s < ns) hpa_gemm::row_sums_add(xv[s], fs1, fs2);
-    float4 wr1[MAXS];
+    // half-tile q = 2t + h in set q % 4: sets 0, 1 = tile 0 (t0), 2, 3 here
+    float4 w2[HS], w3[HS];
+    if (ntl > 1) {
+        ld_half<MAXS>(W, K16W, j0 + 1, kb, s0, ns, 0, nt, w2);
+        ld_half<MAXS>(W, K16W, j0 + 1, kb, s0, ns, 1, nt, w3);
+    }
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < XT_MAX; ++t) {
+    for (int q = 0; q < 2 * XT_MAX; ++q) {
+        const int t = q >> 1, h = q & 1;
         if (t >= ntl) break;
-        if (t + 1 < ntl) {  // the next tile's fragments into the other buffer
-            if (t & 1)
-                ld_tile<MAXS>(W, K16W, j0 + t + 1, kb, s0, ns, nt, wr0);
+        // half-tile q + 3 into the set half-tile q - 1 used (q % 4 == 0: set 3 is tile 1's half 1, still live)
+        const int qn = q + 3;
+        if (q >= 1 && (qn >> 1) < ntl) {
+            if (qn % 4 == 0)
+                ld_half<MAXS>(W, K16W, j0 + (qn >> 1), kb, s0, ns, qn & 1, nt, t0.h0);
+            else if (qn % 4 == 1)
+                ld_half<MAXS>(W, K16W, j0 + (qn >> 1), kb, s0, ns, qn & 1, nt, t0.h1);
+            else if (qn % 4 == 2)
+                ld_half<MAXS>(W, K16W, j0 + (qn >> 1), kb, s0, ns, qn & 1, nt, w2);
             else
-                ld_tile<MAXS>(W, K16W, j0 + t + 1, kb, s0, ns, nt, wr1);
+                ld_half<MAXS>(W, K16W, j0 + (qn >> 1), kb, s0, ns, qn & 1, nt, w3);
         }
-        const f32x4 acc = (t & 1) ? chain_tile<MAXS>(xv, wr1, ns) : chain_tile<MAXS>(xv, wr0, ns);
+        if (q % 4 == 0)
+            chain_half<MAXS>(xv, t0.h0, ns, h, acc);
+        else if (q % 4 == 1)
+            chain_half<MAXS>(xv, t0.h1, ns, h, acc);
+        else if (q % 4 == 2)
+            chain_half<MAXS>(xv, w2, ns, h, acc);
+        else
+            chain_half<MAXS>(xv, w3, ns, h, acc);
+        if (h == 1) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) red[(w * XT_MAX + t) * 256 + g * 64 + lane] = acc[g];
+            for (int g = 0; g < 4; ++g) red[(w * XT_MAX + t) * 256 + g * 64 + lane] = acc[g];
+            acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
     }
 }
 
@@ -1368,14 +1295,14 @@ __global__ __launch_bounds__(768) void decode_chainx_kernel(KA args) {
     PL_STAMP(t_start);
     PL_STORE(0, t_start);
     float fs1 = 0.f, fs2 = 0.f;
-    float4 wr0[MAXS];
+    cx::Tile0<MAXS> t0w;
     // B: attproj(l): res2 = res + att . Wap^T + b
     {
         const int T = a.xt[0], NG = a.xng[0];
         const int g = bid % NG, rb = bid / NG, j0 = g * T;
         const bool has = rb < R && j0 < NCT;
         const int ntl = has ? min(T, NCT - j0) : 0;
-        if (has) cx::ld_tile<MAXS>(a.w_ap, K16, j0, 0, s0, ns, nt, wr0);
+        if (has) cx::ld_tile0<MAXS>(a.w_ap, K16, j0, 0, s0, ns, nt, t0w);
         const bool ep = tid < ntl * 64;
         const int row = rb * 16 + er, col = (j0 + et) * 16 + 4 * eq;
         const int fi = ep ? (int)(hpa::frag_index(row, col, C) * 4) : 0;
@@ -1384,7 +1311,7 @@ __global__ __launch_bounds__(768) void decode_chainx_kernel(KA args) {
             bv = c6::ld4(a.b_ap + col);
             rv = hpa::load_wt16(a.res, fi);
         }
-        if (has) unit_body<MAXS, false>(a.att, K16, a.w_ap, K16, rb, 0, j0, ntl, s0, ns, nt, wr0, sm.red, fs1, fs2);
+        if (has) unit_body<MAXS, false>(a.att, K16, a.w_ap, K16, rb, 0, j0, ntl, s0, ns, nt, t0w, sm.red, fs1, fs2);
         lds_barrier();
         if (ep) {
             float4 v = fold_x(sm.red, et, er, eq);
@@ -1402,7 +1329,7 @@ __global__ __launch_bounds__(768) void decode_chainx_kernel(KA args) {
         const int g = bid % NG, rb = bid / NG, j0 = g * T;
         const bool has = rb < R && j0 < NJ;
         const int ntl = has ? min(T, NJ - j0) : 0;
-        if (has) cx::ld_tile<MAXS>(a.w_fc, K16, j0, 0, s0, ns, nt, wr0);
+        if (has) cx::ld_tile0<MAXS>(a.w_fc, K16, j0, 0, s0, ns, nt, t0w);
         const bool ep = tid < ntl * 64;
         const int row = rb * 16 + er, col = (j0 + et) * 16 + 4 * eq;
         float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f), c2 = c1;
@@ -1414,7 +1341,7 @@ __global__ __launch_bounds__(768) void decode_chainx_kernel(KA args) {
         if (!waitx(a, c6::X1 + (has ? rb : 0), has ? n_b : 0, 2, sm)) return;
         PL_MARK(6);
         fs1 = fs2 = 0.f;
-        if (has) unit_body<MAXS, true>(a.res2, K16, a.w_fc, K16, rb, 0, j0, ntl, s0, ns, nt, wr0, sm.red, fs1, fs2);
+        if (has) unit_body<MAXS, true>(a.res2, K16, a.w_fc, K16, rb, 0, j0, ntl, s0, ns, nt, t0w, sm.red, fs1, fs2);
         hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + w * 32);
         lds_barrier();
         if (ep) {
@@ -1433,7 +1360,7 @@ __global__ __launch_bounds__(768) void decode_chainx_kernel(KA args) {
         const int g = bid % NG, q1 = bid / NG, rb = q1 % R, p = q1 / R, j0 = g * T;
         const bool has = p < 4 && j0 < NCT;
         const int ntl = has ? min(T, NCT - j0) : 0;
-        if (has) cx::ld_tile<MAXS>(a.w_fp, 4 * K16, j0, p * K16, s0, ns, nt, wr0);
+        if (has) cx::ld_tile0<MAXS>(a.w_fp, 4 * K16, j0, p * K16, s0, ns, nt, t0w);
         const bool ep = tid < ntl * 64;
         const int row = rb * 16 + er, col = (j0 + et) * 16 + 4 * eq;
         float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1441,7 +1368,7 @@ __global__ __launch_bounds__(768) void decode_chainx_kernel(KA args) {
         const int n_c = (4 * NCT + a.xt[1] - 1) / a.xt[1];  // fc units of a row block
         if (!waitx(a, c6::H + (has ? rb * 4 : 0), has ? n_c : 0, 3, sm)) return;
         PL_MARK(8);
-        if (has) unit_body<MAXS, false>(a.fch, 4 * K16, a.w_fp, 4 * K16, rb, p * K16, j0, ntl, s0, ns, nt, wr0, sm.red, fs1, fs2);
+        if (has) unit_body<MAXS, false>(a.fch, 4 * K16, a.w_fp, 4 * K16, rb, p * K16, j0, ntl, s0, ns, nt, t0w, sm.red, fs1, fs2);
         lds_barrier();
         float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
         auto slab_at = [&](int pp) { return (((pp * R + rb) * NCT + j0 + et) * 256 + (tid & 63) * 4) * 4; };
@@ -1502,7 +1429,7 @@ __global__ __launch_bounds__(768) void decode_chainx_kernel(KA args) {
         const int g = bid % NG, rb = bid / NG, j0 = g * T;
         const bool has = rb < R && j0 < NJ;
         const int ntl = has ? min(T, NJ - j0) : 0;
-        if (has) cx::ld_tile<MAXS>(a.w_qkv, K16, j0, 0, s0, ns, nt, wr0);
+        if (has) cx::ld_tile0<MAXS>(a.w_qkv, K16, j0, 0, s0, ns, nt, t0w);
         const bool ep = tid < ntl * 64;
         const int row = rb * 16 + er, col = (j0 + et) * 16 + 4 * eq;
         float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f), c2 = c1;
@@ -1514,7 +1441,7 @@ __global__ __launch_bounds__(768) void decode_chainx_kernel(KA args) {
         if (!waitx(a, c6::X2 + (has ? rb : 0), has ? n_d : 0, 4, sm)) return;
         PL_MARK(10);
         fs1 = fs2 = 0.f;
-        if (has) unit_body<MAXS, true>(a.res, K16, a.w_qkv, K16, rb, 0, j0, ntl, s0, ns, nt, wr0, sm.red, fs1, fs2);
+        if (has) unit_body<MAXS, true>(a.res, K16, a.w_qkv, K16, rb, 0, j0, ntl, s0, ns, nt, t0w, sm.red, fs1, fs2);
         hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + w * 32);
         lds_barrier();
         if (ep && row < a.B) {
@@ -1611,11 +1538,6 @@ void fill_ka(const HpaLayerArgs* h, int G, KA& a) {
     a.ctr = h->counters;
     a.err = h->err;
     a.err_sticky = h->err_sticky;
-    a.res2g = h->res2g;
-    a.fchg = h->fchg;
-    a.resg = h->resg;
-    a.slabg = h->slabg;
-    a.epoch = h->epoch;
 }
 
 // blocks per CU of a 768-thread instantiation (occupancy API), cached per kernel
@@ -1641,18 +1563,16 @@ int launch(const HpaLayerArgs* h, int G) {
     return 0;
 }
 
-template <int P, bool BF, int TC, int TD, int TE, bool GR>
+template <int P, bool BF, int TC, int TD, int TE>
 int launch6(const HpaLayerArgs* h, int G) {
-    HPA_REQUIRE(resident_blocks(decode_chain6_kernel<P, BF, TC, TD, TE, GR>) >= 1,
+    HPA_REQUIRE(resident_blocks(decode_chain6_kernel<P, BF, TC, TD, TE>) >= 1,
                 "decode layer: the chain-6 workgroup does not fit a CU");
     const int R = (h->B + 15) / 16;
     HPA_REQUIRE(R * 48 <= G && R * 192 / TC <= G && 4 * R * 48 / TD <= G && R * 144 / TE <= G,
                 "decode layer: chain form 6 needs a unit per workgroup in every phase");
-    HPA_REQUIRE(!GR || (h->res2g && h->fchg && h->resg && h->slabg && h->epoch),
-                "decode layer: chain form 7 needs the granule buffers and the step epoch");
     KA a;
     fill_ka(h, G, a);
-    decode_chain6_kernel<P, BF, TC, TD, TE, GR><<<G, 768, 0, hpa_stream()>>>(a);
+    decode_chain6_kernel<P, BF, TC, TD, TE><<<G, 768, 0, hpa_stream()>>>(a);
     HPA_LAUNCH_CHECK();
     return 0;
 }
@@ -1706,20 +1626,15 @@ int dispatchx(const HpaLayerArgs* h, int G) {
 
 // tiles per unit of fc, fcproj, qkv by row blocks R: the fewest with every
 // phase's units <= 256 workgroups (attproj: 1)
-template <int P, bool BF, bool GR>
-int dispatch6_g(const HpaLayerArgs* h, int G) {
-    switch ((h->B + 15) / 16) {
-        case 1: return launch6<P, BF, 1, 1, 1, GR>(h, G);
-        case 2: return launch6<P, BF, 2, 2, 2, GR>(h, G);
-        case 3: return launch6<P, BF, 3, 3, 2, GR>(h, G);
-        case 4: return launch6<P, BF, 3, 3, 3, GR>(h, G);
-        default: return hpa_fail(__FILE__, __LINE__, "decode layer: chain form 6 needs B <= 64");
-    }
-}
-
 template <int P, bool BF>
 int dispatch6_t(const HpaLayerArgs* h, int G) {
-    return h->chain_only == 7 ? dispatch6_g<P, BF, true>(h, G) : dispatch6_g<P, BF, false>(h, G);
+    switch ((h->B + 15) / 16) {
+        case 1: return launch6<P, BF, 1, 1, 1>(h, G);
+        case 2: return launch6<P, BF, 2, 2, 2>(h, G);
+        case 3: return launch6<P, BF, 3, 3, 2>(h, G);
+        case 4: return launch6<P, BF, 3, 3, 3>(h, G);
+        default: return hpa_fail(__FILE__, __LINE__, "decode layer: chain form 6 needs B <= 64");
+    }
 }
 
 int dispatch6(const HpaLayerArgs* h, int G) {
@@ -1747,9 +1662,9 @@ int dispatch_p(const HpaLayerArgs* h, int G) {
 
 template <int NH>
 int dispatch(const HpaLayerArgs* h, int G) {
-    if (h->chain_only == 6 || h->chain_only == 7) {
+    if (h->chain_only == 6) {
         if constexpr (NH == 12) return dispatch6(h, G);
-        return hpa_fail(__FILE__, __LINE__, "decode layer: chain forms 6 / 7 need C = 768");
+        return hpa_fail(__FILE__, __LINE__, "decode layer: chain form 6 needs C = 768");
     }
     if (h->chain_only >= 2) {  // wide units (C = 768), widths (attproj, fc / fcproj, qkv) by chain_only
         if constexpr (LD<NH>::SW % 3 == 0) {
@@ -1772,7 +1687,7 @@ int dispatch(const HpaLayerArgs* h, int G) {
                     HPA_REQUIRE(fits(12, 4, 4), "decode layer: chain form 5 (12/4/4-wave units) needs B <= 64");
                     return dispatch_p<NH, false, 12, 4, 4>(h, G);
                 default:
-                    return hpa_fail(__FILE__, __LINE__, "decode layer: chain_only must be 0..7");
+                    return hpa_fail(__FILE__, __LINE__, "decode layer: chain_only must be 0..6 or 8");
             }
         } else {
             return hpa_fail(__FILE__, __LINE__, "decode layer: wide units need C = 768");
@@ -1836,12 +1751,12 @@ int hpa_decode_layer_trace(unsigned long long* host, int layers) {
 #endif
 }
 
-// the chain forms 6 / 7 (C = 768) and 8 (C = 768 or 1600): B <= 64, fp32 or
+// the chain forms 6 (C = 768) and 8 (C = 768 or 1600): B <= 64, fp32 or
 // bf16 pool, a unit per workgroup in every phase
 int hpa_decode_chain_eligible(int B, int C, int num_heads, int form) {
     const int G = num_cus();
     if (G <= 0 || C != 64 * num_heads || B < 1 || B > 64) return 0;
-    if (form == 6 || form == 7) {
+    if (form == 6) {
         if (num_heads != 12) return 0;
         const int R = (B + 15) / 16;
         return R * 48 <= G && 4 * R * 48 / (R == 1 ? 1 : R == 2 ? 2 : 3) <= G ? 1 : 0;
@@ -1868,7 +1783,7 @@ int hpa_decode_layer(const HpaLayerArgs* h) {
     HPA_REQUIRE(h->last || (h->w_qkv && h->qkv_c1 && h->qkv_c2 && h->q_out), "decode layer: qkv(l+1) operands");
     HPA_REQUIRE(h->splits >= 1 && h->splits <= HPA_ATTN_MAX_SPLITS, "decode layer: splits 1..16");
     const int G = num_cus();
-    if (h->chain_only >= 6) {
+    if (h->chain_only == 6 || h->chain_only == 8) {
         HPA_REQUIRE(hpa_decode_chain_eligible(h->B, h->C, h->num_heads, h->chain_only),
                     "decode layer: chain form not supported for this shape");
         if (h->chain_only == 8) return h->num_heads == 25 ? dispatchx<25>(h, G) : dispatchx<12>(h, G);

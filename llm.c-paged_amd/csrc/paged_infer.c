@@ -660,19 +660,17 @@ struct GPT2Decode {
     DecShard* shard;
     /* persistent layer (hpa_decode_layer): one launch per layer */
     int pl_want;      /* gpt2_decode_set_layer_kernel: 0 off, 1 auto, 2 full, 3 chain, 4 chain with wide units,
-                         5 chain form 6 (12-wave multi-tile units), 6 form 6 with granule hand-offs (7),
-                         7 chain form 8 (streamed-weight units, C = 768 / 1600) */
+                         5 chain form 6 (12-wave multi-tile units), 6 chain form 8 (streamed-weight
+                         units, C = 768 / 1600) */
     int pl_on;        /* in use: 0 five launches, 1 full persistent layer, 2 attention launch + chain,
                          3 attention launch + chain of wide units (hpa_layer.hip NWU = pl_nwu) */
-    int pl_wform;     /* wide-unit form of the chain (HpaLayerArgs.chain_only 2..7), else 1 */
+    int pl_wform;     /* wide-unit form of the chain (HpaLayerArgs.chain_only 2..6, 8), else 1 */
     int pl_splits;
     int pl_global_B;  /* gpt2_decode_set_global_batch: the batch the picks follow (<= 64); else 0 */
     float* pl_rec;
     float* pl_slab;
     int* pl_ctr;      /* [L][pl_ctr_ints] + the step's error word (DEC_ERR_INTS), zeroed at the start of every step */
     size_t pl_ctr_ints;
-    /* chain form 7: tagged granules of res2 / fch / res / fcproj partials, the step counter */
-    unsigned *pl_res2g, *pl_fchg, *pl_resg, *pl_slabg, *pl_epoch;
     /* gpt2_forward: token at every cached position [B][max_ctx] and, when it
      * fits, the logits of every position [B][max_ctx][V] (managed) */
     int* h_hist;
@@ -781,7 +779,6 @@ static void dec_free(GPT2Decode* d) {
     hpa_free(d->d_fold);
     hpa_free(d->d_attn_ws);
     hpa_free(d->pl_rec); hpa_free(d->pl_slab); hpa_free(d->pl_ctr);
-    hpa_free(d->pl_res2g); hpa_free(d->pl_fchg); hpa_free(d->pl_resg); hpa_free(d->pl_slabg); hpa_free(d->pl_epoch);
     hpa_free(d->d_rng);
     hpa_free(d->pos_logits);
     hpa_host_free(d->h_next);
@@ -926,10 +923,10 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
         case 4: /* round 3's wide units, widths by row blocks: chain_only 2..5 */
             if (c.num_heads == 12) { mode = 3; d->pl_wform = 1 + Rg; }
             break;
-        case 5: case 6: /* form 6 (12-wave multi-tile units); 7: with granule hand-offs */
-            if (c.num_heads == 12) { mode = 3; d->pl_wform = d->pl_want == 6 ? 7 : 6; }
+        case 5: /* form 6 (12-wave multi-tile units) */
+            if (c.num_heads == 12) { mode = 3; d->pl_wform = 6; }
             break;
-        case 7: mode = 3; d->pl_wform = 8; break; /* form 8: streamed-weight units (C = 768, 1600) */
+        case 6: mode = 3; d->pl_wform = 8; break; /* form 8: streamed-weight units (C = 768, 1600) */
         default: /* auto */
             if (c.num_heads == 12) { mode = 3; d->pl_wform = 6; }
             else if (c.channels >= 1024) { mode = 3; d->pl_wform = 8; }
@@ -954,19 +951,6 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
         d->pl_ctr = (int*)hpa_malloc(((size_t)c.num_layers * sz[2] + DEC_ERR_INTS) * sizeof(int));
     }
     if (!d->pl_rec || !d->pl_slab || !d->pl_ctr) return 1;
-    if (d->pl_wform == 7 && !d->pl_res2g) { /* granules: 8 bytes per float, zero tags never match a step's */
-        const size_t Mp = d->Mp, C = c.channels, R = Mp / 16;
-        d->pl_res2g = (unsigned*)hpa_malloc(Mp * C * 8);
-        d->pl_fchg = (unsigned*)hpa_malloc(Mp * 4 * C * 8);
-        d->pl_resg = (unsigned*)hpa_malloc(Mp * C * 8);
-        d->pl_slabg = (unsigned*)hpa_malloc(4 * R * (C / 16) * 256 * 8);
-        d->pl_epoch = (unsigned*)hpa_malloc(64);
-        if (!d->pl_res2g || !d->pl_fchg || !d->pl_resg || !d->pl_slabg || !d->pl_epoch ||
-            hpa_memset_async(d->pl_res2g, 0, Mp * C * 8) || hpa_memset_async(d->pl_fchg, 0, Mp * 4 * C * 8) ||
-            hpa_memset_async(d->pl_resg, 0, Mp * C * 8) || hpa_memset_async(d->pl_slabg, 0, 4 * R * (C / 16) * 256 * 8) ||
-            hpa_memset_async(d->pl_epoch, 0, 64))
-            return 1;
-    }
     d->pl_splits = splits;
     d->pl_on = mode;
     return 0;
@@ -1017,11 +1001,6 @@ static int dec_layer(GPT2* model, int l) {
     a.counters = d->pl_ctr + (size_t)l * d->pl_ctr_ints;
     a.err = d->pl_ctr + (size_t)L * d->pl_ctr_ints; /* this step's (zeroed with the counters) */
     a.err_sticky = d->d_next + d->B;                /* first code of any step, until gpt2_decode_status */
-    a.res2g = d->pl_res2g;
-    a.fchg = d->pl_fchg;
-    a.resg = d->pl_resg;
-    a.slabg = d->pl_slabg;
-    a.epoch = d->pl_epoch;
     return hpa_decode_layer(&a);
 }
 
@@ -1191,7 +1170,7 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
     }
     {
         const char* env = getenv("HPA_LAYER_KERNEL");
-        d->pl_want = env && env[0] >= '0' && env[0] <= '7' ? env[0] - '0' : 1;
+        d->pl_want = env && env[0] >= '0' && env[0] <= '6' ? env[0] - '0' : 1;
     }
     if (dec_layer_setup(model, d)) {
         dec_free(d);
@@ -1422,9 +1401,6 @@ static int dec_launch(GPT2* model) {
     /* persistent layers: the embed kernel also zeroes their hand-off counters */
     const size_t zb = ((size_t)L * d->pl_ctr_ints + DEC_ERR_INTS) * sizeof(int);
     int rc = !pl ? hpa_embed_frag(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C)
-             : d->pl_wform == 7 && d->pl_on == 3
-                 ? hpa_embed_frag_step(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C, d->pl_ctr, zb,
-                                       d->pl_epoch) /* also the step counter of the granule tags */
                  : hpa_embed_frag_zero(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C, d->pl_ctr, zb);
 #define DEC_TRACE(i) \
     if (d->trace_x) rc |= hpa_unpack_frag(d->res, d->B, C, d->trace_x + (size_t)(i) * d->B * C, C)
@@ -1787,7 +1763,7 @@ int gpt2_decode_set_layer_kernel(GPT2* model, int enable) {
     GPT2Decode* d = model->decode;
     if (!d) return 1;
     if (hpa_synchronize()) return 1;
-    d->pl_want = enable < 0 ? 0 : enable > 7 ? 7 : enable;
+    d->pl_want = enable < 0 ? 0 : enable > 6 ? 6 : enable;
     if (dec_layer_setup(model, d)) return 1;
     if (d->graph) { /* recapture with the other step */
         hpa_graph_destroy(d->graph);

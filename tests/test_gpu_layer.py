@@ -56,8 +56,7 @@ def _model(hip, cfgd, params, B, P, layer, kv_dtype=0, splits_env=None, mode=2):
 
 @pytest.mark.parametrize("B,mode", [(64, 2), (32, 2), (16, 2), (8, 2), (64, 3), (40, 3), (8, 3), (16, 4), (8, 4),
                                     (5, 4), (32, 4), (20, 4), (40, 4), (64, 4), (64, 5), (48, 5), (33, 5), (32, 5),
-                                    (20, 5), (16, 5), (8, 5), (5, 5), (64, 6), (48, 6), (40, 6), (32, 6), (17, 6),
-                                    (8, 6), (1, 6)])
+                                    (20, 5), (16, 5), (8, 5), (5, 5), (64, 6), (33, 6), (17, 6), (1, 6)])
 def test_persistent_layer_matches_launch_path_124m(hip, B, mode):
     params = synth.params(GPT2_124M, seed=31)
     ctx = 990
@@ -258,9 +257,6 @@ def test_chain6_rows_independent_of_batch_and_form4(hip):
         for lo, hi in ((0, 8), (40, 64), (8, 48)):
             assert np.array_equal(full[:, :, lo:hi], run(lo, hi)), (lo, hi)
         assert np.array_equal(run(0, 8, traced=False), run(0, 8, mode=4, traced=False))
-        # granule hand-offs change no arithmetic: form 7 = form 6 bit for bit
-        assert np.array_equal(full, run(0, 64, mode=6))
-        assert np.array_equal(run(0, 40, mode=6, traced=False), run(0, 40, mode=5, traced=False))
         g64 = run(0, 64, traced=False)  # graph replay: its last step's residual feeds these logits
         assert np.isfinite(g64).all()
     finally:
@@ -292,8 +288,8 @@ def test_chain8_equals_chain6_124m(hip, B):
         m.close()
         return np.stack(out)
 
-    assert np.array_equal(run(7, True), run(5, True))
-    assert np.array_equal(run(7, False), run(5, False))
+    assert np.array_equal(run(6, True), run(5, True))
+    assert np.array_equal(run(6, False), run(5, False))
 
 
 GPT2_XL = dict(maxT=1024, V=50257, L=48, NH=25, C=1600)
@@ -308,7 +304,7 @@ def test_chain8_xl_matches_launch_path(hip, B):
     ctx, steps = 200, 3
     toks = np.random.default_rng(96).integers(0, GPT2_XL["V"], (steps, B)).astype(np.int32)
     out = []
-    for mode in (7, 0):
+    for mode in (6, 0):
         m = hip.Model(GPT2_XL, params=params)
         m.decode_init(B, 32, ctx + 8)
         assert m.set_layer_kernel(mode) == (mode != 0)

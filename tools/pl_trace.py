@@ -1,8 +1,10 @@
 """Phase timeline of the persistent decode layer (hpa_layer.hip), from the
 trace build's per-(layer, workgroup) s_memrealtime stamps.
 
-usage: HPA_LIB=llm.c-paged_amd/libpaged_hip_trace.so python tools/pl_trace.py [B] [ctx] [mode]
-(mode: 2 full persistent layer, default; 3 attention launch + persistent chain)
+usage: HPA_LIB=llm.c-paged_amd/libpaged_hip_trace.so python tools/pl_trace.py [B] [ctx] [mode] [XL]
+(mode = gpt2_decode_set_layer_kernel: 2 full persistent layer, default; 3
+attention launch + persistent chain; 4 wide units; 5 chain form 6; 6 chain
+form 8; XL: GPT-2 XL, page 32)
 
 Prints, per event, the min / median / max over workgroups of the time since
 the earliest kernel-start stamp of that layer (us), averaged over layers 1..L-2
@@ -29,10 +31,11 @@ def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
     ctx = int(sys.argv[2]) if len(sys.argv) > 2 else 990
     mode = int(sys.argv[3]) if len(sys.argv) > 3 else 2
-    cfg = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
+    xl = len(sys.argv) > 4 and sys.argv[4] == "XL"
+    cfg = dict(maxT=1024, V=50257, L=48, NH=25, C=1600) if xl else dict(maxT=1024, V=50257, L=12, NH=12, C=768)
     hip.init(0)
-    m = hip.Model(cfg, params=synth.params(cfg, seed=3))
-    m.decode_init(B, 16, cfg["maxT"])
+    m = hip.Model(cfg, params=hip.synthetic_params(cfg, seed=3) if xl else synth.params(cfg, seed=3))
+    m.decode_init(B, 32 if xl else 16, cfg["maxT"])
     assert m.set_layer_kernel(mode), "persistent layer not in use"
     m.set_graph(True)
     hip.check(hip.lib().gpt2_decode_fill_random(m.h, ctx, 5), "fill")
