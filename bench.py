@@ -3,10 +3,11 @@
 
 Metric (BASELINE.json): decode tokens/sec, GPT-2 124M paged attention,
 B=64, ctx 1024, page 16, fp32, on 1/2/4/8 MI355X (configs[1] at N=1).  For
-N>1 the decode shards by sequence: the metric's B = 64 is
-split over the ranks (strong scaling, the default), each rank decoding its
-share from its own page pool with replicated weights; --scaling weak keeps 64
-sequences per GPU (BASELINE configs[3]: B = 512 at 8 GPUs).  The one
+N>1 the decode shards by sequence: every rank decodes its own
+64 sequences from its own page pool with replicated weights (weak scaling,
+the default: the north star partitions the pool and the batch by sequence;
+BASELINE configs[3] = B 512 at 8 GPUs); --scaling strong splits the metric's
+B = 64 over the ranks instead (--emulate-rank N times one such rank).  The one
 collective is the end-of-step gather of the logits to rank 0 (--gather ids:
 the greedy ids only), run by the C library over RCCL/xGMI
 (gpt2_decode_gather: double-buffered on its own stream, so step k's gather
@@ -116,8 +117,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64,
-                    help="sequences in total (--scaling strong, the metric's B=64) or per GPU (weak)")
-    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
+                    help="sequences per GPU (--scaling weak, the default: the metric's B=64 on every GPU) or in "
+                         "total (strong)")
+    ap.add_argument("--scaling", default="weak", choices=["strong", "weak"],
+                    help="weak (default): --batch sequences per GPU, the page pool and the batch partition "
+                         "across ranks by sequence (BASELINE configs[3] at N=8: 64 x 8 = 512); strong: --batch in "
+                         "total, split over the ranks")
     ap.add_argument("--ctx", type=int, default=1024)
     ap.add_argument("--page-size", type=int, default=16)
     ap.add_argument("--kv-dtype", default="f32", choices=["f32", "bf16"],
