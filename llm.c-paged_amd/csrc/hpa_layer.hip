@@ -381,6 +381,7 @@ __device__ __forceinline__ f32x4 unit_mfma(const float* A, int K16A, int rb, int
     const int off = ((rb * K16A + kb + wq * SW) * 64 + (int)(threadIdx.x & 63)) * 16;
 #pragma unroll
     for (int s = 0; s < SW; ++s) xv[s] = hpa::load_wt16(A, off + s * 1024);
+    __builtin_amdgcn_sched_barrier(0);  // every A load in flight before the first MFMA (see c6::mfma_t)
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < SW; ++s) {
@@ -790,13 +791,15 @@ __device__ __forceinline__ bool wait6(const KA& a, int ctr, int expected, int co
 }
 
 // the wave's weight fragments of tiles j0 .. j0+T-1, k16 steps kb + 4w ..
-template <int T>
-__device__ __forceinline__ void load_wt(const float* W, int K16W, int j0, int kb, int w, bool nt, float4 (&wr)[T][SPW]) {
+// (NT: non-temporal, one row block reads every tile once; a compile-time
+// choice, so the loads carry no branch between them)
+template <int T, bool NT>
+__device__ __forceinline__ void load_wt(const float* W, int K16W, int j0, int kb, int w, float4 (&wr)[T][SPW]) {
     const float4* wf = reinterpret_cast<const float4*>(W) + ((size_t)j0 * K16W + kb + w * SPW) * 64 + (threadIdx.x & 63);
 #pragma unroll
     for (int t = 0; t < T; ++t)
 #pragma unroll
-        for (int s = 0; s < SPW; ++s) wr[t][s] = nt ? ld_nt(wf + ((size_t)t * K16W + s) * 64) : wf[((size_t)t * K16W + s) * 64];
+        for (int s = 0; s < SPW; ++s) wr[t][s] = NT ? ld_nt(wf + ((size_t)t * K16W + s) * 64) : wf[((size_t)t * K16W + s) * 64];
 }
 
 // the wave's 4 A fragments (sc1: written in this launch or the previous
@@ -809,6 +812,10 @@ __device__ __forceinline__ void mfma_t(const float* A, int K16A, int rb, int kb,
     const int off = ((rb * K16A + kb + w * SPW) * 64 + (int)(threadIdx.x & 63)) * 16;
 #pragma unroll
     for (int s = 0; s < SPW; ++s) xv[s] = hpa::load_wt16(A, off + s * 1024);
+    // all four A loads in flight before the first MFMA: left alone the
+    // scheduler interleaves them two at a time with the MFMAs (two dependent
+    // round trips instead of one, seen in the gfx950 ISA of round 4)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < T; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -863,8 +870,18 @@ __device__ __forceinline__ float4 ln_fold4(const float* wsum, int r, float4 v, f
     return v;
 }
 
+// every storing wave drained.  The builtin form, not inline asm: the
+// compiler must know vmcnt is 0 here, or it waits again before the first
+// register it reuses after the stores -- and vmcnt is in order, so that wait
+// also drained the next phase's weight prefetch issued in between (seen in
+// the gfx950 ISA of round 4: the prefetch had to land before the wait began)
+__device__ __forceinline__ void drain_vm() {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+    asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ void publish6(const KA& a, int ctr, bool did) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    drain_vm();
     lds_barrier();
     if (threadIdx.x == 0 && did) arrive6(a, ctr, 1);
 }
@@ -883,7 +900,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
     const int tid = threadIdx.x;
     const int bid = blockIdx.x;
     const int R = a.R;
-    const bool nt = R == 1;
+    constexpr bool NT = TC == 1 && TD == 1 && TE == 1;  // the one-row-block instantiation: every tile read once
     // epilogue thread's place: tile et, row er, column quad eq
     const int et = tid >> 6, er = (tid & 63) >> 2, eq = tid & 3;
     int* tick = a.ctr + kCtr;  // fcproj K-part tickets [R][NCT / TD]
@@ -897,7 +914,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         const bool has = bid < n;
         const int g = bid % NG, rb = bid / NG;
         float4 wr[T][SPW];
-        if (has) load_wt<T>(a.w_ap, K16, g * T, 0, w, nt, wr);
+        if (has) load_wt<T, NT>(a.w_ap, K16, g * T, 0, w, wr);
         const bool ep = has && tid < T * 64;
         const int row = rb * 16 + er, col = (g * T + et) * 16 + 4 * eq;
         const int fx = (int)hpa::frag_index(row, col, C), fi = fx * 4;
@@ -930,15 +947,15 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         const int n = R * NG;
         const bool has = bid < n;
         const int g = bid % NG, rb = bid / NG;
-        float4 wr[T][SPW];
-        if (has) load_wt<T>(a.w_fc, K16, g * T, 0, w, nt, wr);
         const bool ep = has && tid < T * 64;
         const int row = rb * 16 + er, col = (g * T + et) * 16 + 4 * eq;
         float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f), c2 = c1;
-        if (ep) {
+        if (ep) {  // epilogue operands first: the weight prefetch is the last thing in flight
             c1 = ld4(a.fc_c1 + col);
             c2 = ld4(a.fc_c2 + col);
         }
+        float4 wr[T][SPW];
+        if (has) load_wt<T, NT>(a.w_fc, K16, g * T, 0, w, wr);
         if (!wait6(a, X1 + (has ? rb : 0), has ? NCT : 0, 2, sm)) return;
         PL_MARK(6);
         fs1 = fs2 = 0.f;
@@ -967,12 +984,12 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         const int n = 4 * R * NG;
         const bool has = bid < n;
         const int g = bid % NG, q1 = bid / NG, rb = q1 % R, p = q1 / R;
-        float4 wr[T][SPW];
-        if (has) load_wt<T>(a.w_fp, 4 * K16, g * T, p * K16, w, nt, wr);
         const bool ep = has && tid < T * 64;
         const int row = rb * 16 + er, col = (g * T + et) * 16 + 4 * eq;
         float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
         if (ep) bv = ld4(a.b_fp + col);
+        float4 wr[T][SPW];
+        if (has) load_wt<T, NT>(a.w_fp, 4 * K16, g * T, p * K16, w, wr);
         if (!wait6(a, H + (has ? rb * 4 + p : 0), has ? 4 * NCT / TC / 4 : 0, 3, sm)) return;
         PL_MARK(8);
         if (has) {
@@ -988,7 +1005,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             hpa::store_wt16(a.slab_fp, sx * 4, val);
         }
         PL_MARK(14);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        c6::drain_vm();
         lds_barrier();
         if (has && tid == 0) {
             const int tk = __hip_atomic_fetch_add(tick + rb * NG + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1018,7 +1035,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
                 tr[0] = tot.x; tr[1] = tot.y; tr[2] = tot.z; tr[3] = tot.w;
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        c6::drain_vm();
         lds_barrier();
         if (a.stats_out && last && tid < T * 16) {  // 16-column LNf partial sums of the tiles' rows
             const int t = tid >> 4, r = tid & 15;
@@ -1042,8 +1059,6 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         const int n = R * NG;
         const bool has = bid < n;
         const int g = bid % NG, rb = bid / NG;
-        float4 wr[T][SPW];
-        if (has) load_wt<T>(a.w_qkv, K16, g * T, 0, w, nt, wr);
         const bool ep = has && tid < T * 64;
         const int row = rb * 16 + er, col = (g * T + et) * 16 + 4 * eq;
         float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f), c2 = c1;
@@ -1051,6 +1066,8 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             c1 = ld4(a.qkv_c1 + col);
             c2 = ld4(a.qkv_c2 + col);
         }
+        float4 wr[T][SPW];
+        if (has) load_wt<T, NT>(a.w_qkv, K16, g * T, 0, w, wr);
         if (!wait6(a, X2 + (has ? rb : 0), has ? NCT / TD : 0, 4, sm)) return;
         PL_MARK(10);
         fs1 = fs2 = 0.f;
@@ -1207,6 +1224,7 @@ __device__ __forceinline__ void unit_body(const float* A, int K16A, const float*
 #pragma unroll
     for (int s = 0; s < MAXS; ++s)
         if (s < ns) xv[s] = hpa::load_wt16(A, off + s * 1024);
+    __builtin_amdgcn_sched_barrier(0);  // every A load in flight before the first MFMA (see mfma_t)
     if (STATS)
 #pragma unroll
         for (int s = 0; s < MAXS; ++s)
@@ -1376,7 +1394,7 @@ __global__ __launch_bounds__(768) void decode_chainx_kernel(KA args) {
             val = fold_x(sm.red, et, er, eq);
             hpa::store_wt16(a.slab_fp, slab_at(p), val);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        c6::drain_vm();
         lds_barrier();
         if (has && tid == 0) {
             const int tk = __hip_atomic_fetch_add(tick + rb * NG + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1404,7 +1422,7 @@ __global__ __launch_bounds__(768) void decode_chainx_kernel(KA args) {
                 tr[0] = tot.x; tr[1] = tot.y; tr[2] = tot.z; tr[3] = tot.w;
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        c6::drain_vm();
         lds_barrier();
         if (a.stats_out && last && tid < ntl * 16) {  // 16-column LNf partial sums of the tiles' rows
             const int t = tid >> 4, r = tid & 15;
