@@ -152,6 +152,9 @@ def parse():
                          "6 chain form 8 (streamed weights, also GPT-2 XL); "
                          "-1 the engine's default "
                          "(HPA_LAYER_KERNEL or 1)")
+    ap.add_argument("--lanes", type=int, default=-1, choices=[-1, 0, 1, 2],
+                    help="gpt2_decode_set_lanes: 2 the two-lane step (each lane's attention beside the other "
+                         "lane's chain), 1 one lane, 0 auto, -1 the engine's default")
     ap.add_argument("--picks", default="local", choices=["local", "global"],
                     help="N>1 / --emulate-rank: shape picks by the rank's own batch (default: a rank computes "
                          "what a single-GPU engine of its rows computes) or by the global batch "
@@ -293,6 +296,8 @@ def main():
         model.set_global_batch(B)  # every row as the unsharded engine of B computes it
     if args.layer_kernel >= 0:
         model.set_layer_kernel(args.layer_kernel)
+    if args.lanes >= 0:
+        model.set_lanes(args.lanes)
     if args.sample:
         model.set_sampling(True, seed=1337 + lo)
     if args.gemm_waves or args.gemm_rows or args.gemm_cols:
@@ -449,8 +454,10 @@ def main():
                                       1: "one persistent launch per layer (hpa_decode_layer)",
                                       2: "attention launch + one persistent launch of the GEMM chain "
                                          "(hpa_decode_layer chain_only)",
-                                      3: "attention launch + one persistent launch of the GEMM chain, wide "
-                                         "units (hpa_decode_layer chain_only 2..5)"}[model.layer_form()],
+                                      3: "attention launch + one persistent launch of the GEMM chain in "
+                                         "wide / multi-tile units (hpa_decode_layer chain_only 2..6, 8: "
+                                         "by default form 6 at C = 768, form 8 at C >= 1024)"}[model.layer_form()],
+                       "lanes": model.lanes(),
                        "token_choice": "multinomial (reference sample_mult)" if args.sample else "greedy",
                        "gemm_waves": [int(x) for x in model.gemm_config()[0]],
                        "gemm_row_blocks": [int(x) for x in model.gemm_config()[1]],

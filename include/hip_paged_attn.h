@@ -259,6 +259,17 @@ typedef struct {
                              A is rounded to bf16 (RNE) after the LayerNorm, products are
                              summed in fp32 on v_mfma_f32_16x16x32_bf16 (variant 0, 1
                              or 5; ln_fold_c1 must be NULL); waves 4/8. */
+    /* LOGITS on the activation-resident kernel (variant 4, fp32) only: non-NULL
+     * pick_next makes the launch's last workgroup to finish (an arrival ticket on
+     * pick_count: one int, zero before the first launch, left zero) reduce the
+     * argmax partials as hpa_argmax_final(part_out, ..., pick_next, pick_tokens,
+     * pick_pos, NULL) would: next[m] = the lowest column of row m's maximum;
+     * pick_tokens (nullable) gets it too, pick_pos (nullable) += 1.  Saves the
+     * argmax launch. */
+    int* pick_next;
+    int* pick_tokens;
+    int* pick_pos;
+    int* pick_count;
 } HpaFusedGemm;
 /* LayerNorm folding for hpa_gemm_fused (layernorm_forward :49-89 followed by
  * matmul_forward :92-114, restated): for W [N][K] row-major (device), writes
@@ -365,6 +376,9 @@ typedef struct {
                                      out at once when it is set) */
     int* err_sticky;              /* nullable: the first code also lands here, never zeroed by a
                                      step (gpt2_decode_status reads and clears it) */
+    int stats_mp;                 /* row stride of stats_out; 0: this launch's Mp.  A launch over a
+                                     slice of the batch's row blocks (the engine's two-lane step)
+                                     passes the batch's Mp and stats_out advanced to its first row */
 } HpaLayerArgs;
 /* 1 if the persistent layer applies (shape, CU count, residency), else 0 */
 int hpa_decode_layer_eligible(int B, int C, int num_heads, int splits);

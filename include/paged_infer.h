@@ -226,6 +226,15 @@ int  gpt2_decode_set_layer_kernel(GPT2* model, int enable);
  * launch + persistent chain of 4-wave units, 3 the chain in wide / multi-tile
  * units (forms 4..6 of gpt2_decode_set_layer_kernel) */
 int  gpt2_decode_layer_kernel(GPT2* model);
+/* two-lane step: the batch's row blocks in two lanes on two streams, each
+ * lane's attention launch running beside the other lane's chain launch (chain
+ * form 6, 33..64 rows, one context range per sequence and head; the rows'
+ * numbers are the one-lane step's bit for bit).  lanes: 0 auto (= off: measured
+ * slower, the chain's hand-offs queue behind the attention's K/V stream;
+ * profiles/r4/experiments/two_lane_step.txt), 1 off, 2 on where it applies;
+ * gpt2_decode_lanes: lanes in use (1 or 2) */
+int  gpt2_decode_set_lanes(GPT2* model, int lanes);
+int  gpt2_decode_lanes(GPT2* model);
 /* waits for the queued work; 0, or the code of a timed-out in-launch wait of
  * the persistent layer (the step's outputs are then invalid), which it clears */
 int  gpt2_decode_status(GPT2* model);

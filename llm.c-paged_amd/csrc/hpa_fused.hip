@@ -804,9 +804,27 @@ static void looped_shape(const HpaFusedGemm* g, int Mp, int* nw, int* mt, int* n
     if ((*ntw == 2 && (*mt == 1 || *nw == 16)) || (*ntw == 4 && (*mt != 4 || *nw != 4))) *ntw = 1;
 }
 
+static int gemm_fused_launch(const HpaFusedGemm* g, FG& p);
+
+// the resident logits kernel takes the final pick into its launch (its last
+// workgroup reduces the partials); any other LOGITS path picks afterwards with
+// hpa_argmax_final, so pick_next means the same on every path
 int hpa_gemm_fused(const HpaFusedGemm* g) {
     FG p;
     if (fused_prepare(g, &p)) return 1;
+    const bool pick = g->pick_next != nullptr;
+    HPA_REQUIRE(!pick || (g->epilogue == HPA_FEPI_LOGITS && g->part_out), "gemm_fused: pick_next needs a LOGITS GEMM");
+    const bool fused = pick && g->pick_count && g->w_dtype == HPA_F32 && g->variant == 4 &&
+                       logits_resident_eligible(p, g->epilogue) && logits_resident_grid(p) <= 256;
+    if (!fused) p.pick_next = p.pick_tokens = p.pick_pos = p.pick_count = nullptr;
+    const int rc = gemm_fused_launch(g, p);
+    if (rc || !pick || fused) return rc;
+    const int npart = hpa_logits_partials(g);
+    HPA_REQUIRE(npart > 0, "gemm_fused: logits partials");
+    return hpa_argmax_final(p.part_out, npart, p.Mp, p.M, g->pick_next, g->pick_tokens, g->pick_pos, nullptr);
+}
+
+static int gemm_fused_launch(const HpaFusedGemm* g, FG& p) {
     int nw, mt, ntw;
     if (g->w_dtype == HPA_BF16) {  // bf16 weights: hpa_gemm_bf16.hip
         HPA_REQUIRE(g->K % 32 == 0 && !g->ln_fold_c1 &&

@@ -38,6 +38,10 @@ struct FG {
     int gx, gy;  // column-tile groups x row groups of the launch
     float* sk_slab;  // stream-K (variant 6): [workgroup][2][super-tile] partials
     int* sk_cnt;     // stream-K: [super-tile] arrival counters (zero between launches)
+    int* pick_next;  // resident logits: the last workgroup's final pick (HpaFusedGemm.pick_*)
+    int* pick_tokens;
+    int* pick_pos;
+    int* pick_count;
 };
 
 // XCD-aware workgroup order (MI355X_MICROARCH.md "Workgroup dispatch":
@@ -672,6 +676,10 @@ static inline int fused_prepare(const HpaFusedGemm* g, FG* p) {
     p->fold_c1 = g->ln_fold_c1;
     p->sk_slab = g->sk_slab;
     p->sk_cnt = g->sk_count;
+    p->pick_next = g->pick_next;
+    p->pick_tokens = g->pick_tokens;
+    p->pick_pos = g->pick_pos;
+    p->pick_count = g->pick_count;
     HPA_REQUIRE(!g->ln_fold_c1 || g->epilogue != HPA_FEPI_LOGITS, "gemm_fused: ln_fold_c1 with LOGITS");
     if (g->epilogue == HPA_FEPI_QKV) {
         const HpaKVPool* pool = g->pool;

@@ -1128,6 +1128,9 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
 //   * waits per row block; fcproj's 4 K parts (of C each) are combined by the
 //     last part to draw its ticket, in part order.
 // A wave's K range depends only on K, so a row's sums never depend on B.
+#ifndef HPA_CX_SB
+#define HPA_CX_SB 1  // A/B builds: 0 = no scheduling barrier after form 8's A loads
+#endif
 namespace cx {
 constexpr int NW = 12;
 constexpr int XT_MAX = 7;
@@ -1224,7 +1227,9 @@ __device__ __forceinline__ void unit_body(const float* A, int K16A, const float*
 #pragma unroll
     for (int s = 0; s < MAXS; ++s)
         if (s < ns) xv[s] = hpa::load_wt16(A, off + s * 1024);
+#if HPA_CX_SB
     __builtin_amdgcn_sched_barrier(0);  // every A load in flight before the first MFMA (see mfma_t)
+#endif
     if (STATS)
 #pragma unroll
         for (int s = 0; s < MAXS; ++s)
@@ -1519,8 +1524,8 @@ bool shape_ok(int B, int S, int G) {
 void fill_ka(const HpaLayerArgs* h, int G, KA& a) {
     const HpaKVPool* pool = h->pool;
     a.B = h->B;
-    a.Mp = (h->B + 15) / 16 * 16;
-    a.R = a.Mp / 16;
+    a.R = (h->B + 15) / 16;
+    a.Mp = h->stats_mp > 0 ? h->stats_mp : a.R * 16;  // the stride of stats_out only
     a.S = h->splits;
     a.G = G;
     a.last = h->last;

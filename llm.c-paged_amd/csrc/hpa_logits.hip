@@ -33,6 +33,13 @@
 #ifndef HPA_RES_EXP
 #define HPA_RES_EXP 0  // timing experiments (tools/logits_exp.sh); 0 in the product
 #endif
+// A/B build knobs of the ring form (tools/r4_pick.sh, profiles/r4/logits_walk.txt):
+#ifndef HPA_RG_STRIDED
+#define HPA_RG_STRIDED 0  // 0: a contiguous run of tiles per workgroup; 1: tiles b, b + G, ... (round 3)
+#endif
+#ifndef HPA_RG_PRO
+#define HPA_RG_PRO 1  // prologue DMAs: 0 tiles 0, 1 at the start; 1 tile 1 after the first barrier; 2 both after it
+#endif
 #ifndef HPA_RES_NW
 #define HPA_RES_NW 16  // waves per workgroup (16: 3 k-steps each, 8: 6)
 #endif
@@ -56,6 +63,67 @@ __device__ __forceinline__ void dpp_argmax(float& bv, int& bi) {
     const bool take = v2 > bv || (v2 == bv && i2 < bi);
     bv = take ? v2 : bv;
     bi = take ? i2 : bi;
+}
+
+// the launch's final pick (HpaFusedGemm.pick_*): every workgroup has stored
+// its per-row (max, column) partial write-through; after the drain each draws
+// an arrival ticket, and the last reduces the G partials of every row as
+// argmax_final_kernel (hpa_fused.hip) does -- the largest value, the lowest
+// column among equals, 0 for a row with no finite maximum -- with sc1 loads
+// (MI355X_MICROARCH.md "Valid forms" row 1, as the attention's split merge).
+// Lane = row, so a wave's load of partial t is one contiguous 8*Mp-byte run;
+// wave w takes t = w, w + NWAVES, ..., and the waves' bests fold through
+// `scratch` (NWAVES * 64 * 2 words of the kernel's idle LDS) in wave order.
+template <int NWAVES>
+__device__ __forceinline__ void final_pick(const FG& p, float* scratch) {
+    __shared__ int s_last;
+    const int G = gridDim.x;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's partial store has landed
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(p.pick_count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
+    __syncthreads();
+    if (!s_last) return;
+    if (threadIdx.x == 0) __hip_atomic_store(p.pick_count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int m = min(lane, p.Mp - 1);
+    const __amdgpu_buffer_rsrc_t rs = hpa::wt_rsrc(p.part_out);
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int t0 = w; t0 < G; t0 += 8 * NWAVES) {  // 8 partials per lane in flight
+        u32x2 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int t = min(t0 + j * NWAVES, G - 1);
+            v[j] = __builtin_amdgcn_raw_buffer_load_b64(rs, (t * p.Mp + m) * 8, 0, hpa::kCpolSc1);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float fv = __uint_as_float(v[j].x);
+            const int fi = (int)v[j].y;
+            const bool take = t0 + j * NWAVES < G && (fv > bv || (fv == bv && fi < bi));
+            bv = take ? fv : bv;
+            bi = take ? fi : bi;
+        }
+    }
+    scratch[(w * 64 + lane) * 2] = bv;
+    scratch[(w * 64 + lane) * 2 + 1] = __int_as_float(bi);
+    __syncthreads();
+    if (w == 0 && lane < p.M) {
+#pragma unroll
+        for (int k = 1; k < NWAVES; ++k) {
+            const float v2 = scratch[(k * 64 + lane) * 2];
+            const int i2 = __float_as_int(scratch[(k * 64 + lane) * 2 + 1]);
+            const bool take = v2 > bv || (v2 == bv && i2 < bi);
+            bv = take ? v2 : bv;
+            bi = take ? i2 : bi;
+        }
+        const int id = bi == 0x7fffffff ? 0 : bi;
+        p.pick_next[lane] = id;
+        if (p.pick_tokens) p.pick_tokens[lane] = id;
+        if (p.pick_pos) p.pick_pos[lane] += 1;
+    }
 }
 
 template <int MT>
@@ -246,9 +314,10 @@ __global__ __launch_bounds__(kResNW * 64) void logits_resident_kernel(FG p) {
         if ((e & 15) == 0 && frow < p.Mp) {
             typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
             const u32x2 pv = {__float_as_uint(run_v), (unsigned int)run_i};
-            __builtin_amdgcn_raw_buffer_store_b64(pv, part_rs, ((int)blockIdx.x * p.Mp + frow) * 8, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(pv, part_rs, ((int)blockIdx.x * p.Mp + frow) * 8, 0, hpa::kCpolSc1);
         }
     }
+    if (p.pick_next) final_pick<kResNW>(p, red);  // the fold buffers are idle now
 }
 
 // ---- ring form (round 3, the default): rows split over waves, wte through
@@ -280,6 +349,13 @@ __global__ __launch_bounds__(kResNW * 64) void logits_resident_kernel(FG p) {
 // 3.35 us (6144 MFMA cycles per SIMD = 2.98 us at the 2.06 GHz the chip holds
 // under this load), the loaders' 48 KiB DMA 3.15 us (15 GB/s per CU beside
 // the MFMAs, 25 alone): 3.64 us per iteration, 57.5 us per launch.
+// Round 4 (profiles/r4/logits_walk.txt): a workgroup walks a contiguous run of
+// tiles (the round-3 walk b, b + G, ... wrote 18.6 MB for 12.9 MB of logits:
+// V is odd, so every row segment of a tile shares its end sectors with the
+// neighbouring tiles, written from another XCD; now 13.5 MB), loads nothing
+// past its run (the walk used to re-load its last tile twice), and issues tile
+// 1's DMA after the prologue's activation loads (prologue 5.9 vs 6.8 us); the
+// iteration (3.7 us) is MFMA-bound as before.
 // diagnostic build (-DHPA_RG_TRACE, tools/rg_trace.py): stamps per workgroup
 // -- [0] start, [1] prologue done, [2..15] iteration starts (after the
 // barrier), [16] loop end, [17] end -- as s_memrealtime (10 ns) and
@@ -367,28 +443,45 @@ __global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
     const bool loader = w >= kRgNW - kRgLoaders;
     const int G = gridDim.x;
     const int ntn = p.ntn;
-    int t = blockIdx.x;
+#if HPA_RG_STRIDED
+    int t = blockIdx.x;  // tiles b, b + G, ...
+    constexpr int tstep = 0;
+    const int tend = ntn;
+#else
+    // a contiguous run of column tiles per workgroup (the first ntn % G take
+    // one more): a row's 64-byte segments of neighbouring tiles share 32-byte
+    // sectors (V is odd, so rows are not sector aligned), and written from
+    // one L2 in consecutive iterations they merge there instead of leaving
+    // as partial-sector writes from different XCDs
+    const int tq = ntn / G, trm = ntn % G;
+    int t = (int)blockIdx.x * tq + min((int)blockIdx.x, trm);
+    constexpr int tstep = 1;
+    const int tend = t + tq + ((int)blockIdx.x < trm ? 1 : 0);
+#endif
+    const int TS = tstep ? 1 : G;  // tile stride of the walk
 
     const float* wl = p.w + lane * 4 + (w - (kRgNW - kRgLoaders)) * 256;  // loaders: their 1 KiB chunks
     const unsigned ring_lds = __builtin_amdgcn_readfirstlane(
         (unsigned)(size_t)(__attribute__((address_space(3))) float*)ring);
     // loader chunk j of a tile = k16-step (w - 4) + 4 j
     auto dma_src = [&](int tile) __attribute__((always_inline)) {
-        return wl + (size_t)min(tile, ntn - 1) * kRgTileF;  // past the end: a harmless repeat
+        return wl + (size_t)tile * kRgTileF;  // tile < tend: nothing is loaded past the workgroup's tiles
     };
     auto dma_dst = [&](int stage) __attribute__((always_inline)) {
         return ring_lds + (unsigned)(stage * kRgTileF + (w - (kRgNW - kRgLoaders)) * 256) * 4;
     };
     RG_MARK(0);
-    if (loader) {  // tiles 0 and 1 land during the LN prologue (the loaders take no part in it)
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-            const float* src = dma_src(t + d * G);
+    // the loaders' DMA of tile t + d * TS (d = 0, 1) into stage d, if the walk has it
+    auto dma_pro = [&](int d) __attribute__((always_inline)) {
+        if (t + d * TS < tend) {
+            const float* src = dma_src(t + d * TS);
             const unsigned dst = dma_dst(d);
 #pragma unroll
             for (int j = 0; j < kRgDma; ++j) rg_dma(src + kRgLoaders * j * 256, dst + kRgLoaders * j * 1024);
         }
-    }
+    };
+    if (loader && HPA_RG_PRO < 2) dma_pro(0);  // lands during the LN prologue (the loaders take no part in it)
+    if (loader && HPA_RG_PRO < 1) dma_pro(1);
 
     // prologue loads, all in flight together: LNf statistics partials, the
     // wave's raw activations, LNf gamma / beta (into LDS)
@@ -431,6 +524,8 @@ __global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
         }
     }
     __syncthreads();
+    if (loader && HPA_RG_PRO >= 2) dma_pro(0);  // behind the activation loads in the CU's memory queue
+    if (loader && HPA_RG_PRO >= 1) dma_pro(1);
     if (threadIdx.x < R) {
         const float* tt = lnscr + 8 * threadIdx.x;
         const float s1 = (tt[0] + tt[2]) + (tt[4] + tt[6]);
@@ -505,7 +600,7 @@ __global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
 #ifdef HPA_RG_TRACE
     unsigned long long tr_vm = 0, tr_bar = 0, tr_mf[2] = {0, 0};
 #endif
-    for (; t < ntn; t += G, ++it) {
+    for (; t < tend; t += TS, ++it) {
         // loaders: their DMA of tile t landed (issued two iterations ago;
         // after it, the previous iteration's kRgDma); the barrier makes every
         // loader's landed and frees the stage read in the previous iteration
@@ -513,7 +608,10 @@ __global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
         const unsigned long long tr_w0 = __builtin_amdgcn_s_memrealtime();
 #endif
         if (loader) {
-            __builtin_amdgcn_s_waitcnt((kRgDma & 15) | ((kRgDma >> 4) << 14) | (7 << 4));  // vmcnt(kRgDma) lgkmcnt(0)
+            if (t + TS < tend)  // tile t + TS's kRgDma DMAs may stay in flight
+                __builtin_amdgcn_s_waitcnt((kRgDma & 15) | ((kRgDma >> 4) << 14) | (7 << 4));  // vmcnt(kRgDma) lgkmcnt(0)
+            else
+                __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
 #ifdef HPA_RG_TRACE
             if (w == kRgNC) tr_vm += __builtin_amdgcn_s_memrealtime() - tr_w0;
 #endif
@@ -535,14 +633,16 @@ __global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
             // waves do nothing else, so the stalls of a saturated per-CU
             // memory queue never hold up an MFMA
             const int st2 = stage == 0 ? 2 : stage - 1;
-            const float* dsrc = dma_src(t + 2 * G);
-            const unsigned ddst = dma_dst(st2);
+            if (t + 2 * TS < tend) {
+                const float* dsrc = dma_src(t + 2 * TS);
+                const unsigned ddst = dma_dst(st2);
 #pragma unroll
-            for (int j = 0; j < kRgDma; ++j) rg_dma(dsrc + kRgLoaders * j * 256, ddst + kRgLoaders * j * 1024);
+                for (int j = 0; j < kRgDma; ++j) rg_dma(dsrc + kRgLoaders * j * 256, ddst + kRgLoaders * j * 1024);
+            }
         } else {
             // (waves of a missing row block compute on zeros)
             const float* rb = ring + stage * kRgTileF + lane * 4 + h * NPW * kRgPart * 256;
-            if (owner) epilogue(t - G, (it + 1) & 1, it > 0);
+            if (owner) epilogue(t - TS, (it + 1) & 1, it > 0);
             f32x4 acc[NPW];
 #pragma unroll
             for (int j = 0; j < NPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -587,7 +687,7 @@ __global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
 #endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (owner) epilogue(t - G, (it + 1) & 1, it > 0);
+    if (owner) epilogue(t - TS, (it + 1) & 1, it > 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
     RG_MARK(17);
     // one partial per row: slot blockIdx.x of part_out ([G][Mp][2]); the
@@ -606,9 +706,11 @@ __global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const u32x2 pv = {__float_as_uint(run_v[g]), (unsigned int)run_i[g]};
-            __builtin_amdgcn_raw_buffer_store_b64(pv, part_rs, ((int)blockIdx.x * p.Mp + rbase + g) * 8, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(pv, part_rs, ((int)blockIdx.x * p.Mp + rbase + g) * 8, 0,
+                                                  hpa::kCpolSc1);
         }
     }
+    if (p.pick_next) final_pick<kRgNW>(p, ring);  // the ring is idle now (every DMA drained)
 }
 
 int g_num_cus = 0;

@@ -59,7 +59,8 @@ class HpaFusedGemm(ctypes.Structure):
                 ("bt_stride", ctypes.c_int), ("pos", _V), ("waves", ctypes.c_int),
                 ("row_blocks", ctypes.c_int), ("variant", ctypes.c_int), ("col_tiles", ctypes.c_int),
                 ("row_seq", _V), ("ln_fold_c1", _V), ("sk_slab", _V), ("sk_count", _V),
-                ("w_dtype", ctypes.c_int)]
+                ("w_dtype", ctypes.c_int), ("pick_next", _V), ("pick_tokens", _V), ("pick_pos", _V),
+                ("pick_count", _V)]
 
 
 HPA_FEPI_QKV, HPA_FEPI_RESID, HPA_FEPI_GELU, HPA_FEPI_LOGITS = 0, 1, 2, 3
@@ -240,6 +241,8 @@ def lib():
     _sig(L, "hpa_pool_fill_random_ex", i, [P, v, i, i, i, ctypes.c_uint64, i])
     _sig(L, "hpa_logits_kernel", i, [i, i, i])
     _sig(L, "gpt2_decode_layer_kernel", i, [v])
+    _sig(L, "gpt2_decode_set_lanes", i, [v, i])
+    _sig(L, "gpt2_decode_lanes", i, [v])
     _sig(L, "gpt2_decode_status", i, [v])
     _sig(L, "hpa_decode_layer_eligible", i, [i, i, i, i])
     _sig(L, "hpa_decode_layer_pick_splits", i, [i, i, i])
@@ -630,6 +633,15 @@ class Model:
 
     def layer_kernel(self):
         return bool(lib().gpt2_decode_layer_kernel(self.h))
+
+    def set_lanes(self, lanes):
+        """two-lane step (paged_infer.h gpt2_decode_set_lanes): 0 auto, 1 off,
+        2 on where it applies; returns the lanes now in use"""
+        check(lib().gpt2_decode_set_lanes(self.h, int(lanes)), "set_lanes")
+        return int(lib().gpt2_decode_lanes(self.h))
+
+    def lanes(self):
+        return int(lib().gpt2_decode_lanes(self.h))
 
     def layer_form(self):
         """0 five launches per layer, 1 full persistent layer, 2 attention launch + persistent chain,

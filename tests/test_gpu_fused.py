@@ -376,9 +376,11 @@ def test_logits_resident_rows_independent_of_batch(hip, form):
         assert np.array_equal(i, ids[0][:i.shape[0]])
 
 
-def test_logits_resident_argmax_ties_first_index(hip):
+@pytest.mark.parametrize("form", [0, 12])
+def test_logits_resident_argmax_ties_first_index(hip, form):
     """equal maxima in several column tiles and workgroups: the lowest column
-    wins, as the reference's strict-> scan (paged_infer.c:937-951)"""
+    wins, as the reference's strict-> scan (paged_infer.c:937-951); form 0 =
+    by rows (the 16-wave form at 16 rows), 12 = the ring form"""
     L = hip.lib()
     M, K, N = 16, 768, 50257
     x = np.zeros((M, K), np.float32)
@@ -388,7 +390,7 @@ def test_logits_resident_argmax_ties_first_index(hip):
     cols = [7, 4000, 4001, 25000, 50256]
     W[cols, 0] = 0.5
     fixed = dict(x=x, W=W, bias=np.zeros(N, np.float32), lw=np.ones(K, np.float32), lb=np.zeros(K, np.float32))
-    out, acc, bound, keep = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, 0, ln=True, rng=np.random.default_rng(0),
+    out, acc, bound, keep = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, form, ln=True, rng=np.random.default_rng(0),
                                  fixed=fixed, variant=4)
     got = out.download((M, N))
     assert np.all(got[:, cols] == got[0, 7]) and got[0, 7] > got[0, 8]
@@ -396,6 +398,36 @@ def test_logits_resident_argmax_ties_first_index(hip):
     nxt = hip.DeviceBuffer(M * 4)
     hip.check(L.hpa_argmax_final(keep[-3].ptr, npart, 16, M, nxt.ptr, None, None, None))
     assert np.array_equal(nxt.download(M, np.int32), np.full(M, 7, np.int32))
+
+
+@pytest.mark.parametrize("M,form,variant", [(64, 12, 4), (37, 12, 4), (16, 16, 4), (5, 0, 4), (20, 0, 1)])
+def test_logits_in_launch_pick(hip, M, form, variant):
+    """HpaFusedGemm.pick_next: the resident logits kernel's last workgroup
+    reduces the argmax partials in the launch (both forms), other LOGITS paths
+    pick with hpa_argmax_final after it -- either way next = tokens = the
+    argmax of each row (lowest column among equals), pos += 1, and the arrival
+    counter is left at zero for the next launch (three launches back to back)"""
+    L = hip.lib()
+    rng = np.random.default_rng(41 + M)
+    K, N = 768, 50257
+    out, acc, bound, keep = _run(hip, hip.HPA_FEPI_LOGITS, M, K, N, form, ln=True, rng=rng, variant=variant)
+    got = out.download((M, N))
+    ids = got.argmax(-1).astype(np.int32)
+    g = keep[-1]
+    nxt = hip.DeviceBuffer.from_array(np.full(M, -7, np.int32))
+    tok = hip.DeviceBuffer.from_array(np.full(M, -7, np.int32))
+    pos = hip.DeviceBuffer.from_array(np.arange(M, dtype=np.int32))
+    cnt = hip.DeviceBuffer.from_array(np.zeros(1, np.int32))
+    g.pick_next, g.pick_tokens, g.pick_pos, g.pick_count = nxt.ptr, tok.ptr, pos.ptr, cnt.ptr
+    for it in range(3):
+        hip.check(L.hpa_gemm_fused(ctypes.byref(g)), "gemm_fused pick")
+        hip.check(L.hpa_synchronize())
+        assert np.array_equal(out.download((M, N)), got)
+        assert np.array_equal(nxt.download(M, np.int32), ids), it
+        assert np.array_equal(tok.download(M, np.int32), ids)
+        assert np.array_equal(pos.download(M, np.int32), np.arange(M) + it + 1)
+        assert cnt.download(1, np.int32)[0] == 0
+    g.pick_next = g.pick_tokens = g.pick_pos = g.pick_count = None
 
 
 def test_fused_qkv_appends_into_pages(hip):

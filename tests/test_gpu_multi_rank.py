@@ -242,6 +242,14 @@ def _c4_rank(lo, hi, total, picks, out_path):
             assert np.array_equal(g, m.logits()), t
             lg.append(g)
         m.status()  # no in-launch wait timed out
+        # as the N>1 bench runs: steps enqueued back to back, each step's RCCL
+        # gather on the comm stream beside the next step's persistent chain
+        # launches (every chain workgroup must still become resident: ADVICE r3)
+        for t in range(C4_STEPS):
+            m.step_async(toks[t, lo:hi])
+            m.gather(0)
+        assert np.array_equal(m.gathered(hi - lo, 0), m.logits())
+        m.status()
         info = np.array([m.layer_form(), m.attn_splits(), m.attn_waves()], np.int32)
         m.close()
     finally:

@@ -9,7 +9,7 @@ steps = float(sys.argv[2]) if len(sys.argv) > 2 else 0
 r = list(csv.DictReader(open(path)))
 agg = collections.defaultdict(list)
 for x in r:
-    key = (x["Kernel_Name"].split("(")[0][-40:], x["Grid_Size_X"], x["Grid_Size_Y"], x["Grid_Size_Z"],
+    key = (x["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][-40:], x["Grid_Size_X"], x["Grid_Size_Y"], x["Grid_Size_Z"],
            x["Workgroup_Size_X"], x.get("VGPR_Count", ""), x.get("Accum_VGPR_Count", ""))
     agg[key].append(int(x["End_Timestamp"]) - int(x["Start_Timestamp"]))
 tot = 0
