@@ -390,6 +390,16 @@ int hpa_decode_layer_pick_splits(int B, int num_heads, int max_ctx);
 /* sizes: out[0] = rec floats, out[1] = slab floats, out[2] = counter ints per layer */
 int hpa_decode_layer_sizes(int B, int C, int num_heads, int splits, size_t* out3);
 int hpa_decode_layer(const HpaLayerArgs* a);
+/* the decode step's first launch at GPT-2 124M shapes (C = 768, 12 heads,
+ * B <= 64, LN1 folded into w_qkv / qkv_c1 / qkv_c2 of layer 0): the embedding
+ * wte[tokens[b]] + wpe[pos[b]] (encoder_forward, paged_infer.c:41-47) into
+ * res (frag), layer 0's q into q_out and its K/V into layer 0's pages (chain
+ * form 6's qkv phase), and zero_bytes of `zero` (the step's counter block,
+ * 16-byte granules) zeroed -- one launch for the embed kernel and the qkv
+ * GEMM.  Reads a->B, pool, block_table, bt_stride, pos, res, w_qkv, qkv_c1,
+ * qkv_c2, q_out; the layer fields are ignored. */
+int hpa_decode_first(const HpaLayerArgs* a, const int* tokens, const float* wte, const float* wpe, void* zero,
+                     size_t zero_bytes);
 /* diagnostic builds (-DHPA_LAYER_TRACE) only, else returns 1: per-(layer,
  * workgroup) event stamps [layers][256][16] of the last launches (10 ns
  * ticks); host = NULL clears them */

@@ -97,6 +97,12 @@ struct KA {
     // chain form 8 (wide layers, GPT-2 XL): tiles per unit and tile groups
     // (padded to a multiple of 8) of attproj, fc, fcproj, qkv
     int xt[4], xng[4];
+    // the step's first launch (decode_first6_kernel): the tokens, the
+    // embedding tables, and the step's counter block to zero (16-B granules)
+    const int* tokens;
+    const float *wte, *wpe;
+    int4* zero;
+    int zero_n4;
 };
 
 // diagnostic build (-DHPA_LAYER_TRACE, tools/pl_trace.py): s_memrealtime of
@@ -806,6 +812,10 @@ __device__ __forceinline__ void load_wt(const float* W, int K16W, int j0, int kb
 // one), the T tiles' accumulator chains (each in the one-shot order: steps in
 // order, components x, y, z, w), and (STATS) the LN row partial sums
 template <int T, bool STATS>
+__device__ __forceinline__ void mfma_regs(const float4 (&xv)[SPW], const float4 (&wr)[T][SPW], f32x4 (&acc)[T],
+                                          float& fs1, float& fs2);
+
+template <int T, bool STATS>
 __device__ __forceinline__ void mfma_t(const float* A, int K16A, int rb, int kb, int w, const float4 (&wr)[T][SPW],
                                        f32x4 (&acc)[T], float& fs1, float& fs2) {
     float4 xv[SPW];
@@ -816,6 +826,15 @@ __device__ __forceinline__ void mfma_t(const float* A, int K16A, int rb, int kb,
     // scheduler interleaves them two at a time with the MFMAs (two dependent
     // round trips instead of one, seen in the gfx950 ISA of round 4)
     __builtin_amdgcn_sched_barrier(0);
+    mfma_regs<T, STATS>(xv, wr, acc, fs1, fs2);
+}
+
+// the T tiles' accumulator chains over the wave's 4 A fragments (each in the
+// one-shot order: steps in order, components x, y, z, w) and (STATS) the LN
+// row partial sums
+template <int T, bool STATS>
+__device__ __forceinline__ void mfma_regs(const float4 (&xv)[SPW], const float4 (&wr)[T][SPW], f32x4 (&acc)[T],
+                                          float& fs1, float& fs2) {
 #pragma unroll
     for (int t = 0; t < T; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -886,13 +905,43 @@ __device__ __forceinline__ void publish6(const KA& a, int ctr, bool did) {
     if (threadIdx.x == 0 && did) arrive6(a, ctr, 1);
 }
 
+// qkv epilogue store of 4 columns col..col+3 of `row` (NH = 12): q row-major,
+// or K / V of this token into the sequence's page of the layer at kv_next
+// (add_to_cache, paged_infer.c:505-573)
+template <int P, bool BF>
+__device__ __forceinline__ void qkv_store6(const KA& a, int row, int col, float4 v) {
+    constexpr int NH = 12, C = 768;
+    if (col < C) {
+        *reinterpret_cast<float4*>(a.q_out + (size_t)row * C + col) = v;
+        return;
+    }
+    const int kv = col >= 2 * C;
+    const int c = col - (kv ? 2 * C : C);
+    const int hh = c >> 6, d = c & 63;
+    const int ps = a.pos[row];
+    const int page = a.bt[(size_t)row * a.bt_stride + ps / P];
+    if (page < 0) return;
+    const int pslot = ps % P;
+    const size_t toff = (size_t)page * a.page_elems + ((size_t)kv * NH + hh) * P * 64;
+    if constexpr (BF) {
+        unsigned short* kvt = reinterpret_cast<unsigned short*>(a.kv_next) + toff +
+                              (kv == 0 ? ((d >> 3) * P + pslot) * 8 + (d & 7) : pslot * 64 + d);
+        const unsigned lo = hpa::f32_to_bf16(v.x) | ((unsigned)hpa::f32_to_bf16(v.y) << 16);
+        const unsigned hi = hpa::f32_to_bf16(v.z) | ((unsigned)hpa::f32_to_bf16(v.w) << 16);
+        *reinterpret_cast<uint2*>(kvt) = make_uint2(lo, hi);
+    } else {
+        float* kvt = reinterpret_cast<float*>(a.kv_next) + toff + (kv == 0 ? ((d >> 2) * P + pslot) * 4 : pslot * 64 + d);
+        *reinterpret_cast<float4*>(kvt) = v;
+    }
+}
+
 }  // namespace c6
 
 // TC, TD, TE: tiles per unit of fc, fcproj, qkv (NH = 12; attproj 1)
 template <int P, bool BF, int TC, int TD, int TE>
 __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
     using namespace c6;
-    constexpr int NH = 12, C = 768, K16 = 48, NCT = 48;
+    constexpr int C = 768, K16 = 48, NCT = 48;
     const KA& a = *(const KA*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
     (void)args;
     __shared__ Smem6 sm;
@@ -1079,37 +1128,77 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + w * 32);
         lds_barrier();
         PL_MARK(15);
-        if (ep && row < a.B) {
-            const float4 v = ln_fold4(sm.wsum, er, fold_t<T>(sm.red, et, er, eq), c1, c2);
-            if (col < C) {
-                *reinterpret_cast<float4*>(a.q_out + (size_t)row * C + col) = v;
-            } else {  // K/V of this token into the sequence's page of layer l+1 (add_to_cache)
-                const int kv = col >= 2 * C;
-                const int c = col - (kv ? 2 * C : C);
-                const int hh = c >> 6, d = c & 63;
-                const int ps = a.pos[row];
-                const int page = a.bt[(size_t)row * a.bt_stride + ps / P];
-                if (page >= 0) {
-                    const int pslot = ps % P;
-                    const size_t toff = (size_t)page * a.page_elems + ((size_t)kv * NH + hh) * P * 64;
-                    if constexpr (BF) {
-                        unsigned short* kvt = reinterpret_cast<unsigned short*>(a.kv_next) + toff +
-                                              (kv == 0 ? ((d >> 3) * P + pslot) * 8 + (d & 7) : pslot * 64 + d);
-                        const unsigned lo = hpa::f32_to_bf16(v.x) | ((unsigned)hpa::f32_to_bf16(v.y) << 16);
-                        const unsigned hi = hpa::f32_to_bf16(v.z) | ((unsigned)hpa::f32_to_bf16(v.w) << 16);
-                        *reinterpret_cast<uint2*>(kvt) = make_uint2(lo, hi);
-                    } else {
-                        float* kvt = reinterpret_cast<float*>(a.kv_next) + toff +
-                                     (kv == 0 ? ((d >> 2) * P + pslot) * 4 : pslot * 64 + d);
-                        *reinterpret_cast<float4*>(kvt) = v;
-                    }
-                }
-            }
-        }
+        if (ep && row < a.B)
+            qkv_store6<P, BF>(a, row, col, ln_fold4(sm.wsum, er, fold_t<T>(sm.red, et, er, eq), c1, c2));
     }
     PL_MARK(11);
 }
 
+
+// ------------------------------------------------------------------ the step's first launch (form 6)
+// embed (encoder_forward, paged_infer.c:41-47: wte[token] + wpe[pos] at the
+// absolute position) and layer 0's qkv in ONE launch, which also zeroes the
+// step's counter block and error word: was the embed kernel + the one-shot
+// qkv GEMM (two launches and a boundary, 4.3 + 9.4 us at B = 64).  The qkv is
+// chain form 6's phase E -- (row block, TE tiles) units, LN1 folded, q + K/V
+// of the token into layer 0's pages -- with each wave's A fragments built in
+// registers from the embedding instead of loaded; the tile group 0 unit of a
+// row block also stores the residual stream it built (frag layout, read by
+// layer 0's chain launch).  Rows >= B embed as 0 (padded rows stay 0).
+template <int P, bool BF, int TE>
+__global__ __launch_bounds__(768) void decode_first6_kernel(KA args) {
+    using namespace c6;
+    constexpr int C = 768, K16 = 48, NCT = 48;
+    const KA& a = *(const KA*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
+    (void)args;
+    __shared__ Smem6 sm;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int bid = blockIdx.x;
+    constexpr int T = TE, NG = 3 * NCT / TE;
+    constexpr bool NT = TE == 1;
+    const int g = bid % NG, rb = bid / NG;
+    // the row's token and position first: the embedding loads depend on them,
+    // and vmcnt retires in order, so behind the weight loads they would wait
+    // for those too
+    const int arow = rb * 16 + (lane & 15);
+    const bool live = rb < a.R && arow < a.B;
+    const int tok = live ? a.tokens[arow] : 0, ps = live ? a.pos[arow] : 0;
+    for (int i = bid * 768 + tid; i < a.zero_n4; i += (int)gridDim.x * 768) a.zero[i] = make_int4(0, 0, 0, 0);
+    if (rb >= a.R) return;  // no unit (the grid holds R * NG <= G of them; nothing here waits)
+    const int et = tid >> 6, er = (tid & 63) >> 2, eq = tid & 3;
+    const bool ep = tid < T * 64;
+    const int row = rb * 16 + er, col = (g * T + et) * 16 + 4 * eq;
+    float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f), c2 = c1;
+    if (ep) {
+        c1 = ld4(a.qkv_c1 + col);
+        c2 = ld4(a.qkv_c2 + col);
+    }
+    float4 wr[T][SPW];
+    load_wt<T, NT>(a.w_qkv, K16, g * T, 0, w, wr);
+    // A fragment of k16 step 4w + s: lane holds row 16 rb + (lane & 15),
+    // columns 16 (4w + s) + 4 (lane >> 4) .. + 3 (hpa::frag_index)
+    const float4* te = reinterpret_cast<const float4*>(a.wte + (size_t)tok * C) + (lane >> 4);
+    const float4* pe = reinterpret_cast<const float4*>(a.wpe + (size_t)ps * C) + (lane >> 4);
+    float4 xv[SPW];
+#pragma unroll
+    for (int s = 0; s < SPW; ++s) {
+        const float4 x = te[(w * SPW + s) * 4], y = pe[(w * SPW + s) * 4];
+        xv[s] = live ? make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (g == 0)
+#pragma unroll
+        for (int s = 0; s < SPW; ++s)
+            *reinterpret_cast<float4*>(a.res + ((size_t)(rb * K16 + w * SPW + s) * 64 + lane) * 4) = xv[s];
+    float fs1 = 0.f, fs2 = 0.f;
+    f32x4 acc[T];
+    mfma_regs<T, true>(xv, wr, acc, fs1, fs2);
+    put_red_t<T>(sm.red, w, acc);
+    hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + w * 32);
+    lds_barrier();
+    if (ep && row < a.B)
+        qkv_store6<P, BF>(a, row, col, ln_fold4(sm.wsum, er, fold_t<T>(sm.red, et, er, eq), c1, c2));
+}
 
 // ------------------------------------------------------------------ the chain for wide layers (form 8)
 // GPT-2 XL (C = 1600, NH = 25): the same persistent
@@ -1586,6 +1675,38 @@ int launch(const HpaLayerArgs* h, int G) {
     return 0;
 }
 
+template <int P, bool BF, int TE>
+int launch_first6(const HpaLayerArgs* h, int G, const int* tokens, const float* wte, const float* wpe, void* zero,
+                  size_t zero_bytes) {
+    HPA_REQUIRE(resident_blocks(decode_first6_kernel<P, BF, TE>) >= 1, "decode first: the workgroup does not fit a CU");
+    const int R = (h->B + 15) / 16;
+    HPA_REQUIRE(R * 144 / TE <= G, "decode first: a unit per workgroup");
+    KA a;
+    fill_ka(h, G, a);
+    a.last = 0;
+    a.kv_next = h->pool->base;  // layer 0's pages
+    a.tokens = tokens;
+    a.wte = wte;
+    a.wpe = wpe;
+    a.zero = reinterpret_cast<int4*>(zero);
+    a.zero_n4 = (int)(zero_bytes / 16);
+    decode_first6_kernel<P, BF, TE><<<G, 768, 0, hpa_stream()>>>(a);
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int P, bool BF>
+int dispatch_first6_t(const HpaLayerArgs* h, int G, const int* tokens, const float* wte, const float* wpe, void* zero,
+                      size_t zero_bytes) {
+    switch ((h->B + 15) / 16) {  // qkv tiles per unit as chain form 6's phase E
+        case 1: return launch_first6<P, BF, 1>(h, G, tokens, wte, wpe, zero, zero_bytes);
+        case 2: return launch_first6<P, BF, 2>(h, G, tokens, wte, wpe, zero, zero_bytes);
+        case 3: return launch_first6<P, BF, 2>(h, G, tokens, wte, wpe, zero, zero_bytes);
+        case 4: return launch_first6<P, BF, 3>(h, G, tokens, wte, wpe, zero, zero_bytes);
+        default: return hpa_fail(__FILE__, __LINE__, "decode first: B <= 64");
+    }
+}
+
 template <int P, bool BF, int TC, int TD, int TE>
 int launch6(const HpaLayerArgs* h, int G) {
     HPA_REQUIRE(resident_blocks(decode_chain6_kernel<P, BF, TC, TD, TE>) >= 1,
@@ -1790,6 +1911,33 @@ int hpa_decode_chain_eligible(int B, int C, int num_heads, int form) {
         return chainx_shape(B, num_heads, G, xt, xng) == 0 ? 1 : 0;
     }
     return 0;
+}
+
+int hpa_decode_first(const HpaLayerArgs* h, const int* tokens, const float* wte, const float* wpe, void* zero,
+                     size_t zero_bytes) {
+    HPA_REQUIRE(h && h->pool && h->pool->base && tokens && wte && wpe, "decode first: null operand");
+    const HpaKVPool* pool = h->pool;
+    HPA_REQUIRE(pool->dtype == HPA_F32 || pool->dtype == HPA_BF16, "decode first: fp32 or bf16 pool");
+    HPA_REQUIRE(h->num_heads == 12 && h->C == 768 && pool->head_size == HS && pool->num_heads == 12,
+                "decode first: C = 768, 12 heads of 64");
+    HPA_REQUIRE(h->B >= 1 && h->B <= 64, "decode first: 1..64 rows");
+    HPA_REQUIRE(h->res && h->w_qkv && h->qkv_c1 && h->qkv_c2 && h->q_out && h->block_table && h->pos,
+                "decode first: null operand");
+    HPA_REQUIRE(zero_bytes % 16 == 0 && ((size_t)zero & 15) == 0 && zero_bytes / 16 <= 0x7fffffff,
+                "decode first: the zeroed block must be whole 16-byte granules");
+    const int G = num_cus();
+    const bool bf = pool->dtype == HPA_BF16;
+    switch (pool->page_size) {
+        case 8: return bf ? dispatch_first6_t<8, true>(h, G, tokens, wte, wpe, zero, zero_bytes)
+                          : dispatch_first6_t<8, false>(h, G, tokens, wte, wpe, zero, zero_bytes);
+        case 16: return bf ? dispatch_first6_t<16, true>(h, G, tokens, wte, wpe, zero, zero_bytes)
+                           : dispatch_first6_t<16, false>(h, G, tokens, wte, wpe, zero, zero_bytes);
+        case 32: return bf ? dispatch_first6_t<32, true>(h, G, tokens, wte, wpe, zero, zero_bytes)
+                           : dispatch_first6_t<32, false>(h, G, tokens, wte, wpe, zero, zero_bytes);
+        case 64: return bf ? dispatch_first6_t<64, true>(h, G, tokens, wte, wpe, zero, zero_bytes)
+                           : dispatch_first6_t<64, false>(h, G, tokens, wte, wpe, zero, zero_bytes);
+        default: return hpa_fail(__FILE__, __LINE__, "decode first: page size must be 8, 16, 32 or 64");
+    }
 }
 
 int hpa_decode_layer(const HpaLayerArgs* h) {

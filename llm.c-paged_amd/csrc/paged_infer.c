@@ -1482,6 +1482,34 @@ static int dec_lane_layers(GPT2* model) {
     return rc;
 }
 
+#ifndef DEC_FIRST_LAUNCH
+#define DEC_FIRST_LAUNCH 1 /* A/B builds: 0 = the embed kernel + the one-shot qkv(0) GEMM */
+#endif
+/* the step's first launch under chain form 6 (hpa_decode_first): the
+ * embedding into res, layer 0's q and K/V (LN1 folded), and zb bytes of the
+ * counter block (error word + hand-off counters) zeroed */
+static int dec_first(GPT2* model, size_t zb) {
+    GPT2Decode* d = model->decode;
+    const GPT2Config c = model->config;
+    const ParameterTensors* w = &model->params;
+    const int C = c.channels;
+    HpaLayerArgs a;
+    memset(&a, 0, sizeof(a));
+    a.B = d->B;
+    a.C = C;
+    a.num_heads = c.num_heads;
+    a.pool = &d->pool;
+    a.block_table = d->d_bt;
+    a.bt_stride = d->bt_stride;
+    a.pos = d->d_pos;
+    a.res = d->res;
+    a.w_qkv = wpack_at(d, d->wpack_off[0]); /* layer 0 */
+    a.qkv_c1 = d->d_fold;
+    a.qkv_c2 = d->d_fold + 3 * C;
+    a.q_out = d->d_q;
+    return hpa_decode_first(&a, d->d_tokens, w->wte, w->wpe, d->pl_ctr, zb);
+}
+
 /* the whole step on the library stream */
 static int dec_launch(GPT2* model) {
     GPT2Decode* d = model->decode;
@@ -1492,13 +1520,18 @@ static int dec_launch(GPT2* model) {
     const int lanes = pl && d->lanes == 2 && !d->trace_x ? 2 : 1;
     /* persistent layers: the embed kernel also zeroes their hand-off counters */
     const size_t zb = (DEC_ERR_INTS + (size_t)lanes * L * d->pl_ctr_ints) * sizeof(int);
-    int rc = !pl ? hpa_embed_frag(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C)
-                 : hpa_embed_frag_zero(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C, d->pl_ctr, zb);
+    /* chain form 6 (and form 8 at C = 768, which sums as form 6): embed +
+     * qkv(0) + the counter zeroing in one launch */
+    const int first = pl && DEC_FIRST_LAUNCH && d->pl_on == 3 &&
+                      (d->pl_wform == 6 || (d->pl_wform == 8 && model->config.num_heads == 12));
+    int rc = first ? dec_first(model, zb)
+           : !pl   ? hpa_embed_frag(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C)
+                   : hpa_embed_frag_zero(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C, d->pl_ctr, zb);
 #define DEC_TRACE(i) \
     if (d->trace_x) rc |= hpa_unpack_frag(d->res, d->B, C, d->trace_x + (size_t)(i) * d->B * C, C)
     DEC_TRACE(0);
     if (pl) { /* qkv(0), then one persistent launch per layer */
-        rc |= dec_gemm(model, 0, G_QKV);
+        if (!first) rc |= dec_gemm(model, 0, G_QKV);
         if (lanes == 2) {
             rc |= dec_lane_layers(model);
         } else {

@@ -229,7 +229,7 @@ def test_chain6_rows_independent_of_batch_and_form4(hip):
     entering every layer (gpt2_decode_step_traced; the logits kernel's form
     follows the batch and is tested elsewhere) of B = 64 rows (4 row blocks,
     3 tiles per unit) equals that of B = 8 / 24 / 40 engines bit for bit; at
-    one row block form 6 equals form 4's 12-wave units in every logit; graph
+    one row block form 6 is form 4 within 2e-5 (layer 0's qkv differs: hpa_decode_first); graph
     replay = eager"""
     params = synth.params(GPT2_124M, seed=94)
     steps = 3
@@ -256,7 +256,12 @@ def test_chain6_rows_independent_of_batch_and_form4(hip):
         full = run(0, 64)  # (steps, L+1, B, C)
         for lo, hi in ((0, 8), (40, 64), (8, 48)):
             assert np.array_equal(full[:, :, lo:hi], run(lo, hi)), (lo, hi)
-        assert np.array_equal(run(0, 8, traced=False), run(0, 8, mode=4, traced=False))
+        # form 4 at one row block sums every layer GEMM like form 6's 12-wave
+        # units, but computes layer 0's qkv with the one-shot GEMM where form 6
+        # opens the step with hpa_decode_first (chain order, LN1 folded)
+        d = np.abs(run(0, 8, traced=False) - run(0, 8, mode=4, traced=False)).max()
+        print(f"form 6 vs form 4 at B=8: max |logit diff| {d:.3e}")
+        assert d <= 2e-5
         g64 = run(0, 64, traced=False)  # graph replay: its last step's residual feeds these logits
         assert np.isfinite(g64).all()
     finally:

@@ -1,14 +1,7 @@
 #!/bin/bash
-# round-4 evidence, part a: the full GPU suite, then profile_round.sh a (config 2:
-# bench + CPU baseline, rocprofv3 kernel stats, PMC traffic, MFMA busy, attention
-# scan, small batches), then emulated strong-scaling ranks
+# round-4 evidence, part a: the full GPU suite
 set -u
 o=gpurun_out/r4final; mkdir -p $o; export TMPDIR=/tmp
-timeout -k 10 700 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 300 --timeout-method thread -p no:cacheprovider > $o/pytest_gpu.txt 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 300 --timeout-method thread -p no:cacheprovider > $o/pytest_gpu.txt 2>&1
 rc=$?; tail -3 $o/pytest_gpu.txt; grep -E "^FAILED|^ERROR" $o/pytest_gpu.txt | head
-case $rc in 0|1) ;; *) exit $rc;; esac
-bash tools/profile_round.sh $o a || exit $?
-for n in 2 4 8; do
-  timeout -k 10 200 python -u bench.py --emulate-rank $n --scaling strong --cpu-baseline off > $o/emul$n.log 2>&1 || exit $?
-done
-grep -ho '"ms_per_step": [0-9.]*\|"projected_n_gpu_tokens_per_s": [0-9.]*' $o/emul*.log
+exit $rc
