@@ -644,6 +644,10 @@ struct GPT2Decode {
     int attn_splits;  /* context ranges per (sequence, head) of the decode attention */
     int attn_waves;   /* waves per attention workgroup (hpa_attn_pick_waves of the global batch) */
     void* d_attn_ws;  /* split records + counters (hpa_attn_ws_bytes at HPA_ATTN_MAX_SPLITS) */
+    int attn_flat_want; /* gpt2_decode_set_attn_flat: 0 auto, 1 off, 2 on */
+    int attn_flat;    /* in use: the balanced form (hpa_paged_attention_decode_flat) instead of the split grid */
+    void* d_flat_ws;  /* its records + counters (hpa_attn_flat_ws_bytes) */
+    size_t flat_ws_bytes;
     size_t attn_ws_bytes;
     int sample;       /* 0: greedy argmax; 1: multinomial with per-sequence xorshift */
     unsigned long long* d_rng; /* [B] sampler states */
@@ -787,7 +791,7 @@ static void dec_free(GPT2Decode* d) {
     hpa_free(d->ring_slab); hpa_free(d->ring_cnt);
     hpa_free(d->d_wpack);
     hpa_free(d->d_fold);
-    hpa_free(d->d_attn_ws);
+    hpa_free(d->d_attn_ws); hpa_free(d->d_flat_ws);
     hpa_free(d->pl_rec); hpa_free(d->pl_slab); hpa_free(d->pl_ctr);
     if (d->lane_stream) hpa_stream_destroy(d->lane_stream);
     for (int k = 0; k < 3; k++)
@@ -912,6 +916,21 @@ static int dec_set_splits(GPT2Decode* d, int splits) {
         d->attn_waves = hpa_attn_pick_waves(dec_pick_B(d), d->pool.num_heads, splits, ncu);
     }
     if (dec_lanes_setup(d)) return 1; /* lanes need one context range */
+    {   /* the balanced form on request only: measured slower than the
+         * (sequence, head, range) grid at every small batch (B = 4 / 8 / 16 /
+         * 21: 13.5 / 16.3 / 22.5 / 27.6 us against 9.8 / 13.0 / 19.4 / 23.7,
+         * profiles/r4/experiments/balanced_attention.txt): a run that spans
+         * two pairs folds and publishes them one after the other, so its
+         * dependent round trips add up.  Never under global picks (its sums
+         * depend on the whole batch's contexts). */
+        const int on = d->attn_flat_want == 2 && !d->pl_global_B;
+        if (on && !d->d_flat_ws) {
+            d->flat_ws_bytes = hpa_attn_flat_ws_bytes(d->B, d->pool.num_heads, d->max_ctx);
+            d->d_flat_ws = hpa_malloc(d->flat_ws_bytes);
+            if (!d->d_flat_ws || hpa_memset_async(d->d_flat_ws, 0, d->flat_ws_bytes)) return 1;
+        }
+        d->attn_flat = on && d->B <= 64;
+    }
     if (d->graph) { /* recapture with the new grid */
         hpa_synchronize();
         hpa_graph_destroy(d->graph);
@@ -1067,6 +1086,7 @@ static int dec_layer(GPT2* model, int l, int lane) {
 static int dec_rezero(GPT2Decode* d) {
     int rc = 0;
     if (d->d_attn_ws) rc |= hpa_memset_async(d->d_attn_ws, 0, d->attn_ws_bytes);
+    if (d->d_flat_ws) rc |= hpa_memset_async(d->d_flat_ws, 0, d->flat_ws_bytes);
     if (d->sk_cnt && d->sk_cnt_n) rc |= hpa_memset_async(d->sk_cnt, 0, d->sk_cnt_n * sizeof(int));
     if (d->ring_cnt && d->ring_cnt_n) rc |= hpa_memset_async(d->ring_cnt, 0, d->ring_cnt_n * sizeof(int));
     return rc;
@@ -1431,15 +1451,25 @@ static int dec_pick(GPT2* model, const int* active) {
     return hpa_argmax_final(d->part, npart, d->Mp, d->B, d->d_next, d->d_tokens, d->d_pos, active);
 }
 
+/* one decode-attention launch over rows [r0, r0 + nb) (frag output) in the
+ * engine's form: balanced (attn_flat) or the (sequence, head, range) grid */
+static int dec_attn_call(GPT2Decode* d, int l, int r0, int nb, const int* pos, float* out) {
+    const size_t C = (size_t)d->pool.num_heads * 64;
+    if (d->attn_flat)
+        return hpa_paged_attention_decode_flat(d->d_q + r0 * C, &d->pool, l, d->d_bt + (size_t)r0 * d->bt_stride,
+                                               d->bt_stride, pos, out, nb, d->max_ctx, d->d_flat_ws, 1, 0, 0);
+    return hpa_paged_attention_decode_split_w(d->d_q + r0 * C, &d->pool, l, d->d_bt + (size_t)r0 * d->bt_stride,
+                                              d->bt_stride, pos, out, nb, d->attn_splits, d->d_attn_ws, 1,
+                                              d->attn_waves);
+}
+
 static int dec_attention(GPT2* model, int l, int lane) {
     GPT2Decode* d = model->decode;
     const size_t C = (size_t)model->config.channels;
     int r0, nb, rc = 0;
     dec_lane_rows(d, lane, &r0, &nb);
     if (d->profiling) rc |= hpa_event_record(d->prof_ev[0]);
-    rc |= hpa_paged_attention_decode_split_w(d->d_q + r0 * C, &d->pool, l, d->d_bt + (size_t)r0 * d->bt_stride,
-                                             d->bt_stride, d->d_pos + r0, d->att + r0 * C, nb, d->attn_splits,
-                                             d->d_attn_ws, 1, d->attn_waves);
+    rc |= dec_attn_call(d, l, r0, nb, d->d_pos + r0, d->att + r0 * C);
     if (d->profiling) {
         rc |= hpa_event_record(d->prof_ev[1]);
         const float ms = hpa_event_elapsed_ms(d->prof_ev[0], d->prof_ev[1]); /* waits for this launch */
@@ -1613,6 +1643,19 @@ int gpt2_decode_set_attn_splits(GPT2* model, int splits) {
 }
 
 int gpt2_decode_attn_splits(GPT2* model) { return model->decode ? model->decode->attn_splits : 0; }
+
+/* the balanced attention form (hpa_paged_attention_decode_flat): 0 auto (=
+ * off: measured slower), 1 off, 2 on (not under global picks);
+ * gpt2_decode_attn_flat: in use */
+int gpt2_decode_set_attn_flat(GPT2* model, int mode) {
+    GPT2Decode* d = model ? model->decode : NULL;
+    if (!d || mode < 0 || mode > 2) return 1;
+    if (hpa_synchronize()) return 1;
+    d->attn_flat_want = mode;
+    return dec_set_splits(d, d->attn_splits);
+}
+
+int gpt2_decode_attn_flat(GPT2* model) { return model && model->decode ? model->decode->attn_flat : 0; }
 
 /* waves per attention workgroup the engine picked (hpa_set_attention_waves may override it) */
 int gpt2_decode_attn_waves(GPT2* model) { return model->decode ? model->decode->attn_waves : 0; }
@@ -2082,12 +2125,9 @@ int gpt2_decode_time_attention(GPT2* model, int iters, double* ms_per_launch, do
         for (int b = 0; b < B; b++) h_p[b] = d->h_pos[b] - 1;
         rc |= hpa_memcpy(d_p, h_p, B * sizeof(int));
         /* warm-up launch, then the timed ones */
-        rc |= hpa_paged_attention_decode_split_w(d->d_q, &d->pool, 0, d->d_bt, d->bt_stride, d_p, out, B,
-                                                 d->attn_splits, d->d_attn_ws, 1, d->attn_waves);
+        rc |= dec_attn_call(d, 0, 0, B, d_p, out);
         rc |= hpa_event_record(e0);
-        for (int i = 0; i < iters && !rc; i++)
-            rc |= hpa_paged_attention_decode_split_w(d->d_q, &d->pool, i % L, d->d_bt, d->bt_stride, d_p, out, B,
-                                                     d->attn_splits, d->d_attn_ws, 1, d->attn_waves);
+        for (int i = 0; i < iters && !rc; i++) rc |= dec_attn_call(d, i % L, 0, B, d_p, out);
         rc |= hpa_event_record(e1);
         const float ms = rc ? -1.f : hpa_event_elapsed_ms(e0, e1);
         if (ms < 0) rc = 1;
@@ -2133,8 +2173,7 @@ int gpt2_decode_time_attention_pf(GPT2* model, int iters, double frac, int pf_gr
             rc |= hpa_event_record(e[0]);
             if (nb) rc |= hpa_l3_prefetch((const char*)d->pool.base + (size_t)l * slab, nb, pf_grid);
             rc |= hpa_event_record(e[1]);
-            rc |= hpa_paged_attention_decode_split_w(d->d_q, &d->pool, l, d->d_bt, d->bt_stride, d_p, out, B,
-                                                     d->attn_splits, d->d_attn_ws, 1, d->attn_waves);
+            rc |= dec_attn_call(d, l, 0, B, d_p, out);
             rc |= hpa_event_record(e[2]);
             if (rc) break;
             const float a = hpa_event_elapsed_ms(e[1], e[2]), p = hpa_event_elapsed_ms(e[0], e[1]);
