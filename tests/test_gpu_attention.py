@@ -278,6 +278,18 @@ def test_flat_attention(hip, P, workgroups, waves):
     assert np.abs(out - ref).max() <= TOL
 
 
+@pytest.mark.parametrize("P", [8, 16, 32])
+@pytest.mark.parametrize("workgroups", [0, 64])
+@pytest.mark.parametrize("bf16", [False, True])
+def test_flat16_attention(hip, P, workgroups, bf16):
+    """the balanced form's 16-wave kernel (every tile of a run in flight, one
+    tile per wave, pieces folded by their first wave): ragged contexts, runs
+    spanning several pairs at 64 workgroups, fp32 and bf16 pools"""
+    ctxs = [1, 2, 5, 63, 64, 65, 200, 257, 1024]
+    out, ref = _run_case(hip, P, ctxs, NH=3, waves=16, seed=P + workgroups, flat=workgroups, repeat=3, bf16=bf16)
+    assert np.abs(out - ref).max() <= TOL
+
+
 @pytest.mark.parametrize("workgroups", [0, 5])
 def test_flat_attention_bf16_pool_and_peaked(hip, workgroups):
     ctxs = [1, 2, 7, 63, 64, 65, 200, 257, 1024]
@@ -292,8 +304,9 @@ def test_flat_attention_strong_scaling_shapes(hip, B):
     """the small per-GPU batches at GPT-2 124M shapes (ctx 1024, page 16,
     ragged) on the balanced form: every sequence vs the oracle"""
     ctxs = [1024 - 37 * i for i in range(B)]
-    out, ref = _run_case(hip, 16, ctxs, NH=12, seed=B, flat=0, repeat=2)
-    assert np.abs(out - ref).max() <= TOL
+    for waves in (0, 4):  # 0: the 16-wave kernel where runs fit 16 tiles (here), else 4 waves
+        out, ref = _run_case(hip, 16, ctxs, NH=12, waves=waves, seed=B, flat=0, repeat=2)
+        assert np.abs(out - ref).max() <= TOL, waves
 
 
 @pytest.mark.parametrize("P", [8, 16, 32])

@@ -23,7 +23,7 @@ for B in batches:
     auto = m.attn_flat()
     for flat in (1, 2):
         m.set_attn_flat(flat)
-        for nw in (4, 8):
+        for nw in ((4, 8) if flat == 1 else (0, 4, 8)):  # balanced, 0: the 16-wave kernel where it fits
             pa.check(pa.lib().hpa_set_attention_waves(nw), "waves")
             ms, by = m.time_attention(48)
             form = "balanced" if flat == 2 else f"grid S={m.attn_splits()}"
