@@ -737,12 +737,25 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
 //   * waits are per row block (fcproj: per row block and K part): a unit
 //     waits only for the producers of the rows it reads.
 // T per phase (host, chain6_tiles): the fewest tiles with units <= workgroups.
+#ifndef HPA_C6_GW
+#define HPA_C6_GW 1  // 1: fc / fcproj / qkv wait per 64-column k-group of their A (wave w on its group); 0: per row block (A/B)
+#endif
 namespace c6 {
 constexpr int NW = 12;  // waves per workgroup = waves per unit
 constexpr int SPW = 4;  // k16 steps per wave of a K = 768 range (48 / 12)
 // wait counters: X1 per row block, H per (row block, K part), X2 per row block
 enum { X1 = 0, H = 4, X2 = 20, NCTR = 24 };
 constexpr int kCtr = NCTR * 8 * kPad;  // ints of the sharded counters
+// HPA_C6_GW: 16-column tiles landed per (row block, 64-column k-group) of each
+// phase's A, after the tickets: res2 for fc (12 groups per row block), fch for
+// fcproj (48), res for qkv (12); one 128-B line each
+constexpr int kGC = 0, kGD = 4 * NW * kPad, kGE = kGD + 4 * 4 * NW * kPad;
+constexpr int kGrp = kGE + 4 * NW * kPad;
+__device__ __forceinline__ void arrive_tiles(const KA& a, int base, int rb, int groups_per_rb, int j0, int n) {
+    for (int t = j0; t < j0 + n; ++t)  // tile t of the row block lands in group t / 4
+        __hip_atomic_fetch_add(a.ctr + base + (rb * groups_per_rb + t / 4) * kPad, 1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+}
 
 struct Smem6 {
     float red[NW * 3 * 256];  // [wave][tile][256] accumulators
@@ -750,6 +763,7 @@ struct Smem6 {
     float tile[3 * 16 * 17];  // last layer: [tile][16 rows][17] for the LNf statistics
     int s_ok;
     int s_last;
+    int s_ready;  // HPA_C6_GW: k-groups seen ready by wave 0 (bit 12: the wait failed)
 };
 
 __device__ __forceinline__ void arrive6(const KA& a, int ctr, int n) {
@@ -794,6 +808,51 @@ __device__ __forceinline__ bool wait6(const KA& a, int ctr, int expected, int co
     const bool ok = sm.s_ok != 0;
     lds_barrier();
     return ok;
+}
+
+// HPA_C6_GW: wave 0 polls the 12 k-group counters of a row block (lane k:
+// group k) and publishes the ready set in LDS; wave w goes on as soon as its
+// group is in it, so a wave whose producers finished early starts its A loads
+// and MFMAs early (the late waves then share the matrix pipe with fewer).
+// Bounded like wait6; a failure releases every wave with bit 12 set.
+__device__ __forceinline__ bool wait_grp(const KA& a, int base, int expected, int code, Smem6& sm) {
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    volatile int* rdy = &sm.s_ready;
+    if (wv == 0) {
+        const int lane = threadIdx.x & 63;
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        int fail = 0;
+        for (unsigned it = 0;; ++it) {
+            const int v = lane < NW ? __hip_atomic_load(a.ctr + base + lane * kPad, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)
+                                    : expected;
+            const int m = (int)(__ballot(v >= expected) & 0xFFFull);
+            if (lane == 0) *rdy = m;
+            if (m == 0xFFF) break;
+            if ((it & 7) == 7) {
+                const int e = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if (e) {
+                    fail = 1;
+                    break;
+                }
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+                    if (lane == 0) {
+                        atomicCAS(a.err, 0, code);
+                        if (a.err_sticky) atomicCAS(a.err_sticky, 0, code);
+                    }
+                    fail = 1;
+                    break;
+                }
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (fail && lane == 0) *rdy = 0x1FFF;
+        return !fail;
+    }
+    int r;
+    while (!(((r = *rdy) >> wv) & 1)) __builtin_amdgcn_s_sleep(1);
+    return !(r >> 12);
 }
 
 // the wave's weight fragments of tiles j0 .. j0+T-1, k16 steps kb + 4w ..
@@ -950,9 +1009,14 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
     const int bid = blockIdx.x;
     const int R = a.R;
     constexpr bool NT = TC == 1 && TD == 1 && TE == 1;  // the one-row-block instantiation: every tile read once
+    // k-group waits (HPA_C6_GW): fc always; fcproj and qkv at <= 2 row blocks
+    // (B <= 32: -1.5 % / -3.3 % per step at B = 32 / 8; at B = 64 they cost
+    // what fc's gains, profiles/r4/kgroup_waits.txt)
+    constexpr bool GDE = HPA_C6_GW && TC < 3;
     // epilogue thread's place: tile et, row er, column quad eq
     const int et = tid >> 6, er = (tid & 63) >> 2, eq = tid & 3;
     int* tick = a.ctr + kCtr;  // fcproj K-part tickets [R][NCT / TD]
+    if (HPA_C6_GW && tid == 0) sm.s_ready = 0;  // read first in phase C, after phase B's barriers
     PL_STAMP(t_start);
     PL_STORE(0, t_start);
     float fs1 = 0.f, fs2 = 0.f;
@@ -987,7 +1051,13 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             hpa::store_wt16(a.res2, fi, v);
         }
         PL_MARK(12);
-        publish6(a, X1 + rb, has);
+        if (HPA_C6_GW) {  // the tile's k-group of fc's A
+            drain_vm();
+            lds_barrier();
+            if (tid == 0 && has) arrive_tiles(a, kCtr + 4 * NCT + kGC, rb, NW, g, 1);
+        } else {
+            publish6(a, X1 + rb, has);
+        }
     }
     PL_MARK(5);
     // C: fc(l): fch = gelu(LN2(res2) . Wfc^T + b), LN folded; T = TC tiles
@@ -1005,7 +1075,11 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         }
         float4 wr[T][SPW];
         if (has) load_wt<T, NT>(a.w_fc, K16, g * T, 0, w, wr);
-        if (!wait6(a, X1 + (has ? rb : 0), has ? NCT : 0, 2, sm)) return;
+        if (HPA_C6_GW) {
+            if (has && !wait_grp(a, kCtr + 4 * NCT + kGC + rb * NW * kPad, 4, 2, sm)) return;
+        } else if (!wait6(a, X1 + (has ? rb : 0), has ? NCT : 0, 2, sm)) {
+            return;
+        }
         PL_MARK(6);
         fs1 = fs2 = 0.f;
         if (has) {
@@ -1015,6 +1089,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         }
         hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + w * 32);
         lds_barrier();
+        if (GDE && tid == 0) sm.s_ready = 0;  // every wave is past fc's wait; read again in fcproj's
         if (ep) {
             float4 v = ln_fold4(sm.wsum, er, fold_t<T>(sm.red, et, er, eq), c1, c2);
             const bool live = row < a.B;
@@ -1023,7 +1098,13 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             hpa::store_wt16(a.fch, (int)(hpa::frag_index(row, col, 4 * C) * 4), v);
         }
         PL_MARK(13);
-        publish6(a, H + rb * 4 + (g * T) / NCT, has);  // the K part of fcproj these columns feed
+        if (GDE) {  // the tiles' k-groups of fcproj's A (48 per row block)
+            drain_vm();
+            lds_barrier();
+            if (tid == 0 && has) arrive_tiles(a, kCtr + 4 * NCT + kGD, rb, 4 * NW, g * T, T);
+        } else {
+            publish6(a, H + rb * 4 + (g * T) / NCT, has);  // the K part of fcproj these columns feed
+        }
         PL_MARK(7);
     }
     // D: fcproj(l), K part p of 4, T = TD tiles: partial tiles -> slab; the
@@ -1039,7 +1120,11 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         if (ep) bv = ld4(a.b_fp + col);
         float4 wr[T][SPW];
         if (has) load_wt<T, NT>(a.w_fp, 4 * K16, g * T, p * K16, w, wr);
-        if (!wait6(a, H + (has ? rb * 4 + p : 0), has ? 4 * NCT / TC / 4 : 0, 3, sm)) return;
+        if (GDE) {
+            if (has && !wait_grp(a, kCtr + 4 * NCT + kGD + (rb * 4 * NW + p * NW) * kPad, 4, 3, sm)) return;
+        } else if (!wait6(a, H + (has ? rb * 4 + p : 0), has ? 4 * NCT / TC / 4 : 0, 3, sm)) {
+            return;
+        }
         PL_MARK(8);
         if (has) {
             f32x4 acc[T];
@@ -1047,6 +1132,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             put_red_t<T>(sm.red, w, acc);
         }
         lds_barrier();
+        if (GDE && tid == 0) sm.s_ready = 0;  // every wave is past fcproj's wait; read again in qkv's
         float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
         const int sx = (((p * R + rb) * NG + g) * T * 64 + tid) * 4;  // this part's float4 in the slab (float index)
         if (ep) {
@@ -1099,7 +1185,12 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             a.stats_out[((size_t)j * a.Mp + rr) * 2] = s1;
             a.stats_out[((size_t)j * a.Mp + rr) * 2 + 1] = s2;
         }
-        if (tid == 0 && last) arrive6(a, X2 + rb, 1);
+        if (tid == 0 && last) {
+            if (GDE)
+                arrive_tiles(a, kCtr + 4 * NCT + kGE, rb, NW, g * T, T);  // the tiles' k-groups of qkv's A
+            else
+                arrive6(a, X2 + rb, 1);
+        }
         PL_MARK(9);
     }
     // E: qkv(l+1), T = TE tiles: LN1 folded, q + K/V appended into layer l+1's pages
@@ -1117,7 +1208,11 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         }
         float4 wr[T][SPW];
         if (has) load_wt<T, NT>(a.w_qkv, K16, g * T, 0, w, wr);
-        if (!wait6(a, X2 + (has ? rb : 0), has ? NCT / TD : 0, 4, sm)) return;
+        if (GDE) {
+            if (has && !wait_grp(a, kCtr + 4 * NCT + kGE + rb * NW * kPad, 4, 4, sm)) return;
+        } else if (!wait6(a, X2 + (has ? rb : 0), has ? NCT / TD : 0, 4, sm)) {
+            return;
+        }
         PL_MARK(10);
         fs1 = fs2 = 0.f;
         if (has) {
@@ -1869,7 +1964,7 @@ int hpa_decode_layer_sizes(int B, int C, int num_heads, int splits, size_t* out3
     out3[0] = (size_t)B * num_heads * splits * kRec;
     out3[1] = (size_t)4 * R * nct * 256;  // fcproj K-part partial tiles
     const size_t ints5 = (size_t)kCtrInts + 2 * (size_t)R * nct + (size_t)B * num_heads;
-    const size_t ints6 = (size_t)c6::kCtr + (size_t)R * nct;  // chain form 6: per-row-block counters + tickets
+    const size_t ints6 = (size_t)c6::kCtr + (size_t)4 * nct + c6::kGrp;  // form 6: counters, tickets [4][nct], k-groups
     const size_t ints = ints5 > ints6 ? ints5 : ints6;
     out3[2] = (ints + 31) / 32 * 32;  // whole 128-B lines (memset in multiples of 16 B)
     return 0;
