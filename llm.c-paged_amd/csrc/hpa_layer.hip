@@ -737,6 +737,9 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
 //   * waits are per row block (fcproj: per row block and K part): a unit
 //     waits only for the producers of the rows it reads.
 // T per phase (host, chain6_tiles): the fewest tiles with units <= workgroups.
+#ifndef HPA_C6_DE
+#define HPA_C6_DE 0  // A/B builds: bit 0 fcproj, bit 1 qkv k-group waits at 3-4 row blocks as well
+#endif
 #ifndef HPA_C6_GW
 #define HPA_C6_GW 1  // 1: fc / fcproj / qkv wait per 64-column k-group of their A (wave w on its group); 0: per row block (A/B)
 #endif
@@ -1013,6 +1016,8 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
     // (B <= 32: -1.5 % / -3.3 % per step at B = 32 / 8; at B = 64 they cost
     // what fc's gains, profiles/r4/kgroup_waits.txt)
     constexpr bool GDE = HPA_C6_GW && TC < 3;
+    constexpr bool GD = GDE || (HPA_C6_GW && (HPA_C6_DE & 1));  // A/B builds: fcproj / qkv k-group waits
+    constexpr bool GE = GDE || (HPA_C6_GW && (HPA_C6_DE & 2));  // at 3-4 row blocks too
     // epilogue thread's place: tile et, row er, column quad eq
     const int et = tid >> 6, er = (tid & 63) >> 2, eq = tid & 3;
     int* tick = a.ctr + kCtr;  // fcproj K-part tickets [R][NCT / TD]
@@ -1089,7 +1094,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         }
         hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + w * 32);
         lds_barrier();
-        if (GDE && tid == 0) sm.s_ready = 0;  // every wave is past fc's wait; read again in fcproj's
+        if (GD && tid == 0) sm.s_ready = 0;  // every wave is past fc's wait; read again in fcproj's
         if (ep) {
             float4 v = ln_fold4(sm.wsum, er, fold_t<T>(sm.red, et, er, eq), c1, c2);
             const bool live = row < a.B;
@@ -1098,7 +1103,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             hpa::store_wt16(a.fch, (int)(hpa::frag_index(row, col, 4 * C) * 4), v);
         }
         PL_MARK(13);
-        if (GDE) {  // the tiles' k-groups of fcproj's A (48 per row block)
+        if (GD) {  // the tiles' k-groups of fcproj's A (48 per row block)
             drain_vm();
             lds_barrier();
             if (tid == 0 && has) arrive_tiles(a, kCtr + 4 * NCT + kGD, rb, 4 * NW, g * T, T);
@@ -1120,7 +1125,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         if (ep) bv = ld4(a.b_fp + col);
         float4 wr[T][SPW];
         if (has) load_wt<T, NT>(a.w_fp, 4 * K16, g * T, p * K16, w, wr);
-        if (GDE) {
+        if (GD) {
             if (has && !wait_grp(a, kCtr + 4 * NCT + kGD + (rb * 4 * NW + p * NW) * kPad, 4, 3, sm)) return;
         } else if (!wait6(a, H + (has ? rb * 4 + p : 0), has ? 4 * NCT / TC / 4 : 0, 3, sm)) {
             return;
@@ -1132,7 +1137,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             put_red_t<T>(sm.red, w, acc);
         }
         lds_barrier();
-        if (GDE && tid == 0) sm.s_ready = 0;  // every wave is past fcproj's wait; read again in qkv's
+        if ((GD || GE) && tid == 0) sm.s_ready = 0;  // every wave is past fcproj's wait; read again in qkv's
         float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
         const int sx = (((p * R + rb) * NG + g) * T * 64 + tid) * 4;  // this part's float4 in the slab (float index)
         if (ep) {
@@ -1186,7 +1191,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             a.stats_out[((size_t)j * a.Mp + rr) * 2 + 1] = s2;
         }
         if (tid == 0 && last) {
-            if (GDE)
+            if (GE)
                 arrive_tiles(a, kCtr + 4 * NCT + kGE, rb, NW, g * T, T);  // the tiles' k-groups of qkv's A
             else
                 arrive6(a, X2 + rb, 1);
@@ -1208,7 +1213,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         }
         float4 wr[T][SPW];
         if (has) load_wt<T, NT>(a.w_qkv, K16, g * T, 0, w, wr);
-        if (GDE) {
+        if (GE) {
             if (has && !wait_grp(a, kCtr + 4 * NCT + kGE + rb * NW * kPad, 4, 4, sm)) return;
         } else if (!wait6(a, X2 + (has ? rb : 0), has ? NCT / TD : 0, 4, sm)) {
             return;
