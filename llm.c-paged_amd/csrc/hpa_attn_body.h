@@ -13,9 +13,17 @@ constexpr int HS = 64;
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 // K/V rows are streamed once per step by the one workgroup of their
-// (sequence, head): non-temporal loads (MI355X_MICROARCH.md "nt-weights")
+// (sequence, head): non-temporal loads (MI355X_MICROARCH.md "nt-weights";
+// -DHPA_ATTN_NT=0: default-policy loads, an A/B build)
+#ifndef HPA_ATTN_NT
+#define HPA_ATTN_NT 1
+#endif
 __device__ __forceinline__ float4 load_stream(const float* ptr) {
+#if HPA_ATTN_NT
     const f32x4v v = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(ptr));
+#else
+    const f32x4v v = *reinterpret_cast<const f32x4v*>(ptr);
+#endif
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
