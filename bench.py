@@ -116,6 +116,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--spinup", type=float, default=0.0,
+                    help="seconds of untimed decode steps before the warm-up (positions reset to the start "
+                         "afterwards, so the timed steps decode at the same positions): a fresh box's first "
+                         "seconds of load run slower")
     ap.add_argument("--batch", type=int, default=64,
                     help="sequences per GPU (--scaling weak, the default: the metric's B=64 on every GPU) or in "
                          "total (strong)")
@@ -358,6 +362,17 @@ def main():
             print(f"[bench] rank {rank}: {e} after the {where}; no value reported", file=sys.stderr, flush=True)
             sys.exit(5)
 
+    if args.spinup > 0:  # untimed, before the warm-up; the positions go back to `start` after it
+        one_step(first)
+        sync()
+        t_spin = time.perf_counter() + args.spinup
+        while time.perf_counter() < t_spin:
+            for _ in range(16):
+                one_step(None)
+            sync()
+        model.set_positions(np.full(B_local, start, np.int32))
+        pos_now[0] = start
+        sync()
     one_step(first)
     for _ in range(args.warmup - 1 if args.warmup > 0 else 0):
         one_step(None)
@@ -434,6 +449,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "spinup_s": args.spinup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": args.scaling,
