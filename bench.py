@@ -116,7 +116,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--spinup", type=float, default=0.0,
+    ap.add_argument("--spinup", type=float, default=2.0,
                     help="seconds of untimed decode steps before the warm-up (positions reset to the start "
                          "afterwards, so the timed steps decode at the same positions): a fresh box's first "
                          "seconds of load run slower")
@@ -363,15 +363,20 @@ def main():
             sys.exit(5)
 
     if args.spinup > 0:  # untimed, before the warm-up; the positions go back to `start` after it
-        one_step(first)
+        # local steps only (no gather: ranks may run different counts in the
+        # same time, and a collective must be called by every rank alike)
+        model.step_async(first)
         sync()
-        t_spin = time.perf_counter() + args.spinup
+        t_spin, p = time.perf_counter() + args.spinup, start + 1
         while time.perf_counter() < t_spin:
             for _ in range(16):
-                one_step(None)
+                if p >= ctx:
+                    model.set_positions(np.full(B_local, start, np.int32))
+                    p = start
+                model.step_async(None)
+                p += 1
             sync()
         model.set_positions(np.full(B_local, start, np.int32))
-        pos_now[0] = start
         sync()
     one_step(first)
     for _ in range(args.warmup - 1 if args.warmup > 0 else 0):
