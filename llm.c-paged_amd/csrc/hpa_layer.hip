@@ -1016,8 +1016,8 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
     // (B <= 32: -1.5 % / -3.3 % per step at B = 32 / 8; at B = 64 they cost
     // what fc's gains, profiles/r4/kgroup_waits.txt)
     constexpr bool GDE = HPA_C6_GW && TC < 3;
-    constexpr bool GD = GDE || (HPA_C6_GW && (HPA_C6_DE & 1));  // A/B builds: fcproj / qkv k-group waits
-    constexpr bool GE = GDE || (HPA_C6_GW && (HPA_C6_DE & 2));  // at 3-4 row blocks too
+    constexpr bool GD = GDE || (HPA_C6_GW != 0 && (HPA_C6_DE & 1) != 0);  // A/B builds: fcproj / qkv k-group waits
+    constexpr bool GE = GDE || (HPA_C6_GW != 0 && (HPA_C6_DE & 2) != 0);  // at 3-4 row blocks too
     // epilogue thread's place: tile et, row er, column quad eq
     const int et = tid >> 6, er = (tid & 63) >> 2, eq = tid & 3;
     int* tick = a.ctr + kCtr;  // fcproj K-part tickets [R][NCT / TD]
