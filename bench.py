@@ -3,11 +3,13 @@
 
 Metric (BASELINE.json): decode tokens/sec, GPT-2 124M paged attention,
 B=64, ctx 1024, page 16, fp32, on 1/2/4/8 MI355X (configs[1] at N=1).  For
-N>1 the decode shards by sequence: every rank decodes its own
-64 sequences from its own page pool with replicated weights (weak scaling,
-the default: the north star partitions the pool and the batch by sequence;
-BASELINE configs[3] = B 512 at 8 GPUs); --scaling strong splits the metric's
-B = 64 over the ranks instead (--emulate-rank N times one such rank).  The one
+N>1 the decode shards by sequence: the metric's B = 64 is split
+over the N ranks (strong scaling, the default: BASELINE.md section 3's 2/4/8-GPU
+rows, 32/16/8 sequences per rank), each rank decoding its own rows from its
+own page pool with replicated weights.  --scaling weak gives every rank 64
+sequences instead (BASELINE configs[3]: B = 512 at 8 GPUs) and prints that
+config's own metric string, not the headline's.  --emulate-rank N times rank
+0's engine of an N-GPU run on one GPU.  The one
 collective is the end-of-step gather of the logits to rank 0 (--gather ids:
 the greedy ids only), run by the C library over RCCL/xGMI
 (gpt2_decode_gather: double-buffered on its own stream, so step k's gather
@@ -43,6 +45,8 @@ sys.path.insert(0, os.path.join(REPO, "llm.c-paged_amd"))
 import numpy as np  # noqa: E402
 
 METRIC = "decode tokens/sec GPT-2 124M paged-attn, B=64 T=1024, 1/2/4/8 MI355X"
+# --scaling weak at N > 1 is BASELINE configs[3] (64 sequences per GPU), not the headline metric
+METRIC_WEAK = "decode tokens/sec GPT-2 124M paged-attn, B=64 per GPU (B=512 at 8 GPUs), T=1024, N MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -121,12 +125,12 @@ def parse():
                          "afterwards, so the timed steps decode at the same positions): a fresh box's first "
                          "seconds of load run slower")
     ap.add_argument("--batch", type=int, default=64,
-                    help="sequences per GPU (--scaling weak, the default: the metric's B=64 on every GPU) or in "
-                         "total (strong)")
-    ap.add_argument("--scaling", default="weak", choices=["strong", "weak"],
-                    help="weak (default): --batch sequences per GPU, the page pool and the batch partition "
-                         "across ranks by sequence (BASELINE configs[3] at N=8: 64 x 8 = 512); strong: --batch in "
-                         "total, split over the ranks")
+                    help="sequences in total, split over the ranks (--scaling strong, the default: the metric's "
+                         "B=64), or per GPU (--scaling weak)")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong (default, the metric's 2/4/8-GPU points): --batch in total, split over the "
+                         "ranks; weak: --batch sequences per GPU (BASELINE configs[3] at N=8: 64 x 8 = 512), "
+                         "reported under configs[3]'s own metric string")
     ap.add_argument("--ctx", type=int, default=1024)
     ap.add_argument("--page-size", type=int, default=16)
     ap.add_argument("--kv-dtype", default="f32", choices=["f32", "bf16"],
@@ -445,10 +449,11 @@ def main():
                     "traffic_source": tsrc, "avg_launch_ms": round(attn["avg_ms"], 5),
                     "bytes_per_launch": int(attn["per_launch_bytes"]), "launches_timed": attn["launches"]}
         step_bytes = 0.5 * (bytes_before + bytes_after)
+        weak_n = layout_world > 1 and args.scaling == "weak"
         which = ("configs[4]" if kv_bf16 else "configs[2]" if args.model == "XL" else
-                 "configs[1]" if layout_world == 1 or args.scaling == "strong" else "configs[3]: per-seq sharded pool")
+                 "configs[3]: per-seq sharded pool" if weak_n else "configs[1]")
         result = {
-            "metric": METRIC,
+            "metric": METRIC_WEAK if weak_n else METRIC,
             "value": round(tokens_per_s, 1),
             "unit": "tokens/s",
             "n_gpus": world,

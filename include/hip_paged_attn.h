@@ -493,6 +493,24 @@ int    hpa_comm_gatherv(const void* send, size_t send_bytes, void* recv, const s
  * arguments.  *own_off = root's own rows' offset (its local copy). */
 int    hpa_comm_gather_layout(int nranks, int rank, int root, const size_t* bytes_per_rank, size_t* recv_off,
                               size_t* own_off);
+/* the gather's schedule, host arithmetic only: the point-to-point operations
+ * THIS rank posts for one hpa_comm_gatherv, in posting order.  hpa_comm_gatherv
+ * executes exactly this list (ncclSend / ncclRecv inside one NCCL group, then
+ * the root's local copy), so a host transport can run the same schedule (the
+ * world-size-2..4 gloo tests, tests/test_multi_rank.py).  SEND: send_bytes of
+ * the send buffer to `peer` (offset 0); RECV: `bytes` from `peer` at `offset`
+ * of recv; COPY (root): its own rows into recv at `offset`.  Zero-byte
+ * operations are never listed.  Returns the operation count (<= nranks), -1 on
+ * bad arguments or when max_ops is too small (ops may be NULL to count). */
+enum { HPA_COMM_SEND = 0, HPA_COMM_RECV = 1, HPA_COMM_COPY = 2 };
+typedef struct {
+    int op;        /* HPA_COMM_* */
+    int peer;      /* the other rank (COPY: this rank) */
+    size_t offset; /* byte offset in recv (SEND: 0, in send) */
+    size_t bytes;
+} HpaCommOp;
+int    hpa_comm_gather_plan(int nranks, int rank, int root, const size_t* bytes_per_rank, HpaCommOp* ops,
+                            int max_ops);
 /* timing helpers over the communicator (RCCL all-reduce on the library
  * stream, then a host wait): a barrier, and the maximum of one host double
  * over the ranks (bench.py's max-over-ranks step time) */

@@ -97,33 +97,62 @@ int hpa_comm_gather_layout(int nranks, int rank, int root, const size_t* bytes_p
     return posts;
 }
 
+int hpa_comm_gather_plan(int nranks, int rank, int root, const size_t* bytes_per_rank, HpaCommOp* ops,
+                         int max_ops) {
+    if (nranks < 1 || rank < 0 || rank >= nranks || root < 0 || root >= nranks || !bytes_per_rank || max_ops < 0)
+        return -1;
+    int n = 0;
+    const auto put = [&](int op, int peer, size_t off, size_t bytes) {
+        if (ops && n < max_ops) ops[n] = HpaCommOp{op, peer, off, bytes};
+        ++n;
+    };
+    if (rank != root) {
+        if (bytes_per_rank[rank]) put(HPA_COMM_SEND, root, 0, bytes_per_rank[rank]);
+    } else {
+        size_t off = 0;  // rank order: rank q's rows at sum(bytes[0..q-1]) (hpa_comm_gather_layout)
+        for (int q = 0; q < nranks; ++q) {
+            if (q != root && bytes_per_rank[q]) put(HPA_COMM_RECV, q, off, bytes_per_rank[q]);
+            off += bytes_per_rank[q];
+        }
+        size_t own = 0;
+        for (int q = 0; q < root; ++q) own += bytes_per_rank[q];
+        if (bytes_per_rank[root]) put(HPA_COMM_COPY, root, own, bytes_per_rank[root]);
+    }
+    return ops && n > max_ops ? -1 : n;
+}
+
 // Rank r sends its send_bytes to root, which places them at offset
-// sum(bytes_per_rank[0..r-1]) of recv (rank order; hpa_comm_gather_layout).
-// Enqueued on `stream` (NULL = the library stream); asynchronous.
+// sum(bytes_per_rank[0..r-1]) of recv (rank order): the operations of
+// hpa_comm_gather_plan, point-to-point ones inside one NCCL group, then the
+// root's local copy.  Enqueued on `stream` (NULL = the library stream);
+// asynchronous.
 int hpa_comm_gatherv(const void* send, size_t send_bytes, void* recv, const size_t* bytes_per_rank, int root,
                      void* stream) {
     HPA_REQUIRE(g_comm, "comm_gatherv: hpa_comm_init first");
     HPA_REQUIRE(root >= 0 && root < g_nranks && bytes_per_rank, "comm_gatherv: bad root / counts");
     HPA_REQUIRE(bytes_per_rank[g_rank] == send_bytes, "comm_gatherv: send_bytes != bytes_per_rank[rank]");
+    HPA_REQUIRE(g_rank != root || recv, "comm_gatherv: root needs a receive buffer");
     hipStream_t s = stream ? (hipStream_t)stream : hpa_stream();
-    if (g_rank != root) {
-        if (send_bytes) HPA_NCCL(ncclSend(send, send_bytes, ncclChar, root, g_comm, s));
-        return 0;
+    HpaCommOp* ops = (HpaCommOp*)malloc((size_t)g_nranks * sizeof(HpaCommOp));
+    HPA_REQUIRE(ops, "comm_gatherv: out of host memory");
+    const int n = hpa_comm_gather_plan(g_nranks, g_rank, root, bytes_per_rank, ops, g_nranks);
+    ncclResult_t r = n < 0 ? ncclInvalidArgument : ncclGroupStart();
+    const bool grouped = n >= 0 && r == ncclSuccess;
+    for (int i = 0; i < n && r == ncclSuccess; ++i) {
+        const HpaCommOp& o = ops[i];
+        if (o.op == HPA_COMM_SEND) r = ncclSend(send, o.bytes, ncclChar, o.peer, g_comm, s);
+        else if (o.op == HPA_COMM_RECV) r = ncclRecv((char*)recv + o.offset, o.bytes, ncclChar, o.peer, g_comm, s);
     }
-    HPA_REQUIRE(recv, "comm_gatherv: root needs a receive buffer");
-    size_t* off = (size_t*)malloc((size_t)g_nranks * sizeof(size_t));
-    HPA_REQUIRE(off, "comm_gatherv: out of host memory");
-    size_t own = 0;
-    hpa_comm_gather_layout(g_nranks, g_rank, root, bytes_per_rank, off, &own);
-    ncclResult_t r = ncclGroupStart();
-    for (int q = 0; q < g_nranks && r == ncclSuccess; ++q)
-        if (q != root && bytes_per_rank[q]) r = ncclRecv((char*)recv + off[q], bytes_per_rank[q], ncclChar, q, g_comm, s);
-    const ncclResult_t r2 = ncclGroupEnd();
-    free(off);
+    const ncclResult_t r2 = grouped ? ncclGroupEnd() : ncclSuccess;
+    int copy_rc = 0;
+    for (int i = 0; i < n && r == ncclSuccess && r2 == ncclSuccess; ++i)
+        if (ops[i].op == HPA_COMM_COPY && (char*)recv + ops[i].offset != send)
+            copy_rc |= hipMemcpyAsync((char*)recv + ops[i].offset, send, ops[i].bytes, hipMemcpyDeviceToDevice, s) !=
+                       hipSuccess;
+    free(ops);
     HPA_NCCL(r);
     HPA_NCCL(r2);
-    if (send_bytes && (char*)recv + own != send)
-        HPA_CHECK(hipMemcpyAsync((char*)recv + own, send, send_bytes, hipMemcpyDeviceToDevice, s));
+    HPA_REQUIRE(!copy_rc, "comm_gatherv: root's local copy failed");
     return 0;
 }
 

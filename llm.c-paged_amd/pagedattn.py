@@ -64,6 +64,13 @@ class HpaFusedGemm(ctypes.Structure):
 
 
 HPA_FEPI_QKV, HPA_FEPI_RESID, HPA_FEPI_GELU, HPA_FEPI_LOGITS = 0, 1, 2, 3
+HPA_COMM_SEND, HPA_COMM_RECV, HPA_COMM_COPY = 0, 1, 2
+
+
+class HpaCommOp(ctypes.Structure):
+    """include/hip_paged_attn.h HpaCommOp: one operation of the gather schedule"""
+    _fields_ = [("op", ctypes.c_int), ("peer", ctypes.c_int), ("offset", ctypes.c_size_t),
+                ("bytes", ctypes.c_size_t)]
 
 
 def frag_index(m, k, K):
@@ -93,6 +100,19 @@ GPT2_XL = dict(maxT=1024, V=50257, L=48, NH=25, C=1600)
 
 def config(d):
     return GPT2Config(d["maxT"], d["V"], d["L"], d["NH"], d["C"])
+
+
+def gather_plan(nranks, rank, root, nbytes):
+    """hpa_comm_gather_plan: the (op, peer, offset, bytes) operations this rank
+    posts for one end-of-step gather -- the list hpa_comm_gatherv executes over
+    RCCL (host arithmetic, no GPU needed)"""
+    L = lib()
+    b = (ctypes.c_size_t * nranks)(*nbytes)
+    ops = (HpaCommOp * nranks)()
+    n = L.hpa_comm_gather_plan(nranks, rank, root, b, ops, nranks)
+    if n < 0:
+        raise ValueError("hpa_comm_gather_plan: bad arguments")
+    return [(o.op, o.peer, o.offset, o.bytes) for o in ops[:n]]
 
 
 def build(force=False):
@@ -173,6 +193,7 @@ def lib():
     _sig(L, "hpa_comm_rank", i, [])
     _sig(L, "hpa_comm_gatherv", i, [v, sz, v, ctypes.POINTER(sz), i, v])
     _sig(L, "hpa_comm_gather_layout", i, [i, i, i, ctypes.POINTER(sz), ctypes.POINTER(sz), ctypes.POINTER(sz)])
+    _sig(L, "hpa_comm_gather_plan", i, [i, i, i, ctypes.POINTER(sz), ctypes.POINTER(HpaCommOp), i])
     _sig(L, "hpa_comm_barrier", i, [])
     _sig(L, "hpa_comm_allreduce_max", i, [ctypes.POINTER(ctypes.c_double)])
     _sig(L, "hpa_comm_init_all", i, [i, ctypes.POINTER(i)])

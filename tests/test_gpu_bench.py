@@ -41,3 +41,28 @@ def test_bench_small_batch_split_attention_line():
     d = _bench("--batch", "8")
     assert d["config"]["global_batch"] == 8 and d["config"]["attn_splits"] >= 2
     assert d["value"] > 0 and 0 < d["roofline"]["frac"] < 1
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_default_multi_gpu_line_is_the_metric(n):
+    """the default N>1 line (rehearsed on one GPU with --emulate-rank N) is the
+    headline metric: B = 64 split over the N ranks (BASELINE.md section 3's
+    2/4/8-GPU rows), so value, global_batch and the metric string agree"""
+    d = _bench("--emulate-rank", str(n))
+    base = json.load(open(os.path.join(REPO, "BASELINE.json")))
+    c, e = d["config"], d["emulated_rank"]
+    assert d["metric"] == base["metric"] and d["scaling"] == "strong"
+    assert c["global_batch"] == 64 and c["batch_per_gpu"] == 64 // n and "configs[1]" in c["workload"]
+    assert e["rows"] == 64 // n and e["global_batch"] == 64
+    # value = this GPU's rows; the projection = all N ranks' rows at this step time
+    assert abs(d["value"] - (64 // n) * 1000.0 / d["ms_per_step"]) / d["value"] < 1e-3
+    assert abs(e["projected_n_gpu_tokens_per_s"] * d["ms_per_step"] / 64000.0 - 1) < 1e-2
+
+
+def test_bench_weak_line_is_labelled_config4():
+    """--scaling weak at N>1 (64 sequences per rank) is BASELINE configs[3],
+    reported under its own metric string, never the headline's"""
+    d = _bench("--emulate-rank", "2", "--scaling", "weak")
+    base = json.load(open(os.path.join(REPO, "BASELINE.json")))
+    assert d["metric"] != base["metric"] and "per GPU" in d["metric"]
+    assert d["config"]["global_batch"] == 128 and "configs[3]" in d["config"]["workload"]

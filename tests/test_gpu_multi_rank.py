@@ -3,8 +3,10 @@ the test box.
 
 * Two processes, each a HIP engine (libpaged_hip.so on device 0) decoding
   its shard of the batch (shard.batch_layout), exchanging through a
-  world_size-2 gloo group (RCCL refuses two ranks on one device, so the
-  transport here is gloo; the engines and the sharding are the product's).
+  world_size-2 gloo group on the library's own gather schedule
+  (hpa_comm_gather_plan, what hpa_comm_gatherv posts over RCCL; RCCL refuses
+  two ranks on one device, so the transport here is gloo; the engines, the
+  sharding and the schedule are the product's).
   Rank 0's gathered logits and greedy ids equal an unsharded HIP decode of
   the whole batch bit for bit (same attention split count on both sides:
   GEMM rows never depend on M, so sharding changes no arithmetic).
@@ -54,7 +56,6 @@ def _engine(hip, B):
 
 
 def _worker(rank, world, port, batch, scaling, out_path):
-    import torch
     import torch.distributed as dist
     import pagedattn as hip
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -65,20 +66,20 @@ def _worker(rank, world, port, batch, scaling, out_path):
         counts = [h - l for _, l, h in (shard.batch_layout(batch, world, r, scaling) for r in range(world))]
         m = _engine(hip, hi - lo)
         toks = _tokens(B, SMALL["V"])
+        from test_multi_rank import _run_plan
+        V = SMALL["V"]
+        plan_l = hip.gather_plan(world, rank, 0, [n * V * 4 for n in counts])  # gpt2_decode_gather's bytes
+        plan_i = hip.gather_plan(world, rank, 0, [n * 4 for n in counts])
         logits, ids = [], []
         for t in range(STEPS):
             nxt = m.step(toks[t, lo:hi])
-            lg = torch.zeros(max(counts), SMALL["V"])
-            lg[:hi - lo] = torch.from_numpy(m.logits())
-            nx = torch.zeros(max(counts), dtype=torch.int32)
-            nx[:hi - lo] = torch.from_numpy(nxt)
-            gl = [torch.zeros_like(lg) for _ in range(world)] if rank == 0 else None
-            gi = [torch.zeros_like(nx) for _ in range(world)] if rank == 0 else None
-            dist.gather(lg, gl, dst=0)
-            dist.gather(nx, gi, dst=0)
+            rl = np.zeros(B * V * 4, np.uint8) if rank == 0 else None
+            ri = np.zeros(B * 4, np.uint8) if rank == 0 else None
+            _run_plan(dist, plan_l, np.ascontiguousarray(m.logits(), np.float32).view(np.uint8).ravel(), rl)
+            _run_plan(dist, plan_i, np.ascontiguousarray(nxt, np.int32).view(np.uint8).ravel(), ri)
             if rank == 0:
-                logits.append(np.concatenate([g[:n].numpy() for g, n in zip(gl, counts)]))
-                ids.append(np.concatenate([g[:n].numpy() for g, n in zip(gi, counts)]))
+                logits.append(rl.view(np.float32).reshape(B, V))
+                ids.append(ri.view(np.int32))
         m.close()
         if rank == 0:
             np.savez(out_path, logits=np.stack(logits), ids=np.stack(ids))
@@ -99,6 +100,13 @@ def test_two_hip_engines_sharded_equal_unsharded(hip, tmp_path, batch, scaling):
         p.start()
     for p in procs:
         p.join(120)
+    for p in procs:  # a hung rank must not outlive the test
+        if p.is_alive():
+            p.terminate()
+            p.join(5)
+        if p.is_alive():
+            p.kill()
+            p.join(5)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     got = np.load(out)
     B = batch * world if scaling == "weak" else batch
@@ -265,6 +273,12 @@ def _run_ranks(tmp_path, shards, total, picks):
         p = ctx.Process(target=_c4_rank, args=(lo, hi, total, picks, out))
         p.start()
         p.join(240)
+        if p.is_alive():  # a hung rank must not outlive the test
+            p.terminate()
+            p.join(5)
+        if p.is_alive():
+            p.kill()
+            p.join(5)
         assert p.exitcode == 0, (r, p.exitcode)
         got.append(np.load(out))
         print(f"rank {r} ({lo}..{hi}, picks {picks}) done: form / splits / waves {tuple(got[-1]['info'])}",

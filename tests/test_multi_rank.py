@@ -1,10 +1,16 @@
-"""The N>1 decode path on CPU: world_size-2 `gloo` process groups running
-the sequence sharding (llm.c-paged_amd/shard.py, the same code bench.py
-drives over RCCL) with the oracle's paged decoder as each rank's engine.
+"""The N>1 decode path on CPU: `gloo` process groups of 2-4 ranks running the
+sequence sharding with the oracle's paged decoder as each rank's engine, and
+the END-OF-STEP GATHER SCHEDULE OF THE PRODUCT LIBRARY: every rank asks
+libpaged_hip.so for its operations (hpa_comm_gather_plan -- the exact list
+hpa_comm_gatherv posts as ncclSend / ncclRecv plus the root's local copy,
+llm.c-paged_amd/csrc/hpa_comm.hip) and runs them over gloo point-to-point
+messages.  The per-rank byte counts follow gpt2_decode_gather's bookkeeping
+(rows x V x 4 for the logits, rows x 4 for the ids; paged_infer.c).
 
-Sharding must not change any sequence's result: the logits and greedy ids
-gathered to rank 0 equal, bit for bit, an unsharded decode of the whole
-batch (sequences are independent, no exchange inside a step).
+Sharding must not change any sequence's result: what the root assembles
+equals, bit for bit, an unsharded decode of the whole batch (SURVEY.md 8e:
+sequences are independent, no exchange inside a step).  Covers uneven row
+counts, a rank with zero rows and a non-zero root.
 """
 import os
 import socket
@@ -13,6 +19,7 @@ import numpy as np
 import pytest
 
 import oracle_ctypes as oc
+import pagedattn
 import shard
 import synth
 
@@ -30,43 +37,51 @@ def _tokens(B, steps, V):
     return np.random.default_rng(123).integers(0, V, (steps, B)).astype(np.int32)
 
 
-def _worker(rank, world, port, batch, scaling, mode, out_path, nbuf=1):
+def _run_plan(dist, plan, send, recv):
+    """execute the library's schedule for this rank over gloo: SEND / RECV as
+    point-to-point messages (byte buffers), COPY as the root's local copy"""
     import torch
+    reqs = []
+    for op, peer, off, nb in plan:
+        if op == pagedattn.HPA_COMM_SEND:
+            reqs.append(dist.isend(torch.from_numpy(send[:nb]), peer))
+        elif op == pagedattn.HPA_COMM_RECV:
+            reqs.append(dist.irecv(torch.from_numpy(recv[off:off + nb]), peer))
+        else:
+            recv[off:off + nb] = send[:nb]
+    for r in reqs:
+        r.wait()
+
+
+def _worker(rank, world, port, rows, root, mode, out_path):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        B, lo, hi = shard.batch_layout(batch, world, rank, scaling)
-        counts = [shard.batch_layout(batch, world, r, scaling) for r in range(world)]
-        counts = [h - l for _, l, h in counts]
+        lo = sum(rows[:rank])
+        hi = lo + rows[rank]
+        B = sum(rows)
+        per = SMALL["V"] * 4 if mode == "logits" else 4  # gpt2_decode_gather: bytes per row
+        nbytes = [r * per for r in rows]
+        plan = pagedattn.gather_plan(world, rank, root, nbytes)
         params = synth.params(SMALL, seed=5)
         c = oc.cfg(SMALL["maxT"], SMALL["V"], SMALL["L"], SMALL["NH"], SMALL["C"])
-        dec = oc.PagedDecoder(params, c, hi - lo, 8, SMALL["maxT"], page_seed=17 + rank)
-        g = shard.StepGather(dist, world, rank, counts, SMALL["V"], mode, "cpu", nbuf=nbuf)
+        dec = oc.PagedDecoder(params, c, rows[rank], 8, SMALL["maxT"], page_seed=17 + rank) if rows[rank] else None
         toks = _tokens(B, STEPS, SMALL["V"])
+        recv = np.zeros(sum(nbytes), np.uint8) if rank == root else None
         got = []
         for t in range(STEPS):
-            nxt, logits = dec.step(toks[t, lo:hi])
-            i = t % nbuf
-            if nbuf > 1 and rank == 0 and t >= nbuf:  # the gather of step t - nbuf, read before reuse
-                g.wait(i)
-                got.append(g.result(i).numpy().copy())
-            g.wait(i)
-            buf = g.buffer(i)
-            if mode == "logits":
-                buf[:hi - lo] = torch.from_numpy(logits)
-            else:
-                buf[:hi - lo, 0] = torch.from_numpy(nxt)
-            g.gather(i, async_op=nbuf > 1)
-            if rank == 0 and nbuf == 1:
-                got.append(g.result().numpy().copy())
-        if nbuf > 1:  # drain: the last nbuf steps, in order
-            for t in range(STEPS - nbuf, STEPS):
-                g.wait(t % nbuf)
-                if rank == 0:
-                    got.append(g.result(t % nbuf).numpy().copy())
-        dec.close()
-        if rank == 0:
+            send = np.zeros(max(nbytes[rank], 1), np.uint8)
+            if dec is not None:
+                nxt, logits = dec.step(toks[t, lo:hi])
+                out = logits if mode == "logits" else nxt.astype(np.int32)
+                send[:nbytes[rank]] = np.ascontiguousarray(out).view(np.uint8).ravel()
+            _run_plan(dist, plan, send, recv)
+            if rank == root:
+                got.append(recv.view(np.float32 if mode == "logits" else np.int32).reshape(B, -1).copy())
+        if dec is not None:
+            dec.close()
+        if rank == root:
             np.save(out_path, np.stack(got))
     finally:
         dist.destroy_process_group()
@@ -80,35 +95,76 @@ def _unsharded(B, mode):
     out = []
     for t in range(STEPS):
         nxt, logits = dec.step(toks[t])
-        out.append(logits if mode == "logits" else nxt)
+        out.append(logits if mode == "logits" else nxt.astype(np.int32)[:, None])
     dec.close()
     return np.stack(out)
 
 
-@pytest.mark.parametrize("batch,scaling,mode,nbuf", [(3, "weak", "logits", 1), (5, "strong", "logits", 1),
-                                                     (4, "weak", "ids", 1), (3, "weak", "logits", 2)])
-def test_two_rank_sharded_decode_equals_unsharded(tmp_path, batch, scaling, mode, nbuf):
-    """nbuf = 2: the double-buffered asynchronous gather bench.py overlaps
-    with the next step"""
-    # stdlib spawn: torch is imported by the ranks only, never in the pytest
-    # process (a -m gpu session must not map torch's HIP runtime beside the
-    # library's, and two HIP runtimes in one process abort at exit)
+def _spawn(world, target, args):
+    """stdlib spawn: torch is imported by the ranks only, never in the pytest
+    process (a -m gpu session must not map torch's HIP runtime beside the
+    library's, and two HIP runtimes in one process abort at exit).  A rank
+    still alive after the join timeout is terminated, then killed, before the
+    exit codes are checked, so a hung gloo call cannot outlive
+    the test."""
     import multiprocessing
-    world = 2
-    out = str(tmp_path / "rank0.npy")
     ctx = multiprocessing.get_context("spawn")
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, batch, scaling, mode, out, nbuf)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, *args)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(120)
-    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.terminate()
+            p.join(5)
+        if p.is_alive():
+            p.kill()
+            p.join(5)
+    return [p.exitcode for p in procs]
+
+
+@pytest.mark.parametrize("rows,root,mode", [([3, 3], 0, "logits"), ([3, 2], 0, "logits"), ([2, 2], 1, "ids"),
+                                            ([2, 0, 3], 0, "logits"), ([1, 2, 1, 2], 2, "logits")])
+def test_sharded_decode_through_library_gather_schedule(tmp_path, rows, root, mode):
+    world = len(rows)
+    out = str(tmp_path / "root.npy")
+    codes = _spawn(world, _worker, (_free_port(), rows, root, mode, out))
+    assert all(c == 0 for c in codes), codes
     got = np.load(out)
-    B = batch * world if scaling == "weak" else batch
-    want = _unsharded(B, mode)
+    want = _unsharded(sum(rows), mode)
     assert got.shape == want.shape
     assert np.array_equal(got, want)
+
+
+def test_gather_plan_matches_layout():
+    """the schedule's offsets are hpa_comm_gather_layout's, its RECV count is
+    the layout's post count, and every byte of the root's buffer is written
+    exactly once (the RECVs and the COPY tile it)"""
+    import ctypes
+    L = pagedattn.lib()
+    sz = ctypes.c_size_t
+    for rows, root in [([3, 3], 0), ([4, 3, 0, 5], 0), ([2, 0, 7, 1, 0, 9, 3, 3], 5), ([0, 0, 4], 2), ([1], 0)]:
+        n = len(rows)
+        nb = [r * 40 for r in rows]
+        off = (sz * n)()
+        own = sz()
+        for rank in range(n):
+            posts = L.hpa_comm_gather_layout(n, rank, root, (sz * n)(*nb), off, ctypes.byref(own))
+            plan = pagedattn.gather_plan(n, rank, root, nb)
+            if rank != root:
+                assert plan == ([(pagedattn.HPA_COMM_SEND, root, 0, nb[rank])] if nb[rank] else [])
+                continue
+            recvs = [p for p in plan if p[0] == pagedattn.HPA_COMM_RECV]
+            assert len(recvs) == posts
+            assert all(o == off[q] and b == nb[q] for _, q, o, b in recvs)
+            cover = np.zeros(sum(nb), np.int32)
+            for _, _, o, b in plan:
+                cover[o:o + b] += 1
+            assert (cover == 1).all()
+    assert L.hpa_comm_gather_plan(2, 0, 0, (sz * 2)(8, 8), None, 0) == 2  # count only
+    assert L.hpa_comm_gather_plan(2, 0, 0, (sz * 2)(8, 8), (pagedattn.HpaCommOp * 1)(), 1) == -1  # too small
+    assert L.hpa_comm_gather_plan(2, 2, 0, (sz * 2)(8, 8), None, 0) == -1
 
 
 def test_batch_layout():
