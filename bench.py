@@ -160,12 +160,6 @@ def parse():
                          "6 chain form 8 (streamed weights, also GPT-2 XL); "
                          "-1 the engine's default "
                          "(HPA_LAYER_KERNEL or 1)")
-    ap.add_argument("--attn-flat", type=int, default=-1, choices=[-1, 0, 1, 2],
-                    help="gpt2_decode_set_attn_flat: 2 the balanced attention form, 1 the (sequence, head, "
-                         "range) grid, 0 auto (balanced where B*NH < CUs), -1 the engine's default")
-    ap.add_argument("--lanes", type=int, default=-1, choices=[-1, 0, 1, 2],
-                    help="gpt2_decode_set_lanes: 2 the two-lane step (each lane's attention beside the other "
-                         "lane's chain), 1 one lane, 0 auto, -1 the engine's default")
     ap.add_argument("--picks", default="local", choices=["local", "global"],
                     help="N>1 / --emulate-rank: shape picks by the rank's own batch (default: a rank computes "
                          "what a single-GPU engine of its rows computes) or by the global batch "
@@ -307,10 +301,6 @@ def main():
         model.set_global_batch(B)  # every row as the unsharded engine of B computes it
     if args.layer_kernel >= 0:
         model.set_layer_kernel(args.layer_kernel)
-    if args.lanes >= 0:
-        model.set_lanes(args.lanes)
-    if args.attn_flat >= 0:
-        model.set_attn_flat(args.attn_flat)
     if args.sample:
         model.set_sampling(True, seed=1337 + lo)
     if args.gemm_waves or args.gemm_rows or args.gemm_cols:
@@ -488,9 +478,7 @@ def main():
                                       3: "attention launch + one persistent launch of the GEMM chain in "
                                          "wide / multi-tile units (hpa_decode_layer chain_only 2..6, 8: "
                                          "by default form 6 at C = 768, form 8 at C >= 1024)"}[model.layer_form()],
-                       "lanes": model.lanes(),
-                       "attn_form": "balanced (flattened tiles, one workgroup per CU)" if model.attn_flat()
-                                    else f"(sequence, head) x {splits} range(s)",
+                       "attn_form": f"(sequence, head) x {splits} range(s)",
                        "token_choice": "multinomial (reference sample_mult)" if args.sample else "greedy",
                        "gemm_waves": [int(x) for x in model.gemm_config()[0]],
                        "gemm_row_blocks": [int(x) for x in model.gemm_config()[1]],

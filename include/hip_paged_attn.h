@@ -150,19 +150,6 @@ int hpa_attn_pick_waves(int B, int num_heads, int splits, int num_cus);
 int hpa_paged_attention_decode_split(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
                                      int bt_stride, const int* pos, float* out, int B, int splits, void* ws,
                                      int out_frag);
-/* balanced form for small batches (B <= 64; measured slower than the split
- * grid, so the engine runs it only on request): `workgroups` (0: one per CU) split the flattened list
- * of every (sequence, head)'s 64-token tiles into equal runs; a pair split
- * over several runs is merged by its last workgroup in run order (timing-
- * independent).  Needs every pos[b] < max_ctx; ws: hpa_attn_flat_ws_bytes
- * bytes whose counter part is zero before the first launch (every launch
- * leaves it zero).  waves 4 or 8 (0: 4).  Within fp32 rounding of the single
- * pass; a row's grouping depends on the batch's contexts. */
-size_t hpa_attn_flat_ws_bytes(int B, int num_heads, int max_ctx);
-int hpa_paged_attention_decode_flat(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
-                                    int bt_stride, const int* pos, float* out, int B, int max_ctx, void* ws,
-                                    int out_frag, int waves, int workgroups);
-
 /* synthetic K/V fill of positions [0, ctx) for every sequence with U(-1,1)
  * from a counter-based hash (attention microbench / bench synthetic prefill) */
 int hpa_pool_fill_random(const HpaKVPool* pool, const int* block_table, int bt_stride, int B,

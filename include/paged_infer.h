@@ -226,23 +226,6 @@ int  gpt2_decode_set_layer_kernel(GPT2* model, int enable);
  * launch + persistent chain of 4-wave units, 3 the chain in wide / multi-tile
  * units (forms 4..6 of gpt2_decode_set_layer_kernel) */
 int  gpt2_decode_layer_kernel(GPT2* model);
-/* two-lane step: the batch's row blocks in two lanes on two streams, each
- * lane's attention launch running beside the other lane's chain launch (chain
- * form 6, 33..64 rows, one context range per sequence and head; the rows'
- * numbers are the one-lane step's bit for bit).  lanes: 0 auto (= off: measured
- * slower, the chain's hand-offs queue behind the attention's K/V stream;
- * profiles/r4/experiments/two_lane_step.txt), 1 off, 2 on where it applies;
- * gpt2_decode_lanes: lanes in use (1 or 2) */
-/* the decode attention's balanced form (hpa_paged_attention_decode_flat: the
- * flattened tiles of every (sequence, head) in equal runs, one workgroup per
- * CU): 0 auto (= off: measured slower than the (sequence, head, range)
- * grid at every batch, profiles/r4/experiments/balanced_attention.txt), 1 off,
- * 2 on (not under global picks: its sums depend on every sequence's context);
- * gpt2_decode_attn_flat: 1 when in use */
-int  gpt2_decode_set_attn_flat(GPT2* model, int mode);
-int  gpt2_decode_attn_flat(GPT2* model);
-int  gpt2_decode_set_lanes(GPT2* model, int lanes);
-int  gpt2_decode_lanes(GPT2* model);
 /* waits for the queued work; 0, or the code of a timed-out in-launch wait of
  * the persistent layer (the step's outputs are then invalid), which it clears */
 int  gpt2_decode_status(GPT2* model);

@@ -137,238 +137,6 @@ int launch_decode(const float* q, const HpaKVPool* pool, int layer, const int* b
 
 int g_attn_waves = 0;  // hpa_set_attention_waves: a process-wide override (0: the caller's choice)
 
-// ---- balanced form (round 4, VERDICT r3 item 4: small batches) ----
-// At B*NH below the CU count the per-(sequence, head) grid leaves CUs idle
-// (B = 8: 96 pairs, S = 2 -> 192 workgroups on 256 CUs) and a CU streams at
-// most ~25 GB/s, so the launch runs at 3.9 TB/s.  Here the G workgroups
-// (one per CU) split the FLATTENED list of 64-token tiles -- pair p = b*NH +
-// h holds tiles(b) = ceil((pos[b]+1)/64), pairs in order -- into G equal runs
-// [g*T/G, (g+1)*T/G).  A run covers pieces of one or more pairs; each piece is
-// folded as a workgroup folds a whole pair, then a pair split over several
-// workgroups publishes one record per piece (k = g - the pair's first
-// workgroup) and the last arriver merges them in piece order (split_merge:
-// the result does not depend on timing); a pair inside one run is written
-// directly.  Piece boundaries depend on every sequence's context, so a row's
-// sums (not its value beyond fp32 rounding) depend on the batch.
-template <int P, int NW, bool FRAG, bool BF16>
-__global__ __launch_bounds__(NW * 64, 1) void paged_attn_decode_flat(
-    const float* __restrict__ q, const void* __restrict__ layer_base, size_t page_elems, int NH,
-    const int* __restrict__ block_table, int bt_stride, const int* __restrict__ pos, float* __restrict__ out,
-    float qscale, float m_init, int B, int kmax, float* __restrict__ ws) {
-    constexpr int TILE = P * HS;
-    __shared__ float s_m[NW];
-    __shared__ float s_l[NW];
-    __shared__ float4 s_acc[NW * 16];
-    __shared__ int s_pref[65];  // tiles of sequences 0..b-1 (b <= 64)
-    const int lane = threadIdx.x & 63;
-    if (threadIdx.x < 64) {  // inclusive scan of tiles(b) over the lanes
-        int t = lane < B ? (pos[lane] + 64) >> 6 : 0;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int u = __shfl_up(t, o, 64);
-            if (lane >= o) t += u;
-        }
-        s_pref[lane + 1] = t;
-        if (lane == 0) s_pref[0] = 0;
-    }
-    __syncthreads();
-    const long long T = (long long)NH * s_pref[B];
-    // runs of at least one tile: at most T workgroups take part (an empty run
-    // would be counted by the merge of a pair it never reaches)
-    const int G = (int)min((long long)gridDim.x, T), g = blockIdx.x;
-    if (g >= G) return;
-    long long lo = (long long)g * T / G;
-    const long long hi = (long long)(g + 1) * T / G;
-    // the workgroup holding flattened tile t: the largest g' with g' * T / G <= t
-    auto wg_of = [&](long long t) { return (int)(((t + 1) * G - 1) / T); };
-    int b = 0;
-    while (b + 1 < B && (long long)NH * s_pref[b + 1] <= lo) ++b;
-    const float* fbase = reinterpret_cast<const float*>(layer_base);
-    const unsigned short* hbase = reinterpret_cast<const unsigned short*>(layer_base);
-    int* cnt_all = reinterpret_cast<int*>(ws + (size_t)B * NH * kmax * kRec);
-    while (lo < hi) {
-        while ((long long)NH * s_pref[b + 1] <= lo) ++b;  // the pair's sequence
-        const int tb = s_pref[b + 1] - s_pref[b];
-        const long long pb = (long long)NH * s_pref[b];   // the sequence's first flattened tile
-        const int h = (int)((lo - pb) / tb);
-        const long long ps = pb + (long long)h * tb, pe = ps + tb;  // the pair's flattened tiles
-        const int it0 = (int)(lo - ps);
-        const int it1 = (int)(min(hi, pe) - ps);
-        const int bh = b * NH + h;
-        const int ctx = pos[b] + 1;
-        const float* qh = q + (size_t)bh * HS;
-        const int* bt = block_table + (size_t)b * bt_stride;
-        const int g0 = wg_of(ps), g1 = wg_of(pe - 1);
-        float m = m_init, l = 0.f;
-        if constexpr (BF16) {
-            float4 acc[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
-            attn_tiles_bf16<P, NW>(qh, hbase + (size_t)h * TILE, hbase + (size_t)(NH + h) * TILE, page_elems, bt,
-                                   bt_stride, ctx, it0, it1, qscale, m, l, acc);
-            if (attn_fold_bf16<NW>(m, l, acc, s_m, s_l, s_acc) &&
-                (g0 == g1 || split_merge<2>(ws + (size_t)bh * kmax * kRec, cnt_all + bh, g1 - g0 + 1, g - g0, m, l,
-                                            acc, true))) {
-                const float inv = l == 0.f ? 0.f : 1.f / l;
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const int col = h * HS + 8 * lane + 4 * k;
-                    const size_t oi = FRAG ? hpa::frag_index(b, col, NH * HS) : (size_t)b * NH * HS + col;
-                    *reinterpret_cast<float4*>(out + oi) =
-                        make_float4(acc[k].x * inv, acc[k].y * inv, acc[k].z * inv, acc[k].w * inv);
-                }
-            }
-        } else {
-            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-            attn_tiles<P, NW>(qh, fbase + (size_t)h * TILE, fbase + (size_t)(NH + h) * TILE, page_elems, bt, bt_stride,
-                              ctx, it0, it1, qscale, m, l, acc);
-            if (attn_fold<NW>(m, l, acc, s_m, s_l, s_acc) &&
-                (g0 == g1 ||
-                 split_merge<1>(ws + (size_t)bh * kmax * kRec, cnt_all + bh, g1 - g0 + 1, g - g0, m, l, &acc, true))) {
-                const size_t oi =
-                    FRAG ? hpa::frag_index(b, h * HS + 4 * lane, NH * HS) : ((size_t)b * NH + h) * HS + 4 * lane;
-                const float inv = l == 0.f ? 0.f : 1.f / l;
-                *reinterpret_cast<float4*>(out + oi) = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
-            }
-        }
-        __syncthreads();  // the fold's LDS is reused by the next piece
-        lo = min(hi, pe);
-    }
-}
-
-// The balanced form with every tile of a run in flight at once: 16 waves,
-// wave w takes the run's tile lo + w alone (the host picks this kernel when
-// no run can exceed 16 tiles: B*NH*ceil(max_ctx/64) <= 16 G), the waves of a
-// piece fold in wave (= tile) order through LDS, and each piece's first wave
-// publishes or merges it -- the pieces of a run no longer follow each other.
-template <int P, bool FRAG, bool BF16>
-__global__ __launch_bounds__(1024, 1) void paged_attn_decode_flat16(
-    const float* __restrict__ q, const void* __restrict__ layer_base, size_t page_elems, int NH,
-    const int* __restrict__ block_table, int bt_stride, const int* __restrict__ pos, float* __restrict__ out,
-    float qscale, float m_init, int B, int kmax, float* __restrict__ ws) {
-    constexpr int NW = 16, TILE = P * HS;
-    constexpr int KC = BF16 ? 2 : 1;   // float4 chunks per result lane
-    constexpr int NL = BF16 ? 8 : 16;  // result lanes of a folded wave
-    __shared__ float s_m[NW];
-    __shared__ float s_l[NW];
-    __shared__ float4 s_acc[NW * 16];
-    __shared__ int s_pref[65];
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (threadIdx.x < 64) {
-        int t = lane < B ? (pos[lane] + 64) >> 6 : 0;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int u = __shfl_up(t, o, 64);
-            if (lane >= o) t += u;
-        }
-        s_pref[lane + 1] = t;
-        if (lane == 0) s_pref[0] = 0;
-    }
-    __syncthreads();
-    const long long T = (long long)NH * s_pref[B];
-    const int G = (int)min((long long)gridDim.x, T), g = blockIdx.x;
-    if (g >= G) return;
-    const long long lo = (long long)g * T / G, hi = (long long)(g + 1) * T / G;
-    auto wg_of = [&](long long t) { return (int)(((t + 1) * G - 1) / T); };
-    const long long j = lo + w;  // this wave's tile
-    const bool act = j < hi;
-    int b = 0;
-    if (act)
-        while ((long long)NH * s_pref[b + 1] <= j) ++b;
-    const int tb = max(s_pref[b + 1] - s_pref[b], 1);
-    const long long pb = (long long)NH * s_pref[b];
-    const int h = act ? (int)((j - pb) / tb) : 0;
-    const long long ps = pb + (long long)h * tb, pe = ps + tb;
-    const int bh = b * NH + h;
-    const int ctx = pos[b] + 1;
-    const float* qh = q + (size_t)bh * HS;
-    const int* bt = block_table + (size_t)b * bt_stride;
-    float m = m_init, l = 0.f;
-    float4 acc[KC];
-#pragma unroll
-    for (int k = 0; k < KC; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (act) {
-        const int it = (int)(j - ps);
-        if constexpr (BF16) {
-            const unsigned short* base = reinterpret_cast<const unsigned short*>(layer_base);
-            attn_tiles_bf16<P, 1>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, page_elems, bt,
-                                  bt_stride, ctx, it, it + 1, qscale, m, l, acc, 0);
-        } else {
-            const float* base = reinterpret_cast<const float*>(layer_base);
-            attn_tiles<P, 1>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, page_elems, bt, bt_stride,
-                             ctx, it, it + 1, qscale, m, l, acc[0], 0);
-        }
-    }
-    // the wave's token groups (lane bits above the result lanes), then its sum
-#pragma unroll
-    for (int o = NL; o <= 32; o <<= 1)
-#pragma unroll
-        for (int k = 0; k < KC; ++k) {
-            acc[k].x += __shfl_xor(acc[k].x, o, 64);
-            acc[k].y += __shfl_xor(acc[k].y, o, 64);
-            acc[k].z += __shfl_xor(acc[k].z, o, 64);
-            acc[k].w += __shfl_xor(acc[k].w, o, 64);
-        }
-    l = hpa::wave_sum(l);
-    if (lane == 0) {
-        s_m[w] = m;
-        s_l[w] = l;
-    }
-    if (lane < NL)
-#pragma unroll
-        for (int k = 0; k < KC; ++k) s_acc[w * 16 + lane * KC + k] = acc[k];
-    __syncthreads();
-    const long long j0 = max(lo, ps), j1 = min(hi, pe);  // this wave's piece of the run
-    if (!act || j != j0 || lane >= NL) return;          // one wave per piece goes on
-    const int w0 = (int)(j0 - lo), w1 = (int)(j1 - lo);
-    float M = s_m[w0];
-    for (int i = w0 + 1; i < w1; ++i) M = fmaxf(M, s_m[i]);
-    float L = 0.f;
-    float4 O[KC];
-#pragma unroll
-    for (int k = 0; k < KC; ++k) O[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int i = w0; i < w1; ++i) {  // waves = tiles in order
-        const float f = exp2f(s_m[i] - M);
-        L = fmaf(s_l[i], f, L);
-#pragma unroll
-        for (int k = 0; k < KC; ++k) {
-            const float4 a = s_acc[i * 16 + lane * KC + k];
-            O[k].x = fmaf(a.x, f, O[k].x);
-            O[k].y = fmaf(a.y, f, O[k].y);
-            O[k].z = fmaf(a.z, f, O[k].z);
-            O[k].w = fmaf(a.w, f, O[k].w);
-        }
-    }
-    const int g0 = wg_of(ps), g1 = wg_of(pe - 1);
-    int* cnt = reinterpret_cast<int*>(ws + (size_t)B * NH * kmax * kRec) + bh;
-    if (g0 != g1 && !split_merge<KC>(ws + (size_t)bh * kmax * kRec, cnt, g1 - g0 + 1, g - g0, M, L, O, true)) return;
-    const float inv = L == 0.f ? 0.f : 1.f / L;
-#pragma unroll
-    for (int k = 0; k < KC; ++k) {
-        const int col = h * HS + (BF16 ? 8 * lane + 4 * k : 4 * lane);
-        const size_t oi = FRAG ? hpa::frag_index(b, col, NH * HS) : (size_t)b * NH * HS + col;
-        *reinterpret_cast<float4*>(out + oi) = make_float4(O[k].x * inv, O[k].y * inv, O[k].z * inv, O[k].w * inv);
-    }
-}
-
-template <int P, bool FRAG, bool BF16>
-int launch_flat(const float* q, const HpaKVPool* pool, int layer, const int* bt, int bt_stride, const int* pos,
-                float* out, int B, int nw, int G, int kmax, float* ws) {
-    const void* base = (const char*)pool->base + (size_t)layer * pool->layer_elems * pool->elem_bytes;
-    const float log2e = 1.4426950408889634f;
-    const float qscale = (float)(1.0 / sqrt((double)HS)) * log2e;
-    const float m_init = -10000.0f * log2e;
-    if (nw == 16)
-        paged_attn_decode_flat16<P, FRAG, BF16><<<G, 1024, 0, hpa_stream()>>>(
-            q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init, B, kmax, ws);
-    else if (nw == 8)
-        paged_attn_decode_flat<P, 8, FRAG, BF16><<<G, 512, 0, hpa_stream()>>>(
-            q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init, B, kmax, ws);
-    else
-        paged_attn_decode_flat<P, 4, FRAG, BF16><<<G, 256, 0, hpa_stream()>>>(
-            q, base, pool->page_elems, pool->num_heads, bt, bt_stride, pos, out, qscale, m_init, B, kmax, ws);
-    HPA_LAUNCH_CHECK();
-    return 0;
-}
 
 }  // namespace
 
@@ -473,58 +241,5 @@ int hpa_paged_attention_decode_split_w(const float* q, const HpaKVPool* pool, in
     return attn_dispatch(q, pool, layer, block_table, bt_stride, pos, out, B, out_frag != 0, splits, ws, waves);
 }
 
-// pieces per pair at most: a pair of t tiles meets at most t + 1 runs
-static int flat_kmax(int max_ctx) { return (max_ctx + 63) / 64 + 1; }
-
-size_t hpa_attn_flat_ws_bytes(int B, int num_heads, int max_ctx) {
-    if (B <= 0 || num_heads <= 0 || max_ctx <= 0) return 0;
-    const size_t pairs = (size_t)B * num_heads;
-    return pairs * flat_kmax(max_ctx) * kRec * sizeof(float) + pairs * sizeof(int);
-}
-
-int hpa_paged_attention_decode_flat(const float* q, const HpaKVPool* pool, int layer, const int* block_table,
-                                    int bt_stride, const int* pos, float* out, int B, int max_ctx, void* ws,
-                                    int out_frag, int waves, int workgroups) {
-    HPA_REQUIRE(pool && pool->base, "pool not created");
-    HPA_REQUIRE(pool->dtype == HPA_F32 || pool->dtype == HPA_BF16, "decode attention: fp32 or bf16 pool");
-    HPA_REQUIRE(pool->head_size == HS, "decode attention requires head_size 64");
-    HPA_REQUIRE(layer >= 0 && layer < pool->num_layers, "layer out of range");
-    HPA_REQUIRE(B > 0 && B <= 64 && q && out && block_table && pos && ws, "decode attention flat: B 1..64, workspace");
-    HPA_REQUIRE(max_ctx > 0, "decode attention flat: max_ctx (every pos[b] < max_ctx)");
-    HPA_REQUIRE(((uintptr_t)q & 15) == 0 && ((uintptr_t)out & 15) == 0, "q/out must be 16-byte aligned");
-    HPA_REQUIRE(waves == 0 || waves == 4 || waves == 8 || waves == 16, "decode attention flat: waves 4, 8 or 16");
-    int G = workgroups;
-    if (G <= 0) {
-        int dev = 0;
-        HPA_CHECK(hipGetDevice(&dev));
-        HPA_CHECK(hipDeviceGetAttribute(&G, hipDeviceAttributeMultiprocessorCount, dev));
-    }
-    const int kmax = flat_kmax(max_ctx);
-    // 0: 16 waves with every tile of a run in flight when no run can exceed 16
-    // tiles (B*NH*ceil(max_ctx/64) <= 16 G), else 4; hpa_set_attention_waves
-    // 8 -> 8, any other override -> 4
-    const bool fits16 = (long long)B * pool->num_heads * (kmax - 1) <= 16LL * G;
-    int nw = waves;
-    if (!nw) nw = g_attn_waves == 8 ? 8 : g_attn_waves ? 4 : fits16 ? 16 : 4;
-    HPA_REQUIRE(nw != 16 || fits16,
-                "decode attention flat: 16 waves need B*NH*ceil(max_ctx/64) <= 16 workgroups");
-    const bool bf = pool->dtype == HPA_BF16, frag = out_frag != 0;
-    float* w = (float*)ws;
-#define HPA_FLAT_CASE(PS)                                                                                       \
-    case PS:                                                                                                     \
-        if (bf)                                                                                                  \
-            return frag ? launch_flat<PS, true, true>(q, pool, layer, block_table, bt_stride, pos, out, B, nw, G, kmax, w) \
-                        : launch_flat<PS, false, true>(q, pool, layer, block_table, bt_stride, pos, out, B, nw, G, kmax, w); \
-        return frag ? launch_flat<PS, true, false>(q, pool, layer, block_table, bt_stride, pos, out, B, nw, G, kmax, w)     \
-                    : launch_flat<PS, false, false>(q, pool, layer, block_table, bt_stride, pos, out, B, nw, G, kmax, w);
-    switch (pool->page_size) {
-        HPA_FLAT_CASE(8)
-        HPA_FLAT_CASE(16)
-        HPA_FLAT_CASE(32)
-        HPA_FLAT_CASE(64)
-        default: return hpa_fail(__FILE__, __LINE__, "page size must be 8, 16, 32 or 64");
-    }
-#undef HPA_FLAT_CASE
-}
 
 }  // extern "C"

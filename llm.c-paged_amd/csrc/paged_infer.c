@@ -644,10 +644,6 @@ struct GPT2Decode {
     int attn_splits;  /* context ranges per (sequence, head) of the decode attention */
     int attn_waves;   /* waves per attention workgroup (hpa_attn_pick_waves of the global batch) */
     void* d_attn_ws;  /* split records + counters (hpa_attn_ws_bytes at HPA_ATTN_MAX_SPLITS) */
-    int attn_flat_want; /* gpt2_decode_set_attn_flat: 0 auto, 1 off, 2 on */
-    int attn_flat;    /* in use: the balanced form (hpa_paged_attention_decode_flat) instead of the split grid */
-    void* d_flat_ws;  /* its records + counters (hpa_attn_flat_ws_bytes) */
-    size_t flat_ws_bytes;
     size_t attn_ws_bytes;
     int sample;       /* 0: greedy argmax; 1: multinomial with per-sequence xorshift */
     unsigned long long* d_rng; /* [B] sampler states */
@@ -672,19 +668,11 @@ struct GPT2Decode {
     int pl_splits;
     int pl_global_B;  /* gpt2_decode_set_global_batch: the batch the picks follow (<= 64); else 0 */
     float* pl_rec;
-    float* pl_slab;   /* [2 lanes][pl_slab_n] */
+    float* pl_slab;   /* [pl_slab_n] */
     size_t pl_slab_n;
-    int* pl_ctr;      /* the step's error word (DEC_ERR_INTS), then [2 lanes][L][pl_ctr_ints]; the word and
-                         the lanes in use are zeroed at the start of every step */
+    int* pl_ctr;      /* the step's error word (DEC_ERR_INTS), then [L][pl_ctr_ints]; zeroed at the start of
+                         every step */
     size_t pl_ctr_ints;
-    /* two-lane step (gpt2_decode_set_lanes): the batch's row blocks split in
-     * two lanes on two streams; a lane's attention runs while the other
-     * lane's chain launch runs (the chains one at a time) */
-    int lanes_want;   /* 0 auto, 1 off, 2 on where it applies */
-    int lanes;        /* in use: 1 or 2 */
-    int lane_rows;    /* rows of lane 0 (whole row blocks); lane 1 takes the rest */
-    void* lane_stream;
-    void* lane_ev[3]; /* fork after qkv(0); lane 0's chain done; lane 1's chain done (also the join) */
     /* gpt2_forward: token at every cached position [B][max_ctx] and, when it
      * fits, the logits of every position [B][max_ctx][V] (managed) */
     int* h_hist;
@@ -791,11 +779,8 @@ static void dec_free(GPT2Decode* d) {
     hpa_free(d->ring_slab); hpa_free(d->ring_cnt);
     hpa_free(d->d_wpack);
     hpa_free(d->d_fold);
-    hpa_free(d->d_attn_ws); hpa_free(d->d_flat_ws);
+    hpa_free(d->d_attn_ws);
     hpa_free(d->pl_rec); hpa_free(d->pl_slab); hpa_free(d->pl_ctr);
-    if (d->lane_stream) hpa_stream_destroy(d->lane_stream);
-    for (int k = 0; k < 3; k++)
-        if (d->lane_ev[k]) hpa_event_destroy(d->lane_ev[k]);
     hpa_free(d->d_rng);
     hpa_free(d->pos_logits);
     hpa_host_free(d->h_next);
@@ -890,15 +875,6 @@ static int dec_pick_B(const GPT2Decode* d) {
  * the first code of any step also sticks in d_next[B] for gpt2_decode_status) */
 #define DEC_ERR_INTS 32
 
-static int dec_lanes_setup(GPT2Decode* d);
-
-/* rows [*r0, *r0 + *nb) of lane 0 or 1 of the two-lane step; lane -1: the
- * whole batch (the one-lane step) */
-static void dec_lane_rows(const GPT2Decode* d, int lane, int* r0, int* nb) {
-    *r0 = lane == 1 ? d->lane_rows : 0;
-    *nb = lane < 0 ? d->B : lane == 0 ? d->lane_rows : d->B - d->lane_rows;
-}
-
 /* the attention's context ranges and their workspace (zeroed whenever the
  * split count changes: the counters sit after the records of that count) */
 static int dec_set_splits(GPT2Decode* d, int splits) {
@@ -915,22 +891,6 @@ static int dec_set_splits(GPT2Decode* d, int splits) {
         hpa_device_info(NULL, 0, &ncu, NULL);
         d->attn_waves = hpa_attn_pick_waves(dec_pick_B(d), d->pool.num_heads, splits, ncu);
     }
-    if (dec_lanes_setup(d)) return 1; /* lanes need one context range */
-    {   /* the balanced form on request only: measured slower than the
-         * (sequence, head, range) grid at every small batch (B = 4 / 8 / 16 /
-         * 21: 13.5 / 16.3 / 22.5 / 27.6 us against 9.8 / 13.0 / 19.4 / 23.7,
-         * profiles/r4/experiments/balanced_attention.txt): a run that spans
-         * two pairs folds and publishes them one after the other, so its
-         * dependent round trips add up.  Never under global picks (its sums
-         * depend on the whole batch's contexts). */
-        const int on = d->attn_flat_want == 2 && !d->pl_global_B;
-        if (on && !d->d_flat_ws) {
-            d->flat_ws_bytes = hpa_attn_flat_ws_bytes(d->B, d->pool.num_heads, d->max_ctx);
-            d->d_flat_ws = hpa_malloc(d->flat_ws_bytes);
-            if (!d->d_flat_ws || hpa_memset_async(d->d_flat_ws, 0, d->flat_ws_bytes)) return 1;
-        }
-        d->attn_flat = on && d->B <= 64;
-    }
     if (d->graph) { /* recapture with the new grid */
         hpa_synchronize();
         hpa_graph_destroy(d->graph);
@@ -940,30 +900,6 @@ static int dec_set_splits(GPT2Decode* d, int splits) {
 }
 
 static const float* wpack_at(const GPT2Decode* d, size_t off);
-
-/* the two-lane step applies to chain form 6 at 33..64 rows with one context
- * range per (sequence, head): lane 0 takes the first ceil(R/2) row blocks.
- * Form 6's rows do not depend on the row blocks a launch holds, and the
- * attention's on nothing but the row, so a two-lane step computes the
- * one-lane step's numbers bit for bit (tests/test_gpu_layer.py).  Opt-in
- * only (auto = off): measured slower, 1.40 (eager) / 1.71 (graph) against
- * 1.11 ms per step at B = 64 -- a chain beside an attention launch takes
- * twice as long, its hand-offs queued behind the K/V stream
- * (profiles/r4/experiments/two_lane_step.txt). */
-static int dec_lanes_setup(GPT2Decode* d) {
-    const int R = (d->B + 15) / 16;
-    const int on = d->lanes_want == 2;
-    d->lanes = 1;
-    d->lane_rows = d->B;
-    if (!on || d->pl_on != 3 || d->pl_wform != 6 || R < 3 || d->attn_splits != 1) return 0;
-    if (!d->lane_stream) d->lane_stream = hpa_stream_create();
-    for (int k = 0; k < 3; k++)
-        if (!d->lane_ev[k]) d->lane_ev[k] = hpa_event_create_nt();
-    if (!d->lane_stream || !d->lane_ev[0] || !d->lane_ev[1] || !d->lane_ev[2]) return 1;
-    d->lanes = 2;
-    d->lane_rows = 16 * ((R + 1) / 2);
-    return 0;
-}
 
 /* the persistent layer's workspace, where it applies (fp32 LN-folded weights,
  * the shapes hpa_decode_layer_eligible accepts) */
@@ -1013,34 +949,29 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
     }
     if (!d->pl_slab) {
         d->pl_slab_n = sz[1];
-        d->pl_slab = (float*)hpa_malloc(2 * sz[1] * sizeof(float));
+        d->pl_slab = (float*)hpa_malloc(sz[1] * sizeof(float));
     }
     if (!d->pl_ctr) {
         d->pl_ctr_ints = sz[2];
-        d->pl_ctr = (int*)hpa_malloc((DEC_ERR_INTS + 2 * (size_t)c.num_layers * sz[2]) * sizeof(int));
+        d->pl_ctr = (int*)hpa_malloc((DEC_ERR_INTS + (size_t)c.num_layers * sz[2]) * sizeof(int));
     }
     if (!d->pl_rec || !d->pl_slab || !d->pl_ctr) return 1;
     d->pl_splits = splits;
     d->pl_on = mode;
-    return dec_lanes_setup(d);
+    return 0;
 }
 
-/* layer l of the persistent path: attention(l) .. fcproj(l), qkv(l+1), over
- * the rows of lane `lane` (-1: every row; frag buffers hold whole 16-row
- * blocks, so a lane's rows start r0 * C floats in) */
-static int dec_layer(GPT2* model, int l, int lane) {
+/* layer l of the persistent path: attention(l) .. fcproj(l), qkv(l+1) */
+static int dec_layer(GPT2* model, int l) {
     GPT2Decode* d = model->decode;
     const GPT2Config c = model->config;
     const int C = c.channels, L = c.num_layers;
     const ParameterTensors* w = &model->params;
     const size_t lc = (size_t)l * C;
     const size_t e_layer = d->wpack_off[3] + hpa_frag_elems(C, 4 * C);
-    int r0, nb;
-    dec_lane_rows(d, lane, &r0, &nb);
-    const size_t rc0 = (size_t)r0 * C;
     HpaLayerArgs a;
     memset(&a, 0, sizeof(a));
-    a.B = nb;
+    a.B = d->B;
     a.C = C;
     a.num_heads = c.num_heads;
     a.splits = d->pl_splits;
@@ -1048,14 +979,14 @@ static int dec_layer(GPT2* model, int l, int lane) {
     a.chain_only = d->pl_on == 3 ? d->pl_wform : d->pl_on == 2;
     a.pool = &d->pool;
     a.layer = l;
-    a.block_table = d->d_bt + (size_t)r0 * d->bt_stride;
+    a.block_table = d->d_bt;
     a.bt_stride = d->bt_stride;
-    a.pos = d->d_pos + r0;
-    a.q = d->d_q + rc0;
-    a.att = d->att + rc0;
-    a.res = d->res + rc0;
-    a.res2 = d->res2 + rc0;
-    a.fch = d->fch + 4 * rc0;
+    a.pos = d->d_pos;
+    a.q = d->d_q;
+    a.att = d->att;
+    a.res = d->res;
+    a.res2 = d->res2;
+    a.fch = d->fch;
     a.w_ap = wpack_at(d, e_layer * l + d->wpack_off[1]);
     a.b_ap = w->attprojb + lc;
     a.w_fc = wpack_at(d, e_layer * l + d->wpack_off[2]);
@@ -1067,13 +998,13 @@ static int dec_layer(GPT2* model, int l, int lane) {
         a.w_qkv = wpack_at(d, e_layer * (l + 1) + d->wpack_off[0]);
         a.qkv_c1 = d->d_fold + 14 * (lc + C);
         a.qkv_c2 = a.qkv_c1 + 3 * C;
-        a.q_out = d->d_q + rc0; /* every read of q(l) is done before the first qkv(l+1) store */
+        a.q_out = d->d_q; /* every read of q(l) is done before the first qkv(l+1) store */
     }
-    a.stats_out = a.last ? d->st1 + 2 * (size_t)r0 : NULL; /* LNf statistics for the logits, */
-    a.stats_mp = d->Mp;                                    /* rows of the whole batch */
+    a.stats_out = a.last ? d->st1 : NULL; /* LNf statistics for the logits */
+    a.stats_mp = d->Mp;
     a.rec = d->pl_rec;
-    a.slab = d->pl_slab + (size_t)(lane > 0) * d->pl_slab_n;
-    a.counters = d->pl_ctr + DEC_ERR_INTS + ((size_t)(lane > 0) * L + l) * d->pl_ctr_ints;
+    a.slab = d->pl_slab;
+    a.counters = d->pl_ctr + DEC_ERR_INTS + (size_t)l * d->pl_ctr_ints;
     a.err = d->pl_ctr;                  /* this step's (zeroed with the counters) */
     a.err_sticky = d->d_next + d->B;    /* first code of any step, until gpt2_decode_status */
     return hpa_decode_layer(&a);
@@ -1086,7 +1017,6 @@ static int dec_layer(GPT2* model, int l, int lane) {
 static int dec_rezero(GPT2Decode* d) {
     int rc = 0;
     if (d->d_attn_ws) rc |= hpa_memset_async(d->d_attn_ws, 0, d->attn_ws_bytes);
-    if (d->d_flat_ws) rc |= hpa_memset_async(d->d_flat_ws, 0, d->flat_ws_bytes);
     if (d->sk_cnt && d->sk_cnt_n) rc |= hpa_memset_async(d->sk_cnt, 0, d->sk_cnt_n * sizeof(int));
     if (d->ring_cnt && d->ring_cnt_n) rc |= hpa_memset_async(d->ring_cnt, 0, d->ring_cnt_n * sizeof(int));
     return rc;
@@ -1451,25 +1381,18 @@ static int dec_pick(GPT2* model, const int* active) {
     return hpa_argmax_final(d->part, npart, d->Mp, d->B, d->d_next, d->d_tokens, d->d_pos, active);
 }
 
-/* one decode-attention launch over rows [r0, r0 + nb) (frag output) in the
- * engine's form: balanced (attn_flat) or the (sequence, head, range) grid */
-static int dec_attn_call(GPT2Decode* d, int l, int r0, int nb, const int* pos, float* out) {
-    const size_t C = (size_t)d->pool.num_heads * 64;
-    if (d->attn_flat)
-        return hpa_paged_attention_decode_flat(d->d_q + r0 * C, &d->pool, l, d->d_bt + (size_t)r0 * d->bt_stride,
-                                               d->bt_stride, pos, out, nb, d->max_ctx, d->d_flat_ws, 1, 0, 0);
-    return hpa_paged_attention_decode_split_w(d->d_q + r0 * C, &d->pool, l, d->d_bt + (size_t)r0 * d->bt_stride,
-                                              d->bt_stride, pos, out, nb, d->attn_splits, d->d_attn_ws, 1,
-                                              d->attn_waves);
+/* one decode-attention launch: the (sequence, head, context range) grid,
+ * frag output */
+static int dec_attn_call(GPT2Decode* d, int l, const int* pos, float* out) {
+    return hpa_paged_attention_decode_split_w(d->d_q, &d->pool, l, d->d_bt, d->bt_stride, pos, out, d->B,
+                                              d->attn_splits, d->d_attn_ws, 1, d->attn_waves);
 }
 
-static int dec_attention(GPT2* model, int l, int lane) {
+static int dec_attention(GPT2* model, int l) {
     GPT2Decode* d = model->decode;
-    const size_t C = (size_t)model->config.channels;
-    int r0, nb, rc = 0;
-    dec_lane_rows(d, lane, &r0, &nb);
+    int rc = 0;
     if (d->profiling) rc |= hpa_event_record(d->prof_ev[0]);
-    rc |= dec_attn_call(d, l, r0, nb, d->d_pos + r0, d->att + r0 * C);
+    rc |= dec_attn_call(d, l, d->d_pos, d->att);
     if (d->profiling) {
         rc |= hpa_event_record(d->prof_ev[1]);
         const float ms = hpa_event_elapsed_ms(d->prof_ev[0], d->prof_ev[1]); /* waits for this launch */
@@ -1477,38 +1400,6 @@ static int dec_attention(GPT2* model, int l, int lane) {
         d->prof_ms += ms;
         d->prof_launches++;
     }
-    return rc;
-}
-
-/* the layers of the two-lane step (dec_lanes_setup): lane 0 on the current
- * stream, lane 1 on lane_stream, forked after qkv(0) and joined before the
- * logits.  Per layer a lane runs its attention, then its chain; the chain
- * launches alternate (lane 0's of layer l waits for lane 1's of layer l-1 and
- * lane 1's for lane 0's: two persistent launches never share the chip, so
- * every chain workgroup is resident), while each attention launch is free to
- * run beside the other lane's chain -- the chain's in-launch hand-offs are
- * latency-bound, the attention is HBM-bound. */
-static int dec_lane_layers(GPT2* model) {
-    GPT2Decode* d = model->decode;
-    const int L = model->config.num_layers;
-    void* s0 = hpa_get_stream();
-    int rc = hpa_event_record(d->lane_ev[0]);
-    rc |= hpa_set_stream(d->lane_stream);
-    rc |= hpa_stream_wait_event(d->lane_ev[0]);
-    rc |= hpa_set_stream(s0);
-    for (int l = 0; l < L && !rc; l++) {
-        rc |= dec_attention(model, l, 0);
-        if (l > 0) rc |= hpa_stream_wait_event(d->lane_ev[2]);
-        rc |= dec_layer(model, l, 0);
-        rc |= hpa_event_record(d->lane_ev[1]);
-        rc |= hpa_set_stream(d->lane_stream);
-        rc |= dec_attention(model, l, 1);
-        rc |= hpa_stream_wait_event(d->lane_ev[1]);
-        rc |= dec_layer(model, l, 1);
-        rc |= hpa_event_record(d->lane_ev[2]);
-        rc |= hpa_set_stream(s0);
-    }
-    rc |= hpa_stream_wait_event(d->lane_ev[2]); /* join */
     return rc;
 }
 
@@ -1547,9 +1438,8 @@ static int dec_launch(GPT2* model) {
     const int L = model->config.num_layers;
     const int C = model->config.channels;
     const int pl = d->pl_on && !d->profiling;
-    const int lanes = pl && d->lanes == 2 && !d->trace_x ? 2 : 1;
     /* persistent layers: the embed kernel also zeroes their hand-off counters */
-    const size_t zb = (DEC_ERR_INTS + (size_t)lanes * L * d->pl_ctr_ints) * sizeof(int);
+    const size_t zb = (DEC_ERR_INTS + (size_t)L * d->pl_ctr_ints) * sizeof(int);
     /* chain form 6 (and form 8 at C = 768, which sums as form 6): embed +
      * qkv(0) + the counter zeroing in one launch */
     const int first = pl && DEC_FIRST_LAUNCH && d->pl_on == 3 &&
@@ -1562,14 +1452,10 @@ static int dec_launch(GPT2* model) {
     DEC_TRACE(0);
     if (pl) { /* qkv(0), then one persistent launch per layer */
         if (!first) rc |= dec_gemm(model, 0, G_QKV);
-        if (lanes == 2) {
-            rc |= dec_lane_layers(model);
-        } else {
-            for (int l = 0; l < L && !rc; l++) {
-                if (d->pl_on >= 2) rc |= dec_attention(model, l, -1); /* chain form: the attention's own launch */
-                rc |= dec_layer(model, l, -1);
-                DEC_TRACE(l + 1);
-            }
+        for (int l = 0; l < L && !rc; l++) {
+            if (d->pl_on >= 2) rc |= dec_attention(model, l); /* chain form: the attention's own launch */
+            rc |= dec_layer(model, l);
+            DEC_TRACE(l + 1);
         }
         rc |= dec_gemm(model, 0, G_LOGITS);
         rc |= dec_pick(model, NULL); /* a separate argmax launch: the in-launch pick (HpaFusedGemm.pick_next)
@@ -1578,7 +1464,7 @@ static int dec_launch(GPT2* model) {
     }
     for (int l = 0; l < L && !rc; l++) {
         rc |= dec_gemm(model, l, G_QKV);
-        rc |= dec_attention(model, l, -1);
+        rc |= dec_attention(model, l);
         rc |= dec_gemm(model, l, G_ATTPROJ);
         rc |= dec_gemm(model, l, G_FC);
         rc |= dec_gemm(model, l, G_FCPROJ);
@@ -1643,19 +1529,6 @@ int gpt2_decode_set_attn_splits(GPT2* model, int splits) {
 }
 
 int gpt2_decode_attn_splits(GPT2* model) { return model->decode ? model->decode->attn_splits : 0; }
-
-/* the balanced attention form (hpa_paged_attention_decode_flat): 0 auto (=
- * off: measured slower), 1 off, 2 on (not under global picks);
- * gpt2_decode_attn_flat: in use */
-int gpt2_decode_set_attn_flat(GPT2* model, int mode) {
-    GPT2Decode* d = model ? model->decode : NULL;
-    if (!d || mode < 0 || mode > 2) return 1;
-    if (hpa_synchronize()) return 1;
-    d->attn_flat_want = mode;
-    return dec_set_splits(d, d->attn_splits);
-}
-
-int gpt2_decode_attn_flat(GPT2* model) { return model && model->decode ? model->decode->attn_flat : 0; }
 
 /* waves per attention workgroup the engine picked (hpa_set_attention_waves may override it) */
 int gpt2_decode_attn_waves(GPT2* model) { return model->decode ? model->decode->attn_waves : 0; }
@@ -1948,23 +1821,6 @@ int gpt2_decode_set_layer_kernel(GPT2* model, int enable) {
 
 int gpt2_decode_layer_kernel(GPT2* model) { return model->decode ? model->decode->pl_on : 0; }
 
-/* the two-lane step (dec_lane_layers): 0 auto, 1 off, 2 on where it applies
- * (chain form 6, 33..64 rows, one context range); gpt2_decode_lanes: in use */
-int gpt2_decode_set_lanes(GPT2* model, int lanes) {
-    GPT2Decode* d = model ? model->decode : NULL;
-    if (!d || lanes < 0 || lanes > 2) return 1;
-    if (hpa_synchronize()) return 1;
-    d->lanes_want = lanes;
-    if (dec_lanes_setup(d)) return 1;
-    if (d->graph) {
-        hpa_graph_destroy(d->graph);
-        d->graph = NULL;
-        if (dec_rezero(d)) return 1;
-    }
-    return 0;
-}
-
-int gpt2_decode_lanes(GPT2* model) { return model && model->decode ? model->decode->lanes : 0; }
 
 /* sequences the LRU policy paged out since the last call (their position
  * restarted at 0: the caller must prefill them again); mask (nullable, [B])
@@ -2125,9 +1981,9 @@ int gpt2_decode_time_attention(GPT2* model, int iters, double* ms_per_launch, do
         for (int b = 0; b < B; b++) h_p[b] = d->h_pos[b] - 1;
         rc |= hpa_memcpy(d_p, h_p, B * sizeof(int));
         /* warm-up launch, then the timed ones */
-        rc |= dec_attn_call(d, 0, 0, B, d_p, out);
+        rc |= dec_attn_call(d, 0, d_p, out);
         rc |= hpa_event_record(e0);
-        for (int i = 0; i < iters && !rc; i++) rc |= dec_attn_call(d, i % L, 0, B, d_p, out);
+        for (int i = 0; i < iters && !rc; i++) rc |= dec_attn_call(d, i % L, d_p, out);
         rc |= hpa_event_record(e1);
         const float ms = rc ? -1.f : hpa_event_elapsed_ms(e0, e1);
         if (ms < 0) rc = 1;
@@ -2173,7 +2029,7 @@ int gpt2_decode_time_attention_pf(GPT2* model, int iters, double frac, int pf_gr
             rc |= hpa_event_record(e[0]);
             if (nb) rc |= hpa_l3_prefetch((const char*)d->pool.base + (size_t)l * slab, nb, pf_grid);
             rc |= hpa_event_record(e[1]);
-            rc |= dec_attn_call(d, l, 0, B, d_p, out);
+            rc |= dec_attn_call(d, l, d_p, out);
             rc |= hpa_event_record(e[2]);
             if (rc) break;
             const float a = hpa_event_elapsed_ms(e[1], e[2]), p = hpa_event_elapsed_ms(e[0], e[1]);

@@ -181,8 +181,6 @@ def lib():
     _sig(L, "hpa_pool_fill_random", i, [P, v, i, i, i, ctypes.c_uint64])
     _sig(L, "hpa_paged_attention_decode", i, [v, P, i, v, i, v, v, i])
     _sig(L, "hpa_attn_ws_bytes", sz, [i, i, i])
-    _sig(L, "hpa_attn_flat_ws_bytes", sz, [i, i, i])
-    _sig(L, "hpa_paged_attention_decode_flat", i, [v, P, i, v, i, v, v, i, i, v, i, i, i])
     _sig(L, "hpa_attn_pick_splits", i, [i, i, i, i])
     _sig(L, "hpa_paged_attention_decode_split", i, [v, P, i, v, i, v, v, i, i, v, i])
     _sig(L, "hpa_comm_id_bytes", sz, [])
@@ -264,10 +262,6 @@ def lib():
     _sig(L, "hpa_pool_fill_random_ex", i, [P, v, i, i, i, ctypes.c_uint64, i])
     _sig(L, "hpa_logits_kernel", i, [i, i, i])
     _sig(L, "gpt2_decode_layer_kernel", i, [v])
-    _sig(L, "gpt2_decode_set_lanes", i, [v, i])
-    _sig(L, "gpt2_decode_set_attn_flat", i, [v, i])
-    _sig(L, "gpt2_decode_attn_flat", i, [v])
-    _sig(L, "gpt2_decode_lanes", i, [v])
     _sig(L, "gpt2_decode_status", i, [v])
     _sig(L, "hpa_decode_layer_eligible", i, [i, i, i, i])
     _sig(L, "hpa_decode_layer_pick_splits", i, [i, i, i])
@@ -658,24 +652,6 @@ class Model:
 
     def layer_kernel(self):
         return bool(lib().gpt2_decode_layer_kernel(self.h))
-
-    def set_attn_flat(self, mode):
-        """balanced decode attention (gpt2_decode_set_attn_flat): 0 auto, 1 off,
-        2 on; returns whether it is in use"""
-        check(lib().gpt2_decode_set_attn_flat(self.h, int(mode)), "set_attn_flat")
-        return bool(lib().gpt2_decode_attn_flat(self.h))
-
-    def attn_flat(self):
-        return bool(lib().gpt2_decode_attn_flat(self.h))
-
-    def set_lanes(self, lanes):
-        """two-lane step (paged_infer.h gpt2_decode_set_lanes): 0 auto, 1 off,
-        2 on where it applies; returns the lanes now in use"""
-        check(lib().gpt2_decode_set_lanes(self.h, int(lanes)), "set_lanes")
-        return int(lib().gpt2_decode_lanes(self.h))
-
-    def lanes(self):
-        return int(lib().gpt2_decode_lanes(self.h))
 
     def layer_form(self):
         """0 five launches per layer, 1 full persistent layer, 2 attention launch + persistent chain,

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 
-def _run_case(hip, P, ctxs, NH, waves=4, seed=0, q_scale=2.0, kv=None, splits=0, bf16=False, repeat=1, flat=None):
+def _run_case(hip, P, ctxs, NH, waves=4, seed=0, q_scale=2.0, kv=None, splits=0, bf16=False, repeat=1):
     rng = np.random.default_rng(seed)
     L = hip.lib()
     C = NH * 64
@@ -46,25 +46,7 @@ def _run_case(hip, P, ctxs, NH, waves=4, seed=0, q_scale=2.0, kv=None, splits=0,
     d_q = hip.DeviceBuffer.from_array(q)
     d_bt = hip.DeviceBuffer.from_array(bt)
     d_pos = hip.DeviceBuffer.from_array(pos)
-    if flat is not None:  # balanced form (workgroups), frag output, repeated launches over one workspace
-        Mp = (B + 15) // 16 * 16
-        d_out = hip.DeviceBuffer(Mp * C * 4)
-        max_ctx = max(ctxs)
-        wsb = L.hpa_attn_flat_ws_bytes(B, NH, max_ctx)
-        d_ws = hip.DeviceBuffer(wsb)
-        hip.check(L.hpa_memset_async(d_ws.ptr, 0, wsb))
-        outs = []
-        for _ in range(repeat):
-            hip.check(L.hpa_paged_attention_decode_flat(d_q.ptr, pool.ref, 0, d_bt.ptr, maxp, d_pos.ptr, d_out.ptr, B,
-                                                        max_ctx, d_ws.ptr, 1, waves, flat), "flat attention")
-            hip.check(L.hpa_synchronize())
-            outs.append(hip.from_frag(d_out.download(Mp * C), B, C))
-        for o in outs[1:]:  # fixed merge order: bit-identical every launch
-            assert np.array_equal(o, outs[0])
-        kmax = (max_ctx + 63) // 64 + 1
-        assert not d_ws.download(B * NH, np.int32, offset=B * NH * kmax * 68 * 4).any()  # counters left zero
-        out = outs[0]
-    elif splits:  # split-context form, frag output, repeated launches over one workspace
+    if splits:  # split-context form, frag output, repeated launches over one workspace
         Mp = (B + 15) // 16 * 16
         d_out = hip.DeviceBuffer(Mp * C * 4)
         wsb = L.hpa_attn_ws_bytes(B, NH, splits)
@@ -262,51 +244,6 @@ def test_split_context_attention_strong_scaling_shapes(hip, B):
             vp[i][:m] = v[i * P:i * P + m]
         ref = oc.attention_decode(q[b], kp, vp, n, NH)
         assert np.abs(outs[0][b] - ref).max() <= TOL, b
-
-
-@pytest.mark.parametrize("P", [8, 16, 32])
-@pytest.mark.parametrize("workgroups", [0, 7, 64])
-@pytest.mark.parametrize("waves", [4, 8])
-def test_flat_attention(hip, P, workgroups, waves):
-    """balanced form (hpa_paged_attention_decode_flat): the flattened list of
-    every (sequence, head)'s 64-token tiles cut into equal runs over the
-    workgroups (0 = one per CU, capped at the tile count: one tile each here;
-    7: runs spanning several pairs); ragged contexts, pairs merged across
-    runs in run order, bit-identical relaunch, counters left zero"""
-    ctxs = [1, 2, 5, 63, 64, 65, 200, 257, 1024]
-    out, ref = _run_case(hip, P, ctxs, NH=3, waves=waves, seed=P + workgroups, flat=workgroups, repeat=3)
-    assert np.abs(out - ref).max() <= TOL
-
-
-@pytest.mark.parametrize("P", [8, 16, 32])
-@pytest.mark.parametrize("workgroups", [0, 64])
-@pytest.mark.parametrize("bf16", [False, True])
-def test_flat16_attention(hip, P, workgroups, bf16):
-    """the balanced form's 16-wave kernel (every tile of a run in flight, one
-    tile per wave, pieces folded by their first wave): ragged contexts, runs
-    spanning several pairs at 64 workgroups, fp32 and bf16 pools"""
-    ctxs = [1, 2, 5, 63, 64, 65, 200, 257, 1024]
-    out, ref = _run_case(hip, P, ctxs, NH=3, waves=16, seed=P + workgroups, flat=workgroups, repeat=3, bf16=bf16)
-    assert np.abs(out - ref).max() <= TOL
-
-
-@pytest.mark.parametrize("workgroups", [0, 5])
-def test_flat_attention_bf16_pool_and_peaked(hip, workgroups):
-    ctxs = [1, 2, 7, 63, 64, 65, 200, 257, 1024]
-    out, ref = _run_case(hip, 8, ctxs, NH=3, seed=3, bf16=True, flat=workgroups, repeat=2)
-    assert np.abs(out - ref).max() <= TOL
-    out, ref = _run_case(hip, 16, [300, 999, 64], NH=2, seed=5, q_scale=40.0, flat=workgroups)
-    assert np.abs(out - ref).max() <= TOL
-
-
-@pytest.mark.parametrize("B", [4, 8, 16])
-def test_flat_attention_strong_scaling_shapes(hip, B):
-    """the small per-GPU batches at GPT-2 124M shapes (ctx 1024, page 16,
-    ragged) on the balanced form: every sequence vs the oracle"""
-    ctxs = [1024 - 37 * i for i in range(B)]
-    for waves in (0, 4):  # 0: the 16-wave kernel where runs fit 16 tiles (here), else 4 waves
-        out, ref = _run_case(hip, 16, ctxs, NH=12, waves=waves, seed=B, flat=0, repeat=2)
-        assert np.abs(out - ref).max() <= TOL, waves
 
 
 @pytest.mark.parametrize("P", [8, 16, 32])

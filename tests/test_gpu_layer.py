@@ -297,42 +297,6 @@ def test_chain8_equals_chain6_124m(hip, B):
     assert np.array_equal(run(6, False), run(5, False))
 
 
-@pytest.mark.parametrize("B", [64, 40, 33])
-def test_two_lane_step_equals_one_lane(hip, B):
-    """the two-lane step (gpt2_decode_set_lanes(2): lane 0 = the first
-    ceil(R/2) row blocks on the library stream, lane 1 = the rest on a second
-    stream, each lane's attention beside the other's chain launch) computes
-    the one-lane step's logits, next ids and positions bit for bit, as graph
-    replay and eagerly; below 33 rows or with split contexts it stays off"""
-    params = synth.params(GPT2_124M, seed=96)
-    steps = 4
-    toks = np.random.default_rng(96).integers(0, GPT2_124M["V"], (steps, B)).astype(np.int32)
-
-    def run(lanes, graph=True):
-        m = _model(hip, GPT2_124M, params, B, 16, 1, mode=5)
-        m.set_graph(graph)
-        m.set_attn_splits(1)  # lanes need one context range (33..47 rows pick 2 by default)
-        assert m.set_lanes(lanes) == lanes
-        m.fill_random(700, seed=13)
-        out, ids = [], []
-        for t in range(steps):
-            ids.append(m.step(toks[t]))
-            out.append(m.logits())
-        m.status()
-        pos = m.positions()
-        m.close()
-        return np.stack(out), np.stack(ids), pos
-
-    one = run(1)
-    for graph in (True, False):
-        two = run(2, graph)
-        for a, b in zip(one, two):
-            assert np.array_equal(a, b), graph
-    m = _model(hip, GPT2_124M, params, 32, 16, 1, mode=5)
-    assert m.set_lanes(2) == 1  # 32 rows: two row blocks, no lanes
-    m.close()
-
-
 GPT2_XL = dict(maxT=1024, V=50257, L=48, NH=25, C=1600)
 
 
