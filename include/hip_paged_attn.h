@@ -375,9 +375,9 @@ typedef struct {
                                      out at once when it is set) */
     int* err_sticky;              /* nullable: the first code also lands here, never zeroed by a
                                      step (gpt2_decode_status reads and clears it) */
-    int stats_mp;                 /* row stride of stats_out; 0: this launch's Mp.  A launch over a
-                                     slice of the batch's row blocks (the engine's two-lane step)
-                                     passes the batch's Mp and stats_out advanced to its first row */
+    int stats_mp;                 /* row stride of stats_out; 0: this launch's Mp */
+    int attproj_done;             /* chain form 6: 1 when hpa_decode_attention_ap ran this layer's
+                                     attproj (the chain starts at fc) */
 } HpaLayerArgs;
 /* 1 if the persistent layer applies (shape, CU count, residency), else 0 */
 int hpa_decode_layer_eligible(int B, int C, int num_heads, int splits);
@@ -389,6 +389,22 @@ int hpa_decode_layer_pick_splits(int B, int num_heads, int max_ctx);
 /* sizes: out[0] = rec floats, out[1] = slab floats, out[2] = counter ints per layer */
 int hpa_decode_layer_sizes(int B, int C, int num_heads, int splits, size_t* out3);
 int hpa_decode_layer(const HpaLayerArgs* a);
+/* the decode attention of layer a->layer with chain form 6's attproj phase
+ * in the same launch (one row block, B <= 16, where the attention grid
+ * leaves CUs idle): B*12*splits attention workgroups of `waves` waves (4 or
+ * 8; output att in frag layout, published to the attproj units), then 48
+ * workgroups, one per attproj tile, that load their weights while the
+ * attention streams, wait for the row block's attention outputs and write
+ * res2 in form 6's summation order (bit-identical to the chain's phase B),
+ * arriving on the chain's fc counters; the chain launch then runs with
+ * attproj_done = 1.  Reads B, C, num_heads, splits, pool, layer,
+ * block_table, bt_stride, pos, q, att, res, res2, w_ap, b_ap, rec (split
+ * records + counters as hpa_attn_ws_bytes lays them out; splits > 1),
+ * counters (layer l's block, zero before the step), err, err_sticky. */
+int hpa_decode_attn_ap_eligible(int B, int C, int num_heads, int splits, int waves);
+int hpa_decode_attention_ap(const HpaLayerArgs* a, int waves);
+/* the process-wide attention waves override of hpa_set_attention_waves (0: none) */
+int hpa_get_attention_waves(void);
 /* the decode step's first launch at GPT-2 124M shapes (C = 768, 12 heads,
  * B <= 64, LN1 folded into w_qkv / qkv_c1 / qkv_c2 of layer 0): the embedding
  * wte[tokens[b]] + wpe[pos[b]] (encoder_forward, paged_infer.c:41-47) into

@@ -103,6 +103,9 @@ struct KA {
     const float *wte, *wpe;
     int4* zero;
     int zero_n4;
+    // chain form 6: phase B (attproj) already ran in the attention launch
+    // (decode_attn_ap_kernel, one row block)
+    int attproj_done;
 };
 
 // diagnostic build (-DHPA_LAYER_TRACE, tools/pl_trace.py): s_memrealtime of
@@ -1025,8 +1028,9 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
     PL_STAMP(t_start);
     PL_STORE(0, t_start);
     float fs1 = 0.f, fs2 = 0.f;
-    // B: attproj(l), 1 tile per unit: res2 = res + att . Wap^T + b
-    {
+    // B: attproj(l), 1 tile per unit: res2 = res + att . Wap^T + b (at one row
+    // block the attention launch may have run it: decode_attn_ap_kernel)
+    if (!a.attproj_done) {
         constexpr int T = 1, NG = NCT;
         const int n = R * NG;
         const bool has = bid < n;
@@ -1298,6 +1302,136 @@ __global__ __launch_bounds__(768) void decode_first6_kernel(KA args) {
     lds_barrier();
     if (ep && row < a.B)
         qkv_store6<P, BF>(a, row, col, ln_fold4(sm.wsum, er, fold_t<T>(sm.red, et, er, eq), c1, c2));
+}
+
+// ------------------------------------------------------------------ attention + attproj (form 6, one row block)
+// At one row block (B <= 16) the decode attention's grid -- B*NH*S
+// workgroups -- leaves CUs idle (B = 8: 192 of 256), and chain form 6's
+// attproj phase is its slowest: its 48 units fetch their weights at the
+// chain's start, against the other workgroups' fc prefetch (round-5 trace at
+// B = 8: attproj done at 4.1-4.7 us of a 17.5 us launch, whatever workgroups
+// hold it).  Here the ATTENTION launch carries 48 more workgroups, one per
+// attproj tile: each loads its weight tile while the attention streams, waits
+// (bounded) for the row block's B*NH attention outputs, then computes the
+// tile in form 6's summation order -- 12 virtual waves of 4 k16 steps each,
+// folded in virtual-wave order -- so res2 is bit for bit what the chain's
+// phase B computes, and arrives on the chain's fc k-group counters; the chain
+// launch then skips phase B (HpaLayerArgs.attproj_done).  Attention
+// workgroups never wait on attproj ones (no deadlock at any residency); each
+// (sequence, head) output is published sc1, drained, then one agent-scope add
+// on a counter sharded 8 ways (MI355X_MICROARCH.md "Valid forms", row 1).
+namespace ap {
+constexpr int kAttDone = c6::X1;  // the chain's X1 counters (unused under HPA_C6_GW): outputs per row block
+struct SmemAP {
+    float red[c6::NW * 256];  // [virtual wave][256]
+    int s_ok;
+};
+}  // namespace ap
+
+template <int P, int AW, bool BF>
+__global__ __launch_bounds__(AW * 64) void decode_attn_ap_kernel(KA args) {
+    using namespace c6;
+    constexpr int C = 768, NH = 12, K16 = 48, NCT = 48;
+    constexpr int TILE = P * HS;
+    const KA& a = *(const KA*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
+    (void)args;
+    const int S = a.S;
+    const int n_attn = a.B * NH * S;
+    const int bid = blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    if (bid < n_attn) {  // ---- the decode attention of (sequence, head, range), as paged_attn_decode_f32
+        __shared__ float s_m[AW];
+        __shared__ float s_l[AW];
+        __shared__ float4 s_acc[AW * 16];
+        const int bh = bid / S, sr = bid - bh * S;
+        const int b = bh / NH, h = bh - b * NH;
+        const int ctx = a.pos[b] + 1;
+        const float* __restrict__ qh = a.q + ((size_t)b * NH + h) * HS;
+        const int* bt = a.bt + (size_t)b * a.bt_stride;
+        const int n_it_all = (ctx + 63) >> 6;
+        const int it0 = S == 1 ? 0 : (int)((long long)sr * n_it_all / S);
+        const int n_it = S == 1 ? n_it_all : (int)((long long)(sr + 1) * n_it_all / S);
+        float* rec_bh = S == 1 ? nullptr : a.rec + (size_t)bh * S * kRec;
+        int* cnt = S == 1 ? nullptr : reinterpret_cast<int*>(a.rec + (size_t)n_attn * kRec) + bh;
+        float m = a.m_init, l = 0.f;
+        if constexpr (BF) {
+            const unsigned short* base = reinterpret_cast<const unsigned short*>(a.kv);
+            float4 acc[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+            hpa_attn::attn_tiles_bf16<P, AW>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, a.page_elems,
+                                             bt, a.bt_stride, ctx, it0, n_it, a.qscale, m, l, acc);
+            if (!hpa_attn::attn_fold_bf16<AW>(m, l, acc, s_m, s_l, s_acc)) return;
+            if (S > 1 && !hpa_attn::split_merge<2>(rec_bh, cnt, S, sr, m, l, acc, true)) return;
+            const float inv = l == 0.f ? 0.f : 1.f / l;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {  // dims 8*lane + 4k .. +3
+                const int fx = (int)hpa::frag_index(b, h * HS + 8 * lane + 4 * k, C);
+                hpa::store_wt16(a.att, fx * 4, make_float4(acc[k].x * inv, acc[k].y * inv, acc[k].z * inv, acc[k].w * inv));
+            }
+        } else {
+            const float* base = reinterpret_cast<const float*>(a.kv);
+            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+            hpa_attn::attn_tiles<P, AW>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, a.page_elems, bt,
+                                        a.bt_stride, ctx, it0, n_it, a.qscale, m, l, acc);
+            if (!hpa_attn::attn_fold<AW>(m, l, acc, s_m, s_l, s_acc)) return;
+            if (S > 1 && !hpa_attn::split_merge<1>(rec_bh, cnt, S, sr, m, l, &acc, true)) return;
+            const float inv = l == 0.f ? 0.f : 1.f / l;
+            const int fx = (int)hpa::frag_index(b, h * HS + 4 * lane, C);
+            hpa::store_wt16(a.att, fx * 4, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
+        }
+        // only this wave (its first lanes) stored the output: drain, then one add
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+            __hip_atomic_fetch_add(a.ctr + ap::kAttDone * 8 * kPad + (bid & 7) * kPad, 1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    // ---- attproj tile g of row block 0: res2 = res + att . Wap^T + b
+    __shared__ ap::SmemAP sm;
+    constexpr int VPW = (NW + AW - 1) / AW;  // virtual waves per wave
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tid = threadIdx.x;
+    const int g = bid - n_attn;
+    const int er = (tid & 63) >> 2, eq = tid & 3;  // epilogue thread (tid < 64): row er, columns 4 eq ..
+    const int row = er, col = g * 16 + 4 * eq;
+    const int fi = (int)hpa::frag_index(row, col, C) * 4;
+    float4 wr[VPW][1][SPW];
+#pragma unroll
+    for (int i = 0; i < VPW; ++i)
+        if (w + AW * i < NW) load_wt<1, true>(a.w_ap, K16, g, 0, w + AW * i, wr[i]);  // one reader per tile
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f), rv = bv;
+    if (tid < 64) {
+        bv = ld4(a.b_ap + col);
+        rv = hpa::load_wt16(a.res, fi);
+    }
+    if (!wait6(a, ap::kAttDone, a.B * NH, 1, sm)) return;
+    // every virtual wave's A fragments in flight together, then the MFMAs
+    float4 xv[VPW][SPW];
+#pragma unroll
+    for (int i = 0; i < VPW; ++i)
+        if (w + AW * i < NW)
+#pragma unroll
+            for (int s2 = 0; s2 < SPW; ++s2)
+                xv[i][s2] = hpa::load_wt16(a.att, (((w + AW * i) * SPW + s2) * 64 + lane) * 16);
+    __builtin_amdgcn_sched_barrier(0);
+    float fs1 = 0.f, fs2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPW; ++i)
+        if (w + AW * i < NW) {
+            f32x4 acc[1];
+            mfma_regs<1, false>(xv[i], wr[i], acc, fs1, fs2);
+            put_red_t<1>(sm.red, w + AW * i, acc);
+        }
+    lds_barrier();
+    if (tid < 64) {
+        float4 v = fold_t<1>(sm.red, 0, er, eq);
+        v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
+        const bool live = row < a.B;  // residual_forward(out, res, proj); padded rows stay 0
+        v = live ? make_float4(rv.x + v.x, rv.y + v.y, rv.z + v.z, rv.w + v.w) : make_float4(0.f, 0.f, 0.f, 0.f);
+        hpa::store_wt16(a.res2, fi, v);
+    }
+    drain_vm();
+    lds_barrier();
+    if (tid == 0) arrive_tiles(a, kCtr + 4 * NCT + kGC, 0, NW, g, 1);  // the tile's k-group of fc's A
 }
 
 // ------------------------------------------------------------------ the chain for wide layers (form 8)
@@ -1750,6 +1884,7 @@ void fill_ka(const HpaLayerArgs* h, int G, KA& a) {
     a.ctr = h->counters;
     a.err = h->err;
     a.err_sticky = h->err_sticky;
+    a.attproj_done = h->attproj_done;
 }
 
 // blocks per CU of a 768-thread instantiation (occupancy API), cached per kernel
@@ -1819,6 +1954,21 @@ int launch6(const HpaLayerArgs* h, int G) {
     decode_chain6_kernel<P, BF, TC, TD, TE><<<G, 768, 0, hpa_stream()>>>(a);
     HPA_LAUNCH_CHECK();
     return 0;
+}
+
+template <int P, bool BF, int AW>
+int launch_attn_ap(const HpaLayerArgs* h) {
+    KA a;
+    fill_ka(h, num_cus(), a);
+    const int grid = h->B * 12 * h->splits + 48;  // attention units, then one workgroup per attproj tile
+    decode_attn_ap_kernel<P, AW, BF><<<grid, AW * 64, 0, hpa_stream()>>>(a);
+    HPA_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int P, bool BF>
+int dispatch_attn_ap_t(const HpaLayerArgs* h, int waves) {
+    return waves == 8 ? launch_attn_ap<P, BF, 8>(h) : launch_attn_ap<P, BF, 4>(h);
 }
 
 // chain form 8: tiles per unit T (<= cx::XT_MAX) and tile groups NG (padded
@@ -2037,6 +2187,31 @@ int hpa_decode_first(const HpaLayerArgs* h, const int* tokens, const float* wte,
         case 64: return bf ? dispatch_first6_t<64, true>(h, G, tokens, wte, wpe, zero, zero_bytes)
                            : dispatch_first6_t<64, false>(h, G, tokens, wte, wpe, zero, zero_bytes);
         default: return hpa_fail(__FILE__, __LINE__, "decode first: page size must be 8, 16, 32 or 64");
+    }
+}
+
+int hpa_decode_attn_ap_eligible(int B, int C, int num_heads, int splits, int waves) {
+    const int G = num_cus();
+    return HPA_C6_GW && C == 768 && num_heads == 12 && B >= 1 && B <= 16 && splits >= 1 &&
+           splits <= HPA_ATTN_MAX_SPLITS && (waves == 4 || waves == 8) && G > 0 && B * 12 * splits + 48 <= G;
+}
+
+int hpa_decode_attention_ap(const HpaLayerArgs* h, int waves) {
+    HPA_REQUIRE(h && h->pool && h->pool->base, "attention + attproj: pool");
+    const HpaKVPool* pool = h->pool;
+    HPA_REQUIRE(pool->dtype == HPA_F32 || pool->dtype == HPA_BF16, "attention + attproj: fp32 or bf16 pool");
+    HPA_REQUIRE(pool->head_size == HS && h->layer >= 0 && h->layer < pool->num_layers, "attention + attproj: layer");
+    HPA_REQUIRE(hpa_decode_attn_ap_eligible(h->B, h->C, h->num_heads, h->splits, waves),
+                "attention + attproj: C = 768, 12 heads, B <= 16, waves 4 / 8, B*12*splits + 48 <= CUs");
+    HPA_REQUIRE(h->q && h->att && h->res && h->res2 && h->w_ap && h->b_ap && h->block_table && h->pos &&
+                    h->counters && h->err && (h->splits == 1 || h->rec),
+                "attention + attproj: null operand");
+    switch (pool->page_size) {
+        case 8: return pool->dtype == HPA_BF16 ? dispatch_attn_ap_t<8, true>(h, waves) : dispatch_attn_ap_t<8, false>(h, waves);
+        case 16: return pool->dtype == HPA_BF16 ? dispatch_attn_ap_t<16, true>(h, waves) : dispatch_attn_ap_t<16, false>(h, waves);
+        case 32: return pool->dtype == HPA_BF16 ? dispatch_attn_ap_t<32, true>(h, waves) : dispatch_attn_ap_t<32, false>(h, waves);
+        case 64: return pool->dtype == HPA_BF16 ? dispatch_attn_ap_t<64, true>(h, waves) : dispatch_attn_ap_t<64, false>(h, waves);
+        default: return hpa_fail(__FILE__, __LINE__, "attention + attproj: page size 8, 16, 32 or 64");
     }
 }
 

@@ -961,8 +961,8 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
     return 0;
 }
 
-/* layer l of the persistent path: attention(l) .. fcproj(l), qkv(l+1) */
-static int dec_layer(GPT2* model, int l) {
+/* the persistent path's arguments of layer l: attention(l) .. fcproj(l), qkv(l+1) */
+static void dec_layer_args(GPT2* model, int l, HpaLayerArgs* ap) {
     GPT2Decode* d = model->decode;
     const GPT2Config c = model->config;
     const int C = c.channels, L = c.num_layers;
@@ -1007,7 +1007,41 @@ static int dec_layer(GPT2* model, int l) {
     a.counters = d->pl_ctr + DEC_ERR_INTS + (size_t)l * d->pl_ctr_ints;
     a.err = d->pl_ctr;                  /* this step's (zeroed with the counters) */
     a.err_sticky = d->d_next + d->B;    /* first code of any step, until gpt2_decode_status */
+    *ap = a;
+}
+
+/* layer l's persistent launch; attproj_done: the attention launch ran its
+ * attproj (hpa_decode_attention_ap) */
+static int dec_layer(GPT2* model, int l, int attproj_done) {
+    HpaLayerArgs a;
+    dec_layer_args(model, l, &a);
+    a.attproj_done = attproj_done;
     return hpa_decode_layer(&a);
+}
+
+#ifndef DEC_ATTN_AP
+#define DEC_ATTN_AP 1 /* A/B builds: 0 = attproj stays the chain's phase B at every batch */
+#endif
+/* waves of the attention + attproj launch where it applies to this step
+ * (chain form 6, one row block, the attention grid plus 48 workgroups
+ * within the CUs), else 0 */
+static int dec_attn_ap_waves(GPT2* model) {
+    GPT2Decode* d = model->decode;
+    if (!DEC_ATTN_AP || d->pl_on != 3 || d->pl_wform != 6 || d->profiling) return 0;
+    const int ov = hpa_get_attention_waves();
+    const int nw = ov ? ov : d->attn_waves;
+    return hpa_decode_attn_ap_eligible(d->B, model->config.channels, model->config.num_heads, d->attn_splits, nw)
+               ? nw : 0;
+}
+
+/* layer l's attention with the chain's attproj in the same launch */
+static int dec_attention_ap(GPT2* model, int l, int waves) {
+    GPT2Decode* d = model->decode;
+    HpaLayerArgs a;
+    dec_layer_args(model, l, &a);
+    a.splits = d->attn_splits;
+    a.rec = (float*)d->d_attn_ws;
+    return hpa_decode_attention_ap(&a, waves);
 }
 
 /* the in-launch arrival counters of the attention's split merge, of the
@@ -1452,9 +1486,11 @@ static int dec_launch(GPT2* model) {
     DEC_TRACE(0);
     if (pl) { /* qkv(0), then one persistent launch per layer */
         if (!first) rc |= dec_gemm(model, 0, G_QKV);
+        const int apw = dec_attn_ap_waves(model);
         for (int l = 0; l < L && !rc; l++) {
-            if (d->pl_on >= 2) rc |= dec_attention(model, l); /* chain form: the attention's own launch */
-            rc |= dec_layer(model, l);
+            /* chain form: the attention's own launch (with attproj at one row block) */
+            if (d->pl_on >= 2) rc |= apw ? dec_attention_ap(model, l, apw) : dec_attention(model, l);
+            rc |= dec_layer(model, l, apw != 0);
             DEC_TRACE(l + 1);
         }
         rc |= dec_gemm(model, 0, G_LOGITS);
@@ -1650,12 +1686,44 @@ static int prefill_gemm(GPT2* model, int l, int which, int R) {
     return hpa_gemm_fused(&g);
 }
 
+/* the logits of EVERY prefill row (gpt2_forward's window, paged_infer.c:727:
+ * the reference writes logits for all T rows): LNf(res) . wte^T over the R
+ * packed rows into rows_out [R][V] (device), one LOGITS GEMM on the looped /
+ * bf16 kernels (any row count); its argmax partials go to a scratch buffer */
+static int prefill_all_logits(GPT2* model, int R, float* rows_out) {
+    GPT2Decode* d = model->decode;
+    const GPT2Config c = model->config;
+    const int C = c.channels, V = c.vocab_size;
+    const size_t Rp = (size_t)(R + 15) / 16 * 16;
+    float* part = (float*)hpa_malloc((size_t)(V + 15) / 16 * Rp * 2 * sizeof(float));
+    if (!part) return 1;
+    HpaFusedGemm g;
+    memset(&g, 0, sizeof(g));
+    g.M = R;
+    g.w_dtype = d->w_bf16 ? HPA_BF16 : HPA_F32;
+    g.epilogue = HPA_FEPI_LOGITS;
+    g.x = d->pf_res;
+    g.K = C;
+    g.ln_stats = d->pf_st1; /* the last fcproj's 16-column statistics (prefill_gemm) */
+    g.ln_ntiles = C / 16;
+    g.ln_w = model->params.lnfw;
+    g.ln_b = model->params.lnfb;
+    g.w = wpack_at(d, d->wpack_off[4]);
+    g.N = V;
+    g.out = rows_out;
+    g.part_out = part;
+    const int rc = hpa_gemm_fused(&g) || hpa_synchronize();
+    hpa_free(part);
+    return rc;
+}
+
 /* One pass over lens[b] >= 0 new tokens of every sequence b (tokens packed
  * in sequence order): all rows through the fused GEMMs, causal multi-query
  * paged attention per sequence, then the last row of every sequence with
  * lens[b] > 0 through the logits and the greedy / sampled pick.  Sequences
- * with lens[b] = 0 are untouched (position, next token, sampler state). */
-static int dec_prefill_rows(GPT2* model, const int* tokens, const int* lens, int* next_tokens) {
+ * with lens[b] = 0 are untouched (position, next token, sampler state).
+ * all_logits (device [R][V], nullable): every row's logits too. */
+static int dec_prefill_rows(GPT2* model, const int* tokens, const int* lens, int* next_tokens, float* all_logits) {
     GPT2Decode* d = model->decode;
     if (!d) { fprintf(stderr, "[paged_infer] gpt2_decode_init first\n"); return 1; }
     const GPT2Config c = model->config;
@@ -1715,6 +1783,7 @@ static int dec_prefill_rows(GPT2* model, const int* tokens, const int* lens, int
         rc |= prefill_gemm(model, l, G_FC, (int)R);
         rc |= prefill_gemm(model, l, G_FCPROJ, (int)R);
     }
+    if (all_logits && !rc) rc |= prefill_all_logits(model, (int)R, all_logits);
     /* last row of every active sequence -> the decode rows, logits, pick; the
      * pick advances pos by one: set pos = start + len - 1 first */
     for (int b = 0; b < B; b++) hst[b] = d->h_pos[b] + (lens[b] > 0 ? lens[b] - 1 : 0);
@@ -1738,7 +1807,7 @@ int gpt2_decode_prefill(GPT2* model, const int* tokens, int T, int* next_tokens)
     int* lens = (int*)malloc(d->B * sizeof(int));
     if (!lens) return 1;
     for (int b = 0; b < d->B; b++) lens[b] = T;
-    const int rc = dec_prefill_rows(model, tokens, lens, next_tokens);
+    const int rc = dec_prefill_rows(model, tokens, lens, next_tokens, NULL);
     free(lens);
     return rc;
 }
@@ -1746,7 +1815,7 @@ int gpt2_decode_prefill(GPT2* model, const int* tokens, int T, int* next_tokens)
 int gpt2_decode_prefill_ragged(GPT2* model, const int* tokens, const int* lens, int* next_tokens) {
     if (!model->decode) { fprintf(stderr, "[paged_infer] gpt2_decode_init first\n"); return 1; }
     if (!lens || !tokens) return 1;
-    return dec_prefill_rows(model, tokens, lens, next_tokens);
+    return dec_prefill_rows(model, tokens, lens, next_tokens, NULL);
 }
 
 int gpt2_decode_release(GPT2* model, int seq) {
@@ -2314,8 +2383,35 @@ void gpt2_forward(GPT2* model, int* inputs, int* targets, size_t B, size_t T, si
         if (gpt2_decode_set_positions(model, p)) PI_FATAL("rewind failed");
         free(p);
     }
+    const int n_new = offset + (int)T - start;
+    if (n_new >= 2 && d->pos_logits) {
+        /* the window's changed positions in ONE multi-row prefill pass that
+         * returns every row's logits (the reference's T-row matmul_forward,
+         * :703-704 / :727), not n_new single-row decode steps */
+        int* toks = (int*)malloc(B * (size_t)n_new * sizeof(int));
+        int* lens = (int*)malloc(B * sizeof(int));
+        float* rows = (float*)hpa_malloc(B * (size_t)n_new * V * sizeof(float));
+        if (!toks || !lens || !rows) PI_FATAL("prefill window allocation failed");
+        for (size_t b = 0; b < B; b++) {
+            lens[b] = n_new;
+            for (int t = 0; t < n_new; t++) {
+                const int tk = inputs[b * T + (start - offset) + t];
+                toks[b * n_new + t] = tk;
+                d->h_hist[b * d->max_ctx + start + t] = tk;
+            }
+        }
+        if (dec_prefill_rows(model, toks, lens, NULL, rows)) PI_FATAL("window prefill failed");
+        if (gpt2_decode_evicted(model, NULL) > 0) PI_FATAL("gpt2_forward: page pool too small, a sequence was evicted");
+        for (size_t b = 0; b < B; b++) /* rows of sequence b: positions start .. start+n_new-1 */
+            PI_CHECK(hpa_memcpy_async(d->pos_logits + (b * d->max_ctx + start) * V, rows + b * (size_t)n_new * V,
+                                      (size_t)n_new * V * sizeof(float)));
+        PI_CHECK(hpa_synchronize());
+        hpa_free(rows);
+        free(lens);
+        free(toks);
+    }
     int* tok = (int*)malloc(B * sizeof(int));
-    for (int pos = start; pos < offset + (int)T; pos++) {
+    for (int pos = n_new >= 2 && d->pos_logits ? offset + (int)T : start; pos < offset + (int)T; pos++) {
         for (size_t b = 0; b < B; b++) {
             tok[b] = inputs[b * T + (pos - offset)];
             d->h_hist[b * d->max_ctx + pos] = tok[b];

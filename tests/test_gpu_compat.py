@@ -125,6 +125,41 @@ def test_gpt2_forward_reference_main_fill_loop(hip):
     m.close()
 
 
+def test_gpt2_forward_config1_prompt_one_pass(hip):
+    """BASELINE config 1's own API path at its shape: GPT-2 124M (all 12
+    layers, V = 50257), B = 1, page 16, a 64-token prompt passed to the
+    drop-in gpt2_forward at offset 0 (paged_infer.c:575-729).  The first
+    window is ONE multi-row prefill pass returning every row's logits (the
+    reference's T-row matmul_forward, :703-704, :727), not 64 single-row
+    decode steps; every row must equal the oracle's full forward, and the
+    sliding windows after it (one new position each: a decode step) too."""
+    L = hip.lib()
+    cfgd = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
+    params = synth.params(cfgd, seed=41)
+    m = hip.Model(cfgd, params=params)
+    T, total, V = 64, 68, cfgd["V"]
+    gen = np.random.default_rng(41).integers(0, V, total).astype(np.int32)
+    c = oc.cfg(cfgd["maxT"], V, cfgd["L"], cfgd["NH"], cfgd["C"])
+    full = oc.gpt2_forward(params, c, gen[None, :].copy())[0]  # (total, V): causal, so rows < T are the window's
+    strict = full[:T]
+    L.gpt2_forward(m.h, np.ascontiguousarray(gen[:T]).ctypes.data_as(_I), None, 1, T, total, 0)
+    lg = np.ctypeslib.as_array(L.gpt2_acts_logits(m.h), shape=(T, V)).copy()
+    d = np.abs(lg - strict).max()
+    print(f"config-1 prompt: 64 rows through one prefill pass, max |logit diff| vs oracle {d:.2e}")
+    assert d <= 2e-4
+    s = np.sort(strict, -1)
+    clear = (s[:, -1] - s[:, -2]) > 4 * d
+    assert np.array_equal(lg.argmax(-1)[clear], strict.argmax(-1)[clear]) and clear.mean() > 0.9
+    pr = np.ctypeslib.as_array(L.gpt2_acts_probs(m.h), shape=(T, V))
+    assert np.abs(pr.sum(-1) - 1.0).max() < 1e-4
+    for t in range(T + 1, total + 1):  # sliding windows: one new position each
+        off = t - T
+        L.gpt2_forward(m.h, np.ascontiguousarray(gen[off:t]).ctypes.data_as(_I), None, 1, T, total, off)
+        lg = np.ctypeslib.as_array(L.gpt2_acts_logits(m.h), shape=(T, V))
+        assert np.abs(lg - full[off:t]).max() <= 2e-4, t
+    m.close()
+
+
 def test_external_manager_survives_engine_teardown(hip):
     """a caller-owned manager (model.manager, paged_infer.c:986-987) gets its
     pages back and its default backend when the engine goes away
