@@ -390,17 +390,18 @@ int hpa_decode_layer_pick_splits(int B, int num_heads, int max_ctx);
 int hpa_decode_layer_sizes(int B, int C, int num_heads, int splits, size_t* out3);
 int hpa_decode_layer(const HpaLayerArgs* a);
 /* the decode attention of layer a->layer with chain form 6's attproj phase
- * in the same launch (one row block, B <= 16, where the attention grid
- * leaves CUs idle): B*12*splits attention workgroups of `waves` waves (4 or
- * 8; output att in frag layout, published to the attproj units), then 48
- * workgroups, one per attproj tile, that load their weights while the
- * attention streams, wait for the row block's attention outputs and write
- * res2 in form 6's summation order (bit-identical to the chain's phase B),
- * arriving on the chain's fc counters; the chain launch then runs with
- * attproj_done = 1.  Reads B, C, num_heads, splits, pool, layer,
- * block_table, bt_stride, pos, q, att, res, res2, w_ap, b_ap, rec (split
- * records + counters as hpa_attn_ws_bytes lays them out; splits > 1),
- * counters (layer l's block, zero before the step), err, err_sticky. */
+ * in the same launch (C = 768, B <= 64): B*12*splits attention workgroups of
+ * `waves` waves (4 or 8; output att in frag layout, published per row block
+ * to the attproj units), then 48 workgroups per 16-row block, one per
+ * attproj tile, that load their weights while the attention streams, wait
+ * for their row block's attention outputs and write res2 in form 6's
+ * summation order (bit-identical to the chain's phase B), arriving on the
+ * chain's fc counters; the chain launch then runs with attproj_done = 1.
+ * Attention workgroups never wait on attproj ones.  Reads B, C, num_heads,
+ * splits, pool, layer, block_table, bt_stride, pos, q, att, res, res2, w_ap,
+ * b_ap, rec (split records + counters as hpa_attn_ws_bytes lays them out;
+ * splits > 1), counters (layer l's block, zero before the step), err,
+ * err_sticky. */
 int hpa_decode_attn_ap_eligible(int B, int C, int num_heads, int splits, int waves);
 int hpa_decode_attention_ap(const HpaLayerArgs* a, int waves);
 /* the process-wide attention waves override of hpa_set_attention_waves (0: none) */

@@ -1329,7 +1329,7 @@ struct SmemAP {
 }  // namespace ap
 
 template <int P, int AW, bool BF>
-__global__ __launch_bounds__(AW * 64) void decode_attn_ap_kernel(KA args) {
+__global__ __launch_bounds__(AW * 64, AW == 4 ? 3 : 2) void decode_attn_ap_kernel(KA args, const float* __restrict__ q) {
     using namespace c6;
     constexpr int C = 768, NH = 12, K16 = 48, NCT = 48;
     constexpr int TILE = P * HS;
@@ -1346,7 +1346,7 @@ __global__ __launch_bounds__(AW * 64) void decode_attn_ap_kernel(KA args) {
         const int bh = bid / S, sr = bid - bh * S;
         const int b = bh / NH, h = bh - b * NH;
         const int ctx = a.pos[b] + 1;
-        const float* __restrict__ qh = a.q + ((size_t)b * NH + h) * HS;
+        const float* __restrict__ qh = q + ((size_t)b * NH + h) * HS;  // a restrict parameter: scalar loads
         const int* bt = a.bt + (size_t)b * a.bt_stride;
         const int n_it_all = (ctx + 63) >> 6;
         const int it0 = S == 1 ? 0 : (int)((long long)sr * n_it_all / S);
@@ -1378,32 +1378,42 @@ __global__ __launch_bounds__(AW * 64) void decode_attn_ap_kernel(KA args) {
             const int fx = (int)hpa::frag_index(b, h * HS + 4 * lane, C);
             hpa::store_wt16(a.att, fx * 4, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
         }
-        // only this wave (its first lanes) stored the output: drain, then one add
+        // only this wave (its first lanes) stored the output: drain, then one
+        // add on its row block's counter
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0)
-            __hip_atomic_fetch_add(a.ctr + ap::kAttDone * 8 * kPad + (bid & 7) * kPad, 1, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(a.ctr + (ap::kAttDone + (b >> 4)) * 8 * kPad + (bid & 7) * kPad, 1,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
-    // ---- attproj tile g of row block 0: res2 = res + att . Wap^T + b
+    // ---- attproj tile g of row block rb: res2 = res + att . Wap^T + b (unit
+    // u = rb * 48 + g: n_attn is a multiple of 8, so a tile's row blocks share
+    // an XCD and re-read its weights from that L2)
     __shared__ ap::SmemAP sm;
     constexpr int VPW = (NW + AW - 1) / AW;  // virtual waves per wave
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int tid = threadIdx.x;
-    const int g = bid - n_attn;
+    const int u = bid - n_attn, g = u % NCT, rb = u / NCT;
     const int er = (tid & 63) >> 2, eq = tid & 3;  // epilogue thread (tid < 64): row er, columns 4 eq ..
-    const int row = er, col = g * 16 + 4 * eq;
+    const int row = rb * 16 + er, col = g * 16 + 4 * eq;
     const int fi = (int)hpa::frag_index(row, col, C) * 4;
     float4 wr[VPW][1][SPW];
+    if (a.R == 1) {  // one reader per weight tile: non-temporal
 #pragma unroll
-    for (int i = 0; i < VPW; ++i)
-        if (w + AW * i < NW) load_wt<1, true>(a.w_ap, K16, g, 0, w + AW * i, wr[i]);  // one reader per tile
+        for (int i = 0; i < VPW; ++i)
+            if (w + AW * i < NW) load_wt<1, true>(a.w_ap, K16, g, 0, w + AW * i, wr[i]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < VPW; ++i)
+            if (w + AW * i < NW) load_wt<1, false>(a.w_ap, K16, g, 0, w + AW * i, wr[i]);
+    }
     float4 bv = make_float4(0.f, 0.f, 0.f, 0.f), rv = bv;
     if (tid < 64) {
         bv = ld4(a.b_ap + col);
         rv = hpa::load_wt16(a.res, fi);
     }
-    if (!wait6(a, ap::kAttDone, a.B * NH, 1, sm)) return;
+    const int live_rows = a.B - rb * 16 < 16 ? a.B - rb * 16 : 16;
+    if (!wait6(a, ap::kAttDone + rb, live_rows * NH, 1, sm)) return;
     // every virtual wave's A fragments in flight together, then the MFMAs
     float4 xv[VPW][SPW];
 #pragma unroll
@@ -1411,7 +1421,7 @@ __global__ __launch_bounds__(AW * 64) void decode_attn_ap_kernel(KA args) {
         if (w + AW * i < NW)
 #pragma unroll
             for (int s2 = 0; s2 < SPW; ++s2)
-                xv[i][s2] = hpa::load_wt16(a.att, (((w + AW * i) * SPW + s2) * 64 + lane) * 16);
+                xv[i][s2] = hpa::load_wt16(a.att, (((rb * K16 + (w + AW * i) * SPW + s2) * 64) + lane) * 16);
     __builtin_amdgcn_sched_barrier(0);
     float fs1 = 0.f, fs2 = 0.f;
 #pragma unroll
@@ -1431,7 +1441,7 @@ __global__ __launch_bounds__(AW * 64) void decode_attn_ap_kernel(KA args) {
     }
     drain_vm();
     lds_barrier();
-    if (tid == 0) arrive_tiles(a, kCtr + 4 * NCT + kGC, 0, NW, g, 1);  // the tile's k-group of fc's A
+    if (tid == 0) arrive_tiles(a, kCtr + 4 * NCT + kGC, rb, NW, g, 1);  // the tile's k-group of fc's A
 }
 
 // ------------------------------------------------------------------ the chain for wide layers (form 8)
@@ -1960,8 +1970,9 @@ template <int P, bool BF, int AW>
 int launch_attn_ap(const HpaLayerArgs* h) {
     KA a;
     fill_ka(h, num_cus(), a);
-    const int grid = h->B * 12 * h->splits + 48;  // attention units, then one workgroup per attproj tile
-    decode_attn_ap_kernel<P, AW, BF><<<grid, AW * 64, 0, hpa_stream()>>>(a);
+    const int grid = h->B * 12 * h->splits + 48 * ((h->B + 15) / 16);  // attention units, then one workgroup
+                                                                         // per attproj (row block, tile)
+    decode_attn_ap_kernel<P, AW, BF><<<grid, AW * 64, 0, hpa_stream()>>>(a, h->q);
     HPA_LAUNCH_CHECK();
     return 0;
 }
@@ -2191,9 +2202,8 @@ int hpa_decode_first(const HpaLayerArgs* h, const int* tokens, const float* wte,
 }
 
 int hpa_decode_attn_ap_eligible(int B, int C, int num_heads, int splits, int waves) {
-    const int G = num_cus();
-    return HPA_C6_GW && C == 768 && num_heads == 12 && B >= 1 && B <= 16 && splits >= 1 &&
-           splits <= HPA_ATTN_MAX_SPLITS && (waves == 4 || waves == 8) && G > 0 && B * 12 * splits + 48 <= G;
+    return HPA_C6_GW && C == 768 && num_heads == 12 && B >= 1 && B <= 64 && splits >= 1 &&
+           splits <= HPA_ATTN_MAX_SPLITS && (waves == 4 || waves == 8) && num_cus() > 0;
 }
 
 int hpa_decode_attention_ap(const HpaLayerArgs* h, int waves) {
@@ -2202,7 +2212,7 @@ int hpa_decode_attention_ap(const HpaLayerArgs* h, int waves) {
     HPA_REQUIRE(pool->dtype == HPA_F32 || pool->dtype == HPA_BF16, "attention + attproj: fp32 or bf16 pool");
     HPA_REQUIRE(pool->head_size == HS && h->layer >= 0 && h->layer < pool->num_layers, "attention + attproj: layer");
     HPA_REQUIRE(hpa_decode_attn_ap_eligible(h->B, h->C, h->num_heads, h->splits, waves),
-                "attention + attproj: C = 768, 12 heads, B <= 16, waves 4 / 8, B*12*splits + 48 <= CUs");
+                "attention + attproj: C = 768, 12 heads, B <= 64, waves 4 / 8");
     HPA_REQUIRE(h->q && h->att && h->res && h->res2 && h->w_ap && h->b_ap && h->block_table && h->pos &&
                     h->counters && h->err && (h->splits == 1 || h->rec),
                 "attention + attproj: null operand");

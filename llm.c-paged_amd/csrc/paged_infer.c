@@ -1020,14 +1020,14 @@ static int dec_layer(GPT2* model, int l, int attproj_done) {
 }
 
 #ifndef DEC_ATTN_AP
-#define DEC_ATTN_AP 1 /* A/B builds: 0 = attproj stays the chain's phase B at every batch */
+#define DEC_ATTN_AP 2 /* A/B builds: 0 = attproj stays the chain's phase B; 1 = moved at one row block only */
 #endif
 /* waves of the attention + attproj launch where it applies to this step
- * (chain form 6, one row block, the attention grid plus 48 workgroups
- * within the CUs), else 0 */
+ * (chain form 6, attention waves 4 or 8), else 0 */
 static int dec_attn_ap_waves(GPT2* model) {
     GPT2Decode* d = model->decode;
     if (!DEC_ATTN_AP || d->pl_on != 3 || d->pl_wform != 6 || d->profiling) return 0;
+    if (DEC_ATTN_AP == 1 && d->B > 16) return 0;
     const int ov = hpa_get_attention_waves();
     const int nw = ov ? ov : d->attn_waves;
     return hpa_decode_attn_ap_eligible(d->B, model->config.channels, model->config.num_heads, d->attn_splits, nw)
