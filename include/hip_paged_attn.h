@@ -375,11 +375,9 @@ typedef struct {
                                      out at once when it is set) */
     int* err_sticky;              /* nullable: the first code also lands here, never zeroed by a
                                      step (gpt2_decode_status reads and clears it) */
-    int stats_mp;                 /* row stride of stats_out; 0: this launch's Mp */
-    int attproj_done;             /* chain form 6: 1 when hpa_decode_attention_ap / hpa_decode_k1 ran
-                                     this layer's attproj (the chain starts at fc) */
-    int qkv_skip;                 /* chain form 6: 1 = no qkv(l+1) phase (the next layer's
-                                     hpa_decode_k1 computes it) */
+    int stats_mp;                 /* row stride of stats_out; 0: this launch's Mp.  A launch over a
+                                     slice of the batch's row blocks (the engine's two-lane step)
+                                     passes the batch's Mp and stats_out advanced to its first row */
 } HpaLayerArgs;
 /* 1 if the persistent layer applies (shape, CU count, residency), else 0 */
 int hpa_decode_layer_eligible(int B, int C, int num_heads, int splits);
@@ -391,39 +389,6 @@ int hpa_decode_layer_pick_splits(int B, int num_heads, int max_ctx);
 /* sizes: out[0] = rec floats, out[1] = slab floats, out[2] = counter ints per layer */
 int hpa_decode_layer_sizes(int B, int C, int num_heads, int splits, size_t* out3);
 int hpa_decode_layer(const HpaLayerArgs* a);
-/* the decode attention of layer a->layer with chain form 6's attproj phase
- * in the same launch (C = 768, B <= 64): B*12*splits attention workgroups of
- * `waves` waves (4 or 8; output att in frag layout, published per row block
- * to the attproj units), then 48 workgroups per 16-row block, one per
- * attproj tile, that load their weights while the attention streams, wait
- * for their row block's attention outputs and write res2 in form 6's
- * summation order (bit-identical to the chain's phase B), arriving on the
- * chain's fc counters; the chain launch then runs with attproj_done = 1.
- * Attention workgroups never wait on attproj ones.  Reads B, C, num_heads,
- * splits, pool, layer, block_table, bt_stride, pos, q, att, res, res2, w_ap,
- * b_ap, rec (split records + counters as hpa_attn_ws_bytes lays them out;
- * splits > 1), counters (layer l's block, zero before the step), err,
- * err_sticky. */
-int hpa_decode_attn_ap_eligible(int B, int C, int num_heads, int splits, int waves);
-int hpa_decode_attention_ap(const HpaLayerArgs* a, int waves);
-/* layer l's FIRST launch of the two-launch layer (C = 768, B <= 64; the
- * engine's default under chain form 6): qkv(l) | attention(l) | attproj(l).
- * R*144 qkv tiles (chain form 6's phase E summation order, LN1 folded from
- * w_qkv / qkv_c1 / qkv_c2 of layer l; q into q_out, K/V into layer l's pages
- * at pos, write-through), then B*12*splits attention units of `waves` waves
- * (each issues its first 64-token tile's K/V loads before it waits for its
- * head's 12 qkv tiles; the tile holding pos is read after, write-through
- * visible), then 48*R attproj tiles as hpa_decode_attention_ap; the second
- * launch is hpa_decode_layer with attproj_done = qkv_skip = 1 (fc, fcproj).
- * tokens non-NULL (layer 0): qkv's A is the embedding wte[token] + wpe[pos],
- * stored into res too.  Every workgroup zeroes its slice of `zero` and
- * `zero2` (16-byte granules): the counter blocks no launch still reads.
- * Reads the fields hpa_decode_attention_ap reads plus w_qkv, qkv_c1, qkv_c2,
- * q_out (q is read back from q_out). */
-int hpa_decode_k1(const HpaLayerArgs* a, int waves, const int* tokens, const float* wte, const float* wpe,
-                  void* zero, size_t zero_bytes, void* zero2, size_t zero2_bytes);
-/* the process-wide attention waves override of hpa_set_attention_waves (0: none) */
-int hpa_get_attention_waves(void);
 /* the decode step's first launch at GPT-2 124M shapes (C = 768, 12 heads,
  * B <= 64, LN1 folded into w_qkv / qkv_c1 / qkv_c2 of layer 0): the embedding
  * wte[tokens[b]] + wpe[pos[b]] (encoder_forward, paged_infer.c:41-47) into

@@ -150,8 +150,6 @@ int hpa_set_attention_waves(int nw) {
     return 0;
 }
 
-int hpa_get_attention_waves(void) { return g_attn_waves; }
-
 // 8 waves when the B*NH*S workgroups leave CUs without one (each workgroup
 // then has a CU's memory pipe to itself and its tiles take half the trips),
 // else 4.  tools/attn_scan_r3.py, profiles/r3/attn_scan_r3.txt (ctx 1020):

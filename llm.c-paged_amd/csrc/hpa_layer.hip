@@ -103,13 +103,6 @@ struct KA {
     const float *wte, *wpe;
     int4* zero;
     int zero_n4;
-    // chain form 6: phase B (attproj) already ran in the attention launch
-    // (decode_attn_ap_kernel / decode_k1_kernel); qkv_skip: no phase E (the
-    // next layer's K1 computes its qkv)
-    int attproj_done, qkv_skip;
-    // K1: a second counter range to zero (layer 0: the error words)
-    int4* zero2;
-    int zero2_n4;
 };
 
 // diagnostic build (-DHPA_LAYER_TRACE, tools/pl_trace.py): s_memrealtime of
@@ -1032,9 +1025,8 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
     PL_STAMP(t_start);
     PL_STORE(0, t_start);
     float fs1 = 0.f, fs2 = 0.f;
-    // B: attproj(l), 1 tile per unit: res2 = res + att . Wap^T + b (at one row
-    // block the attention launch may have run it: decode_attn_ap_kernel)
-    if (!a.attproj_done) {
+    // B: attproj(l), 1 tile per unit: res2 = res + att . Wap^T + b
+    {
         constexpr int T = 1, NG = NCT;
         const int n = R * NG;
         const bool has = bid < n;
@@ -1207,8 +1199,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         PL_MARK(9);
     }
     // E: qkv(l+1), T = TE tiles: LN1 folded, q + K/V appended into layer l+1's pages
-    // (qkv_skip: the next layer's K1 launch computes it)
-    if (!a.last && !a.qkv_skip) {
+    if (!a.last) {
         constexpr int T = TE, NG = 3 * NCT / TE;
         const int n = R * NG;
         const bool has = bid < n;
@@ -1307,454 +1298,6 @@ __global__ __launch_bounds__(768) void decode_first6_kernel(KA args) {
     lds_barrier();
     if (ep && row < a.B)
         qkv_store6<P, BF>(a, row, col, ln_fold4(sm.wsum, er, fold_t<T>(sm.red, et, er, eq), c1, c2));
-}
-
-// ------------------------------------------------------------------ attention + attproj (form 6, one row block)
-// At one row block (B <= 16) the decode attention's grid -- B*NH*S
-// workgroups -- leaves CUs idle (B = 8: 192 of 256), and chain form 6's
-// attproj phase is its slowest: its 48 units fetch their weights at the
-// chain's start, against the other workgroups' fc prefetch (round-5 trace at
-// B = 8: attproj done at 4.1-4.7 us of a 17.5 us launch, whatever workgroups
-// hold it).  Here the ATTENTION launch carries 48 more workgroups, one per
-// attproj tile: each loads its weight tile while the attention streams, waits
-// (bounded) for the row block's B*NH attention outputs, then computes the
-// tile in form 6's summation order -- 12 virtual waves of 4 k16 steps each,
-// folded in virtual-wave order -- so res2 is bit for bit what the chain's
-// phase B computes, and arrives on the chain's fc k-group counters; the chain
-// launch then skips phase B (HpaLayerArgs.attproj_done).  Attention
-// workgroups never wait on attproj ones (no deadlock at any residency); each
-// (sequence, head) output is published sc1, drained, then one agent-scope add
-// on a counter sharded 8 ways (MI355X_MICROARCH.md "Valid forms", row 1).
-namespace ap {
-constexpr int kAttDone = c6::X1;  // the chain's X1 counters (unused under HPA_C6_GW): outputs per row block
-struct SmemAP {
-    float red[c6::NW * 256];  // [virtual wave][256]
-    int s_ok;
-};
-}  // namespace ap
-
-template <int P, int AW, bool BF>
-__global__ __launch_bounds__(AW * 64, AW == 4 ? 3 : 2) void decode_attn_ap_kernel(KA args, const float* __restrict__ q) {
-    using namespace c6;
-    constexpr int C = 768, NH = 12, K16 = 48, NCT = 48;
-    constexpr int TILE = P * HS;
-    const KA& a = *(const KA*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
-    (void)args;
-    const int S = a.S;
-    const int n_attn = a.B * NH * S;
-    const int bid = blockIdx.x;
-    const int lane = threadIdx.x & 63;
-    if (bid < n_attn) {  // ---- the decode attention of (sequence, head, range), as paged_attn_decode_f32
-        __shared__ float s_m[AW];
-        __shared__ float s_l[AW];
-        __shared__ float4 s_acc[AW * 16];
-        const int bh = bid / S, sr = bid - bh * S;
-        const int b = bh / NH, h = bh - b * NH;
-        const int ctx = a.pos[b] + 1;
-        const float* __restrict__ qh = q + ((size_t)b * NH + h) * HS;  // a restrict parameter: scalar loads
-        const int* bt = a.bt + (size_t)b * a.bt_stride;
-        const int n_it_all = (ctx + 63) >> 6;
-        const int it0 = S == 1 ? 0 : (int)((long long)sr * n_it_all / S);
-        const int n_it = S == 1 ? n_it_all : (int)((long long)(sr + 1) * n_it_all / S);
-        float* rec_bh = S == 1 ? nullptr : a.rec + (size_t)bh * S * kRec;
-        int* cnt = S == 1 ? nullptr : reinterpret_cast<int*>(a.rec + (size_t)n_attn * kRec) + bh;
-        float m = a.m_init, l = 0.f;
-        if constexpr (BF) {
-            const unsigned short* base = reinterpret_cast<const unsigned short*>(a.kv);
-            float4 acc[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
-            hpa_attn::attn_tiles_bf16<P, AW>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, a.page_elems,
-                                             bt, a.bt_stride, ctx, it0, n_it, a.qscale, m, l, acc);
-            if (!hpa_attn::attn_fold_bf16<AW>(m, l, acc, s_m, s_l, s_acc)) return;
-            if (S > 1 && !hpa_attn::split_merge<2>(rec_bh, cnt, S, sr, m, l, acc, true)) return;
-            const float inv = l == 0.f ? 0.f : 1.f / l;
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {  // dims 8*lane + 4k .. +3
-                const int fx = (int)hpa::frag_index(b, h * HS + 8 * lane + 4 * k, C);
-                hpa::store_wt16(a.att, fx * 4, make_float4(acc[k].x * inv, acc[k].y * inv, acc[k].z * inv, acc[k].w * inv));
-            }
-        } else {
-            const float* base = reinterpret_cast<const float*>(a.kv);
-            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-            hpa_attn::attn_tiles<P, AW>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, a.page_elems, bt,
-                                        a.bt_stride, ctx, it0, n_it, a.qscale, m, l, acc);
-            if (!hpa_attn::attn_fold<AW>(m, l, acc, s_m, s_l, s_acc)) return;
-            if (S > 1 && !hpa_attn::split_merge<1>(rec_bh, cnt, S, sr, m, l, &acc, true)) return;
-            const float inv = l == 0.f ? 0.f : 1.f / l;
-            const int fx = (int)hpa::frag_index(b, h * HS + 4 * lane, C);
-            hpa::store_wt16(a.att, fx * 4, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
-        }
-        // only this wave (its first lanes) stored the output: drain, then one
-        // add on its row block's counter
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-            __hip_atomic_fetch_add(a.ctr + (ap::kAttDone + (b >> 4)) * 8 * kPad + (bid & 7) * kPad, 1,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    // ---- attproj tile g of row block rb: res2 = res + att . Wap^T + b (unit
-    // u = rb * 48 + g: n_attn is a multiple of 8, so a tile's row blocks share
-    // an XCD and re-read its weights from that L2)
-    __shared__ ap::SmemAP sm;
-    constexpr int VPW = (NW + AW - 1) / AW;  // virtual waves per wave
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int tid = threadIdx.x;
-    const int u = bid - n_attn, g = u % NCT, rb = u / NCT;
-    const int er = (tid & 63) >> 2, eq = tid & 3;  // epilogue thread (tid < 64): row er, columns 4 eq ..
-    const int row = rb * 16 + er, col = g * 16 + 4 * eq;
-    const int fi = (int)hpa::frag_index(row, col, C) * 4;
-    float4 wr[VPW][1][SPW];
-    if (a.R == 1) {  // one reader per weight tile: non-temporal
-#pragma unroll
-        for (int i = 0; i < VPW; ++i)
-            if (w + AW * i < NW) load_wt<1, true>(a.w_ap, K16, g, 0, w + AW * i, wr[i]);
-    } else {
-#pragma unroll
-        for (int i = 0; i < VPW; ++i)
-            if (w + AW * i < NW) load_wt<1, false>(a.w_ap, K16, g, 0, w + AW * i, wr[i]);
-    }
-    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f), rv = bv;
-    if (tid < 64) {
-        bv = ld4(a.b_ap + col);
-        rv = hpa::load_wt16(a.res, fi);
-    }
-    const int live_rows = a.B - rb * 16 < 16 ? a.B - rb * 16 : 16;
-    if (!wait6(a, ap::kAttDone + rb, live_rows * NH, 1, sm)) return;
-    // every virtual wave's A fragments in flight together, then the MFMAs
-    float4 xv[VPW][SPW];
-#pragma unroll
-    for (int i = 0; i < VPW; ++i)
-        if (w + AW * i < NW)
-#pragma unroll
-            for (int s2 = 0; s2 < SPW; ++s2)
-                xv[i][s2] = hpa::load_wt16(a.att, (((rb * K16 + (w + AW * i) * SPW + s2) * 64) + lane) * 16);
-    __builtin_amdgcn_sched_barrier(0);
-    float fs1 = 0.f, fs2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < VPW; ++i)
-        if (w + AW * i < NW) {
-            f32x4 acc[1];
-            mfma_regs<1, false>(xv[i], wr[i], acc, fs1, fs2);
-            put_red_t<1>(sm.red, w + AW * i, acc);
-        }
-    lds_barrier();
-    if (tid < 64) {
-        float4 v = fold_t<1>(sm.red, 0, er, eq);
-        v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
-        const bool live = row < a.B;  // residual_forward(out, res, proj); padded rows stay 0
-        v = live ? make_float4(rv.x + v.x, rv.y + v.y, rv.z + v.z, rv.w + v.w) : make_float4(0.f, 0.f, 0.f, 0.f);
-        hpa::store_wt16(a.res2, fi, v);
-    }
-    drain_vm();
-    lds_barrier();
-    if (tid == 0) arrive_tiles(a, kCtr + 4 * NCT + kGC, rb, NW, g, 1);  // the tile's k-group of fc's A
-}
-
-// ------------------------------------------------------------------ the attention launch (form 6 + K1)
-// Layer l as TWO launches (round 5): K1 = qkv(l) | attention(l) | attproj(l),
-// K2 = chain form 6's fc(l) -> fcproj(l) (attproj_done, qkv_skip).  The qkv
-// phase leaves the chain (where it sat behind a seam at the chain's end) for
-// the attention launch, where the attention's K/V stream hides it: an
-// attention unit's first 64-token tile does not depend on q, so every wave
-// issues its first tile's K/V loads (when the tile ends before pos) BEFORE it
-// waits for its head's q.  Roles by workgroup index, each role waiting only
-// on roles with lower indices (dispatched earlier, and never waiting
-// themselves on later ones, so the launch drains at any residency):
-//   [0, 144 R)            qkv tile (row block rb, 16-column tile j): form 6's
-//                         phase E in 12 virtual waves (the summation order
-//                         of every form-6 batch), LN1 folded; q, K and V of
-//                         the token stored write-through (q into q_out, K/V
-//                         into layer l's pages at pos: add_to_cache); one add
-//                         per tile on the (rb, head) counter.  FIRST: A built
-//                         from the embedding wte[token] + wpe[pos] (tile 0
-//                         also stores res), as decode_first6_kernel.
-//   [.., + 12 B S)        attention (sequence, head, range): first tile in
-//                         flight, wait for the head's 12 qkv tiles, q by sc1
-//                         loads, the tile holding pos loaded sc1 (its K/V row
-//                         was written in this launch), output as
-//                         decode_attn_ap_kernel.
-//   [.., + 48 R)          attproj tile, as decode_attn_ap_kernel.
-// Every workgroup also zeroes its slice of the finished counter blocks (the
-// previous layer's; at layer 0 the last layer's and the step's error words).
-namespace k1 {
-constexpr int kQkvDone = c6::kCtr + 4 * 48 + c6::kGrp;  // [R][12] one line each: qkv tiles landed per (rb, head)
-constexpr int kInts = 4 * 12 * kPad;                    // ints of that region
-struct SmemK1 {
-    float red[c6::NW * 256];
-    float wsum[c6::NW * 32];
-    int s_ok;
-};
-// wave 0 polls ONE counter until it reaches `expected` (bounded, as wait6);
-// the other waves wait at the barrier
-__device__ __forceinline__ bool wait_at(const KA& a, const int* c, int expected, int code, SmemK1& sm) {
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (wv == 0) {
-        const int lane = threadIdx.x & 63;
-        int ok = 0;
-        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-        for (unsigned it = 0;; ++it) {
-            const int v = __builtin_amdgcn_readfirstlane(
-                lane == 0 ? __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0);
-            if (v >= expected) {
-                ok = 1;
-                break;
-            }
-            if ((it & 7) == 7) {
-                const int e = __builtin_amdgcn_readfirstlane(
-                    __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                if (e) break;
-                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
-                    if (lane == 0) {
-                        atomicCAS(a.err, 0, code);
-                        if (a.err_sticky) atomicCAS(a.err_sticky, 0, code);
-                    }
-                    break;
-                }
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        if (lane == 0) sm.s_ok = ok;
-    }
-    lds_barrier();
-    const bool ok = sm.s_ok != 0;
-    lds_barrier();
-    return ok;
-}
-__device__ __forceinline__ void store_wt8(void* base, int byte_off, uint2 v) {
-    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-    const u32x2 d = {v.x, v.y};
-    __builtin_amdgcn_raw_buffer_store_b64(d, hpa::wt_rsrc(base), byte_off, 0, hpa::kCpolSc1);
-}
-// K1's qkv epilogue store of columns col..col+3 of `row` (NH = 12), write-
-// through: q row-major into q_out, K / V of this token into the sequence's
-// page of layer l (a.kv) at pos (add_to_cache, paged_infer.c:505-573)
-template <int P, bool BF>
-__device__ __forceinline__ void qkv_store(const KA& a, int row, int col, float4 v) {
-    constexpr int NH = 12, C = 768;
-    if (col < C) {
-        hpa::store_wt16(a.q_out, (row * C + col) * 4, v);
-        return;
-    }
-    const int kv = col >= 2 * C;
-    const int c = col - (kv ? 2 * C : C);
-    const int hh = c >> 6, d = c & 63;
-    const int ps = a.pos[row];
-    const int page = a.bt[(size_t)row * a.bt_stride + ps / P];
-    if (page < 0) return;
-    const int pslot = ps % P;
-    const size_t toff = (size_t)page * a.page_elems + ((size_t)kv * NH + hh) * P * 64;
-    void* base = const_cast<void*>(a.kv);
-    if constexpr (BF) {
-        const size_t e = toff + (kv == 0 ? ((d >> 3) * P + pslot) * 8 + (d & 7) : pslot * 64 + d);
-        const unsigned lo = hpa::f32_to_bf16(v.x) | ((unsigned)hpa::f32_to_bf16(v.y) << 16);
-        const unsigned hi = hpa::f32_to_bf16(v.z) | ((unsigned)hpa::f32_to_bf16(v.w) << 16);
-        store_wt8(base, (int)(e * 2), make_uint2(lo, hi));
-    } else {
-        const size_t e = toff + (kv == 0 ? ((d >> 2) * P + pslot) * 4 : pslot * 64 + d);
-        hpa::store_wt16(base, (int)(e * 4), v);
-    }
-}
-}  // namespace k1
-
-template <int P, int AW, bool BF, bool FIRST>
-__global__ __launch_bounds__(AW * 64, AW == 4 ? 3 : 2) void decode_k1_kernel(KA args, const float* __restrict__ q) {
-    using namespace c6;
-    constexpr int C = 768, NH = 12, K16 = 48, NCT = 48, NQT = 144;
-    constexpr int VPW = (NW + AW - 1) / AW;  // virtual waves (of form 6's 12) per wave
-    const KA& a = *(const KA*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
-    (void)args;
-    __shared__ k1::SmemK1 sm;
-    const int R = a.R, S = a.S;
-    const int nq = R * NQT, na = a.B * NH * S;
-    const int bid = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // the finished counter blocks (previous layer; at layer 0 the last layer's and the error words)
-    for (int i = bid * AW * 64 + tid; i < a.zero_n4; i += (int)gridDim.x * AW * 64) a.zero[i] = make_int4(0, 0, 0, 0);
-    for (int i = bid * AW * 64 + tid; i < a.zero2_n4; i += (int)gridDim.x * AW * 64) a.zero2[i] = make_int4(0, 0, 0, 0);
-    if (bid < nq) {  // ---------------------------------------------- qkv tile (rb, j)
-        const int rb = bid / NQT, j = bid - rb * NQT;
-        const int er = (tid & 63) >> 2, eq = tid & 3;
-        const int row = rb * 16 + er, col = j * 16 + 4 * eq;
-        float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f), c2 = c1;
-        if (tid < 64) {
-            c1 = ld4(a.qkv_c1 + col);
-            c2 = ld4(a.qkv_c2 + col);
-        }
-        float4 wr[VPW][1][SPW];
-        if (R == 1) {
-#pragma unroll
-            for (int i = 0; i < VPW; ++i)
-                if (w + AW * i < NW) load_wt<1, true>(a.w_qkv, K16, j, 0, w + AW * i, wr[i]);
-        } else {
-#pragma unroll
-            for (int i = 0; i < VPW; ++i)
-                if (w + AW * i < NW) load_wt<1, false>(a.w_qkv, K16, j, 0, w + AW * i, wr[i]);
-        }
-        float4 xv[VPW][SPW];
-        if constexpr (FIRST) {  // A from the embedding (encoder_forward, paged_infer.c:41-47)
-            const int arow = rb * 16 + (lane & 15);
-            const bool live = arow < a.B;
-            const int tok = live ? a.tokens[arow] : 0, ps = live ? a.pos[arow] : 0;
-            const float4* te = reinterpret_cast<const float4*>(a.wte + (size_t)tok * C) + (lane >> 4);
-            const float4* pe = reinterpret_cast<const float4*>(a.wpe + (size_t)ps * C) + (lane >> 4);
-#pragma unroll
-            for (int i = 0; i < VPW; ++i) {
-                const int v = w + AW * i;
-                if (v < NW)
-#pragma unroll
-                    for (int s2 = 0; s2 < SPW; ++s2) {
-                        const float4 x = te[(v * SPW + s2) * 4], y = pe[(v * SPW + s2) * 4];
-                        xv[i][s2] = live ? make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
-            }
-            if (j == 0)  // the residual stream entering layer 0: read by this launch's attproj (sc1) and K2
-#pragma unroll
-                for (int i = 0; i < VPW; ++i)
-                    if (w + AW * i < NW)
-#pragma unroll
-                        for (int s2 = 0; s2 < SPW; ++s2)
-                            hpa::store_wt16(a.res, ((rb * K16 + (w + AW * i) * SPW + s2) * 64 + lane) * 16, xv[i][s2]);
-        } else {
-#pragma unroll
-            for (int i = 0; i < VPW; ++i)
-                if (w + AW * i < NW)
-#pragma unroll
-                    for (int s2 = 0; s2 < SPW; ++s2)
-                        xv[i][s2] = hpa::load_wt16(a.res, ((rb * K16 + (w + AW * i) * SPW + s2) * 64 + lane) * 16);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < VPW; ++i)
-            if (w + AW * i < NW) {
-                f32x4 acc[1];
-                float f1 = 0.f, f2 = 0.f;
-                mfma_regs<1, true>(xv[i], wr[i], acc, f1, f2);
-                put_red_t<1>(sm.red, w + AW * i, acc);
-                hpa_gemm::row_sums_publish(f1, f2, sm.wsum + (w + AW * i) * 32);
-            }
-        lds_barrier();
-        if (tid < 64 && row < a.B)
-            k1::qkv_store<P, BF>(a, row, col, ln_fold4(sm.wsum, er, fold_t<1>(sm.red, 0, er, eq), c1, c2));
-        drain_vm();
-        lds_barrier();
-        if (tid == 0)
-            __hip_atomic_fetch_add(a.ctr + k1::kQkvDone + (rb * NH + (j % NCT) / 4) * kPad, 1, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    if (bid < nq + na) {  // ----------------------------------------- attention (sequence, head, range)
-        constexpr int TILE = P * HS;
-        __shared__ float s_m[AW];
-        __shared__ float s_l[AW];
-        __shared__ float4 s_acc[AW * 16];
-        const int ub = bid - nq;
-        const int bh = ub / S, sr = ub - bh * S;
-        const int b = bh / NH, h = bh - b * NH, rb = b >> 4;
-        const int ctx = a.pos[b] + 1;
-        const int* bt = a.bt + (size_t)b * a.bt_stride;
-        const int n_it_all = (ctx + 63) >> 6;
-        const int it0 = S == 1 ? 0 : (int)((long long)sr * n_it_all / S);
-        const int it1 = S == 1 ? n_it_all : (int)((long long)(sr + 1) * n_it_all / S);
-        if (!k1::wait_at(a, a.ctr + k1::kQkvDone + (rb * NH + h) * kPad, 12, 1, sm)) return;  // the head's q, K, V tiles
-        // q: scalar loads through a restrict pointer, as the stand-alone kernel
-        // (its 256-B row of this head was written write-through by a qkv tile
-        // of this launch and is first read here, after the wait; at kernel
-        // start no cache holds it).  K/V: non-temporal loads, which bypass L1;
-        // the page row at pos, written write-through in this launch, is first
-        // read here too.
-        // (z = 0, read from LDS after the wait's barriers: the q address depends
-        // on it, so no load of q can be scheduled above the wait)
-        const int z = __builtin_amdgcn_readfirstlane(*(volatile int*)&sm.s_ok) - 1;
-        const float* __restrict__ qh = q + ((size_t)b * NH + h) * HS + z;
-        float m = a.m_init, l = 0.f;
-        float4 acc[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
-        if constexpr (BF) {
-            const unsigned short* base = reinterpret_cast<const unsigned short*>(a.kv);
-            hpa_attn::attn_tiles_bf16<P, AW>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, a.page_elems,
-                                             bt, a.bt_stride, ctx, it0, it1, a.qscale, m, l, acc);
-        } else {
-            const float* base = reinterpret_cast<const float*>(a.kv);
-            hpa_attn::attn_tiles<P, AW>(qh, base + (size_t)h * TILE, base + (size_t)(NH + h) * TILE, a.page_elems, bt,
-                                        a.bt_stride, ctx, it0, it1, a.qscale, m, l, acc[0]);
-        }
-        float* rec_bh = S == 1 ? nullptr : a.rec + (size_t)bh * S * kRec;
-        int* cnt = S == 1 ? nullptr : reinterpret_cast<int*>(a.rec + (size_t)na * kRec) + bh;
-        if constexpr (BF) {
-            if (!hpa_attn::attn_fold_bf16<AW>(m, l, acc, s_m, s_l, s_acc)) return;
-            if (S > 1 && !hpa_attn::split_merge<2>(rec_bh, cnt, S, sr, m, l, acc, true)) return;
-            const float inv = l == 0.f ? 0.f : 1.f / l;
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {  // dims 8*lane + 4k .. +3
-                const int fx = (int)hpa::frag_index(b, h * HS + 8 * lane + 4 * k, C);
-                hpa::store_wt16(a.att, fx * 4, make_float4(acc[k].x * inv, acc[k].y * inv, acc[k].z * inv, acc[k].w * inv));
-            }
-        } else {
-            if (!hpa_attn::attn_fold<AW>(m, l, acc[0], s_m, s_l, s_acc)) return;
-            if (S > 1 && !hpa_attn::split_merge<1>(rec_bh, cnt, S, sr, m, l, acc, true)) return;
-            const float inv = l == 0.f ? 0.f : 1.f / l;
-            const int fx = (int)hpa::frag_index(b, h * HS + 4 * lane, C);
-            hpa::store_wt16(a.att, fx * 4, make_float4(acc[0].x * inv, acc[0].y * inv, acc[0].z * inv, acc[0].w * inv));
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the one storing wave drained, then one add
-        if (lane == 0)
-            __hip_atomic_fetch_add(a.ctr + (ap::kAttDone + rb) * 8 * kPad + (bid & 7) * kPad, 1, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    // ------------------------------------------------------------------ attproj tile (rb, g)
-    const int u = bid - nq - na, g = u % NCT, rb = u / NCT;
-    if (rb >= R) return;
-    const int er = (tid & 63) >> 2, eq = tid & 3;
-    const int row = rb * 16 + er, col = g * 16 + 4 * eq;
-    const int fi = (int)hpa::frag_index(row, col, C) * 4;
-    float4 wr[VPW][1][SPW];
-    if (R == 1) {
-#pragma unroll
-        for (int i = 0; i < VPW; ++i)
-            if (w + AW * i < NW) load_wt<1, true>(a.w_ap, K16, g, 0, w + AW * i, wr[i]);
-    } else {
-#pragma unroll
-        for (int i = 0; i < VPW; ++i)
-            if (w + AW * i < NW) load_wt<1, false>(a.w_ap, K16, g, 0, w + AW * i, wr[i]);
-    }
-    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f), rv = bv;
-    if (tid < 64) {
-        bv = ld4(a.b_ap + col);
-        if (!FIRST) rv = hpa::load_wt16(a.res, fi);  // FIRST: res is written in this launch (qkv tile 0)
-    }
-    const int live_rows = a.B - rb * 16 < 16 ? a.B - rb * 16 : 16;
-    if (!wait6(a, ap::kAttDone + rb, live_rows * NH, 1, sm)) return;
-    // (layer 0: res was stored sc1 by qkv tile 0 before its (rb, head 0) add,
-    // which the row block's attention outputs waited for; never read here before)
-    if (FIRST && tid < 64) rv = hpa::load_wt16(a.res, fi);
-    float4 xv[VPW][SPW];
-#pragma unroll
-    for (int i = 0; i < VPW; ++i)
-        if (w + AW * i < NW)
-#pragma unroll
-            for (int s2 = 0; s2 < SPW; ++s2)
-                xv[i][s2] = hpa::load_wt16(a.att, (((rb * K16 + (w + AW * i) * SPW + s2) * 64) + lane) * 16);
-    __builtin_amdgcn_sched_barrier(0);
-    float fs1 = 0.f, fs2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < VPW; ++i)
-        if (w + AW * i < NW) {
-            f32x4 acc[1];
-            mfma_regs<1, false>(xv[i], wr[i], acc, fs1, fs2);
-            put_red_t<1>(sm.red, w + AW * i, acc);
-        }
-    lds_barrier();
-    if (tid < 64) {
-        float4 v = fold_t<1>(sm.red, 0, er, eq);
-        v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
-        const bool live = row < a.B;
-        v = live ? make_float4(rv.x + v.x, rv.y + v.y, rv.z + v.z, rv.w + v.w) : make_float4(0.f, 0.f, 0.f, 0.f);
-        hpa::store_wt16(a.res2, fi, v);
-    }
-    drain_vm();
-    lds_barrier();
-    if (tid == 0) arrive_tiles(a, kCtr + 4 * NCT + kGC, rb, NW, g, 1);  // the tile's k-group of fc's A
 }
 
 // ------------------------------------------------------------------ the chain for wide layers (form 8)
@@ -2207,8 +1750,6 @@ void fill_ka(const HpaLayerArgs* h, int G, KA& a) {
     a.ctr = h->counters;
     a.err = h->err;
     a.err_sticky = h->err_sticky;
-    a.attproj_done = h->attproj_done;
-    a.qkv_skip = h->qkv_skip;
 }
 
 // blocks per CU of a 768-thread instantiation (occupancy API), cached per kernel
@@ -2278,51 +1819,6 @@ int launch6(const HpaLayerArgs* h, int G) {
     decode_chain6_kernel<P, BF, TC, TD, TE><<<G, 768, 0, hpa_stream()>>>(a);
     HPA_LAUNCH_CHECK();
     return 0;
-}
-
-template <int P, bool BF, int AW>
-int launch_attn_ap(const HpaLayerArgs* h) {
-    KA a;
-    fill_ka(h, num_cus(), a);
-    const int grid = h->B * 12 * h->splits + 48 * ((h->B + 15) / 16);  // attention units, then one workgroup
-                                                                         // per attproj (row block, tile)
-    decode_attn_ap_kernel<P, AW, BF><<<grid, AW * 64, 0, hpa_stream()>>>(a, h->q);
-    HPA_LAUNCH_CHECK();
-    return 0;
-}
-
-template <int P, bool BF>
-int dispatch_attn_ap_t(const HpaLayerArgs* h, int waves) {
-    return waves == 8 ? launch_attn_ap<P, BF, 8>(h) : launch_attn_ap<P, BF, 4>(h);
-}
-
-template <int P, bool BF, int AW, bool FIRST>
-int launch_k1(const HpaLayerArgs* h, const int* tokens, const float* wte, const float* wpe, void* z1, size_t z1b,
-              void* z2, size_t z2b) {
-    KA a;
-    fill_ka(h, num_cus(), a);
-    a.tokens = tokens;
-    a.wte = wte;
-    a.wpe = wpe;
-    a.zero = reinterpret_cast<int4*>(z1);
-    a.zero_n4 = (int)(z1b / 16);
-    a.zero2 = reinterpret_cast<int4*>(z2);
-    a.zero2_n4 = (int)(z2b / 16);
-    const int R = (h->B + 15) / 16;
-    const int grid = R * 144 + h->B * 12 * h->splits + 48 * R;  // qkv tiles, attention units, attproj tiles
-    decode_k1_kernel<P, AW, BF, FIRST><<<grid, AW * 64, 0, hpa_stream()>>>(a, h->q_out);
-    HPA_LAUNCH_CHECK();
-    return 0;
-}
-
-template <int P, bool BF>
-int dispatch_k1_t(const HpaLayerArgs* h, int waves, const int* tokens, const float* wte, const float* wpe, void* z1,
-                  size_t z1b, void* z2, size_t z2b) {
-    if (tokens)
-        return waves == 8 ? launch_k1<P, BF, 8, true>(h, tokens, wte, wpe, z1, z1b, z2, z2b)
-                          : launch_k1<P, BF, 4, true>(h, tokens, wte, wpe, z1, z1b, z2, z2b);
-    return waves == 8 ? launch_k1<P, BF, 8, false>(h, tokens, wte, wpe, z1, z1b, z2, z2b)
-                      : launch_k1<P, BF, 4, false>(h, tokens, wte, wpe, z1, z1b, z2, z2b);
 }
 
 // chain form 8: tiles per unit T (<= cx::XT_MAX) and tile groups NG (padded
@@ -2473,8 +1969,7 @@ int hpa_decode_layer_sizes(int B, int C, int num_heads, int splits, size_t* out3
     out3[0] = (size_t)B * num_heads * splits * kRec;
     out3[1] = (size_t)4 * R * nct * 256;  // fcproj K-part partial tiles
     const size_t ints5 = (size_t)kCtrInts + 2 * (size_t)R * nct + (size_t)B * num_heads;
-    const size_t ints6 = (size_t)c6::kCtr + (size_t)4 * nct + c6::kGrp + k1::kInts;  // form 6: counters, tickets
-                                                                                        // [4][nct], k-groups, K1's
+    const size_t ints6 = (size_t)c6::kCtr + (size_t)4 * nct + c6::kGrp;  // form 6: counters, tickets [4][nct], k-groups
     const size_t ints = ints5 > ints6 ? ints5 : ints6;
     out3[2] = (ints + 31) / 32 * 32;  // whole 128-B lines (memset in multiples of 16 B)
     return 0;
@@ -2542,58 +2037,6 @@ int hpa_decode_first(const HpaLayerArgs* h, const int* tokens, const float* wte,
         case 64: return bf ? dispatch_first6_t<64, true>(h, G, tokens, wte, wpe, zero, zero_bytes)
                            : dispatch_first6_t<64, false>(h, G, tokens, wte, wpe, zero, zero_bytes);
         default: return hpa_fail(__FILE__, __LINE__, "decode first: page size must be 8, 16, 32 or 64");
-    }
-}
-
-int hpa_decode_k1(const HpaLayerArgs* h, int waves, const int* tokens, const float* wte, const float* wpe, void* zero,
-                  size_t zero_bytes, void* zero2, size_t zero2_bytes) {
-    HPA_REQUIRE(h && h->pool && h->pool->base, "decode K1: pool");
-    const HpaKVPool* pool = h->pool;
-    HPA_REQUIRE(pool->dtype == HPA_F32 || pool->dtype == HPA_BF16, "decode K1: fp32 or bf16 pool");
-    HPA_REQUIRE(pool->head_size == HS && h->layer >= 0 && h->layer < pool->num_layers, "decode K1: layer");
-    HPA_REQUIRE(pool->layer_elems * pool->elem_bytes < (size_t)0x7fffffff, "decode K1: a layer's pool slab must be < 2 GiB");
-    HPA_REQUIRE(hpa_decode_attn_ap_eligible(h->B, h->C, h->num_heads, h->splits, waves),
-                "decode K1: C = 768, 12 heads, B <= 64, waves 4 / 8");
-    HPA_REQUIRE(h->q_out && h->att && h->res && h->res2 && h->w_ap && h->b_ap && h->w_qkv && h->qkv_c1 &&
-                    h->qkv_c2 && h->block_table && h->pos && h->counters && h->err && (h->splits == 1 || h->rec) &&
-                    (!tokens || (wte && wpe)),
-                "decode K1: null operand");
-    HPA_REQUIRE(zero_bytes % 16 == 0 && zero2_bytes % 16 == 0 && ((size_t)zero & 15) == 0 && ((size_t)zero2 & 15) == 0,
-                "decode K1: zeroed ranges must be whole 16-byte granules");
-    switch (pool->page_size) {
-        case 8: return pool->dtype == HPA_BF16 ? dispatch_k1_t<8, true>(h, waves, tokens, wte, wpe, zero, zero_bytes, zero2, zero2_bytes)
-                                               : dispatch_k1_t<8, false>(h, waves, tokens, wte, wpe, zero, zero_bytes, zero2, zero2_bytes);
-        case 16: return pool->dtype == HPA_BF16 ? dispatch_k1_t<16, true>(h, waves, tokens, wte, wpe, zero, zero_bytes, zero2, zero2_bytes)
-                                                : dispatch_k1_t<16, false>(h, waves, tokens, wte, wpe, zero, zero_bytes, zero2, zero2_bytes);
-        case 32: return pool->dtype == HPA_BF16 ? dispatch_k1_t<32, true>(h, waves, tokens, wte, wpe, zero, zero_bytes, zero2, zero2_bytes)
-                                                : dispatch_k1_t<32, false>(h, waves, tokens, wte, wpe, zero, zero_bytes, zero2, zero2_bytes);
-        case 64: return pool->dtype == HPA_BF16 ? dispatch_k1_t<64, true>(h, waves, tokens, wte, wpe, zero, zero_bytes, zero2, zero2_bytes)
-                                                : dispatch_k1_t<64, false>(h, waves, tokens, wte, wpe, zero, zero_bytes, zero2, zero2_bytes);
-        default: return hpa_fail(__FILE__, __LINE__, "decode K1: page size 8, 16, 32 or 64");
-    }
-}
-
-int hpa_decode_attn_ap_eligible(int B, int C, int num_heads, int splits, int waves) {
-    return HPA_C6_GW && C == 768 && num_heads == 12 && B >= 1 && B <= 64 && splits >= 1 &&
-           splits <= HPA_ATTN_MAX_SPLITS && (waves == 4 || waves == 8) && num_cus() > 0;
-}
-
-int hpa_decode_attention_ap(const HpaLayerArgs* h, int waves) {
-    HPA_REQUIRE(h && h->pool && h->pool->base, "attention + attproj: pool");
-    const HpaKVPool* pool = h->pool;
-    HPA_REQUIRE(pool->dtype == HPA_F32 || pool->dtype == HPA_BF16, "attention + attproj: fp32 or bf16 pool");
-    HPA_REQUIRE(pool->head_size == HS && h->layer >= 0 && h->layer < pool->num_layers, "attention + attproj: layer");
-    HPA_REQUIRE(hpa_decode_attn_ap_eligible(h->B, h->C, h->num_heads, h->splits, waves),
-                "attention + attproj: C = 768, 12 heads, B <= 64, waves 4 / 8");
-    HPA_REQUIRE(h->q && h->att && h->res && h->res2 && h->w_ap && h->b_ap && h->block_table && h->pos &&
-                    h->counters && h->err && (h->splits == 1 || h->rec),
-                "attention + attproj: null operand");
-    switch (pool->page_size) {
-        case 8: return pool->dtype == HPA_BF16 ? dispatch_attn_ap_t<8, true>(h, waves) : dispatch_attn_ap_t<8, false>(h, waves);
-        case 16: return pool->dtype == HPA_BF16 ? dispatch_attn_ap_t<16, true>(h, waves) : dispatch_attn_ap_t<16, false>(h, waves);
-        case 32: return pool->dtype == HPA_BF16 ? dispatch_attn_ap_t<32, true>(h, waves) : dispatch_attn_ap_t<32, false>(h, waves);
-        case 64: return pool->dtype == HPA_BF16 ? dispatch_attn_ap_t<64, true>(h, waves) : dispatch_attn_ap_t<64, false>(h, waves);
-        default: return hpa_fail(__FILE__, __LINE__, "attention + attproj: page size 8, 16, 32 or 64");
     }
 }
 

@@ -673,7 +673,6 @@ struct GPT2Decode {
     int* pl_ctr;      /* the step's error word (DEC_ERR_INTS), then [L][pl_ctr_ints]; zeroed at the start of
                          every step */
     size_t pl_ctr_ints;
-    size_t pl_ctr_n;  /* ints of pl_ctr */
     /* gpt2_forward: token at every cached position [B][max_ctx] and, when it
      * fits, the logits of every position [B][max_ctx][V] (managed) */
     int* h_hist;
@@ -954,20 +953,16 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
     }
     if (!d->pl_ctr) {
         d->pl_ctr_ints = sz[2];
-        d->pl_ctr_n = DEC_ERR_INTS + (size_t)c.num_layers * sz[2];
-        d->pl_ctr = (int*)hpa_malloc(d->pl_ctr_n * sizeof(int));
+        d->pl_ctr = (int*)hpa_malloc((DEC_ERR_INTS + (size_t)c.num_layers * sz[2]) * sizeof(int));
     }
     if (!d->pl_rec || !d->pl_slab || !d->pl_ctr) return 1;
-    /* every counter block zero: the K1 layer zeroes a block only after its
-     * last use, so a form change must start from clean blocks */
-    if (hpa_memset_async(d->pl_ctr, 0, d->pl_ctr_n * sizeof(int))) return 1;
     d->pl_splits = splits;
     d->pl_on = mode;
     return 0;
 }
 
-/* the persistent path's arguments of layer l: attention(l) .. fcproj(l), qkv(l+1) */
-static void dec_layer_args(GPT2* model, int l, HpaLayerArgs* ap) {
+/* layer l of the persistent path: attention(l) .. fcproj(l), qkv(l+1) */
+static int dec_layer(GPT2* model, int l) {
     GPT2Decode* d = model->decode;
     const GPT2Config c = model->config;
     const int C = c.channels, L = c.num_layers;
@@ -1012,71 +1007,7 @@ static void dec_layer_args(GPT2* model, int l, HpaLayerArgs* ap) {
     a.counters = d->pl_ctr + DEC_ERR_INTS + (size_t)l * d->pl_ctr_ints;
     a.err = d->pl_ctr;                  /* this step's (zeroed with the counters) */
     a.err_sticky = d->d_next + d->B;    /* first code of any step, until gpt2_decode_status */
-    *ap = a;
-}
-
-/* layer l's persistent launch; attproj_done: the attention launch ran its
- * attproj (hpa_decode_attention_ap / hpa_decode_k1); qkv_skip: the next
- * layer's K1 computes qkv(l+1) */
-static int dec_layer(GPT2* model, int l, int attproj_done, int qkv_skip) {
-    HpaLayerArgs a;
-    dec_layer_args(model, l, &a);
-    a.attproj_done = attproj_done;
-    a.qkv_skip = qkv_skip;
     return hpa_decode_layer(&a);
-}
-
-#ifndef DEC_K1
-#define DEC_K1 1 /* A/B builds: 0 = the round-4 layer (qkv(l+1) at the chain's end, attproj as DEC_ATTN_AP says) */
-#endif
-/* layer l's K1 launch (hpa_decode_k1): qkv(l) | attention(l) | attproj(l);
- * it zeroes the counter block of the layer before (at layer 0: the last
- * layer's, and the step's error words) */
-static int dec_k1(GPT2* model, int l, int waves) {
-    GPT2Decode* d = model->decode;
-    const GPT2Config c = model->config;
-    const int C = c.channels, L = c.num_layers;
-    const size_t lc = (size_t)l * C;
-    const size_t e_layer = d->wpack_off[3] + hpa_frag_elems(C, 4 * C);
-    HpaLayerArgs a;
-    dec_layer_args(model, l, &a);
-    a.splits = d->attn_splits;
-    a.rec = (float*)d->d_attn_ws;
-    a.w_qkv = wpack_at(d, e_layer * l + d->wpack_off[0]); /* layer l's qkv (LN1 folded) */
-    a.qkv_c1 = d->d_fold + 14 * lc;
-    a.qkv_c2 = a.qkv_c1 + 3 * C;
-    a.q_out = d->d_q;
-    int* blk = d->pl_ctr + DEC_ERR_INTS;
-    const size_t bb = d->pl_ctr_ints * sizeof(int);
-    if (l == 0)
-        return hpa_decode_k1(&a, waves, d->d_tokens, model->params.wte, model->params.wpe, blk + (size_t)(L - 1) * d->pl_ctr_ints,
-                             bb, d->pl_ctr, DEC_ERR_INTS * sizeof(int));
-    return hpa_decode_k1(&a, waves, NULL, NULL, NULL, blk + (size_t)(l - 1) * d->pl_ctr_ints, bb, NULL, 0);
-}
-
-#ifndef DEC_ATTN_AP
-#define DEC_ATTN_AP 2 /* A/B builds: 0 = attproj stays the chain's phase B; 1 = moved at one row block only */
-#endif
-/* waves of the attention + attproj launch where it applies to this step
- * (chain form 6, attention waves 4 or 8), else 0 */
-static int dec_attn_ap_waves(GPT2* model) {
-    GPT2Decode* d = model->decode;
-    if (!DEC_ATTN_AP || d->pl_on != 3 || d->pl_wform != 6 || d->profiling) return 0;
-    if (DEC_ATTN_AP == 1 && d->B > 16) return 0;
-    const int ov = hpa_get_attention_waves();
-    const int nw = ov ? ov : d->attn_waves;
-    return hpa_decode_attn_ap_eligible(d->B, model->config.channels, model->config.num_heads, d->attn_splits, nw)
-               ? nw : 0;
-}
-
-/* layer l's attention with the chain's attproj in the same launch */
-static int dec_attention_ap(GPT2* model, int l, int waves) {
-    GPT2Decode* d = model->decode;
-    HpaLayerArgs a;
-    dec_layer_args(model, l, &a);
-    a.splits = d->attn_splits;
-    a.rec = (float*)d->d_attn_ws;
-    return hpa_decode_attention_ap(&a, waves);
 }
 
 /* the in-launch arrival counters of the attention's split merge, of the
@@ -1088,7 +1019,6 @@ static int dec_rezero(GPT2Decode* d) {
     if (d->d_attn_ws) rc |= hpa_memset_async(d->d_attn_ws, 0, d->attn_ws_bytes);
     if (d->sk_cnt && d->sk_cnt_n) rc |= hpa_memset_async(d->sk_cnt, 0, d->sk_cnt_n * sizeof(int));
     if (d->ring_cnt && d->ring_cnt_n) rc |= hpa_memset_async(d->ring_cnt, 0, d->ring_cnt_n * sizeof(int));
-    if (d->pl_ctr && d->pl_ctr_n) rc |= hpa_memset_async(d->pl_ctr, 0, d->pl_ctr_n * sizeof(int));
     return rc;
 }
 
@@ -1510,39 +1440,21 @@ static int dec_launch(GPT2* model) {
     const int pl = d->pl_on && !d->profiling;
     /* persistent layers: the embed kernel also zeroes their hand-off counters */
     const size_t zb = (DEC_ERR_INTS + (size_t)L * d->pl_ctr_ints) * sizeof(int);
-    int rc = 0;
-#define DEC_TRACE(i) \
-    if (d->trace_x) rc |= hpa_unpack_frag(d->res, d->B, C, d->trace_x + (size_t)(i) * d->B * C, C)
-    /* chain form 6 as two launches per layer: K1 (qkv | attention | attproj)
-     * and the chain's fc -> fcproj; each counter block is zeroed by the
-     * launch after its last use */
-    const int k1w = DEC_K1 && pl ? dec_attn_ap_waves(model) : 0;
-    if (k1w) {
-        for (int l = 0; l < L && !rc; l++) {
-            rc |= dec_k1(model, l, k1w);
-            if (l == 0) DEC_TRACE(0); /* the embedding, stored by K1(0) */
-            rc |= dec_layer(model, l, 1, 1);
-            DEC_TRACE(l + 1);
-        }
-        rc |= dec_gemm(model, 0, G_LOGITS);
-        rc |= dec_pick(model, NULL);
-        return rc;
-    }
     /* chain form 6 (and form 8 at C = 768, which sums as form 6): embed +
      * qkv(0) + the counter zeroing in one launch */
     const int first = pl && DEC_FIRST_LAUNCH && d->pl_on == 3 &&
                       (d->pl_wform == 6 || (d->pl_wform == 8 && model->config.num_heads == 12));
-    rc = first ? dec_first(model, zb)
-       : !pl   ? hpa_embed_frag(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C)
-               : hpa_embed_frag_zero(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C, d->pl_ctr, zb);
+    int rc = first ? dec_first(model, zb)
+           : !pl   ? hpa_embed_frag(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C)
+                   : hpa_embed_frag_zero(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C, d->pl_ctr, zb);
+#define DEC_TRACE(i) \
+    if (d->trace_x) rc |= hpa_unpack_frag(d->res, d->B, C, d->trace_x + (size_t)(i) * d->B * C, C)
     DEC_TRACE(0);
     if (pl) { /* qkv(0), then one persistent launch per layer */
         if (!first) rc |= dec_gemm(model, 0, G_QKV);
-        const int apw = dec_attn_ap_waves(model);
         for (int l = 0; l < L && !rc; l++) {
-            /* chain form: the attention's own launch (with attproj at one row block) */
-            if (d->pl_on >= 2) rc |= apw ? dec_attention_ap(model, l, apw) : dec_attention(model, l);
-            rc |= dec_layer(model, l, apw != 0, 0);
+            if (d->pl_on >= 2) rc |= dec_attention(model, l); /* chain form: the attention's own launch */
+            rc |= dec_layer(model, l);
             DEC_TRACE(l + 1);
         }
         rc |= dec_gemm(model, 0, G_LOGITS);
