@@ -477,7 +477,9 @@ def main():
                                          "(hpa_decode_layer chain_only)",
                                       3: "attention launch + one persistent launch of the GEMM chain in "
                                          "wide / multi-tile units (hpa_decode_layer chain_only 2..6, 8: "
-                                         "by default form 6 at C = 768, form 8 at C >= 1024)"}[model.layer_form()],
+                                         "by default form 6 at C = 768, form 8 at C >= 1024)",
+                                      4: "attention launch + one persistent launch of the bf16-weight GEMM "
+                                         "chain (hpa_decode_chain_b16)"}[model.layer_form()],
                        "attn_form": f"(sequence, head) x {splits} range(s)",
                        "token_choice": "multinomial (reference sample_mult)" if args.sample else "greedy",
                        "gemm_waves": [int(x) for x in model.gemm_config()[0]],

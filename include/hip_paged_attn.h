@@ -399,6 +399,46 @@ int hpa_decode_layer(const HpaLayerArgs* a);
  * qkv_c2, q_out; the layer fields are ignored. */
 int hpa_decode_first(const HpaLayerArgs* a, const int* tokens, const float* wte, const float* wpe, void* zero,
                      size_t zero_bytes);
+/* ---------------- bf16-weight decode chain (hpa_chain_b16.hip) ----------------
+ * The layer's GEMMs on bf16 weights (BASELINE config 5) as ONE persistent
+ * launch after the layer's decode-attention launch:
+ *   attproj(l) -> fc(l) -> fcproj(l) -> qkv(l+1)
+ * (gpt2_forward, paged_infer.c:659-722), in place of four bf16 GEMM launches.
+ * C = 768, 12 heads, B = 1..256; one 8-wave workgroup per CU; LayerNorms on
+ * the operand path with the row statistics from the consumer's own operand
+ * fragments; weights in the bf16 frag layout (hpa_pack_frag_bf16); operands
+ * rounded to bf16, fp32 accumulation.  Same hand-off protocol, bounded spins
+ * and error words as hpa_decode_layer. */
+typedef struct {
+    int B, layer, last;           /* last: no qkv(l+1) phase; stats_out then written */
+    const HpaKVPool* pool;        /* fp32 or bf16 pages; K/V of layer l+1 appended */
+    const int* block_table;
+    int bt_stride;
+    const int* pos;
+    const float* att;             /* attention output of layer l, frag [Mp][C] */
+    float* res;                   /* residual in (frag [Mp][C]); fcproj writes the next */
+    float* res2;                  /* res + attproj, frag [Mp][C] */
+    float* fch;                   /* gelu(fc), bf16 frag layout [Mp][4C] (half the buffer) */
+    const void* w_ap;             /* bf16 frag packs: attprojw [C][C], fcw [4C][C], */
+    const void* w_fc;             /* fcprojw [C][4C], qkvw of layer l+1 [3C][C] */
+    const void* w_fp;
+    const void* w_qkv;
+    const float *b_ap, *ln2_w, *ln2_b, *b_fc, *b_fp, *ln1_w, *ln1_b, *b_qkv; /* ln1 / b_qkv: layer l+1 */
+    float* q_out;                 /* q of layer l+1 [B][C] row-major */
+    float* stats_out;             /* last layer: LNf statistics [C/16][stats_mp][2] of res; else NULL */
+    int stats_mp;                 /* 0: ceil(B/16)*16 */
+    float* slab;                  /* fcproj K-part partials (hpa_decode_chain_b16_sizes out[0] floats) */
+    int* counters;                /* this layer's counter block (out[1] ints), zero before the launch */
+    int* err;                     /* as HpaLayerArgs.err / err_sticky */
+    int* err_sticky;
+} HpaChainB16Args;
+int hpa_decode_chain_b16_eligible(int B, int C, int num_heads);
+/* out2 = {slab floats, counter ints per layer} */
+int hpa_decode_chain_b16_sizes(int B, size_t* out2);
+int hpa_decode_chain_b16(const HpaChainB16Args* a);
+/* diagnostic builds (-DHPA_LAYER_TRACE) only, else returns 1: the bf16
+ * chain's per-(layer, workgroup) event stamps, as hpa_decode_layer_trace */
+int hpa_decode_chain_b16_trace(unsigned long long* host, int layers);
 /* diagnostic builds (-DHPA_LAYER_TRACE) only, else returns 1: per-(layer,
  * workgroup) event stamps [layers][256][16] of the last launches (10 ns
  * ticks); host = NULL clears them */

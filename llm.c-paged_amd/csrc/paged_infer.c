@@ -663,7 +663,8 @@ struct GPT2Decode {
                          5 chain form 6 (12-wave multi-tile units), 6 chain form 8 (streamed-weight
                          units, C = 768 / 1600) */
     int pl_on;        /* in use: 0 five launches, 1 full persistent layer, 2 attention launch + chain,
-                         3 attention launch + chain of wide units (hpa_layer.hip NWU = pl_nwu) */
+                         3 attention launch + chain of wide units (hpa_layer.hip NWU = pl_nwu),
+                         4 attention launch + the bf16-weight chain (hpa_chain_b16.hip) */
     int pl_wform;     /* wide-unit form of the chain (HpaLayerArgs.chain_only 2..6, 8), else 1 */
     int pl_splits;
     int pl_global_B;  /* gpt2_decode_set_global_batch: the batch the picks follow (<= 64); else 0 */
@@ -903,9 +904,32 @@ static const float* wpack_at(const GPT2Decode* d, size_t off);
 
 /* the persistent layer's workspace, where it applies (fp32 LN-folded weights,
  * the shapes hpa_decode_layer_eligible accepts) */
+static int dec_chain_b16_setup(GPT2* model, GPT2Decode* d) {
+    const GPT2Config c = model->config;
+    size_t sz[2];
+    if (!hpa_decode_chain_b16_eligible(d->B, c.channels, c.num_heads)) return 0;
+    if (hpa_decode_chain_b16_sizes(d->B, sz)) return 1;
+    if (!d->pl_slab || d->pl_slab_n < sz[0]) {
+        hpa_free(d->pl_slab);
+        d->pl_slab_n = sz[0];
+        d->pl_slab = (float*)hpa_malloc(sz[0] * sizeof(float));
+    }
+    if (!d->pl_ctr || d->pl_ctr_ints < sz[1]) {
+        hpa_free(d->pl_ctr);
+        d->pl_ctr_ints = sz[1];
+        d->pl_ctr = (int*)hpa_malloc((DEC_ERR_INTS + (size_t)c.num_layers * sz[1]) * sizeof(int));
+    }
+    if (!d->pl_slab || !d->pl_ctr) return 1;
+    d->pl_on = 4;
+    return 0;
+}
+
 static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
     const GPT2Config c = model->config;
     d->pl_on = 0;
+    /* bf16 weights (BASELINE config 5): the bf16 chain (hpa_chain_b16.hip),
+     * B <= 256, in place of four GEMM launches per layer */
+    if (d->pl_want && d->w_bf16) return dec_chain_b16_setup(model, d);
     if (!d->pl_want || d->w_bf16 || !d->d_fold) return 0;
     const int Bg = dec_pick_B(d); /* the batch the picks follow */
     if (Bg > 64) return 0;
@@ -961,6 +985,51 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
     return 0;
 }
 
+/* layer l's bf16 chain: attproj(l) .. fcproj(l), qkv(l+1) (pl_on 4) */
+static int dec_layer_b16(GPT2* model, int l) {
+    GPT2Decode* d = model->decode;
+    const GPT2Config c = model->config;
+    const int C = c.channels, L = c.num_layers;
+    const ParameterTensors* w = &model->params;
+    const size_t lc = (size_t)l * C;
+    const size_t e_layer = d->wpack_off[3] + hpa_frag_elems(C, 4 * C);
+    HpaChainB16Args a;
+    memset(&a, 0, sizeof(a));
+    a.B = d->B;
+    a.layer = l;
+    a.last = l + 1 == L;
+    a.pool = &d->pool;
+    a.block_table = d->d_bt;
+    a.bt_stride = d->bt_stride;
+    a.pos = d->d_pos;
+    a.att = d->att;
+    a.res = d->res;
+    a.res2 = d->res2;
+    a.fch = d->fch;
+    a.w_ap = wpack_at(d, e_layer * l + d->wpack_off[1]);
+    a.b_ap = w->attprojb + lc;
+    a.ln2_w = w->ln2w + lc;
+    a.ln2_b = w->ln2b + lc;
+    a.w_fc = wpack_at(d, e_layer * l + d->wpack_off[2]);
+    a.b_fc = w->fcb + 4 * lc;
+    a.w_fp = wpack_at(d, e_layer * l + d->wpack_off[3]);
+    a.b_fp = w->fcprojb + lc;
+    if (!a.last) {
+        a.w_qkv = wpack_at(d, e_layer * (l + 1) + d->wpack_off[0]);
+        a.b_qkv = w->qkvb + 3 * (lc + C);
+        a.ln1_w = w->ln1w + lc + C;
+        a.ln1_b = w->ln1b + lc + C;
+        a.q_out = d->d_q; /* every read of q(l) was the attention launch's, before this one */
+    }
+    a.stats_out = a.last ? d->st1 : NULL; /* LNf statistics for the logits */
+    a.stats_mp = d->Mp;
+    a.slab = d->pl_slab;
+    a.counters = d->pl_ctr + DEC_ERR_INTS + (size_t)l * d->pl_ctr_ints;
+    a.err = d->pl_ctr;
+    a.err_sticky = d->d_next + d->B;
+    return hpa_decode_chain_b16(&a);
+}
+
 /* layer l of the persistent path: attention(l) .. fcproj(l), qkv(l+1) */
 static int dec_layer(GPT2* model, int l) {
     GPT2Decode* d = model->decode;
@@ -969,6 +1038,7 @@ static int dec_layer(GPT2* model, int l) {
     const ParameterTensors* w = &model->params;
     const size_t lc = (size_t)l * C;
     const size_t e_layer = d->wpack_off[3] + hpa_frag_elems(C, 4 * C);
+    if (d->pl_on == 4) return dec_layer_b16(model, l);
     HpaLayerArgs a;
     memset(&a, 0, sizeof(a));
     a.B = d->B;

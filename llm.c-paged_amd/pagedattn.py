@@ -266,6 +266,7 @@ def lib():
     _sig(L, "hpa_decode_layer_eligible", i, [i, i, i, i])
     _sig(L, "hpa_decode_layer_pick_splits", i, [i, i, i])
     _sig(L, "hpa_decode_layer_trace", i, [v, i])
+    _sig(L, "hpa_decode_chain_b16_trace", i, [v, i])
     _sig(L, "hpa_logits_trace", i, [v])
     _sig(L, "gpt2_decode_evicted", i, [v, _I])
     _sig(L, "gpt2_decode_read_kv", i, [v, i, i, i, _F, _F])
@@ -645,7 +646,8 @@ class Model:
     def set_layer_kernel(self, on):
         """layer loop: 0 five launches, 2 full persistent layer, 3 attention
         launch + persistent chain, 4 the chain with wide units (B <= 16,
-        C = 768), 1 the form measured fastest for the batch;
+        C = 768), 1 the form measured fastest for the batch (bf16 weights:
+        any nonzero value is the bf16 chain, B <= 256);
         returns whether a persistent form is now in use"""
         check(lib().gpt2_decode_set_layer_kernel(self.h, int(on)), "set_layer_kernel")
         return bool(lib().gpt2_decode_layer_kernel(self.h))
@@ -655,7 +657,7 @@ class Model:
 
     def layer_form(self):
         """0 five launches per layer, 1 full persistent layer, 2 attention launch + persistent chain,
-        3 the chain with wide units"""
+        3 the chain with wide units, 4 the bf16-weight chain (hpa_chain_b16.hip)"""
         return int(lib().gpt2_decode_layer_kernel(self.h))
 
     def status(self):

@@ -182,7 +182,7 @@ def test_config5_end_to_end_full_context(hip):
 
 # ---------------------------------------------------------------- per-layer pinning
 def _layer_pinned_run(hip, cfgd, params, B, P, ctx0, steps, seed, kv_bf16=False, w_bf16=False, layer_rtol=1e-5,
-                      tol=LOGIT_TOL, max_exempt_frac=0.02, max_ctx=None):
+                      tol=LOGIT_TOL, max_exempt_frac=0.02, max_ctx=None, layer_form=None):
     """Each layer on the GPU's own input: gpt2_decode_step_traced returns the
     residual stream entering every layer (and LNf), the oracle runs layer l
     from the GPU's stream[l] (oracle_paged_step_ex) and its output is compared
@@ -195,6 +195,8 @@ def _layer_pinned_run(hip, cfgd, params, B, P, ctx0, steps, seed, kv_bf16=False,
     model = hip.Model(cfgd, params=params)
     model.decode_init(B, P, max_ctx, kv_dtype=hip.HPA_BF16 if kv_bf16 else hip.HPA_F32,
                       w_dtype=hip.HPA_BF16 if w_bf16 else hip.HPA_F32)
+    if layer_form is not None:  # the layer loop the test is about (bench's default)
+        assert model.layer_form() == layer_form
     model.fill_random(ctx0, seed=seed)
     c = oc.cfg(cfgd["maxT"], cfgd["V"], cfgd["L"], cfgd["NH"], cfgd["C"])
     orc = oc.PagedDecoder(params, c, B, P, max_ctx, page_seed=seed, kv_bf16=kv_bf16, w_bf16=w_bf16)
@@ -244,18 +246,34 @@ def test_config5_layer_pinned_full_context(hip):
     the 2 % near-tie bar"""
     params = _params(hip, CFG_124M_2K, 56)
     _layer_pinned_run(hip, CFG_124M_2K, params, B=32, P=8, ctx0=2048 - 10, steps=10, seed=56, kv_bf16=True,
-                      w_bf16=True, layer_rtol=BF16_LAYER_RTOL, tol=BF16_PINNED_LOGIT_TOL)
+                      w_bf16=True, layer_rtol=BF16_LAYER_RTOL, tol=BF16_PINNED_LOGIT_TOL, layer_form=4)
 
 
-def test_config5_layer_pinned_full_batch(hip):
+@pytest.mark.parametrize("chain", [True, False], ids=["bf16_chain", "five_launches"])
+def test_config5_layer_pinned_full_batch(hip, chain, monkeypatch):
     """config 5's real batch, B=256 (bf16 weights + bf16 KV, page 8, the
-    2048-row wpe): the GEMMs run the A-resident bf16 kernel (variant 5, M >
-    112) on the shape they serve, each layer on the GPU's own input against
-    the oracle; a short context (the GEMMs do not depend on it; the pools
-    bounded to 64 positions), ids at the 2 % near-tie bar"""
+    2048-row wpe): the layer loop the bench runs -- the bf16 chain
+    (hpa_chain_b16.hip, one persistent launch per layer) -- and the five-launch
+    loop (A-resident bf16 GEMMs, variant 5) on the shape they serve, each layer
+    on the GPU's own input against the oracle; a short context (the GEMMs do
+    not depend on it; the pools bounded to 64 positions), ids at the 2 %
+    near-tie bar"""
+    if not chain:
+        monkeypatch.setenv("HPA_LAYER_KERNEL", "0")
     params = _params(hip, CFG_124M_2K, 58)
     _layer_pinned_run(hip, CFG_124M_2K, params, B=256, P=8, ctx0=40, steps=4, seed=58, kv_bf16=True,
-                      w_bf16=True, layer_rtol=BF16_LAYER_RTOL, tol=BF16_PINNED_LOGIT_TOL, max_ctx=64)
+                      w_bf16=True, layer_rtol=BF16_LAYER_RTOL, tol=BF16_PINNED_LOGIT_TOL, max_ctx=64,
+                      layer_form=4 if chain else 0)
+
+
+@pytest.mark.parametrize("B,P,kv_bf16", [(1, 16, False), (40, 8, True), (200, 8, False)])
+def test_bf16_chain_ragged_batches(hip, B, P, kv_bf16):
+    """the bf16 chain at batches that are not whole row groups of 32: one row
+    (one row block), 40 rows (3 row blocks: the last row group has one block)
+    and 200 rows (13 blocks), fp32 and bf16 pools; every layer against the oracle"""
+    params = _params(hip, CFG_124M, 60 + B)
+    _layer_pinned_run(hip, CFG_124M, params, B=B, P=P, ctx0=30, steps=3, seed=60 + B, kv_bf16=kv_bf16, w_bf16=True,
+                      layer_rtol=BF16_LAYER_RTOL, tol=BF16_PINNED_LOGIT_TOL, max_ctx=64, layer_form=4)
 
 
 def test_config2_layer_pinned_full_context(hip):

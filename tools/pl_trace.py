@@ -1,10 +1,11 @@
 """Phase timeline of the persistent decode layer (hpa_layer.hip), from the
 trace build's per-(layer, workgroup) s_memrealtime stamps.
 
-usage: HPA_LIB=llm.c-paged_amd/libpaged_hip_trace.so python tools/pl_trace.py [B] [ctx] [mode] [XL]
+usage: HPA_LIB=llm.c-paged_amd/libpaged_hip_trace.so python tools/pl_trace.py [B] [ctx] [mode] [XL|b16]
 (mode = gpt2_decode_set_layer_kernel: 2 full persistent layer, default; 3
 attention launch + persistent chain; 4 wide units; 5 chain form 6; 6 chain
-form 8; XL: GPT-2 XL, page 32)
+form 8; XL: GPT-2 XL, page 32; b16: the bf16-weight chain, hpa_chain_b16.hip,
+at config 5's pool -- maxT 2048, page 8, bf16 KV -- with any nonzero mode)
 
 Prints, per event, the min / median / max over workgroups of the time since
 the earliest kernel-start stamp of that layer (us), averaged over layers 1..L-2
@@ -32,10 +33,16 @@ def main():
     ctx = int(sys.argv[2]) if len(sys.argv) > 2 else 990
     mode = int(sys.argv[3]) if len(sys.argv) > 3 else 2
     xl = len(sys.argv) > 4 and sys.argv[4] == "XL"
+    b16 = len(sys.argv) > 4 and sys.argv[4] == "b16"
     cfg = dict(maxT=1024, V=50257, L=48, NH=25, C=1600) if xl else dict(maxT=1024, V=50257, L=12, NH=12, C=768)
+    if b16:
+        cfg["maxT"] = 2048
     hip.init(0)
-    m = hip.Model(cfg, params=hip.synthetic_params(cfg, seed=3) if xl else synth.params(cfg, seed=3))
-    m.decode_init(B, 32 if xl else 16, cfg["maxT"])
+    m = hip.Model(cfg, params=hip.synthetic_params(cfg, seed=3) if xl or b16 else synth.params(cfg, seed=3))
+    if b16:
+        m.decode_init(B, 8, cfg["maxT"], kv_dtype=hip.HPA_BF16, w_dtype=hip.HPA_BF16)
+    else:
+        m.decode_init(B, 32 if xl else 16, cfg["maxT"])
     assert m.set_layer_kernel(mode), "persistent layer not in use"
     m.set_graph(True)
     hip.check(hip.lib().gpt2_decode_fill_random(m.h, ctx, 5), "fill")
@@ -43,12 +50,13 @@ def main():
     for _ in range(8):
         m.step(toks)
     L = hip.lib()
-    if L.hpa_decode_layer_trace(None, 0) != 0:
+    read = L.hpa_decode_chain_b16_trace if b16 else L.hpa_decode_layer_trace
+    if read(None, 0) != 0:
         raise SystemExit("not a trace build (make XFLAGS=-DHPA_LAYER_TRACE)")
     m.step(toks)
     m.status()
     buf = np.zeros((cfg["L"], 256, 16), np.uint64)  # 16 event slots per (layer, workgroup)
-    hip.check(L.hpa_decode_layer_trace(buf.ctypes.data_as(ctypes.c_void_p), cfg["L"]), "trace")
+    hip.check(read(buf.ctypes.data_as(ctypes.c_void_p), cfg["L"]), "trace")
     rows = {k: [] for k in range(len(EVENTS))}
     spans = []
     for layer in range(1, cfg["L"] - 1):
