@@ -436,6 +436,14 @@ int hpa_decode_chain_b16_eligible(int B, int C, int num_heads);
 /* out2 = {slab floats, counter ints per layer} */
 int hpa_decode_chain_b16_sizes(int B, size_t* out2);
 int hpa_decode_chain_b16(const HpaChainB16Args* a);
+/* the step's first launch on this path: the embedding wte[tokens[b]] +
+ * wpe[pos[b]] (encoder_forward, paged_infer.c:41-47) into res, layer 0's q
+ * and K/V (the chain's qkv phase; w_qkv / b_qkv / ln1_* of layer 0), and
+ * zero_bytes of `zero` (the step's counter block) zeroed -- one launch for
+ * the embed kernel and the qkv(0) GEMM.  Reads B, pool, block_table,
+ * bt_stride, pos, res, w_qkv, b_qkv, ln1_w, ln1_b, q_out. */
+int hpa_decode_chain_b16_first(const HpaChainB16Args* a, const int* tokens, const float* wte, const float* wpe,
+                               void* zero, size_t zero_bytes);
 /* diagnostic builds (-DHPA_LAYER_TRACE) only, else returns 1: the bf16
  * chain's per-(layer, workgroup) event stamps, as hpa_decode_layer_trace */
 int hpa_decode_chain_b16_trace(unsigned long long* host, int layers);

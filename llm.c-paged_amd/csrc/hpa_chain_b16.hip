@@ -78,6 +78,12 @@ struct Args {
     int* ctr;
     int* err;
     int* err_sticky;
+    // the step's first launch (FIRST): the tokens, the embedding tables, and
+    // the step's counter block to zero (16-byte granules)
+    const int* tokens;
+    const float *wte, *wpe;
+    int4* zero;
+    int zero_n4;
 };
 
 struct Smem {
@@ -114,6 +120,7 @@ __device__ __forceinline__ void drain_vm() {
 }
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
 
 __device__ __forceinline__ bf16x8 pack_bf16(float4 a, float4 b) {
     u16x8 u;
@@ -202,20 +209,45 @@ __device__ __forceinline__ void load_w(const uint4* W, int K32W, int j0, int kb,
 // waves' partial sums through LDS, in wave order; one-pass form as
 // layernorm_forward's statistics elsewhere in the engine), rounded to bf16,
 // then the RG x T chains of 3 MFMAs
-template <int RG, int T, bool LN>
+// EMB (the step's first launch): A is the embedding wte[token] + wpe[pos]
+// (encoder_forward, paged_infer.c:41-47; rows >= B are 0) built in registers
+// from ea's tables, and stored to ea->res (frag layout) when store_res
+template <int RG, int T, bool LN, bool EMB = false>
 __device__ __forceinline__ void unit_mma(const float* A, int K16A, int rb0, int R, int kb, const uint4 (&wr)[T][SPW],
-                                         const float* lnw, const float* lnb, Smem& sm, f32x4 (&acc)[RG][T]) {
+                                         const float* lnw, const float* lnb, Smem& sm, f32x4 (&acc)[RG][T],
+                                         const Args* ea = nullptr, bool store_res = false) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float4 xa[RG][SPW][2];
 #pragma unroll
     for (int r = 0; r < RG; ++r) {
         const int rb = min(rb0 + r, R - 1);
+        if constexpr (EMB) {
+            const int row = rb * 16 + (lane & 15);
+            const bool live = row < ea->B;
+            const float* te = ea->wte + (size_t)(live ? ea->tokens[row] : 0) * C;
+            const float* pe = ea->wpe + (size_t)(live ? ea->pos[row] : 0) * C;
 #pragma unroll
-        for (int s = 0; s < SPW; ++s)
+            for (int s = 0; s < SPW; ++s)
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
-                xa[r][s][h] = hpa::load_wt16(A, ((rb * K16A + 2 * (kb + w * SPW + s) + h) * 64 + lane) * 16);
+                for (int h = 0; h < 2; ++h) {
+                    const int col = 32 * (kb + w * SPW + s) + 16 * h + 4 * (lane >> 4);
+                    xa[r][s][h] = live ? add4(ld4(te + col), ld4(pe + col)) : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            if (store_res && rb0 + r < R)
+#pragma unroll
+                for (int s = 0; s < SPW; ++s)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+                        reinterpret_cast<float4*>(ea->res)[(rb * K16A + 2 * (kb + w * SPW + s) + h) * 64 + lane] =
+                            xa[r][s][h];
+        } else {
+#pragma unroll
+            for (int s = 0; s < SPW; ++s)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    xa[r][s][h] = hpa::load_wt16(A, ((rb * K16A + 2 * (kb + w * SPW + s) + h) * 64 + lane) * 16);
+        }
     }
     float4 lg[SPW][2], lb[SPW][2];
     if (LN) {
@@ -349,8 +381,6 @@ __device__ __forceinline__ void where(int e, int rb0, int j0, int& row, int& col
     col = (j0 + q % T) * 16 + 4 * (e & 3);
 }
 
-__device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
-
 // qkv epilogue store of columns col..col+3 of `row`: q row-major, or K / V of
 // this token into the sequence's page of layer l+1 (add_to_cache,
 // paged_infer.c:505-573; fp32 pool K [chunk of 4][slot][4], bf16 pool K
@@ -384,7 +414,11 @@ __device__ __forceinline__ void qkv_store(const Args& a, int row, int col, float
 
 }  // namespace cb
 
-template <int P, bool BF>
+// FIRST: the step's first launch -- the counter block zeroed, then only
+// phase E on the embedding (layer 0's q and K/V; the tile group 0 unit of a
+// row block also stores the residual stream it built): the embed kernel and
+// the qkv(0) GEMM in one launch
+template <int P, bool BF, bool FIRST>
 __global__ __launch_bounds__(512) void decode_chain_b16_kernel(cb::Args args) {
     using namespace cb;
     const Args& a = *(const Args*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -396,9 +430,11 @@ __global__ __launch_bounds__(512) void decode_chain_b16_kernel(cb::Args args) {
     const int R = a.R, RH = (a.R + 1) / 2;  // row blocks, row groups of two
     const int Mp = R * 16;
     CB_MARK(0);
+    if constexpr (FIRST)
+        for (int i = bid * NT + tid; i < a.zero_n4; i += gridDim.x * NT) a.zero[i] = make_int4(0, 0, 0, 0);
 
     // B: attproj(l): res2 = res + att . Wap^T + b; unit (row block, 3 tiles)
-    {
+    if constexpr (!FIRST) {
         constexpr int RG = 1, T = 3, NE = RG * T * 64;
         const bool has = bid < R * NG_B;
         const int g = bid % NG_B, rb = bid / NG_B;
@@ -432,7 +468,7 @@ __global__ __launch_bounds__(512) void decode_chain_b16_kernel(cb::Args args) {
         CB_MARK(5);
     }
     // C: fc(l): fch = gelu(LN2(res2) . Wfc^T + b); unit (2 row blocks, 6 tiles)
-    {
+    if constexpr (!FIRST) {
         constexpr int RG = 2, T = 6, NE = RG * T * 64;
         const bool has = bid < RH * NG_C;
         const int g = bid % NG_C, rg = bid / NG_C, rb0 = 2 * rg;
@@ -487,7 +523,7 @@ __global__ __launch_bounds__(512) void decode_chain_b16_kernel(cb::Args args) {
     }
     // D: fcproj(l), K part p of 4: partial tiles -> slab; the last part of a
     // (row quad, tile group) adds the parts in order + bias + res2 -> res
-    {
+    if constexpr (!FIRST) {
         constexpr int RG = 4, T = 3, NE = RG * T * 64;
         const int RQ = (R + 3) / 4;
         const bool has = bid < RQ * 4 * NG_D;
@@ -591,11 +627,11 @@ __global__ __launch_bounds__(512) void decode_chain_b16_kernel(cb::Args args) {
             }
         };
         pre();
-        if (!wait_lines(a, kX2 + rb, 1, has ? 1 : 0, NG_D, 4, sm)) return;
+        if (!FIRST && !wait_lines(a, kX2 + rb, 1, has ? 1 : 0, NG_D, 4, sm)) return;
         CB_MARK(10);
         if (has) {
             f32x4 acc[RG][T];
-            unit_mma<RG, T, true>(a.res, K16, rb, R, 0, wr, a.ln1_w, a.ln1_b, sm, acc);
+            unit_mma<RG, T, true, FIRST>(a.res, K16, rb, R, 0, wr, a.ln1_w, a.ln1_b, sm, acc, &a, g == 0);
             put_red<RG, T>(sm.red, acc);
         }
         lds_barrier();
@@ -624,12 +660,14 @@ int num_cus_b16() {
     return g_ncu_b16;
 }
 
-template <int P, bool BF>
-int launch_b16(const HpaChainB16Args* h, int G) {
+template <int P, bool BF, bool FIRST = false>
+int launch_b16(const HpaChainB16Args* h, int G, const int* tokens = nullptr, const float* wte = nullptr,
+               const float* wpe = nullptr, void* zero = nullptr, size_t zero_bytes = 0) {
     static int resident = -1;
     if (resident < 0) {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, decode_chain_b16_kernel<P, BF>, 512, 0) != hipSuccess)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, decode_chain_b16_kernel<P, BF, FIRST>, 512, 0) !=
+            hipSuccess)
             nb = 0;
         resident = nb;
     }
@@ -669,7 +707,12 @@ int launch_b16(const HpaChainB16Args* h, int G) {
     a.ctr = h->counters;
     a.err = h->err;
     a.err_sticky = h->err_sticky;
-    decode_chain_b16_kernel<P, BF><<<G, 512, 0, hpa_stream()>>>(a);
+    a.tokens = tokens;
+    a.wte = wte;
+    a.wpe = wpe;
+    a.zero = reinterpret_cast<int4*>(zero);
+    a.zero_n4 = (int)(zero_bytes / 16);
+    decode_chain_b16_kernel<P, BF, FIRST><<<G, 512, 0, hpa_stream()>>>(a);
     HPA_LAUNCH_CHECK();
     return 0;
 }
@@ -713,6 +756,35 @@ int hpa_decode_chain_b16_trace(unsigned long long* host, int layers) {
     (void)layers;
     return 1;
 #endif
+}
+
+int hpa_decode_chain_b16_first(const HpaChainB16Args* h, const int* tokens, const float* wte, const float* wpe,
+                               void* zero, size_t zero_bytes) {
+    HPA_REQUIRE(h && h->pool && h->pool->base && tokens && wte && wpe, "decode chain bf16 first: null operand");
+    const HpaKVPool* pool = h->pool;
+    HPA_REQUIRE(pool->dtype == HPA_F32 || pool->dtype == HPA_BF16, "decode chain bf16 first: fp32 or bf16 pool");
+    HPA_REQUIRE(pool->head_size == 64 && pool->num_heads == 12, "decode chain bf16 first: 12 heads of 64");
+    HPA_REQUIRE(hpa_decode_chain_b16_eligible(h->B, 768, 12), "decode chain bf16 first: 1..256 rows");
+    HPA_REQUIRE(h->res && h->w_qkv && h->b_qkv && h->ln1_w && h->ln1_b && h->q_out && h->block_table && h->pos,
+                "decode chain bf16 first: null operand");
+    HPA_REQUIRE(zero_bytes % 16 == 0 && ((size_t)zero & 15) == 0 && zero_bytes / 16 <= 0x7fffffff,
+                "decode chain bf16 first: the zeroed block must be whole 16-byte granules");
+    HpaChainB16Args f = *h;
+    f.layer = -1;  // K/V into layer 0's pages (layer + 1)
+    f.last = 0;
+    const int G = num_cus_b16();
+    const bool bf = pool->dtype == HPA_BF16;
+    switch (pool->page_size) {
+        case 8: return bf ? launch_b16<8, true, true>(&f, G, tokens, wte, wpe, zero, zero_bytes)
+                          : launch_b16<8, false, true>(&f, G, tokens, wte, wpe, zero, zero_bytes);
+        case 16: return bf ? launch_b16<16, true, true>(&f, G, tokens, wte, wpe, zero, zero_bytes)
+                           : launch_b16<16, false, true>(&f, G, tokens, wte, wpe, zero, zero_bytes);
+        case 32: return bf ? launch_b16<32, true, true>(&f, G, tokens, wte, wpe, zero, zero_bytes)
+                           : launch_b16<32, false, true>(&f, G, tokens, wte, wpe, zero, zero_bytes);
+        case 64: return bf ? launch_b16<64, true, true>(&f, G, tokens, wte, wpe, zero, zero_bytes)
+                           : launch_b16<64, false, true>(&f, G, tokens, wte, wpe, zero, zero_bytes);
+        default: return hpa_fail(__FILE__, __LINE__, "decode chain bf16 first: page size must be 8, 16, 32 or 64");
+    }
 }
 
 int hpa_decode_chain_b16(const HpaChainB16Args* h) {

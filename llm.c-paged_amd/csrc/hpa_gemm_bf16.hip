@@ -274,9 +274,6 @@ __global__ __launch_bounds__(NW * 64) void gemm_b16_ares_kernel(FG p, int cpw) {
     }
 }
 
-#ifndef HPA_B16_LOGITS_U
-#define HPA_B16_LOGITS_U 8  // A/B builds: the logits' weight steps in flight per wave
-#endif
 template <int NW, int MT, int KC>
 static int launch_ares_t(FG p, int epi, int rounds) {
     constexpr int U = 8;
@@ -297,7 +294,7 @@ static int launch_ares_t(FG p, int epi, int rounds) {
         case HPA_FEPI_QKV: gemm_b16_ares_kernel<NW, HPA_FEPI_QKV, MT, KC, U><<<grid, block, 0, hpa_stream()>>>(p, cpw); break;
         case HPA_FEPI_RESID: gemm_b16_ares_kernel<NW, HPA_FEPI_RESID, MT, KC, U><<<grid, block, 0, hpa_stream()>>>(p, cpw); break;
         case HPA_FEPI_GELU: gemm_b16_ares_kernel<NW, HPA_FEPI_GELU, MT, KC, U><<<grid, block, 0, hpa_stream()>>>(p, cpw); break;
-        case HPA_FEPI_LOGITS: gemm_b16_ares_kernel<NW, HPA_FEPI_LOGITS, MT, KC, HPA_B16_LOGITS_U><<<grid, block, 0, hpa_stream()>>>(p, cpw); break;
+        case HPA_FEPI_LOGITS: gemm_b16_ares_kernel<NW, HPA_FEPI_LOGITS, MT, KC, U><<<grid, block, 0, hpa_stream()>>>(p, cpw); break;
         default: return hpa_fail(__FILE__, __LINE__, "gemm_fused bf16: unknown epilogue");
     }
     HPA_LAUNCH_CHECK();

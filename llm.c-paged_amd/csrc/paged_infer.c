@@ -1501,6 +1501,26 @@ static int dec_first(GPT2* model, size_t zb) {
     return hpa_decode_first(&a, d->d_tokens, w->wte, w->wpe, d->pl_ctr, zb);
 }
 
+/* the bf16 chain's first launch: embedding + qkv(0) + the counter zeroing */
+static int dec_first_b16(GPT2* model, size_t zb) {
+    GPT2Decode* d = model->decode;
+    const ParameterTensors* w = &model->params;
+    HpaChainB16Args a;
+    memset(&a, 0, sizeof(a));
+    a.B = d->B;
+    a.pool = &d->pool;
+    a.block_table = d->d_bt;
+    a.bt_stride = d->bt_stride;
+    a.pos = d->d_pos;
+    a.res = d->res;
+    a.w_qkv = wpack_at(d, d->wpack_off[0]); /* layer 0 */
+    a.b_qkv = w->qkvb;
+    a.ln1_w = w->ln1w;
+    a.ln1_b = w->ln1b;
+    a.q_out = d->d_q;
+    return hpa_decode_chain_b16_first(&a, d->d_tokens, w->wte, w->wpe, d->pl_ctr, zb);
+}
+
 /* the whole step on the library stream */
 static int dec_launch(GPT2* model) {
     GPT2Decode* d = model->decode;
@@ -1512,9 +1532,9 @@ static int dec_launch(GPT2* model) {
     const size_t zb = (DEC_ERR_INTS + (size_t)L * d->pl_ctr_ints) * sizeof(int);
     /* chain form 6 (and form 8 at C = 768, which sums as form 6): embed +
      * qkv(0) + the counter zeroing in one launch */
-    const int first = pl && DEC_FIRST_LAUNCH && d->pl_on == 3 &&
-                      (d->pl_wform == 6 || (d->pl_wform == 8 && model->config.num_heads == 12));
-    int rc = first ? dec_first(model, zb)
+    const int first = pl && DEC_FIRST_LAUNCH && ((d->pl_on == 3 &&
+                      (d->pl_wform == 6 || (d->pl_wform == 8 && model->config.num_heads == 12))) || d->pl_on == 4);
+    int rc = first ? (d->pl_on == 4 ? dec_first_b16(model, zb) : dec_first(model, zb))
            : !pl   ? hpa_embed_frag(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C)
                    : hpa_embed_frag_zero(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C, d->pl_ctr, zb);
 #define DEC_TRACE(i) \

@@ -87,7 +87,9 @@ def test_pack_frag_bf16_layout(hip):
     ("RESID", 64, 768, 768, 8, 4, 1, True, 5), ("RESID", 80, 3072, 768, 4, 1, 2, False, 5),
     ("RESID", 48, 1600, 1600, 8, 2, 3, True, 5), ("RESID", 37, 768, 784, 4, 1, 1, True, 5),
     ("GELU", 256, 768, 3072, 8, 4, 2, True, 5), ("GELU", 64, 768, 3072, 4, 2, 1, True, 5),
-    ("LOGITS", 64, 768, 50257, 8, 4, 4, True, 5), ("LOGITS", 256, 768, 50257, 8, 2, 8, True, 5)])
+    ("LOGITS", 64, 768, 50257, 8, 4, 4, True, 5), ("LOGITS", 256, 768, 50257, 8, 2, 8, True, 5),
+    # automatic rounds at config 5's batch, and 50 rows (padded rows 50..63 of the last row group)
+    ("LOGITS", 256, 768, 50257, 8, 4, 0, True, 5), ("LOGITS", 50, 768, 50257, 8, 4, 0, True, 5)])
 def test_fused_bf16_weights(hip, epi, M, K, N, waves, rb, ct, ln, variant):
     """w_dtype = HPA_BF16: every epilogue against the f64 product of the
     bf16-rounded operands (LN applied before the rounding)"""
