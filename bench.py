@@ -154,12 +154,11 @@ def parse():
     ap.add_argument("--attn-splits", type=int, default=0, help="attention context ranges (0 = by shape)")
     ap.add_argument("--layer-kernel", type=int, default=-1, choices=[-1, 0, 1, 2, 3, 4, 5, 6],
                     help="gpt2_decode_set_layer_kernel: 0 five launches per layer; 1 auto (the form measured "
-                         "fastest for the batch: the attention launch + the persistent chain with wide units); "
-                         "2 the full persistent layer (attention inside); 3 the attention launch + the chain "
-                         "(4-wave units); 4 the chain with wide units; 5 chain form 6 (12-wave multi-tile units); "
-                         "6 chain form 8 (streamed weights, also GPT-2 XL); "
-                         "-1 the engine's default "
-                         "(HPA_LAYER_KERNEL or 1)")
+                         "fastest for the batch: chain form 6 at C = 768, form 8 at C >= 1024, the bf16 chain "
+                         "on bf16 weights); 3 the attention launch + the chain (4-wave units); 5 chain form 6 "
+                         "(12-wave multi-tile units); 6 chain form 8 (streamed weights, also GPT-2 XL); 2 the "
+                         "full persistent layer and 4 the wide-unit chain: A/B builds (-DHPA_AB) only; "
+                         "-1 the engine's default (HPA_LAYER_KERNEL or 1)")
     ap.add_argument("--picks", default="local", choices=["local", "global"],
                     help="N>1 / --emulate-rank: shape picks by the rank's own batch (default: a rank computes "
                          "what a single-GPU engine of its rows computes) or by the global batch "

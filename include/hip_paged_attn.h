@@ -65,6 +65,11 @@ void* hpa_stream_create(void);
 int   hpa_stream_destroy(void* stream);
 int   hpa_stream_wait_event(void* ev);
 const char* hpa_last_error(void);
+/* build flags of this library: bit 0 = an A/B build (-DHPA_AB: the layer
+ * forms measured slower -- the full persistent layer, the wide-unit chains --
+ * and the measurement env knobs HPA_LAYER_SPLITS, HPA_GEMM_RING,
+ * HPA_LOGITS_FORM, HPA_BF16_ARES; the product library has none of them) */
+int hpa_build_flags(void);
 /* hipGraph capture of everything enqueued on the current stream between
  * begin and end (the decode step: 5 launches per layer); replay with
  * hpa_graph_launch.  Kernel arguments are frozen at capture, so per-step

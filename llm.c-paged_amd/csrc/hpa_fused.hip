@@ -831,11 +831,15 @@ static int gemm_fused_launch(const HpaFusedGemm* g, FG& p) {
                         (g->variant == 0 || g->variant == 4 || g->variant == 5 || g->variant == 1),
                     "gemm_fused bf16: K % 32, no ln_fold_c1, variant 0/1/5");
         int pk[3];
-        // HPA_BF16_ARES=0: no A-resident default (measurement knob; variant 5 still honoured)
+        // A/B builds: HPA_BF16_ARES=0 = no A-resident default (variant 5 still honoured)
+#ifdef HPA_AB
         static const int ares_default = [] {
             const char* e = getenv("HPA_BF16_ARES");
             return !(e && e[0] == '0');
         }();
+#else
+        constexpr int ares_default = 1;
+#endif
         if (g->variant == 5 ||
             (g->variant != 1 && ares_default && hpa_fused_pick_bf16_ares(g->M, g->N, g->K, pk))) {
             if (g->variant == 5) hpa_fused_pick_bf16_ares(g->M, g->N, g->K, pk);

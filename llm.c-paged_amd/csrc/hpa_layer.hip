@@ -1910,6 +1910,14 @@ int dispatch(const HpaLayerArgs* h, int G) {
         if constexpr (NH == 12) return dispatch6(h, G);
         return hpa_fail(__FILE__, __LINE__, "decode layer: chain form 6 needs C = 768");
     }
+#ifndef HPA_AB
+    // measured slower than the forms the engine picks: in A/B builds only
+    if (h->chain_only >= 2)
+        return hpa_fail(__FILE__, __LINE__, "decode layer: wide-unit chain forms 2..5 are in A/B builds only (-DHPA_AB)");
+    if (!h->chain_only)
+        return hpa_fail(__FILE__, __LINE__, "decode layer: the full persistent layer is in A/B builds only (-DHPA_AB)");
+    return dispatch_p<NH, false>(h, G);
+#else
     if (h->chain_only >= 2) {  // wide units (C = 768), widths (attproj, fc / fcproj, qkv) by chain_only
         if constexpr (LD<NH>::SW % 3 == 0) {
             const int R = (h->B + 15) / 16, nct = LD<NH>::NCT;
@@ -1938,6 +1946,7 @@ int dispatch(const HpaLayerArgs* h, int G) {
         }
     }
     return h->chain_only ? dispatch_p<NH, false>(h, G) : dispatch_p<NH, true>(h, G);
+#endif
 }
 
 }  // namespace

@@ -715,13 +715,17 @@ __global__ __launch_bounds__(kRgNW * 64) void logits_ring_kernel(FG p) {
 
 int g_num_cus = 0;
 
-// HPA_LOGITS_FORM=16 / ring: force a form (A/B knob); else 0 = the caller's
+// A/B builds: HPA_LOGITS_FORM=16 / ring forces a form; else 0 = the caller's
 int logits_form() {
+#ifdef HPA_AB
     static const int f = [] {
         const char* e = getenv("HPA_LOGITS_FORM");
         return (e && e[0] == '1' && e[1] == '6') ? 16 : (e && e[0] == 'r') ? 12 : 0;
     }();
     return f;
+#else
+    return 0;
+#endif
 }
 
 

@@ -17,6 +17,14 @@ int hpa_fail(const char* file, int line, const char* what) {
     return 1;
 }
 
+int hpa_build_flags(void) {
+#ifdef HPA_AB
+    return 1;
+#else
+    return 0;
+#endif
+}
+
 constexpr int kMaxDevices = 64;
 hipStream_t g_dev_streams[kMaxDevices];
 hipStream_t hpa_stream() { return g_stream; }

@@ -958,9 +958,16 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
             else if (c.channels >= 1024) { mode = 3; d->pl_wform = 8; }
             break;
     }
+#ifndef HPA_AB
+    /* the full persistent layer (2) and the wide-unit chains (4) measured
+     * slower than the forms picked here: A/B builds only (hpa_build_flags) */
+    if (mode == 1 || (mode == 3 && d->pl_wform >= 2 && d->pl_wform <= 5)) return 0;
+#endif
     int splits = hpa_decode_layer_pick_splits(Bg, c.num_heads, d->max_ctx);
-    const char* env = getenv("HPA_LAYER_SPLITS");
+#ifdef HPA_AB
+    const char* env = getenv("HPA_LAYER_SPLITS"); /* the full persistent layer's attention ranges */
     if (env && atoi(env) > 0) splits = atoi(env);
+#endif
     if (mode >= 2) splits = 1; /* no attention phase: no split records */
     if (d->pl_wform >= 6 ? !hpa_decode_chain_eligible(d->B, c.channels, c.num_heads, d->pl_wform)
                          : !hpa_decode_layer_eligible(d->B, c.channels, c.num_heads, splits))
@@ -1402,16 +1409,20 @@ static void dec_gemm_desc(GPT2* model, int l, int which, HpaFusedGemm* g) {
     }
 }
 
-/* GPT-2 XL's qkv / fc: 1 (default) the ring kernel; HPA_GEMM_RING=0 the
- * looped kernel, =2 the ring with its K split over workgroups (A/B knobs; XL
- * step 10.31 / 10.41 / 10.43 ms) */
+/* GPT-2 XL's qkv / fc: 1 the ring kernel; in A/B builds HPA_GEMM_RING=0 the
+ * looped kernel, =2 the ring with its K split over workgroups (XL step
+ * 10.31 / 10.41 / 10.43 ms) */
 static int dec_ring_allowed(void) {
+#ifdef HPA_AB
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("HPA_GEMM_RING");
         v = e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
     }
     return v;
+#else
+    return 1;
+#endif
 }
 
 static int dec_gemm(GPT2* model, int l, int which) {

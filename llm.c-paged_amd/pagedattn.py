@@ -169,6 +169,7 @@ def lib():
     _sig(L, "hpa_stream_wait_event", i, [v])
     _sig(L, "hpa_event_synchronize", i, [v])
     _sig(L, "hpa_last_error", ctypes.c_char_p, [])
+    _sig(L, "hpa_build_flags", i, [])
     _sig(L, "hpa_device_info", i, [ctypes.c_char_p, i, _I, ctypes.POINTER(sz)])
     _sig(L, "hpa_set_attention_waves", i, [i])
     _sig(L, "hpa_attn_pick_waves", i, [i, i, i, i])
