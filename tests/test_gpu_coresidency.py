@@ -1,0 +1,83 @@
+"""Persistent launches beside a co-running kernel.
+
+The decode step's persistent launches (chain form 6, the bf16 chain, their
+first launches) put one workgroup on every CU and hand data between
+workgroups by spinning on counters, so they assume every workgroup becomes
+resident.  A concurrent kernel -- an RCCL collective of the bench's
+overlapped gather, another process's work -- can hold CUs; the persistent
+workgroups that do not fit then start only when it exits, and the resident
+ones wait for them (bounded: 200 ms per wait, after which the step reports a
+nonzero status instead of hanging).
+
+Forward progress therefore needs exactly this: the co-runner finishes on its
+own within the bound.  Here a helper kernel (tests/helpers/occupier.hip) holds
+whole CUs (1024 threads + 160 KiB LDS per workgroup, so no persistent
+workgroup can share them) for 5 ms on its own non-blocking stream, launched
+just before a decode step; the step must report status 0, give bit-identical
+logits and ids to the same step run alone, and the occupier must have
+finished.  Holding 16 / 64 CUs the persistent workgroups find room on the
+others (a CU takes two of them where registers allow: the step is < 1 ms
+slower); holding 200 of 256 they cannot all be resident, so the launch
+waits for the occupier -- the step takes the occupier's 5 ms (asserted > 3 ms)
+and still completes with status 0 and the same bits.
+"""
+import ctypes
+import os
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HELPER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "helpers", "libocc.so")
+GPT2_124M = dict(maxT=1024, V=50257, L=12, NH=12, C=768)
+
+
+def _occ():
+    if not os.path.exists(HELPER):
+        pytest.fail("tests/helpers/libocc.so missing: run __graft_entry__.build()")
+    lib = ctypes.CDLL(HELPER)
+    lib.occ_launch.argtypes = [ctypes.c_int, ctypes.c_longlong, ctypes.c_int, ctypes.c_void_p]
+    lib.occ_launch.restype = ctypes.c_int
+    lib.occ_sync.restype = ctypes.c_int
+    return lib
+
+
+@pytest.mark.parametrize("B,w_bf16,blocks", [(64, False, 16), (64, False, 200), (8, False, 64), (256, True, 16),
+                                             (256, True, 200)],
+                         ids=["form6_b64_16cu", "form6_b64_200cu", "form6_b8_64cu", "bf16chain_b256_16cu",
+                              "bf16chain_b256_200cu"])
+def test_persistent_step_beside_cu_holding_kernel(hip, B, w_bf16, blocks):
+    occ = _occ()
+    params = hip.synthetic_params(GPT2_124M, seed=70)
+    toks = np.random.default_rng(70).integers(0, GPT2_124M["V"], (3, B)).astype(np.int32)
+    done = hip.DeviceBuffer.from_array(np.zeros(1, np.int32))
+    runs = []
+    for co in (False, True):
+        m = hip.Model(GPT2_124M, params=params)
+        m.decode_init(B, 16 if not w_bf16 else 8, 320, w_dtype=hip.HPA_BF16 if w_bf16 else hip.HPA_F32)
+        assert m.layer_form() in (3, 4), m.layer_form()
+        m.set_graph(True)
+        m.fill_random(300, seed=7)
+        ids, lg, ms = [], [], []
+        for t in range(toks.shape[0]):
+            hip.check(hip.lib().hpa_synchronize(), "sync")
+            if co:  # 5 ms of whole CUs held on another stream, issued right before the step
+                assert occ.occ_launch(blocks, 500000, 160 * 1024, done.ptr) == 0
+            t0 = time.perf_counter()
+            ids.append(m.step(toks[t]))
+            lg.append(m.logits())
+            ms.append((time.perf_counter() - t0) * 1e3)
+            m.status()  # raises on a timed-out in-launch wait
+            assert occ.occ_sync() == 0
+        m.close()
+        runs.append((np.stack(ids), np.stack(lg), ms))
+    (i0, l0, ms0), (i1, l1, ms1) = runs
+    n_done = int(done.download(1, np.int32)[0])
+    print(f"B={B} {'bf16 chain' if w_bf16 else 'form 6'}: step ms alone {np.round(ms0, 2)}, beside {blocks} "
+          f"held CUs (5 ms) {np.round(ms1, 2)}; occupier workgroups finished {n_done}")
+    assert n_done == blocks * toks.shape[0]
+    assert np.array_equal(i0, i1) and np.array_equal(l0, l1)
+    if blocks >= 200:  # the launch could not be resident: it waited for the occupier, within the bound
+        assert min(ms1) > 3.0, ms1
