@@ -380,9 +380,7 @@ typedef struct {
                                      out at once when it is set) */
     int* err_sticky;              /* nullable: the first code also lands here, never zeroed by a
                                      step (gpt2_decode_status reads and clears it) */
-    int stats_mp;                 /* row stride of stats_out; 0: this launch's Mp.  A launch over a
-                                     slice of the batch's row blocks (the engine's two-lane step)
-                                     passes the batch's Mp and stats_out advanced to its first row */
+    int stats_mp;                 /* row stride of stats_out; 0: this launch's Mp */
 } HpaLayerArgs;
 /* 1 if the persistent layer applies (shape, CU count, residency), else 0 */
 int hpa_decode_layer_eligible(int B, int C, int num_heads, int splits);
