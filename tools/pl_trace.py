@@ -79,6 +79,21 @@ def main():
         md = np.mean([np.median(r) for r in rows[k]])
         mx = np.mean([r.max() for r in rows[k]])
         print(f"{name:14s} {n:4d} {mn:7.2f} {md:7.2f} {mx:7.2f}")
+    if len(sys.argv) > 5:  # "active N": also over workgroups 0..N-1 only (the units of a phase at one row block)
+        na = int(sys.argv[6]) if len(sys.argv) > 6 else 48
+        print(f"-- workgroups 0..{na - 1} only")
+        for k, name in enumerate(EVENTS):
+            vals = []
+            for layer in range(1, cfg["L"] - 1):
+                t = buf[layer].astype(np.int64)
+                t0 = t[:, 0][t[:, 0] > 0].min()
+                v = t[:na, k]
+                v = v[v > 0]
+                if len(v):
+                    vals.append((v - t0) / 100.0)
+            if vals:
+                print(f"{name:14s} {na:4d} {np.mean([r.min() for r in vals]):7.2f} "
+                      f"{np.mean([np.median(r) for r in vals]):7.2f} {np.mean([r.max() for r in vals]):7.2f}")
     m.close()
 
 
