@@ -891,6 +891,12 @@ static int dec_set_splits(GPT2Decode* d, int splits) {
         int ncu = 0;
         hpa_device_info(NULL, 0, &ncu, NULL);
         d->attn_waves = hpa_attn_pick_waves(dec_pick_B(d), d->pool.num_heads, splits, ncu);
+        /* bf16 pools with >= 8 (sequence, head, range) workgroups per CU: 8 waves (a workgroup
+         * moves half the bytes per tile; config 5: 3.287-3.291 vs 3.298-3.305 ms per step,
+         * paired runs, profiles/r5/experiments/c5_attention_waves.txt) */
+        if (d->pool.dtype == HPA_BF16 && ncu > 0 &&
+            (long)dec_pick_B(d) * d->pool.num_heads * splits >= 8L * ncu)
+            d->attn_waves = 8;
     }
     if (d->graph) { /* recapture with the new grid */
         hpa_synchronize();
