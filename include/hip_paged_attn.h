@@ -454,6 +454,10 @@ int hpa_decode_chain_b16_trace(unsigned long long* host, int layers);
  * workgroup) event stamps [layers][256][16] of the last launches (10 ns
  * ticks); host = NULL clears them */
 int hpa_decode_layer_trace(unsigned long long* host, int layers);
+/* diagnostic builds only, else returns 1: chain form 8's fc phase of layer 5,
+ * per wave ([256][12][16] u64 s_memtime: A loads issued, each half-tile's
+ * MFMAs issued, loop done); host = NULL clears them */
+int hpa_decode_cx_wave_trace(unsigned long long* host);
 /* diagnostic builds (-DHPA_RG_TRACE) only, else returns 1: the ring logits
  * kernel's per-workgroup stamps of the last launch: [2][256][24] u64, s_memrealtime
  * (10 ns ticks) then s_memtime (shader clock) */

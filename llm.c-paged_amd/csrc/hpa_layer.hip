@@ -115,6 +115,14 @@ struct KA {
 #define HPA_PL_QREG 1
 #endif
 __device__ unsigned long long g_pl_trace[64][256][16];
+// form 8's fc phase of one layer, per wave (s_memtime, shader clock): [0] A
+// loads issued, [1 + q] half-tile q's MFMAs issued, [15] loop done
+__device__ unsigned long long g_cx_wave[256][12][16];
+#define CX_WSTAMP(on, slot)                                                                              \
+    do {                                                                                                 \
+        if ((on) && (threadIdx.x & 63) == 0 && blockIdx.x < 256)                                         \
+            g_cx_wave[blockIdx.x][threadIdx.x >> 6][slot] = (unsigned long long)__builtin_amdgcn_s_memtime(); \
+    } while (0)
 #define PL_MARK(k)                                                                                     \
     do {                                                                                               \
         if (threadIdx.x == 0 && a.layer < 64 && blockIdx.x < 256)                                      \
@@ -136,6 +144,9 @@ __device__ unsigned long long g_pl_trace[64][256][16];
     } while (0)
 #define PL_STORE(k, var) \
     do {                 \
+    } while (0)
+#define CX_WSTAMP(on, slot) \
+    do {                    \
     } while (0)
 #endif
 
@@ -1407,7 +1418,8 @@ __device__ __forceinline__ void ld_tile0(const float* W, int K16W, int j, int kb
 template <int MAXS, bool STATS>
 __device__ __forceinline__ void unit_body(const float* A, int K16A, const float* W, int K16W, int rb, int kb, int j0,
                                           int ntl, int s0, int ns, bool nt, Tile0<MAXS>& t0, float* red,
-                                          float& fs1, float& fs2) {
+                                          float& fs1, float& fs2, bool wtrace = false) {
+    (void)wtrace;
     constexpr int HS = HalfT<MAXS>::HS;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -1419,6 +1431,7 @@ __device__ __forceinline__ void unit_body(const float* A, int K16A, const float*
 #if HPA_CX_SB
     __builtin_amdgcn_sched_barrier(0);  // every A load in flight before the first MFMA (see mfma_t)
 #endif
+    CX_WSTAMP(wtrace, 0);
     if (STATS)
 #pragma unroll
         for (int s = 0; s < MAXS; ++s)
@@ -1454,12 +1467,14 @@ __device__ __forceinline__ void unit_body(const float* A, int K16A, const float*
             chain_half<MAXS>(xv, w2, ns, h, acc);
         else
             chain_half<MAXS>(xv, w3, ns, h, acc);
+        CX_WSTAMP(wtrace, 1 + q);
         if (h == 1) {
 #pragma unroll
             for (int g = 0; g < 4; ++g) red[(w * XT_MAX + t) * 256 + g * 64 + lane] = acc[g];
             acc = f32x4{0.f, 0.f, 0.f, 0.f};
         }
     }
+    CX_WSTAMP(wtrace, 15);
 }
 
 // epilogue element of thread tid: tile et = tid / 64 of the unit, row er,
@@ -1553,7 +1568,8 @@ __global__ __launch_bounds__(768) void decode_chainx_kernel(KA args) {
         if (!waitx(a, c6::X1 + (has ? rb : 0), has ? n_b : 0, 2, sm)) return;
         PL_MARK(6);
         fs1 = fs2 = 0.f;
-        if (has) unit_body<MAXS, true>(a.res2, K16, a.w_fc, K16, rb, 0, j0, ntl, s0, ns, nt, t0w, sm.red, fs1, fs2);
+        if (has) unit_body<MAXS, true>(a.res2, K16, a.w_fc, K16, rb, 0, j0, ntl, s0, ns, nt, t0w, sm.red, fs1, fs2,
+                                       a.layer == 5);
         hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + w * 32);
         lds_barrier();
         if (ep) {
@@ -1982,6 +1998,23 @@ int hpa_decode_layer_sizes(int B, int C, int num_heads, int splits, size_t* out3
     const size_t ints = ints5 > ints6 ? ints5 : ints6;
     out3[2] = (ints + 31) / 32 * 32;  // whole 128-B lines (memset in multiples of 16 B)
     return 0;
+}
+
+// trace build only: form 8's per-wave fc stamps of layer 5 ([256][12][16] u64,
+// s_memtime); host NULL clears them.  Returns 1 in the product build.
+int hpa_decode_cx_wave_trace(unsigned long long* host) {
+#ifdef HPA_LAYER_TRACE
+    if (!host) {
+        static unsigned long long zero[256 * 12 * 16];
+        HPA_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_cx_wave), zero, sizeof(zero)));
+        return 0;
+    }
+    HPA_CHECK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_cx_wave), sizeof(unsigned long long) * 256 * 12 * 16));
+    return 0;
+#else
+    (void)host;
+    return 1;
+#endif
 }
 
 // trace build only: copy the per-(layer, workgroup) event stamps of the last

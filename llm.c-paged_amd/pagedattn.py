@@ -268,6 +268,7 @@ def lib():
     _sig(L, "hpa_decode_layer_pick_splits", i, [i, i, i])
     _sig(L, "hpa_decode_layer_trace", i, [v, i])
     _sig(L, "hpa_decode_chain_b16_trace", i, [v, i])
+    _sig(L, "hpa_decode_cx_wave_trace", i, [v])
     _sig(L, "hpa_logits_trace", i, [v])
     _sig(L, "gpt2_decode_evicted", i, [v, _I])
     _sig(L, "gpt2_decode_read_kv", i, [v, i, i, i, _F, _F])
