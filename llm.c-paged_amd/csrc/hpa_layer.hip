@@ -978,11 +978,25 @@ __device__ __forceinline__ void publish6(const KA& a, int ctr, bool did) {
     if (threadIdx.x == 0 && did) arrive6(a, ctr, 1);
 }
 
+// the K / V destination of a qkv epilogue lane, resolved while the unit's
+// weights stream and before its wait: the token's position, then its page
+// (two dependent loads; issued behind the MFMAs they were the epilogue's
+// tail).  qkv_pos6 goes before the weight loads (vmcnt retires in order),
+// qkv_page6 after them.
+__device__ __forceinline__ int qkv_pos6(const KA& a, bool ep, int row, int col) {
+    return ep && row < a.B && col >= 768 ? a.pos[row] : 0;
+}
+template <int P>
+__device__ __forceinline__ int qkv_page6(const KA& a, bool ep, int row, int col, int ps) {
+    return ep && row < a.B && col >= 768 ? a.bt[(size_t)row * a.bt_stride + ps / P] : -1;
+}
+
 // qkv epilogue store of 4 columns col..col+3 of `row` (NH = 12): q row-major,
-// or K / V of this token into the sequence's page of the layer at kv_next
-// (add_to_cache, paged_infer.c:505-573)
+// or K / V of this token (position ps, page `page` from qkv_pos6 / qkv_page6)
+// into the sequence's page of the layer at kv_next (add_to_cache,
+// paged_infer.c:505-573)
 template <int P, bool BF>
-__device__ __forceinline__ void qkv_store6(const KA& a, int row, int col, float4 v) {
+__device__ __forceinline__ void qkv_store6(const KA& a, int row, int col, int ps, int page, float4 v) {
     constexpr int NH = 12, C = 768;
     if (col < C) {
         *reinterpret_cast<float4*>(a.q_out + (size_t)row * C + col) = v;
@@ -991,8 +1005,6 @@ __device__ __forceinline__ void qkv_store6(const KA& a, int row, int col, float4
     const int kv = col >= 2 * C;
     const int c = col - (kv ? 2 * C : C);
     const int hh = c >> 6, d = c & 63;
-    const int ps = a.pos[row];
-    const int page = a.bt[(size_t)row * a.bt_stride + ps / P];
     if (page < 0) return;
     const int pslot = ps % P;
     const size_t toff = (size_t)page * a.page_elems + ((size_t)kv * NH + hh) * P * 64;
@@ -1217,6 +1229,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         const int g = bid % NG, rb = bid / NG;
         const bool ep = has && tid < T * 64;
         const int row = rb * 16 + er, col = (g * T + et) * 16 + 4 * eq;
+        const int kps = qkv_pos6(a, ep, row, col);
         float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f), c2 = c1;
         if (ep) {
             c1 = ld4(a.qkv_c1 + col);
@@ -1224,6 +1237,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         }
         float4 wr[T][SPW];
         if (has) load_wt<T, NT>(a.w_qkv, K16, g * T, 0, w, wr);
+        const int kpage = qkv_page6<P>(a, ep, row, col, kps);
         if (GE) {
             if (has && !wait_grp(a, kCtr + 4 * NCT + kGE + rb * NW * kPad, 4, 4, sm)) return;
         } else if (!wait6(a, X2 + (has ? rb : 0), has ? NCT / TD : 0, 4, sm)) {
@@ -1240,7 +1254,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         lds_barrier();
         PL_MARK(15);
         if (ep && row < a.B)
-            qkv_store6<P, BF>(a, row, col, ln_fold4(sm.wsum, er, fold_t<T>(sm.red, et, er, eq), c1, c2));
+            qkv_store6<P, BF>(a, row, col, kps, kpage, ln_fold4(sm.wsum, er, fold_t<T>(sm.red, et, er, eq), c1, c2));
     }
     PL_MARK(11);
 }
@@ -1280,6 +1294,7 @@ __global__ __launch_bounds__(768) void decode_first6_kernel(KA args) {
     const int et = tid >> 6, er = (tid & 63) >> 2, eq = tid & 3;
     const bool ep = tid < T * 64;
     const int row = rb * 16 + er, col = (g * T + et) * 16 + 4 * eq;
+    const int kps = qkv_pos6(a, ep, row, col);
     float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f), c2 = c1;
     if (ep) {
         c1 = ld4(a.qkv_c1 + col);
@@ -1287,6 +1302,7 @@ __global__ __launch_bounds__(768) void decode_first6_kernel(KA args) {
     }
     float4 wr[T][SPW];
     load_wt<T, NT>(a.w_qkv, K16, g * T, 0, w, wr);
+    const int kpage = qkv_page6<P>(a, ep, row, col, kps);
     // A fragment of k16 step 4w + s: lane holds row 16 rb + (lane & 15),
     // columns 16 (4w + s) + 4 (lane >> 4) .. + 3 (hpa::frag_index)
     const float4* te = reinterpret_cast<const float4*>(a.wte + (size_t)tok * C) + (lane >> 4);
@@ -1308,7 +1324,7 @@ __global__ __launch_bounds__(768) void decode_first6_kernel(KA args) {
     hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + w * 32);
     lds_barrier();
     if (ep && row < a.B)
-        qkv_store6<P, BF>(a, row, col, ln_fold4(sm.wsum, er, fold_t<T>(sm.red, et, er, eq), c1, c2));
+        qkv_store6<P, BF>(a, row, col, kps, kpage, ln_fold4(sm.wsum, er, fold_t<T>(sm.red, et, er, eq), c1, c2));
 }
 
 // ------------------------------------------------------------------ the chain for wide layers (form 8)
