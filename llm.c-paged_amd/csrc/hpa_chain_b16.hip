@@ -382,11 +382,12 @@ __device__ __forceinline__ void where(int e, int rb0, int j0, int& row, int& col
 }
 
 // qkv epilogue store of columns col..col+3 of `row`: q row-major, or K / V of
-// this token into the sequence's page of layer l+1 (add_to_cache,
-// paged_infer.c:505-573; fp32 pool K [chunk of 4][slot][4], bf16 pool K
-// [chunk of 8][slot][8] RNE, V [slot][64])
+// this token (position ps, page `page`, loaded by phase E before its wait)
+// into the sequence's page of layer l+1 (add_to_cache, paged_infer.c:505-573;
+// fp32 pool K [chunk of 4][slot][4], bf16 pool K [chunk of 8][slot][8] RNE,
+// V [slot][64])
 template <int P, bool BF>
-__device__ __forceinline__ void qkv_store(const Args& a, int row, int col, float4 v) {
+__device__ __forceinline__ void qkv_store(const Args& a, int row, int col, int ps, int page, float4 v) {
     constexpr int NH = 12;
     if (col < C) {
         *reinterpret_cast<float4*>(a.q_out + (size_t)row * C + col) = v;
@@ -395,8 +396,6 @@ __device__ __forceinline__ void qkv_store(const Args& a, int row, int col, float
     const int kv = col >= 2 * C;
     const int c = col - (kv ? 2 * C : C);
     const int hh = c >> 6, d = c & 63;
-    const int ps = a.pos[row];
-    const int page = a.bt[(size_t)row * a.bt_stride + ps / P];
     if (page < 0) return;  // no page (host bug): never write below the pool
     const int pslot = ps % P;
     const size_t toff = (size_t)page * a.page_elems + ((size_t)kv * NH + hh) * P * 64;
@@ -616,7 +615,19 @@ __global__ __launch_bounds__(512) void decode_chain_b16_kernel(cb::Args args) {
         const int g = bid % NG_E, rb = bid / NG_E;
         uint4 wr[T][SPW];
         float4 bv[2];
+        int kps[2], kpage[2];  // K/V destination (position, page), resolved while the weights stream
+        auto kv_lane = [&](int i, int& row) __attribute__((always_inline)) {
+            const int e = tid + i * NT;
+            int col;
+            where<T>(e, rb, g * T, row, col);
+            return has && e < NE && row < a.B && col >= C && col < 3 * C;
+        };
         auto pre = [&]() {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {  // positions ahead of the weights (vmcnt retires in order)
+                int row;
+                kps[i] = kv_lane(i, row) ? a.pos[row] : 0;
+            }
             if (has) load_w<T>(a.w_qkv, K32, g * T, 0, w, wr, NJ - 1);
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
@@ -624,6 +635,11 @@ __global__ __launch_bounds__(512) void decode_chain_b16_kernel(cb::Args args) {
                 int row, col;
                 where<T>(e, rb, g * T, row, col);
                 bv[i] = has && e < NE && col < 3 * C ? ld4(a.b_qkv + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                int row;
+                kpage[i] = kv_lane(i, row) ? a.bt[(size_t)row * a.bt_stride + kps[i] / P] : -1;
             }
         };
         pre();
@@ -641,7 +657,7 @@ __global__ __launch_bounds__(512) void decode_chain_b16_kernel(cb::Args args) {
             int row, col;
             where<T>(e, rb, g * T, row, col);
             if (has && e < NE && row < a.B && col < 3 * C)
-                qkv_store<P, BF>(a, row, col, add4(fold<RG, T>(sm.red, e), bv[i]));
+                qkv_store<P, BF>(a, row, col, kps[i], kpage[i], add4(fold<RG, T>(sm.red, e), bv[i]));
         }
         CB_MARK(15);
     }

@@ -1673,14 +1673,17 @@ __global__ __launch_bounds__(768) void decode_chainx_kernel(KA args) {
         const int g = bid % NG, rb = bid / NG, j0 = g * T;
         const bool has = rb < R && j0 < NJ;
         const int ntl = has ? min(T, NJ - j0) : 0;
-        if (has) cx::ld_tile0<MAXS>(a.w_qkv, K16, j0, 0, s0, ns, nt, t0w);
         const bool ep = tid < ntl * 64;
         const int row = rb * 16 + er, col = (j0 + et) * 16 + 4 * eq;
+        // the K/V destination while the weights stream (as c6::qkv_pos6 / qkv_page6)
+        const int kps = ep && row < a.B && col >= C ? a.pos[row] : 0;
+        if (has) cx::ld_tile0<MAXS>(a.w_qkv, K16, j0, 0, s0, ns, nt, t0w);
         float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f), c2 = c1;
         if (ep) {
             c1 = c6::ld4(a.qkv_c1 + col);
             c2 = c6::ld4(a.qkv_c2 + col);
         }
+        const int kpage = ep && row < a.B && col >= C ? a.bt[(size_t)row * a.bt_stride + kps / P] : -1;
         const int n_d = (NCT + a.xt[2] - 1) / a.xt[2];  // fcproj tile groups of a row block
         if (!waitx(a, c6::X2 + (has ? rb : 0), has ? n_d : 0, 4, sm)) return;
         PL_MARK(10);
@@ -1696,11 +1699,9 @@ __global__ __launch_bounds__(768) void decode_chainx_kernel(KA args) {
                 const int kv = col >= 2 * C;
                 const int c = col - (kv ? 2 * C : C);
                 const int hh = c >> 6, d = c & 63;
-                const int ps = a.pos[row];
-                const int page = a.bt[(size_t)row * a.bt_stride + ps / P];
-                if (page >= 0) {
-                    const int pslot = ps % P;
-                    const size_t toff = (size_t)page * a.page_elems + ((size_t)kv * NH + hh) * P * 64;
+                if (kpage >= 0) {
+                    const int pslot = kps % P;
+                    const size_t toff = (size_t)kpage * a.page_elems + ((size_t)kv * NH + hh) * P * 64;
                     if constexpr (BF) {
                         unsigned short* kvt = reinterpret_cast<unsigned short*>(a.kv_next) + toff +
                                               (kv == 0 ? ((d >> 3) * P + pslot) * 8 + (d & 7) : pslot * 64 + d);
