@@ -152,13 +152,16 @@ def parse():
     ap.add_argument("--attn-waves", type=int, default=0,
                     help="waves per attention workgroup for every launch (0 = the engine's pick by batch)")
     ap.add_argument("--attn-splits", type=int, default=0, help="attention context ranges (0 = by shape)")
-    ap.add_argument("--layer-kernel", type=int, default=-1, choices=[-1, 0, 1, 2, 3, 4, 5, 6],
+    ap.add_argument("--layer-kernel", type=int, default=-1, choices=[-1, 0, 1, 2, 3, 4, 5, 6, 7],
                     help="gpt2_decode_set_layer_kernel: 0 five launches per layer; 1 auto (the form measured "
                          "fastest for the batch: chain form 6 at C = 768, form 8 at C >= 1024, the bf16 chain "
                          "on bf16 weights); 3 the attention launch + the chain (4-wave units); 5 chain form 6 "
                          "(12-wave multi-tile units); 6 chain form 8 (streamed weights, also GPT-2 XL); 2 the "
-                         "full persistent layer and 4 the wide-unit chain: A/B builds (-DHPA_AB) only; "
+                         "full persistent layer and 4 the wide-unit chain: A/B builds (-DHPA_AB) only; 7 the "
+                         "pipelined halves (one launch for every layer, attention and GEMM chain on disjoint CUs); "
                          "-1 the engine's default (HPA_LAYER_KERNEL or 1)")
+    ap.add_argument("--pipe-g", type=int, default=0,
+                    help="CUs of the pipelined halves' GEMM role (form 7; multiple of 8; 0 = the default 64)")
     ap.add_argument("--picks", default="local", choices=["local", "global"],
                     help="N>1 / --emulate-rank: shape picks by the rank's own batch (default: a rank computes "
                          "what a single-GPU engine of its rows computes) or by the global batch "
@@ -300,6 +303,8 @@ def main():
         model.set_global_batch(B)  # every row as the unsharded engine of B computes it
     if args.layer_kernel >= 0:
         model.set_layer_kernel(args.layer_kernel)
+    if args.pipe_g:
+        model.set_pipe_split(args.pipe_g)
     if args.sample:
         model.set_sampling(True, seed=1337 + lo)
     if args.gemm_waves or args.gemm_rows or args.gemm_cols:
@@ -355,6 +360,17 @@ def main():
             print(f"[bench] rank {rank}: {e} after the {where}; no value reported", file=sys.stderr, flush=True)
             sys.exit(5)
 
+    # under rocprofv3 the spin-up launches its steps eagerly: the profiler's
+    # hipGraphLaunch path faults after a few hundred to a few thousand graph
+    # replays (SIGSEGV inside the tool library, reproduced with no part of this
+    # library loaded by tools/micro/graph_replay.hip), and
+    # the 2 s spin-up replays ~1,800 step graphs.  Eager steps keep the GPU as
+    # busy (the step is ~40 launches of ~1 ms of kernels); the warm-up and
+    # timed steps stay graph replays.
+    profiled = any(k.startswith("ROCPROF") for k in os.environ)
+    spin_eager = args.spinup > 0 and profiled and not args.no_graph
+    if spin_eager:
+        model.set_graph(False)
     if args.spinup > 0:  # untimed, before the warm-up; the positions go back to `start` after it
         # local steps only (no gather: ranks may run different counts in the
         # same time, and a collective must be called by every rank alike)
@@ -371,6 +387,8 @@ def main():
             sync()
         model.set_positions(np.full(B_local, start, np.int32))
         sync()
+    if spin_eager:
+        model.set_graph(True)
     one_step(first)
     for _ in range(args.warmup - 1 if args.warmup > 0 else 0):
         one_step(None)
@@ -449,6 +467,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "spinup_s": args.spinup,
+            "spinup_eager": spin_eager,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": args.scaling,
@@ -478,7 +497,10 @@ def main():
                                          "wide / multi-tile units (hpa_decode_layer chain_only 2..6, 8: "
                                          "by default form 6 at C = 768, form 8 at C >= 1024)",
                                       4: "attention launch + one persistent launch of the bf16-weight GEMM "
-                                         "chain (hpa_decode_chain_b16)"}[model.layer_form()],
+                                         "chain (hpa_decode_chain_b16)",
+                                      5: "one persistent launch of every layer: the batch in two halves, "
+                                         "attention of one beside the GEMM chain of the other on disjoint CUs "
+                                         "(hpa_decode_pipe)"}[model.layer_form()],
                        "attn_form": f"(sequence, head) x {splits} range(s)",
                        "token_choice": "multinomial (reference sample_mult)" if args.sample else "greedy",
                        "gemm_waves": [int(x) for x in model.gemm_config()[0]],

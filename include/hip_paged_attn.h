@@ -402,6 +402,56 @@ int hpa_decode_layer(const HpaLayerArgs* a);
  * qkv_c2, q_out; the layer fields are ignored. */
 int hpa_decode_first(const HpaLayerArgs* a, const int* tokens, const float* wte, const float* wpe, void* zero,
                      size_t zero_bytes);
+/* ---------------- pipelined halves (hpa_pipe.hip) ----------------
+ * The whole layer loop of a decode step (gpt2_forward, paged_infer.c:659-722,
+ * every layer l = 0..L-1: attention(l) -> attproj(l) -> fc(l) -> fcproj(l) ->
+ * qkv(l+1)) as ONE persistent launch, after the step's first launch
+ * (hpa_decode_first: embedding, qkv(0), the counter block zeroed) and before
+ * the logits.  The batch is cut into two halves of row blocks; the CUs take
+ * fixed roles: `g_cus` CUs run the GEMM chain of one half while the others
+ * stream the paged attention of the other half (software pipeline, slot s:
+ * attention(s/2, s%2) beside chain((s-1)/2, (s-1)%2)).  The attention is
+ * paged_attn_decode_f32's (4 waves per (sequence, head), one context range)
+ * and the chain units are chain form 6's (12 waves over K), so a step equals
+ * the chain-form step bit for bit.  GPT-2 124M shapes: C = 768, 12 heads,
+ * fp32 weights (LN-folded frag packs) and an fp32 pool, 17..64 rows with both
+ * halves non-empty.  Bounded spins, error words as hpa_decode_layer. */
+typedef struct {
+    const float *w_ap, *b_ap;                 /* layer l: attprojw (frag), attprojb */
+    const float *w_fc, *fc_c1, *fc_c2;        /* LN2-folded fcw (frag), c1, c2 */
+    const float *w_fp, *b_fp;                 /* fcprojw (frag), fcprojb */
+    const float *w_qkv, *qkv_c1, *qkv_c2;     /* layer l+1's LN1-folded qkvw (NULL at the last layer) */
+} HpaPipeLayer;
+typedef struct {
+    int B, num_layers;
+    const HpaKVPool* pool;        /* fp32 pages; layer l+1's K/V appended by qkv(l+1) */
+    const int* block_table;
+    int bt_stride;
+    const int* pos;
+    const HpaPipeLayer* layers;   /* DEVICE array [num_layers] */
+    float* q;                     /* q [B][C] row-major: layer 0's from the first launch, rewritten per layer */
+    float* att;                   /* frag [Mp][C] */
+    float* res;                   /* residual (frag [Mp][C]): the embedding in, the last layer's out */
+    float* res2;                  /* frag [Mp][C] */
+    float* fch;                   /* frag [Mp][4C] */
+    float* slab;                  /* fcproj K-part partials: hpa_decode_pipe_sizes out[0] floats */
+    float* stats_out;             /* LNf statistics of the last layer's res [C/16][stats_mp][2] */
+    int stats_mp;
+    int* counters;                /* [num_layers][layer_ctr_ints], zero before the launch */
+    size_t layer_ctr_ints;        /* >= hpa_decode_pipe_sizes out[1] */
+    int* err;                     /* as HpaLayerArgs.err / err_sticky */
+    int* err_sticky;
+    int g_cus;                    /* CUs of the GEMM role (multiple of 8; 0: 64) */
+} HpaPipeArgs;
+/* 1 if the pipelined-halves launch applies to B rows (C, heads, pool dtype, CU count) */
+int hpa_decode_pipe_eligible(int B, int C, int num_heads, int kv_dtype);
+/* out2 = {slab floats, counter ints per layer} */
+int hpa_decode_pipe_sizes(int B, size_t* out2);
+int hpa_decode_pipe(const HpaPipeArgs* a);
+/* diagnostic builds (-DHPA_PIPE_TRACE) only: the per-(layer, half, workgroup)
+ * event stamps of the last launch, [2 * layers][256][12] u64 (10-ns ticks);
+ * host NULL clears them; returns 1 in the product library */
+int hpa_decode_pipe_trace(unsigned long long* host, int layers);
 /* ---------------- bf16-weight decode chain (hpa_chain_b16.hip) ----------------
  * The layer's GEMMs on bf16 weights (BASELINE config 5) as ONE persistent
  * launch after the layer's decode-attention launch:

@@ -222,9 +222,17 @@ int  gpt2_decode_attn_waves(GPT2* model);
  * workgroups: a GPU shared with another process's persistent kernels should
  * use 0. */
 int  gpt2_decode_set_layer_kernel(GPT2* model, int enable);
+/* 7: the pipelined halves (hpa_decode_pipe, hpa_pipe.hip): the step's first
+ * launch, ONE persistent launch of every layer with the batch in two halves
+ * (the GEMM chain of one half on g_cus CUs beside the attention of the other
+ * on the rest), the logits; bit-identical to form 5.  GPT-2 124M shapes, fp32
+ * weights and pool, 17..64 rows (else form 5).  Traced steps run form 5. */
+/* CUs of the pipelined halves' GEMM role (multiple of 8; 0: the default, 64) */
+int  gpt2_decode_set_pipe_split(GPT2* model, int g_cus);
 /* the form in use: 0 five launches, 1 full persistent layer, 2 attention
  * launch + persistent chain of 4-wave units, 3 the chain in wide / multi-tile
- * units (forms 4..6 of gpt2_decode_set_layer_kernel) */
+ * units (forms 4..6 of gpt2_decode_set_layer_kernel), 4 the bf16-weight
+ * chain, 5 the pipelined halves (form 7) */
 int  gpt2_decode_layer_kernel(GPT2* model);
 /* waits for the queued work; 0, or the code of a timed-out in-launch wait of
  * the persistent layer (the step's outputs are then invalid), which it clears */

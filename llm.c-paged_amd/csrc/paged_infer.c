@@ -674,6 +674,12 @@ struct GPT2Decode {
     int* pl_ctr;      /* the step's error word (DEC_ERR_INTS), then [L][pl_ctr_ints]; zeroed at the start of
                          every step */
     size_t pl_ctr_ints;
+    /* pipelined halves (hpa_decode_pipe, pl_on 5): the per-layer operand
+     * table on the device, the fcproj partials, the GEMM role's CUs */
+    HpaPipeLayer* d_pipe_lay;
+    float* pipe_slab;
+    size_t pipe_slab_n;
+    int pipe_g;
     /* gpt2_forward: token at every cached position [B][max_ctx] and, when it
      * fits, the logits of every position [B][max_ctx][V] (managed) */
     int* h_hist;
@@ -782,6 +788,7 @@ static void dec_free(GPT2Decode* d) {
     hpa_free(d->d_fold);
     hpa_free(d->d_attn_ws);
     hpa_free(d->pl_rec); hpa_free(d->pl_slab); hpa_free(d->pl_ctr);
+    hpa_free(d->d_pipe_lay); hpa_free(d->pipe_slab);
     hpa_free(d->d_rng);
     hpa_free(d->pos_logits);
     hpa_host_free(d->h_next);
@@ -930,6 +937,53 @@ static int dec_chain_b16_setup(GPT2* model, GPT2Decode* d) {
     return 0;
 }
 
+/* the pipelined halves (pl_on 5) where hpa_decode_pipe applies: the
+ * per-layer operand table (the pointers dec_layer hands chain form 6), the
+ * fcproj partials, and counter blocks of at least its size */
+static int dec_pipe_setup(GPT2* model, GPT2Decode* d) {
+    const GPT2Config c = model->config;
+    const ParameterTensors* w = &model->params;
+    const int C = c.channels, L = c.num_layers;
+    if (!hpa_decode_pipe_eligible(d->B, C, c.num_heads, d->pool.dtype)) return 0; /* form 6 stays */
+    size_t sz[2];
+    if (hpa_decode_pipe_sizes(d->B, sz)) return 1;
+    if (!d->pipe_slab || d->pipe_slab_n < sz[0]) {
+        hpa_free(d->pipe_slab);
+        d->pipe_slab_n = sz[0];
+        d->pipe_slab = (float*)hpa_malloc(sz[0] * sizeof(float));
+    }
+    if (d->pl_ctr_ints < sz[1]) {
+        hpa_free(d->pl_ctr);
+        d->pl_ctr_ints = sz[1];
+        d->pl_ctr = (int*)hpa_malloc((DEC_ERR_INTS + (size_t)L * sz[1]) * sizeof(int));
+    }
+    if (!d->pipe_slab || !d->pl_ctr) return 1;
+    HpaPipeLayer* h = (HpaPipeLayer*)calloc((size_t)L, sizeof(HpaPipeLayer));
+    if (!h) return 1;
+    const size_t e_layer = d->wpack_off[3] + hpa_frag_elems(C, 4 * C);
+    for (int l = 0; l < L; l++) {
+        const size_t lc = (size_t)l * C;
+        h[l].w_ap = wpack_at(d, e_layer * l + d->wpack_off[1]);
+        h[l].b_ap = w->attprojb + lc;
+        h[l].w_fc = wpack_at(d, e_layer * l + d->wpack_off[2]);
+        h[l].fc_c1 = d->d_fold + 14 * lc + 6 * C;
+        h[l].fc_c2 = h[l].fc_c1 + 4 * C;
+        h[l].w_fp = wpack_at(d, e_layer * l + d->wpack_off[3]);
+        h[l].b_fp = w->fcprojb + lc;
+        if (l + 1 < L) {
+            h[l].w_qkv = wpack_at(d, e_layer * (l + 1) + d->wpack_off[0]);
+            h[l].qkv_c1 = d->d_fold + 14 * (lc + C);
+            h[l].qkv_c2 = h[l].qkv_c1 + 3 * C;
+        }
+    }
+    if (!d->d_pipe_lay) d->d_pipe_lay = (HpaPipeLayer*)hpa_malloc((size_t)L * sizeof(HpaPipeLayer));
+    const int rc = !d->d_pipe_lay || hpa_memcpy(d->d_pipe_lay, h, (size_t)L * sizeof(HpaPipeLayer));
+    free(h);
+    if (rc) return 1;
+    d->pl_on = 5;
+    return 0;
+}
+
 static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
     const GPT2Config c = model->config;
     d->pl_on = 0;
@@ -959,6 +1013,9 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
             if (c.num_heads == 12) { mode = 3; d->pl_wform = 6; }
             break;
         case 6: mode = 3; d->pl_wform = 8; break; /* form 8: streamed-weight units (C = 768, 1600) */
+        case 7: /* the pipelined halves over chain form 6's units (form 6 where it does not apply) */
+            if (c.num_heads == 12) { mode = 3; d->pl_wform = 6; }
+            break;
         default: /* auto */
             if (c.num_heads == 12) { mode = 3; d->pl_wform = 6; }
             else if (c.channels >= 1024) { mode = 3; d->pl_wform = 8; }
@@ -995,6 +1052,7 @@ static int dec_layer_setup(GPT2* model, GPT2Decode* d) {
     if (!d->pl_rec || !d->pl_slab || !d->pl_ctr) return 1;
     d->pl_splits = splits;
     d->pl_on = mode;
+    if (d->pl_want == 7 && mode == 3 && d->pl_wform == 6) return dec_pipe_setup(model, d);
     return 0;
 }
 
@@ -1059,7 +1117,7 @@ static int dec_layer(GPT2* model, int l) {
     a.num_heads = c.num_heads;
     a.splits = d->pl_splits;
     a.last = l + 1 == L;
-    a.chain_only = d->pl_on == 3 ? d->pl_wform : d->pl_on == 2;
+    a.chain_only = d->pl_on == 3 || d->pl_on == 5 ? d->pl_wform : d->pl_on == 2;
     a.pool = &d->pool;
     a.layer = l;
     a.block_table = d->d_bt;
@@ -1259,7 +1317,7 @@ int gpt2_decode_init_w(GPT2* model, int B, int page_size, int max_ctx, int kv_dt
     }
     {
         const char* env = getenv("HPA_LAYER_KERNEL");
-        d->pl_want = env && env[0] >= '0' && env[0] <= '6' ? env[0] - '0' : 1;
+        d->pl_want = env && env[0] >= '0' && env[0] <= '7' ? env[0] - '0' : 1;
     }
     if (dec_layer_setup(model, d)) {
         dec_free(d);
@@ -1538,6 +1596,34 @@ static int dec_first_b16(GPT2* model, size_t zb) {
     return hpa_decode_chain_b16_first(&a, d->d_tokens, w->wte, w->wpe, d->pl_ctr, zb);
 }
 
+/* every layer of the step as the pipelined halves' one launch (pl_on 5) */
+static int dec_pipe(GPT2* model) {
+    GPT2Decode* d = model->decode;
+    HpaPipeArgs a;
+    memset(&a, 0, sizeof(a));
+    a.B = d->B;
+    a.num_layers = model->config.num_layers;
+    a.pool = &d->pool;
+    a.block_table = d->d_bt;
+    a.bt_stride = d->bt_stride;
+    a.pos = d->d_pos;
+    a.layers = d->d_pipe_lay;
+    a.q = d->d_q;
+    a.att = d->att;
+    a.res = d->res;
+    a.res2 = d->res2;
+    a.fch = d->fch;
+    a.slab = d->pipe_slab;
+    a.stats_out = d->st1; /* LNf statistics for the logits */
+    a.stats_mp = d->Mp;
+    a.counters = d->pl_ctr + DEC_ERR_INTS;
+    a.layer_ctr_ints = d->pl_ctr_ints;
+    a.err = d->pl_ctr;
+    a.err_sticky = d->d_next + d->B;
+    a.g_cus = d->pipe_g;
+    return hpa_decode_pipe(&a);
+}
+
 /* the whole step on the library stream */
 static int dec_launch(GPT2* model) {
     GPT2Decode* d = model->decode;
@@ -1549,7 +1635,7 @@ static int dec_launch(GPT2* model) {
     const size_t zb = (DEC_ERR_INTS + (size_t)L * d->pl_ctr_ints) * sizeof(int);
     /* chain form 6 (and form 8 at C = 768, which sums as form 6): embed +
      * qkv(0) + the counter zeroing in one launch */
-    const int first = pl && DEC_FIRST_LAUNCH && ((d->pl_on == 3 &&
+    const int first = pl && DEC_FIRST_LAUNCH && (((d->pl_on == 3 || d->pl_on == 5) &&
                       (d->pl_wform == 6 || (d->pl_wform == 8 && model->config.num_heads == 12))) || d->pl_on == 4);
     int rc = first ? (d->pl_on == 4 ? dec_first_b16(model, zb) : dec_first(model, zb))
            : !pl   ? hpa_embed_frag(d->d_tokens, d->d_pos, w->wte, w->wpe, d->res, d->st1, d->B, C)
@@ -1557,6 +1643,12 @@ static int dec_launch(GPT2* model) {
 #define DEC_TRACE(i) \
     if (d->trace_x) rc |= hpa_unpack_frag(d->res, d->B, C, d->trace_x + (size_t)(i) * d->B * C, C)
     DEC_TRACE(0);
+    if (pl && d->pl_on == 5 && first && !d->trace_x) { /* the pipelined halves: every layer in one launch */
+        rc |= dec_pipe(model);
+        rc |= dec_gemm(model, 0, G_LOGITS);
+        rc |= dec_pick(model, NULL);
+        return rc;
+    }
     if (pl) { /* qkv(0), then one persistent launch per layer */
         if (!first) rc |= dec_gemm(model, 0, G_QKV);
         for (int l = 0; l < L && !rc; l++) {
@@ -1949,7 +2041,7 @@ int gpt2_decode_set_layer_kernel(GPT2* model, int enable) {
     GPT2Decode* d = model->decode;
     if (!d) return 1;
     if (hpa_synchronize()) return 1;
-    d->pl_want = enable < 0 ? 0 : enable > 6 ? 6 : enable;
+    d->pl_want = enable < 0 ? 0 : enable > 7 ? 7 : enable;
     if (dec_layer_setup(model, d)) return 1;
     if (d->graph) { /* recapture with the other step */
         hpa_graph_destroy(d->graph);
@@ -1960,6 +2052,19 @@ int gpt2_decode_set_layer_kernel(GPT2* model, int enable) {
 }
 
 int gpt2_decode_layer_kernel(GPT2* model) { return model->decode ? model->decode->pl_on : 0; }
+
+int gpt2_decode_set_pipe_split(GPT2* model, int g_cus) {
+    GPT2Decode* d = model->decode;
+    if (!d || g_cus < 0 || g_cus % 8) return 1;
+    if (hpa_synchronize()) return 1;
+    d->pipe_g = g_cus;
+    if (d->graph) { /* recapture with the other split */
+        hpa_graph_destroy(d->graph);
+        d->graph = NULL;
+        if (dec_rezero(d)) return 1;
+    }
+    return 0;
+}
 
 
 /* sequences the LRU policy paged out since the last call (their position

@@ -263,6 +263,8 @@ def lib():
     _sig(L, "hpa_pool_fill_random_ex", i, [P, v, i, i, i, ctypes.c_uint64, i])
     _sig(L, "hpa_logits_kernel", i, [i, i, i])
     _sig(L, "gpt2_decode_layer_kernel", i, [v])
+    _sig(L, "gpt2_decode_set_pipe_split", i, [v, i])
+    _sig(L, "hpa_decode_pipe_eligible", i, [i, i, i, i])
     _sig(L, "gpt2_decode_status", i, [v])
     _sig(L, "hpa_decode_layer_eligible", i, [i, i, i, i])
     _sig(L, "hpa_decode_layer_pick_splits", i, [i, i, i])
@@ -657,9 +659,14 @@ class Model:
     def layer_kernel(self):
         return bool(lib().gpt2_decode_layer_kernel(self.h))
 
+    def set_pipe_split(self, g_cus):
+        """CUs of the pipelined halves' GEMM role (form 7; multiple of 8, 0 = 64)"""
+        check(lib().gpt2_decode_set_pipe_split(self.h, int(g_cus)), "set_pipe_split")
+
     def layer_form(self):
         """0 five launches per layer, 1 full persistent layer, 2 attention launch + persistent chain,
-        3 the chain with wide units, 4 the bf16-weight chain (hpa_chain_b16.hip)"""
+        3 the chain with wide units, 4 the bf16-weight chain (hpa_chain_b16.hip), 5 the pipelined
+        halves (hpa_pipe.hip)"""
         return int(lib().gpt2_decode_layer_kernel(self.h))
 
     def status(self):
