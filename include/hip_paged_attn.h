@@ -246,7 +246,9 @@ typedef struct {
                              2/4); 4 (waves 4, row_blocks 4); 0 = by shape.  A hint:
                              where M's row blocks or the waves cannot carry it, 1 */
     const int* row_seq;   /* QKV: block-table row of each GEMM row (NULL = the row
-                             itself; prefill rows b*T+t -> b) */
+                             itself; prefill rows b*T+t -> b); LOGITS (looped and
+                             bf16 kernels): the output row of each GEMM row
+                             (gpt2_forward's per-position logits, written in place) */
     const float* ln_fold_c1; /* non-NULL: the LayerNorm is folded into w (packed by
                              hpa_ln_fold_pack: w = W*ln_w per column k, bias = c2):
                              A is x as it stands, and the epilogue applies

@@ -18,6 +18,7 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 #ifndef HPA_ATTN_NT
 #define HPA_ATTN_NT 1
 #endif
+constexpr int kCpolNt = HPA_ATTN_NT ? 2 : 0;  // buffer-load cache policy: nt (gfx940+ aux bit 1)
 __device__ __forceinline__ float4 load_stream(const float* ptr) {
 #if HPA_ATTN_NT
     const f32x4v v = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(ptr));
@@ -41,14 +42,15 @@ __device__ __forceinline__ int first_tile_pid(const int* __restrict__ bt, int bt
     return it < it_end && tok < (unsigned)ctx ? raw : lane0;
 }
 
-// The 64-token tiles it = it_begin + w, it_begin + w + NW, ... < it_end of
+// Single-buffered form (rounds 1-5; -DHPA_ATTN_SWP=0 builds): the tiles
+// it = it_begin + w, it_begin + w + NW, ... < it_end of
 // one (sequence, head), folded into this wave's online-softmax state
 // (m, l: log2 domain; acc: lane (g = lane>>4, d4 = lane&15) holds dims
 // 4*d4..+3 summed over tokens t0 + 4i + g).  One memory round trip per tile:
 // the tile's page ids were fetched during the previous tile; K and V rows are
 // issued together (both depend only on the page ids), then the next ids.
 template <int P, int NW>
-__device__ __forceinline__ void attn_tiles(const float* __restrict__ qh, const float* __restrict__ kbase,
+__device__ __forceinline__ void attn_tiles_single(const float* __restrict__ qh, const float* __restrict__ kbase,
                                            const float* __restrict__ vbase, size_t page_elems,
                                            const int* __restrict__ bt, int bt_len, int ctx, int it_begin,
                                            int it_end, float qscale, float& m, float& l, float4& acc,
@@ -114,6 +116,125 @@ __device__ __forceinline__ void attn_tiles(const float* __restrict__ qh, const f
             acc.w = fmaf(pi, vv[i].w, acc.w);
         }
     }
+}
+
+#ifndef HPA_ATTN_SWP
+#define HPA_ATTN_SWP 1  // 0 (A/B builds): the single-buffered loop below
+#endif
+
+// The 64-token tiles it = it_begin + w, it_begin + w + NW, ... < it_end of
+// one (sequence, head), folded into this wave's online-softmax state (m, l:
+// log2 domain; acc: lane (g = lane>>4, d4 = lane&15) holds dims 4*d4..+3
+// summed over tokens t0 + 4i + g).
+// Software-pipelined (round 6): the next tile's K rows are issued as soon as
+// this tile's QK^T has consumed its K registers, and its V rows as soon as
+// this tile's PV has consumed the V registers, so one tile's loads are in
+// flight through the other tile's softmax and PV / QK^T.  The single-buffered
+// loop (attn_tiles_single) issued K and V together and then waited with no
+// load in flight during its math: a wave's CU rate was ~26 GB/s.  Same
+// registers (one K and one V set live), same arithmetic in the same order:
+// bit-identical results.  Page ids are fetched one tile ahead (unconditional
+// loads: past the range they re-read entry 0 of the row).
+template <int P, int NW>
+__device__ __forceinline__ void attn_tiles(const float* __restrict__ qh, const float* __restrict__ kbase,
+                                           const float* __restrict__ vbase, size_t page_elems,
+                                           const int* __restrict__ bt, int bt_len, int ctx, int it_begin,
+                                           int it_end, float qscale, float& m, float& l, float4& acc,
+                                           int w = (int)(threadIdx.x >> 6)) {
+#if !HPA_ATTN_SWP
+    attn_tiles_single<P, NW>(qh, kbase, vbase, page_elems, bt, bt_len, ctx, it_begin, it_end, qscale, m, l, acc, w);
+#else
+    static_assert(P % 4 == 0 && 64 % P == 0, "page size must divide 64 and be a multiple of 4");
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 4;
+    const int d4 = lane & 15;
+    const int v_lane_off = g * HS + d4 * 4;
+    int it = it_begin + w;
+    if (it >= it_end) return;
+    int pid = first_tile_pid<P>(bt, bt_len, ctx, it, it_end);
+    float4 kv[16], vv[16];
+    auto load_k = [&](int itx, int pidx) {
+        const unsigned tokx = ((unsigned)itx << 6) + lane;
+        const float* kt = kbase + (size_t)(unsigned)pidx * page_elems + (tokx % P) * 4;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) kv[c] = load_stream(kt + c * P * 4);
+    };
+    // PV operands: the row address splits into a wave-uniform part (page of
+    // tokens t0+4i..+3, slot (4i)%P; t0 % P == 0: the SGPR offset of a buffer
+    // load) and a per-lane offset that is the same for every i.  Rows past
+    // the context take an out-of-range offset: the buffer load returns 0
+    // without a fetch, so the loads need no branch (exec-masked loads kept
+    // the loop's registers from fitting once they were carried to the next
+    // trip)
+    const __amdgpu_buffer_rsrc_t vrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(vbase), 0, 0x7fffffff,
+                                                                           0x00020000);
+    auto load_v = [&](int itx, int pidx) {
+        const unsigned t0x = (unsigned)itx << 6;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int vpid = __builtin_amdgcn_readlane(pidx, 4 * i);
+            const int soff = (int)(((size_t)(unsigned)vpid * page_elems + ((4 * i) % P) * HS) * 4);
+            const int voff = (t0x + 4 * i + g) < (unsigned)ctx ? v_lane_off * 4 : (int)0x80000000u;
+            const hpa::u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(vrsrc, voff, soff, kCpolNt);
+            vv[i] = make_float4(__uint_as_float(d.x), __uint_as_float(d.y), __uint_as_float(d.z), __uint_as_float(d.w));
+        }
+    };
+    auto page_ids = [&](int itx) {  // tile itx's page ids (entry 0 past the range: never used)
+        const unsigned t0x = (unsigned)itx << 6, tokx = t0x + lane;
+        return bt[itx < it_end ? (tokx < (unsigned)ctx ? tokx : t0x) / P : 0];
+    };
+    // QK^T: lane-per-token over 16 chunks of 4 dims (q in SGPRs)
+    auto qk = [&](int itx) {
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+            s = fmaf(qh[4 * c + 0], kv[c].x, s);
+            s = fmaf(qh[4 * c + 1], kv[c].y, s);
+            s = fmaf(qh[4 * c + 2], kv[c].z, s);
+            s = fmaf(qh[4 * c + 3], kv[c].w, s);
+        }
+        return ((unsigned)itx << 6) + lane < (unsigned)ctx ? s * qscale : -INFINITY;
+    };
+    // online softmax (log2 domain), then PV
+    auto softmax_pv = [&](float s) {
+        const float mt = hpa::wave_max(s);
+        const float mn = fmaxf(m, mt);
+        const float alpha = exp2f(m - mn);
+        const float p = exp2f(s - mn);
+        l = fmaf(l, alpha, p);
+        acc.x *= alpha;
+        acc.y *= alpha;
+        acc.z *= alpha;
+        acc.w *= alpha;
+        m = mn;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float pi = __shfl(p, 4 * i + g, 64);
+            acc.x = fmaf(pi, vv[i].x, acc.x);
+            acc.y = fmaf(pi, vv[i].y, acc.y);
+            acc.z = fmaf(pi, vv[i].z, acc.z);
+            acc.w = fmaf(pi, vv[i].w, acc.w);
+        }
+    };
+    load_k(it, pid);
+    load_v(it, pid);
+    int itn = it + NW;
+    int pidn = page_ids(itn);
+    while (itn < it_end) {
+        const float s = qk(it);
+        __builtin_amdgcn_sched_barrier(0);  // K registers consumed before the next K lands in them
+        load_k(itn, pidn);
+        softmax_pv(s);
+        __builtin_amdgcn_sched_barrier(0);  // V registers consumed before the next V lands in them
+        load_v(itn, pidn);
+        it = itn;
+        pid = pidn;
+        itn += NW;
+        pidn = page_ids(itn);
+    }
+    softmax_pv(qk(it));
+    (void)pid;
+#endif
 }
 
 // ---- bf16 KV pool (BASELINE config 5): storage only, every product and

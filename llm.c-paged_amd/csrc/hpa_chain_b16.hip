@@ -101,7 +101,7 @@ struct Smem {
 __device__ unsigned long long g_cb_trace[64][256][16];
 #define CB_MARK(k)                                                                                     \
     do {                                                                                               \
-        if (threadIdx.x == 0 && a.layer < 64 && blockIdx.x < 256)                                      \
+        if (threadIdx.x == 0 && a.layer >= 0 && a.layer < 64 && blockIdx.x < 256)                      \
             g_cb_trace[a.layer][blockIdx.x][k] = (unsigned long long)__builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else

@@ -33,7 +33,7 @@ struct FG {
     const int* bt;
     int bt_stride;
     const int* pos;
-    const int* row_seq;  // QKV: block-table row per GEMM row (NULL: the row)
+    const int* row_seq;  // QKV: block-table row per GEMM row; LOGITS: output row per GEMM row (NULL: the row)
     const float* fold_c1;  // LN folded into w: out = rstd*(acc - mean*c1) + bias (bias = c2)
     int gx, gy;  // column-tile groups x row groups of the launch
     float* sk_slab;  // stream-K (variant 6): [workgroup][2][super-tile] partials
@@ -223,8 +223,8 @@ struct Epi {
                     val = live ? pre_res[i] + val : 0.f;  // residual_forward(out, res, proj)
                     if (row < p.Mp && col < p.N) p.out[hpa::frag_index(row, col, p.N)] = val;
                     tile[(j * R + lrow) * 17 + lcol] = val;
-                } else {  // LOGITS
-                    if (live) p.out[(size_t)row * p.N + col] = val;
+                } else {  // LOGITS (row_seq: the output row of each GEMM row)
+                    if (live) p.out[(size_t)(p.row_seq ? p.row_seq[row] : row) * p.N + col] = val;
                     tile[(j * R + lrow) * 17 + lcol] = live ? val : -INFINITY;
                 }
             }

@@ -870,12 +870,15 @@ static int dec_init_weights(GPT2* model, GPT2Decode* d) {
 
 /* the batch every shape pick follows: the global batch a shard was told
  * (gpt2_decode_set_global_batch, so its rows equal the unsharded engine's
- * bit for bit) where that is <= 64 -- above 64 the unsharded engine has no
- * persistent forms and a shard's own B is the better guide --
- * else the engine's own B (a shard then computes what a single-GPU engine of
- * its rows computes) */
+ * bit for bit) where the unsharded engine has a persistent layer form for it
+ * -- <= 64 rows on fp32 weights (chain forms 6 / 8), <= 256 on bf16 weights
+ * (the bf16 chain) -- above that the unsharded engine runs five launches per
+ * layer and a shard's own B is the better guide; else the
+ * engine's own B (a shard then computes what a single-GPU engine of its rows
+ * computes) */
 static int dec_pick_B(const GPT2Decode* d) {
-    return d->pl_global_B > 0 && d->pl_global_B <= 64 ? d->pl_global_B : d->B;
+    const int lim = d->w_bf16 ? 256 : 64;
+    return d->pl_global_B > 0 && d->pl_global_B <= lim ? d->pl_global_B : d->B;
 }
 
 /* ints after the per-layer counter blocks: the step's own error word (zeroed
@@ -915,8 +918,8 @@ static int dec_set_splits(GPT2Decode* d, int splits) {
 
 static const float* wpack_at(const GPT2Decode* d, size_t off);
 
-/* the persistent layer's workspace, where it applies (fp32 LN-folded weights,
- * the shapes hpa_decode_layer_eligible accepts) */
+/* the bf16-weight chain's workspace (hpa_chain_b16.hip: B <= 256, C = 768,
+ * 12 heads): the fcproj K-part partials and the per-layer counter blocks */
 static int dec_chain_b16_setup(GPT2* model, GPT2Decode* d) {
     const GPT2Config c = model->config;
     size_t sz[2];
@@ -1853,7 +1856,7 @@ static int prefill_gemm(GPT2* model, int l, int which, int R) {
  * the reference writes logits for all T rows): LNf(res) . wte^T over the R
  * packed rows into rows_out [R][V] (device), one LOGITS GEMM on the looped /
  * bf16 kernels (any row count); its argmax partials go to a scratch buffer */
-static int prefill_all_logits(GPT2* model, int R, float* rows_out) {
+static int prefill_all_logits(GPT2* model, int R, float* rows_out, const int* out_rows) {
     GPT2Decode* d = model->decode;
     const GPT2Config c = model->config;
     const int C = c.channels, V = c.vocab_size;
@@ -1874,6 +1877,7 @@ static int prefill_all_logits(GPT2* model, int R, float* rows_out) {
     g.w = wpack_at(d, d->wpack_off[4]);
     g.N = V;
     g.out = rows_out;
+    g.row_seq = out_rows; /* LOGITS: GEMM row -> row of rows_out (NULL: the same) */
     g.part_out = part;
     const int rc = hpa_gemm_fused(&g) || hpa_synchronize();
     hpa_free(part);
@@ -1886,7 +1890,8 @@ static int prefill_all_logits(GPT2* model, int R, float* rows_out) {
  * lens[b] > 0 through the logits and the greedy / sampled pick.  Sequences
  * with lens[b] = 0 are untouched (position, next token, sampler state).
  * all_logits (device [R][V], nullable): every row's logits too. */
-static int dec_prefill_rows(GPT2* model, const int* tokens, const int* lens, int* next_tokens, float* all_logits) {
+static int dec_prefill_rows(GPT2* model, const int* tokens, const int* lens, int* next_tokens, float* all_logits,
+                            const int* all_rows) {
     GPT2Decode* d = model->decode;
     if (!d) { fprintf(stderr, "[paged_infer] gpt2_decode_init first\n"); return 1; }
     const GPT2Config c = model->config;
@@ -1946,7 +1951,7 @@ static int dec_prefill_rows(GPT2* model, const int* tokens, const int* lens, int
         rc |= prefill_gemm(model, l, G_FC, (int)R);
         rc |= prefill_gemm(model, l, G_FCPROJ, (int)R);
     }
-    if (all_logits && !rc) rc |= prefill_all_logits(model, (int)R, all_logits);
+    if (all_logits && !rc) rc |= prefill_all_logits(model, (int)R, all_logits, all_rows);
     /* last row of every active sequence -> the decode rows, logits, pick; the
      * pick advances pos by one: set pos = start + len - 1 first */
     for (int b = 0; b < B; b++) hst[b] = d->h_pos[b] + (lens[b] > 0 ? lens[b] - 1 : 0);
@@ -1970,7 +1975,7 @@ int gpt2_decode_prefill(GPT2* model, const int* tokens, int T, int* next_tokens)
     int* lens = (int*)malloc(d->B * sizeof(int));
     if (!lens) return 1;
     for (int b = 0; b < d->B; b++) lens[b] = T;
-    const int rc = dec_prefill_rows(model, tokens, lens, next_tokens, NULL);
+    const int rc = dec_prefill_rows(model, tokens, lens, next_tokens, NULL, NULL);
     free(lens);
     return rc;
 }
@@ -1978,7 +1983,7 @@ int gpt2_decode_prefill(GPT2* model, const int* tokens, int T, int* next_tokens)
 int gpt2_decode_prefill_ragged(GPT2* model, const int* tokens, const int* lens, int* next_tokens) {
     if (!model->decode) { fprintf(stderr, "[paged_infer] gpt2_decode_init first\n"); return 1; }
     if (!lens || !tokens) return 1;
-    return dec_prefill_rows(model, tokens, lens, next_tokens, NULL);
+    return dec_prefill_rows(model, tokens, lens, next_tokens, NULL, NULL);
 }
 
 int gpt2_decode_release(GPT2* model, int seq) {
@@ -2321,9 +2326,10 @@ double gpt2_decode_step_bytes(GPT2* model, double* attn_bytes) {
  * (the default) picks by the engine's own B, so a shard computes exactly what
  * a single-GPU engine of its rows computes (the small-batch forms: what the
  * metric's 2/4/8-GPU points time); total > 0 picks as the unsharded engine of
- * `total` sequences does where total <= 64, so each of a shard's rows equals
- * that engine's row bit for bit (row results depend on M only through these
- * picks); above 64 the unsharded engine has no persistent forms and the
+ * `total` sequences does where total <= 64 (fp32 weights) or 256 (bf16
+ * weights: the bf16 chain's range), so each of a shard's rows equals that
+ * engine's row bit for bit (row results depend on M only through these
+ * picks); above that the unsharded engine has no persistent forms and the
  * engine's own B is used.  Needs no communicator (tests emulate a rank of an
  * N-GPU decode on one GPU with it).  Replaces the global-batch picks that
  * gpt2_decode_shard used to force. */
@@ -2566,23 +2572,25 @@ void gpt2_forward(GPT2* model, int* inputs, int* targets, size_t B, size_t T, si
          * :703-704 / :727), not n_new single-row decode steps */
         int* toks = (int*)malloc(B * (size_t)n_new * sizeof(int));
         int* lens = (int*)malloc(B * sizeof(int));
-        float* rows = (float*)hpa_malloc(B * (size_t)n_new * V * sizeof(float));
-        if (!toks || !lens || !rows) PI_FATAL("prefill window allocation failed");
+        int* map = (int*)malloc(B * (size_t)n_new * sizeof(int));
+        int* d_map = (int*)hpa_malloc(B * (size_t)n_new * sizeof(int));
+        if (!toks || !lens || !map || !d_map) PI_FATAL("prefill window allocation failed");
         for (size_t b = 0; b < B; b++) {
             lens[b] = n_new;
             for (int t = 0; t < n_new; t++) {
                 const int tk = inputs[b * T + (start - offset) + t];
                 toks[b * n_new + t] = tk;
+                map[b * n_new + t] = (int)(b * d->max_ctx) + start + t; /* its row of pos_logits */
                 d->h_hist[b * d->max_ctx + start + t] = tk;
             }
         }
-        if (dec_prefill_rows(model, toks, lens, NULL, rows)) PI_FATAL("window prefill failed");
+        /* every row's logits straight into its position's row of pos_logits
+         * (the GEMM's output row map): no [B][n_new][V] staging copy */
+        PI_CHECK(hpa_memcpy(d_map, map, B * (size_t)n_new * sizeof(int)));
+        if (dec_prefill_rows(model, toks, lens, NULL, d->pos_logits, d_map)) PI_FATAL("window prefill failed");
         if (gpt2_decode_evicted(model, NULL) > 0) PI_FATAL("gpt2_forward: page pool too small, a sequence was evicted");
-        for (size_t b = 0; b < B; b++) /* rows of sequence b: positions start .. start+n_new-1 */
-            PI_CHECK(hpa_memcpy_async(d->pos_logits + (b * d->max_ctx + start) * V, rows + b * (size_t)n_new * V,
-                                      (size_t)n_new * V * sizeof(float)));
-        PI_CHECK(hpa_synchronize());
-        hpa_free(rows);
+        hpa_free(d_map);
+        free(map);
         free(lens);
         free(toks);
     }

@@ -276,6 +276,45 @@ def test_bf16_chain_ragged_batches(hip, B, P, kv_bf16):
                       layer_rtol=BF16_LAYER_RTOL, tol=BF16_PINNED_LOGIT_TOL, max_ctx=64, layer_form=4)
 
 
+@pytest.mark.parametrize("B,parts", [(40, (16, 24)), (96, (32, 64))])
+def test_bf16_chain_shards_equal_unsharded(hip, B, parts):
+    """the bf16 chain sums a row in an order that depends on neither
+    the batch nor the row's place in it, and with gpt2_decode_set_global_batch
+    a shard's attention splits and waves follow the global batch (up to the
+    bf16 chain's 256 rows): every shard's logits and ids equal the unsharded
+    engine's rows bit for bit (B = 40 as 16 + 24; B = 96 as 32 + 64, a global
+    batch above 64)"""
+    params = _params(hip, CFG_124M, 62)
+    ctx, steps = 300, 2
+    toks = np.random.default_rng(62).integers(0, CFG_124M["V"], (steps, B)).astype(np.int32)
+
+    def run(rows, lo, total):
+        m = hip.Model(CFG_124M, params=params)
+        m.decode_init(rows, 16, 512, w_dtype=hip.HPA_BF16)
+        if total:
+            m.set_global_batch(total)
+        assert m.layer_form() == 4  # the bf16 chain
+        m.set_graph(True)
+        m.fill_random(ctx, seed=9, seq_offset=lo)
+        lg, ids = [], []
+        for t in range(steps):
+            ids.append(m.step(toks[t, lo:lo + rows]))
+            lg.append(m.logits())
+        m.status()
+        splits, waves = m.attn_splits(), m.attn_waves()
+        m.close()
+        return np.stack(lg), np.stack(ids), (splits, waves)
+
+    ref_l, ref_i, ref_shape = run(B, 0, 0)
+    lo = 0
+    for rows in parts:
+        lg, ids, shape = run(rows, lo, B)
+        assert shape == ref_shape, (rows, shape, ref_shape)
+        assert np.array_equal(ids, ref_i[:, lo:lo + rows])
+        assert np.array_equal(lg, ref_l[:, lo:lo + rows]), float(np.abs(lg - ref_l[:, lo:lo + rows]).max())
+        lo += rows
+
+
 def test_config2_layer_pinned_full_context(hip):
     """the fp32 headline path (its default layer form) layer by layer: B=64,
     page 16, positions ~1014-1023"""

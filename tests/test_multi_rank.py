@@ -37,9 +37,10 @@ def _tokens(B, steps, V):
     return np.random.default_rng(123).integers(0, V, (steps, B)).astype(np.int32)
 
 
-def _run_plan(dist, plan, send, recv):
-    """execute the library's schedule for this rank over gloo: SEND / RECV as
-    point-to-point messages (byte buffers), COPY as the root's local copy"""
+def _post_plan(dist, plan, send, recv):
+    """post the library's schedule for this rank over gloo: SEND / RECV as
+    point-to-point messages (byte buffers), COPY as the root's local copy;
+    returns the pending requests"""
     import torch
     reqs = []
     for op, peer, off, nb in plan:
@@ -49,11 +50,15 @@ def _run_plan(dist, plan, send, recv):
             reqs.append(dist.irecv(torch.from_numpy(recv[off:off + nb]), peer))
         else:
             recv[off:off + nb] = send[:nb]
-    for r in reqs:
-        r.wait()
+    return reqs
 
 
-def _worker(rank, world, port, rows, root, mode, out_path):
+def _worker(rank, world, port, rows, root, mode, out_path, nbuf=1):
+    """nbuf = 1: each step's gather completes before the next step; nbuf = 2:
+    gpt2_decode_gather's double buffering -- step k's gather (send / receive
+    buffers k % 2) is still in flight while step k+1 fills the other pair, and
+    a pair is reused only after the gather that last used it (two steps
+    earlier) has completed"""
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -68,17 +73,29 @@ def _worker(rank, world, port, rows, root, mode, out_path):
         c = oc.cfg(SMALL["maxT"], SMALL["V"], SMALL["L"], SMALL["NH"], SMALL["C"])
         dec = oc.PagedDecoder(params, c, rows[rank], 8, SMALL["maxT"], page_seed=17 + rank) if rows[rank] else None
         toks = _tokens(B, STEPS, SMALL["V"])
-        recv = np.zeros(sum(nbytes), np.uint8) if rank == root else None
-        got = []
+        sends = [np.zeros(max(nbytes[rank], 1), np.uint8) for _ in range(nbuf)]
+        recvs = [np.zeros(sum(nbytes), np.uint8) if rank == root else None for _ in range(nbuf)]
+        got, pending = [], []  # pending: (requests, step) of gathers still in flight
+
+        def complete(k):  # wait for step k's gather; the root keeps what it assembled
+            reqs, step = pending.pop(0)
+            assert step == k
+            for r in reqs:
+                r.wait()
+            if rank == root:
+                got.append(recvs[k % nbuf].view(np.float32 if mode == "logits" else np.int32).reshape(B, -1).copy())
+
         for t in range(STEPS):
-            send = np.zeros(max(nbytes[rank], 1), np.uint8)
+            if pending and pending[0][1] <= t - nbuf:  # buffer pair t % nbuf is free again
+                complete(pending[0][1])
+            send = sends[t % nbuf]
             if dec is not None:
                 nxt, logits = dec.step(toks[t, lo:hi])
                 out = logits if mode == "logits" else nxt.astype(np.int32)
                 send[:nbytes[rank]] = np.ascontiguousarray(out).view(np.uint8).ravel()
-            _run_plan(dist, plan, send, recv)
-            if rank == root:
-                got.append(recv.view(np.float32 if mode == "logits" else np.int32).reshape(B, -1).copy())
+            pending.append((_post_plan(dist, plan, send, recvs[t % nbuf]), t))
+        while pending:
+            complete(pending[0][1])
         if dec is not None:
             dec.close()
         if rank == root:
@@ -124,12 +141,15 @@ def _spawn(world, target, args):
     return [p.exitcode for p in procs]
 
 
-@pytest.mark.parametrize("rows,root,mode", [([3, 3], 0, "logits"), ([3, 2], 0, "logits"), ([2, 2], 1, "ids"),
-                                            ([2, 0, 3], 0, "logits"), ([1, 2, 1, 2], 2, "logits")])
-def test_sharded_decode_through_library_gather_schedule(tmp_path, rows, root, mode):
+@pytest.mark.parametrize("rows,root,mode,nbuf", [([3, 3], 0, "logits", 1), ([3, 2], 0, "logits", 1),
+                                                 ([2, 2], 1, "ids", 1), ([2, 0, 3], 0, "logits", 1),
+                                                 ([1, 2, 1, 2], 2, "logits", 1),
+                                                 # double-buffered, overlapped with the next step
+                                                 ([3, 2], 0, "logits", 2), ([2, 0, 3], 1, "ids", 2)])
+def test_sharded_decode_through_library_gather_schedule(tmp_path, rows, root, mode, nbuf):
     world = len(rows)
     out = str(tmp_path / "root.npy")
-    codes = _spawn(world, _worker, (_free_port(), rows, root, mode, out))
+    codes = _spawn(world, _worker, (_free_port(), rows, root, mode, out, nbuf))
     assert all(c == 0 for c in codes), codes
     got = np.load(out)
     want = _unsharded(sum(rows), mode)
