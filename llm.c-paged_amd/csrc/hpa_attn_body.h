@@ -119,22 +119,23 @@ __device__ __forceinline__ void attn_tiles_single(const float* __restrict__ qh, 
 }
 
 #ifndef HPA_ATTN_SWP
-#define HPA_ATTN_SWP 1  // 0 (A/B builds): the single-buffered loop below
+#define HPA_ATTN_SWP 0  // 1 (A/B builds): the software-pipelined loop (measured slower, profiles/r6/experiments/attn_swp.txt)
 #endif
 
 // The 64-token tiles it = it_begin + w, it_begin + w + NW, ... < it_end of
 // one (sequence, head), folded into this wave's online-softmax state (m, l:
 // log2 domain; acc: lane (g = lane>>4, d4 = lane&15) holds dims 4*d4..+3
 // summed over tokens t0 + 4i + g).
-// Software-pipelined (round 6): the next tile's K rows are issued as soon as
-// this tile's QK^T has consumed its K registers, and its V rows as soon as
-// this tile's PV has consumed the V registers, so one tile's loads are in
-// flight through the other tile's softmax and PV / QK^T.  The single-buffered
-// loop (attn_tiles_single) issued K and V together and then waited with no
-// load in flight during its math: a wave's CU rate was ~26 GB/s.  Same
-// registers (one K and one V set live), same arithmetic in the same order:
-// bit-identical results.  Page ids are fetched one tile ahead (unconditional
-// loads: past the range they re-read entry 0 of the row).
+// The product runs the single-buffered loop (attn_tiles_single: K and V of a
+// tile issued together, one memory round trip per tile).  HPA_ATTN_SWP=1 (A/B
+// builds, round 6) software-pipelines it: the next tile's K rows are issued
+// as soon as this tile's QK^T has consumed its K registers, and its V rows as
+// soon as this tile's PV has consumed the V registers (same registers, same
+// arithmetic in the same order: bit-identical).  Measured: faster only at 4
+// waves per CU (B = 8, S = 1: 15.6 vs 16.9 us), equal at the engine's picks
+// and slower at B = 64 (65.6 vs 64.9 us; step 1.120 vs 1.100 ms,
+// profiles/r6/experiments/attn_swp.txt): a CU's K/V stream is not bound by
+// the math between tiles.
 template <int P, int NW>
 __device__ __forceinline__ void attn_tiles(const float* __restrict__ qh, const float* __restrict__ kbase,
                                            const float* __restrict__ vbase, size_t page_elems,
