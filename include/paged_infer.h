@@ -288,8 +288,9 @@ double gpt2_decode_step_bytes(GPT2* model, double* attention_bytes);
  * returns the device rows of the last gather after gpt2_decode_gather_wait. */
 /* the batch the shape picks follow (attention splits / waves, layer-loop
  * form, logits form): 0 (default) the engine's own B -- a shard computes what
- * a single-GPU engine of its rows computes; total > 0 (<= 64 applies, above
- * that the own B) -- what the unsharded engine of `total` rows computes, bit
+ * a single-GPU engine of its rows computes; total > 0 (<= 64 applies with
+ * fp32 weights, <= 256 with bf16 weights -- the bf16 chain's row limit --
+ * above that the own B) -- what the unsharded engine of `total` rows computes, bit
  * for bit.  No communicator needed.  Replaces the global-batch picks
  * gpt2_decode_shard forced until round 3. */
 int    gpt2_decode_set_global_batch(GPT2* model, int total);

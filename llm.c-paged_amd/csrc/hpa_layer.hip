@@ -751,6 +751,9 @@ __global__ __launch_bounds__(768) void decode_layer_kernel(KA args) {
 #ifndef HPA_C6_DE
 #define HPA_C6_DE 0  // A/B builds: bit 0 fcproj, bit 1 qkv k-group waits at 3-4 row blocks as well
 #endif
+#ifndef HPA_C6_EARLY
+#define HPA_C6_EARLY 0  // A/B builds: 1 = non-storing waves prefetch the next phase's weights right after their MFMAs (measured slower, profiles/r6/experiments/c6_early.txt)
+#endif
 #ifndef HPA_C6_GW
 #define HPA_C6_GW 1  // 1: fc / fcproj / qkv wait per 64-column k-group of their A (wave w on its group); 0: per row block (A/B)
 #endif
@@ -887,6 +890,13 @@ __device__ __forceinline__ void load_wt(const float* W, int K16W, int j0, int kb
 template <int T, bool STATS>
 __device__ __forceinline__ void mfma_regs(const float4 (&xv)[SPW], const float4 (&wr)[T][SPW], f32x4 (&acc)[T],
                                           float& fs1, float& fs2);
+
+// the wave's 4 A fragments (sc1: written in this launch or the previous one)
+__device__ __forceinline__ void load_a4(const float* A, int K16A, int rb, int kb, int w, float4 (&xv)[SPW]) {
+    const int off = ((rb * K16A + kb + w * SPW) * 64 + (int)(threadIdx.x & 63)) * 16;
+#pragma unroll
+    for (int s = 0; s < SPW; ++s) xv[s] = hpa::load_wt16(A, off + s * 1024);
+}
 
 template <int T, bool STATS>
 __device__ __forceinline__ void mfma_t(const float* A, int K16A, int rb, int kb, int w, const float4 (&wr)[T][SPW],
@@ -1048,12 +1058,32 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
     PL_STAMP(t_start);
     PL_STORE(0, t_start);
     float fs1 = 0.f, fs2 = 0.f;
+    // every phase's unit of this workgroup (the geometry is fixed per launch)
+    constexpr int NGB = NCT, NGC = 4 * NCT / TC, NGD = NCT / TD, NGE = 3 * NCT / TE;
+    const bool hasB = bid < R * NGB, hasC = bid < R * NGC, hasD = bid < 4 * R * NGD, hasE = bid < R * NGE;
+    const int gB = bid % NGB, rbB = bid / NGB;
+    const int gC = bid % NGC, rbC = bid / NGC;
+    const int gD = bid % NGD, rbD = (bid / NGD) % R, pD = (bid / NGD) / R;
+    const int gE = bid % NGE, rbE = bid / NGE;
+    // Early weight prefetch (HPA_C6_EARLY, round 6): a wave that stores
+    // nothing in phase X (waves >= T_X: only waves 0..T_X-1 run X's epilogue)
+    // issues phase X+1's weight fragments (and epilogue operands) right after
+    // its MFMAs of phase X (behind their operand waits), so they stream during
+    // X's MFMAs, epilogue and seam instead of being issued at the seam, where
+    // the A gather after the
+    // wait queued behind them in the CU's memory pipe (MI355X_MICROARCH.md
+    // "gather-pass": 1.0-1.7 us queued vs 0.3-0.65 quiet).  Such a wave skips
+    // the publish drain (it stored nothing; the drain would wait for its
+    // prefetch).  The storing waves keep the round-5 order (drain, then the
+    // next phase's operands).  Same loads, same arithmetic: same bits.
+    constexpr bool EARLY = HPA_C6_EARLY != 0;
     // B: attproj(l), 1 tile per unit: res2 = res + att . Wap^T + b
+    float4 c1C = make_float4(0.f, 0.f, 0.f, 0.f), c2C = c1C;
+    float4 wrC[TC][SPW];
     {
-        constexpr int T = 1, NG = NCT;
-        const int n = R * NG;
-        const bool has = bid < n;
-        const int g = bid % NG, rb = bid / NG;
+        constexpr int T = 1;
+        const bool has = hasB;
+        const int g = gB, rb = rbB;
         float4 wr[T][SPW];
         if (has) load_wt<T, NT>(a.w_ap, K16, g * T, 0, w, wr);
         const bool ep = has && tid < T * 64;
@@ -1065,10 +1095,23 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             rv = hpa::load_wt16(a.res, fi);
         }
         PL_MARK(4);
+        const bool early = EARLY && w >= T;  // a wave with no store in this phase
+        const bool epC = hasC && tid < TC * 64;
+        const int colC = (gC * TC + et) * 16 + 4 * eq;
+        float4 xv[SPW];
+        if (has) load_a4(a.att, K16, rb, 0, w, xv);
+        __builtin_amdgcn_sched_barrier(0);
         if (has) {
             f32x4 acc[T];
-            mfma_t<T, false>(a.att, K16, rb, 0, w, wr, acc, fs1, fs2);
+            mfma_regs<T, false>(xv, wr, acc, fs1, fs2);
             put_red_t<T>(sm.red, w, acc);
+        }
+        if (early) {  // behind the MFMAs' operand waits (issued here they cannot delay them)
+            if (epC) {
+                c1C = ld4(a.fc_c1 + colC);
+                c2C = ld4(a.fc_c2 + colC);
+            }
+            if (hasC) load_wt<TC, NT>(a.w_fc, K16, gC * TC, 0, w, wrC);
         }
         lds_barrier();
         if (ep) {
@@ -1079,86 +1122,105 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             hpa::store_wt16(a.res2, fi, v);
         }
         PL_MARK(12);
+        if (!early) drain_vm();  // the storing waves
+        lds_barrier();
         if (HPA_C6_GW) {  // the tile's k-group of fc's A
-            drain_vm();
-            lds_barrier();
             if (tid == 0 && has) arrive_tiles(a, kCtr + 4 * NCT + kGC, rb, NW, g, 1);
         } else {
-            publish6(a, X1 + rb, has);
+            if (tid == 0 && has) arrive6(a, X1 + rb, 1);
+        }
+        if (!early) {  // the round-5 order: epilogue operands, then the weights
+            if (epC) {
+                c1C = ld4(a.fc_c1 + colC);
+                c2C = ld4(a.fc_c2 + colC);
+            }
+            if (hasC) load_wt<TC, NT>(a.w_fc, K16, gC * TC, 0, w, wrC);
         }
     }
     PL_MARK(5);
     // C: fc(l): fch = gelu(LN2(res2) . Wfc^T + b), LN folded; T = TC tiles
+    float4 bvD = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 wrD[TD][SPW];
     {
-        constexpr int T = TC, NG = 4 * NCT / TC;
-        const int n = R * NG;
-        const bool has = bid < n;
-        const int g = bid % NG, rb = bid / NG;
+        constexpr int T = TC;
+        const bool has = hasC;
+        const int g = gC, rb = rbC;
         const bool ep = has && tid < T * 64;
         const int row = rb * 16 + er, col = (g * T + et) * 16 + 4 * eq;
-        float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f), c2 = c1;
-        if (ep) {  // epilogue operands first: the weight prefetch is the last thing in flight
-            c1 = ld4(a.fc_c1 + col);
-            c2 = ld4(a.fc_c2 + col);
-        }
-        float4 wr[T][SPW];
-        if (has) load_wt<T, NT>(a.w_fc, K16, g * T, 0, w, wr);
         if (HPA_C6_GW) {
             if (has && !wait_grp(a, kCtr + 4 * NCT + kGC + rb * NW * kPad, 4, 2, sm)) return;
         } else if (!wait6(a, X1 + (has ? rb : 0), has ? NCT : 0, 2, sm)) {
             return;
         }
         PL_MARK(6);
+        const bool early = EARLY && w >= T;
+        const bool epD = hasD && tid < TD * 64;
+        const int colD = (gD * TD + et) * 16 + 4 * eq;
         fs1 = fs2 = 0.f;
+        float4 xv[SPW];
+        if (has) load_a4(a.res2, K16, rb, 0, w, xv);
+        __builtin_amdgcn_sched_barrier(0);
         if (has) {
             f32x4 acc[T];
-            mfma_t<T, true>(a.res2, K16, rb, 0, w, wr, acc, fs1, fs2);
+            mfma_regs<T, true>(xv, wrC, acc, fs1, fs2);
             put_red_t<T>(sm.red, w, acc);
         }
         hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + w * 32);
+        if (early) {
+            if (epD) bvD = ld4(a.b_fp + colD);
+            if (hasD) load_wt<TD, NT>(a.w_fp, 4 * K16, gD * TD, pD * K16, w, wrD);
+        }
         lds_barrier();
         if (GD && tid == 0) sm.s_ready = 0;  // every wave is past fc's wait; read again in fcproj's
         if (ep) {
-            float4 v = ln_fold4(sm.wsum, er, fold_t<T>(sm.red, et, er, eq), c1, c2);
+            float4 v = ln_fold4(sm.wsum, er, fold_t<T>(sm.red, et, er, eq), c1C, c2C);
             const bool live = row < a.B;
             v = live ? make_float4(hpa::gelu_ref(v.x), hpa::gelu_ref(v.y), hpa::gelu_ref(v.z), hpa::gelu_ref(v.w))
                      : make_float4(0.f, 0.f, 0.f, 0.f);
             hpa::store_wt16(a.fch, (int)(hpa::frag_index(row, col, 4 * C) * 4), v);
         }
         PL_MARK(13);
+        if (!early) drain_vm();
+        lds_barrier();
         if (GD) {  // the tiles' k-groups of fcproj's A (48 per row block)
-            drain_vm();
-            lds_barrier();
             if (tid == 0 && has) arrive_tiles(a, kCtr + 4 * NCT + kGD, rb, 4 * NW, g * T, T);
         } else {
-            publish6(a, H + rb * 4 + (g * T) / NCT, has);  // the K part of fcproj these columns feed
+            if (tid == 0 && has) arrive6(a, H + rb * 4 + (g * T) / NCT, 1);  // the K part of fcproj these columns feed
+        }
+        if (!early) {
+            if (epD) bvD = ld4(a.b_fp + colD);
+            if (hasD) load_wt<TD, NT>(a.w_fp, 4 * K16, gD * TD, pD * K16, w, wrD);
         }
         PL_MARK(7);
     }
     // D: fcproj(l), K part p of 4, T = TD tiles: partial tiles -> slab; the
     // last part of (row block, tile group) adds the parts in order + bias + res2
+    float4 wrE[TE][SPW];
+    const bool epE = hasE && tid < TE * 64;
+    const int rowE = rbE * 16 + er, colE = (gE * TE + et) * 16 + 4 * eq;
+    int kps = 0;  // qkv(l+1)'s K/V destination: the row's position (c6::qkv_pos6)
     {
-        constexpr int T = TD, NG = NCT / TD;
-        const int n = 4 * R * NG;
-        const bool has = bid < n;
-        const int g = bid % NG, q1 = bid / NG, rb = q1 % R, p = q1 / R;
+        constexpr int T = TD, NG = NGD;
+        const bool has = hasD;
+        const int g = gD, rb = rbD, p = pD;
         const bool ep = has && tid < T * 64;
         const int row = rb * 16 + er, col = (g * T + et) * 16 + 4 * eq;
-        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ep) bv = ld4(a.b_fp + col);
-        float4 wr[T][SPW];
-        if (has) load_wt<T, NT>(a.w_fp, 4 * K16, g * T, p * K16, w, wr);
         if (GD) {
             if (has && !wait_grp(a, kCtr + 4 * NCT + kGD + (rb * 4 * NW + p * NW) * kPad, 4, 3, sm)) return;
         } else if (!wait6(a, H + (has ? rb * 4 + p : 0), has ? 4 * NCT / TC / 4 : 0, 3, sm)) {
             return;
         }
         PL_MARK(8);
+        const bool early = EARLY && w >= T && !a.last;  // qkv(l+1)'s weights (the storing waves: after the combine)
+        float4 xv[SPW];
+        if (has) load_a4(a.fch, 4 * K16, rb, p * K16, w, xv);
+        __builtin_amdgcn_sched_barrier(0);
         if (has) {
             f32x4 acc[T];
-            mfma_t<T, false>(a.fch, 4 * K16, rb, p * K16, w, wr, acc, fs1, fs2);
+            mfma_regs<T, false>(xv, wrD, acc, fs1, fs2);
             put_red_t<T>(sm.red, w, acc);
         }
+        if (early && hasE) load_wt<TE, NT>(a.w_qkv, K16, gE * TE, 0, w, wrE);
         lds_barrier();
         if ((GD || GE) && tid == 0) sm.s_ready = 0;  // every wave is past fcproj's wait; read again in qkv's
         float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1168,7 +1230,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             hpa::store_wt16(a.slab_fp, sx * 4, val);
         }
         PL_MARK(14);
-        c6::drain_vm();
+        if (!early) c6::drain_vm();
         lds_barrier();
         if (has && tid == 0) {
             const int tk = __hip_atomic_fetch_add(tick + rb * NG + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1188,7 +1250,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
             for (int qq = 1; qq < 4; ++qq) {
                 tot.x += pv[qq].x; tot.y += pv[qq].y; tot.z += pv[qq].z; tot.w += pv[qq].w;
             }
-            tot.x += bv.x; tot.y += bv.y; tot.z += bv.z; tot.w += bv.w;
+            tot.x += bvD.x; tot.y += bvD.y; tot.z += bvD.z; tot.w += bvD.w;
             const bool live = row < a.B;
             tot = live ? make_float4(rv.x + tot.x, rv.y + tot.y, rv.z + tot.z, rv.w + tot.w)
                        : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1198,7 +1260,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
                 tr[0] = tot.x; tr[1] = tot.y; tr[2] = tot.z; tr[3] = tot.w;
             }
         }
-        c6::drain_vm();
+        if (!early) c6::drain_vm();
         lds_barrier();
         if (a.stats_out && last && tid < T * 16) {  // 16-column LNf partial sums of the tiles' rows
             const int t = tid >> 4, r = tid & 15;
@@ -1220,23 +1282,26 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
                 arrive6(a, X2 + rb, 1);
         }
         PL_MARK(9);
+        if (!a.last) {  // the position before the weights (vmcnt retires in order; the page load needs it)
+            kps = qkv_pos6(a, epE, rowE, colE);
+            if (!early && hasE) load_wt<TE, NT>(a.w_qkv, K16, gE * TE, 0, w, wrE);
+        }
     }
     // E: qkv(l+1), T = TE tiles: LN1 folded, q + K/V appended into layer l+1's pages
     if (!a.last) {
-        constexpr int T = TE, NG = 3 * NCT / TE;
-        const int n = R * NG;
-        const bool has = bid < n;
-        const int g = bid % NG, rb = bid / NG;
-        const bool ep = has && tid < T * 64;
-        const int row = rb * 16 + er, col = (g * T + et) * 16 + 4 * eq;
-        const int kps = qkv_pos6(a, ep, row, col);
+        constexpr int T = TE;
+        const bool has = hasE;
+        const int g = gE, rb = rbE;
+        const bool ep = epE;
+        const int row = rowE, col = colE;
+        // the epilogue waves' operands (waves 0..TE-1 store in D too: issued
+        // after D's drain, as in round 5): the position (above, ahead of the
+        // weights), the LN-fold operands, then the page
         float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f), c2 = c1;
         if (ep) {
             c1 = ld4(a.qkv_c1 + col);
             c2 = ld4(a.qkv_c2 + col);
         }
-        float4 wr[T][SPW];
-        if (has) load_wt<T, NT>(a.w_qkv, K16, g * T, 0, w, wr);
         const int kpage = qkv_page6<P>(a, ep, row, col, kps);
         if (GE) {
             if (has && !wait_grp(a, kCtr + 4 * NCT + kGE + rb * NW * kPad, 4, 4, sm)) return;
@@ -1247,7 +1312,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
         fs1 = fs2 = 0.f;
         if (has) {
             f32x4 acc[T];
-            mfma_t<T, true>(a.res, K16, rb, 0, w, wr, acc, fs1, fs2);
+            mfma_t<T, true>(a.res, K16, rb, 0, w, wrE, acc, fs1, fs2);
             put_red_t<T>(sm.red, w, acc);
         }
         hpa_gemm::row_sums_publish(fs1, fs2, sm.wsum + w * 32);

@@ -17,6 +17,8 @@
 #   trace:CFG          per-workgroup phase trace of the chain (-DHPA_LAYER_TRACE build)
 #   ab:NAME:FLAGS:CFG  A/B library (make BUILD=build_NAME LIB=libpl_NAME.so XFLAGS="FLAGS"),
 #                      bench CFG on it -> bench_CFG_NAME.txt
+#   lib:NAME:CFG       bench CFG on a prebuilt library (NAME "prod" = libpaged_hip.so,
+#                      else llm.c-paged_amd/libpl_NAME.so), no CPU baseline -> bench_CFG_NAME_<n>.txt
 #   py:NAME:ARGS       python -u ARGS (a tools/ probe)         -> NAME.txt
 #   exe:NAME:ARGS      a built probe binary                    -> NAME.txt
 #   rocexe:NAME:ARGS   the same under rocprofv3 --kernel-trace --stats -> NAME.txt
@@ -70,6 +72,11 @@ for st in "$@"; do
     ab)
       run "build_ab_$a" 900 make -s -C llm.c-paged_amd -j16 BUILD="build_$a" LIB="libpl_$a.so" XFLAGS="$b"
       HPA_LIB="llm.c-paged_amd/libpl_$a.so" run "bench_${c}_$a" 600 python -u bench.py --cpu-baseline off $(cfg_args "$c") ;;
+    lib)
+      lf=llm.c-paged_amd/libpl_$a.so; [ "$a" = prod ] && lf=llm.c-paged_amd/libpaged_hip.so
+      n=1; while [ -e "$o/bench_${b}_${a}_$n.txt" ]; do n=$((n+1)); done
+      HPA_LIB="$lf" run "bench_${b}_${a}_$n" 600 python -u bench.py --cpu-baseline off $(cfg_args "$b")
+      grep -h '"ms_per_step"' "$o/bench_${b}_${a}_$n.txt" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('[gpu.sh] $a $b', d['ms_per_step'], d['value'])" ;;
     py) run "$a" 600 python -u $b ;;
     exe) run "$a" 600 $b ;;
     rocexe)  # the trace database stays on the box (/tmp): only the log comes back
