@@ -64,6 +64,14 @@ int   hpa_event_synchronize(void* ev);     /* host waits until the work before e
 void* hpa_stream_create(void);
 int   hpa_stream_destroy(void* stream);
 int   hpa_stream_wait_event(void* ev);
+/* a dependency through a device word (round 6): write_value -- the current
+ * stream sets *flag = value once its earlier work is done; wait_value -- the
+ * current stream waits until *flag >= value.  The decode gather's
+ * compute -> comm hand-off uses it: a pending event wait on another stream
+ * slows the decode stream's kernels ~25 us per step, a pending wait-value
+ * 5-9 us (profiles/r6/recv_coresidency.txt). */
+int   hpa_stream_write_value32(unsigned* flag, unsigned value);
+int   hpa_stream_wait_value32(unsigned* flag, unsigned value);
 const char* hpa_last_error(void);
 /* build flags of this library: bit 0 = an A/B build (-DHPA_AB: the layer
  * forms measured slower -- the full persistent layer, the wide-unit chains --

@@ -1291,7 +1291,7 @@ __global__ __launch_bounds__(768) void decode_chain6_kernel(KA args) {
     if (!a.last) {
         constexpr int T = TE;
         const bool has = hasE;
-        const int g = gE, rb = rbE;
+        const int rb = rbE;
         const bool ep = epE;
         const int row = rowE, col = colE;
         // the epilogue waves' operands (waves 0..TE-1 store in D too: issued

@@ -216,6 +216,22 @@ int hpa_stream_wait_event(void* ev) {
     return 0;
 }
 
+/* a cross-stream dependency through a device word instead of an event: the
+ * current stream writes `value` to *flag once its earlier work is done, and
+ * the current stream of the waiter blocks until *flag >= value.  Measured
+ * (profiles/r6/recv_coresidency.txt): a stream waiting on an EVENT of the
+ * decode stream slows the decode stream's own kernels by ~25 us per step
+ * while the wait is pending; a pending wait-value costs 5-9 us. */
+int hpa_stream_write_value32(unsigned* flag, unsigned value) {
+    HPA_CHECK(hipStreamWriteValue32(g_stream, flag, value, 0));
+    return 0;
+}
+
+int hpa_stream_wait_value32(unsigned* flag, unsigned value) {
+    HPA_CHECK(hipStreamWaitValue32(g_stream, flag, value, hipStreamWaitValueGte, 0xffffffffu));
+    return 0;
+}
+
 int hpa_event_record(void* ev) {
     HPA_CHECK(hipEventRecord((hipEvent_t)ev, g_stream));
     return 0;

@@ -596,8 +596,9 @@ typedef struct {
     float* recv[2];   /* root: [sum rows][V] */
     int* send_ids[2];
     int* recv_ids[2];
-    void* ev_ready[2]; /* send buffer k filled (compute stream) */
-    void* ev_done[2];  /* gather from buffer k done (comm stream) */
+    unsigned* d_seq;  /* device word: gathers whose send copy is done (compute stream) */
+    unsigned seq;     /* gathers posted */
+    void* ev_done[2]; /* gather from buffer k done (comm stream) */
     int k, last, pending[2];
 } DecShard;
 
@@ -747,9 +748,9 @@ static void dec_shard_free(GPT2Decode* d) {
     }
     for (int k = 0; k < 2; k++) {
         hpa_free(s->send[k]); hpa_free(s->recv[k]); hpa_free(s->send_ids[k]); hpa_free(s->recv_ids[k]);
-        hpa_event_destroy(s->ev_ready[k]);
         hpa_event_destroy(s->ev_done[k]);
     }
+    hpa_free(s->d_seq);
     hpa_stream_destroy(s->stream);
     free(s->rows);
     free(s->bytes);
@@ -2400,11 +2401,11 @@ int gpt2_decode_shard(GPT2* model, const int* rows_per_rank, int root) {
             s->recv[k] = (float*)hpa_malloc((size_t)total * V * 4);
             s->recv_ids[k] = (int*)hpa_malloc((size_t)total * 4);
         }
-        s->ev_ready[k] = hpa_event_create_nt();
         s->ev_done[k] = hpa_event_create_nt();
-        ok = s->send[k] && s->send_ids[k] && (rank != root || (s->recv[k] && s->recv_ids[k])) && s->ev_ready[k] &&
-             s->ev_done[k];
+        ok = s->send[k] && s->send_ids[k] && (rank != root || (s->recv[k] && s->recv_ids[k])) && s->ev_done[k];
     }
+    s->d_seq = ok ? (unsigned*)hpa_malloc(64) : NULL;
+    ok = ok && s->d_seq && hpa_memset_async(s->d_seq, 0, 64) == 0 && hpa_synchronize() == 0;
     if (!ok) { dec_shard_free(d); return 1; }
     return 0;
 }
@@ -2430,10 +2431,15 @@ int gpt2_decode_gather(GPT2* model, int what) {
     void* src = what ? (void*)d->d_next : (void*)d->d_logits;
     void* snd = what ? (void*)s->send_ids[k] : (void*)s->send[k];
     rc |= hpa_memcpy_async(snd, src, (size_t)d->B * per);
-    rc |= hpa_event_record(s->ev_ready[k]);
+    /* compute -> comm through a device word, not an event: a stream waiting
+     * on an event of the decode stream slows the decode kernels ~25 us per
+     * step while the wait is pending; a wait-value 5-9 us
+     * (profiles/r6/recv_coresidency.txt) */
+    const unsigned seq = ++s->seq;
+    rc |= hpa_stream_write_value32(s->d_seq, seq);
     for (int r = 0; r < s->nranks; r++) s->bytes[r] = (size_t)s->rows[r] * per;
     hpa_set_stream(s->stream);
-    rc |= hpa_stream_wait_event(s->ev_ready[k]);
+    rc |= hpa_stream_wait_value32(s->d_seq, seq);
     rc |= hpa_comm_gatherv(snd, (size_t)d->B * per, what ? (void*)s->recv_ids[k] : (void*)s->recv[k], s->bytes,
                            s->root, s->stream);
     rc |= hpa_event_record(s->ev_done[k]);

@@ -81,3 +81,41 @@ def test_persistent_step_beside_cu_holding_kernel(hip, B, w_bf16, blocks):
     assert np.array_equal(i0, i1) and np.array_equal(l0, l1)
     if blocks >= 200:  # the launch could not be resident: it waited for the occupier, within the bound
         assert min(ms1) > 3.0, ms1
+
+
+@pytest.mark.parametrize("B", [8, 64])
+def test_persistent_steps_beside_rccl_shaped_receive(hip, B):
+    """the bench's N>1 pattern with an RCCL-shaped receive:
+    after every step a kernel with ncclDevKernel_Generic's resources (256
+    VGPRs, 37,664 B LDS, 512 threads; tests/helpers/occupier.hip) is launched
+    behind the step on another stream, 64 workgroups held 200 us, while the
+    next step is enqueued; every step reports status 0 with the ids and logits
+    of the same steps run alone (the per-step cost: tools/recv_coresidency.py,
+    profiles/r6/recv_coresidency.txt)"""
+    occ = _occ()
+    occ.occ_recv_after.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_longlong, ctypes.c_int,
+                                   ctypes.c_void_p, ctypes.c_int]
+    occ.occ_recv_after.restype = ctypes.c_int
+    params = hip.synthetic_params(GPT2_124M, seed=75)
+    toks = np.random.default_rng(75).integers(0, GPT2_124M["V"], (4, B)).astype(np.int32)
+    done = hip.DeviceBuffer.from_array(np.zeros(1, np.int32))
+    runs = []
+    for co in (False, True):
+        m = hip.Model(GPT2_124M, params=params)
+        m.decode_init(B, 16, 320)
+        m.set_graph(True)
+        m.fill_random(300, seed=8)
+        ids, lg = [], []
+        for t in range(toks.shape[0]):
+            m.step_async(toks[t])
+            if co:
+                assert occ.occ_recv_after(hip.lib().hpa_get_stream(), 64, 512, 20000, 37664, done.ptr, 7) == 0
+            lg.append(m.logits())
+            ids.append(lg[-1].argmax(-1))
+        hip.check(hip.lib().hpa_device_synchronize(), "sync")
+        m.status()
+        assert occ.occ_sync() == 0
+        m.close()
+        runs.append((np.stack(ids), np.stack(lg)))
+    assert int(done.download(1, np.int32)[0]) == 64 * toks.shape[0]
+    assert np.array_equal(runs[0][0], runs[1][0]) and np.array_equal(runs[0][1], runs[1][1])

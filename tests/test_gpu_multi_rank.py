@@ -66,7 +66,11 @@ def _worker(rank, world, port, batch, scaling, out_path):
         counts = [h - l for _, l, h in (shard.batch_layout(batch, world, r, scaling) for r in range(world))]
         m = _engine(hip, hi - lo)
         toks = _tokens(B, SMALL["V"])
-        from test_multi_rank import _run_plan
+        from test_multi_rank import _post_plan
+
+        def _run_plan(dist, plan, send, recv):
+            for r in _post_plan(dist, plan, send, recv):
+                r.wait()
         V = SMALL["V"]
         plan_l = hip.gather_plan(world, rank, 0, [n * V * 4 for n in counts])  # gpt2_decode_gather's bytes
         plan_i = hip.gather_plan(world, rank, 0, [n * 4 for n in counts])
