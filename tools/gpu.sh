@@ -14,7 +14,8 @@
 #                      -> prof_CFG/ + kstats_CFG.txt (per-kernel averages)
 #   pmc:CFG            FETCH_SIZE / WRITE_SIZE, separate --pmc passes -> pmc_CFG/traffic.txt
 #   mfma:CFG           SQ_INSTS_MFMA / SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE -> mfma_CFG/
-#   trace:CFG          per-workgroup phase trace of the chain (-DHPA_LAYER_TRACE build)
+#   trace:B[:MODE[:X]] per-workgroup phase trace of the chain (tools/pl_trace.py B 990 MODE X on the
+#                      prebuilt -DHPA_LAYER_TRACE library llm.c-paged_amd/libpl_trace.so)
 #   ab:NAME:FLAGS:CFG  A/B library (make BUILD=build_NAME LIB=libpl_NAME.so XFLAGS="FLAGS"),
 #                      bench CFG on it -> bench_CFG_NAME.txt
 #   lib:NAME:CFG       bench CFG on a prebuilt library (NAME "prod" = libpaged_hip.so,
@@ -68,7 +69,8 @@ for st in "$@"; do
       python3 tools/kstats.py "$o/prof_$a/run_kernel_trace.csv" 0 > "$o/kstats_$a.txt" ;;
     pmc) run "pmc_$a" 900 bash tools/pmc_traffic.sh "$o/pmc_$a" --steps 6 --warmup 2 $(cfg_args "$a") ;;
     mfma) run "mfma_$a" 600 bash tools/pmc_mfma.sh "$o/mfma_$a" --steps 6 --warmup 2 $(cfg_args "$a") ;;
-    trace) run "trace_$a" 600 python -u tools/pl_trace.py $(cfg_args "$a") ;;
+    trace)  # trace:B[:MODE[:XL|b16]] on llm.c-paged_amd/libpl_trace.so (make BUILD=build_trace LIB=libpl_trace.so XFLAGS=-DHPA_LAYER_TRACE)
+      HPA_LIB=llm.c-paged_amd/libpl_trace.so run "trace_${a}_${b:-5}${c:-}" 600 python -u tools/pl_trace.py "$a" 990 "${b:-5}" ${c:-} ;;
     ab)
       run "build_ab_$a" 900 make -s -C llm.c-paged_amd -j16 BUILD="build_$a" LIB="libpl_$a.so" XFLAGS="$b"
       HPA_LIB="llm.c-paged_amd/libpl_$a.so" run "bench_${c}_$a" 600 python -u bench.py --cpu-baseline off $(cfg_args "$c") ;;
