@@ -169,7 +169,7 @@ def parse():
     ap.add_argument("--emulate-rank", type=int, default=0,
                     help="N: on one GPU, time rank 0's engine of an N-GPU run (B/N rows for --scaling strong, "
                          "B for weak, with --picks), and report the per-rank step and the N-GPU projection; "
-                         "no collective (the gather overlaps the next step)")
+                         "rank 0's gather (--gather) runs every step on a 1-rank communicator")
     ap.add_argument("--sample", action="store_true",
                     help="multinomial sampling as the reference driver (default: greedy argmax)")
     ap.add_argument("--gemm-waves", default="", help="fused GEMM waves qkv,attproj,fc,fcproj,logits (0 = auto)")
@@ -335,6 +335,17 @@ def main():
     gather = world > 1 and not args.gather.startswith("none")
     if gather:
         model.shard(counts, root=0)
+    # --emulate-rank: rank 0's gather runs too, on a 1-rank communicator (its
+    # local cost -- the compute -> comm hand-off, the send copy, RCCL's kernel
+    # on the comm stream beside the next step: profiles/r6/recv_coresidency.txt)
+    emul_gather = bool(emulate) and not args.gather.startswith("none")
+    if emul_gather:
+        n = L.hpa_comm_id_bytes()
+        uid = ctypes.create_string_buffer(n)
+        pagedattn.check(L.hpa_comm_unique_id(uid, n), "comm_unique_id")
+        pagedattn.check(L.hpa_comm_init(1, 0, uid), "comm_init (1 rank)")
+        model.shard([B_local], root=0)
+        gather = True
     what = 0 if args.gather == "logits" else 1
     first = rng.integers(0, cfgd["V"], B_local).astype(np.int32)
     pos_now = [start]
@@ -522,14 +533,19 @@ def main():
                 "n_gpus": emulate, "rank": 0, "rows": B_local, "global_batch": B, "scaling": args.scaling,
                 "ms_per_step": round(ms_per_step, 4),
                 "projected_n_gpu_tokens_per_s": round(sum(counts) * args.steps / elapsed, 1),
+                "gather": (f"the library's {args.gather} gather every step on a 1-rank RCCL communicator (its "
+                           f"local cost; the peers' transfer is not modelled)" if emul_gather else "none"),
                 "note": "one GPU running rank 0's engine of an N-GPU decode; value = this GPU's tokens/s; "
-                        "the projection assumes every rank steps as fast and the logits gather stays hidden "
-                        "behind the next step (it overlaps on its own stream); not a multi-GPU measurement"}
+                        "the projection assumes every rank steps as fast and the peers' share of the gather "
+                        "stays hidden behind the next step (it overlaps on its own stream); not a multi-GPU "
+                        "measurement"}
             result["n_gpus"] = 1
         if prefill_stats:
             result["prefill"] = prefill_stats
         print(json.dumps(result), flush=True)
     model.close()
+    if emul_gather:
+        L.hpa_comm_destroy()
     if world > 1:
         pagedattn.check(L.hpa_comm_barrier(), "comm barrier")
         L.hpa_comm_destroy()

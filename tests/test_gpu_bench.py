@@ -57,6 +57,8 @@ def test_bench_default_multi_gpu_line_is_the_metric(n):
     # value = this GPU's rows; the projection = all N ranks' rows at this step time
     assert abs(d["value"] - (64 // n) * 1000.0 / d["ms_per_step"]) / d["value"] < 1e-3
     assert abs(e["projected_n_gpu_tokens_per_s"] * d["ms_per_step"] / 64000.0 - 1) < 1e-2
+    assert "1-rank RCCL communicator" in e["gather"]  # rank 0's gather runs in the timed steps
+    assert d["status"] == 0
 
 
 def test_bench_weak_line_is_labelled_config4():
