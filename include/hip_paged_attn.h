@@ -70,6 +70,7 @@ int   hpa_stream_wait_event(void* ev);
  * compute -> comm hand-off uses it: a pending event wait on another stream
  * slows the decode stream's kernels ~25 us per step, a pending wait-value
  * 5-9 us (profiles/r6/recv_coresidency.txt). */
+int   hpa_stream_value_ops(void);  /* 1 if the device supports them (else use events) */
 int   hpa_stream_write_value32(unsigned* flag, unsigned value);
 int   hpa_stream_wait_value32(unsigned* flag, unsigned value);
 const char* hpa_last_error(void);

@@ -222,6 +222,15 @@ int hpa_stream_wait_event(void* ev) {
  * (profiles/r6/recv_coresidency.txt): a stream waiting on an EVENT of the
  * decode stream slows the decode stream's own kernels by ~25 us per step
  * while the wait is pending; a pending wait-value costs 5-9 us. */
+/* 1 if the current device runs hipStreamWaitValue32 (the gather's hand-off;
+ * else the caller falls back to an event) */
+int hpa_stream_value_ops(void) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, dev) != hipSuccess) return 0;
+    return v != 0;
+}
+
 int hpa_stream_write_value32(unsigned* flag, unsigned value) {
     HPA_CHECK(hipStreamWriteValue32(g_stream, flag, value, 0));
     return 0;

@@ -596,7 +596,9 @@ typedef struct {
     float* recv[2];   /* root: [sum rows][V] */
     int* send_ids[2];
     int* recv_ids[2];
-    unsigned* d_seq;  /* device word: gathers whose send copy is done (compute stream) */
+    unsigned* d_seq;  /* device word: gathers whose send copy is done (compute stream); NULL where
+                         the device has no stream value ops: ev_ready then */
+    void* ev_ready[2];
     unsigned seq;     /* gathers posted */
     void* ev_done[2]; /* gather from buffer k done (comm stream) */
     int k, last, pending[2];
@@ -749,6 +751,7 @@ static void dec_shard_free(GPT2Decode* d) {
     for (int k = 0; k < 2; k++) {
         hpa_free(s->send[k]); hpa_free(s->recv[k]); hpa_free(s->send_ids[k]); hpa_free(s->recv_ids[k]);
         hpa_event_destroy(s->ev_done[k]);
+        hpa_event_destroy(s->ev_ready[k]);
     }
     hpa_free(s->d_seq);
     hpa_stream_destroy(s->stream);
@@ -2404,8 +2407,12 @@ int gpt2_decode_shard(GPT2* model, const int* rows_per_rank, int root) {
         s->ev_done[k] = hpa_event_create_nt();
         ok = s->send[k] && s->send_ids[k] && (rank != root || (s->recv[k] && s->recv_ids[k])) && s->ev_done[k];
     }
-    s->d_seq = ok ? (unsigned*)hpa_malloc(64) : NULL;
-    ok = ok && s->d_seq && hpa_memset_async(s->d_seq, 0, 64) == 0 && hpa_synchronize() == 0;
+    if (ok && hpa_stream_value_ops()) {
+        s->d_seq = (unsigned*)hpa_malloc(64);
+        ok = s->d_seq && hpa_memset_async(s->d_seq, 0, 64) == 0 && hpa_synchronize() == 0;
+    } else {
+        for (int k = 0; k < 2 && ok; k++) ok = (s->ev_ready[k] = hpa_event_create_nt()) != NULL;
+    }
     if (!ok) { dec_shard_free(d); return 1; }
     return 0;
 }
@@ -2436,10 +2443,10 @@ int gpt2_decode_gather(GPT2* model, int what) {
      * step while the wait is pending; a wait-value 5-9 us
      * (profiles/r6/recv_coresidency.txt) */
     const unsigned seq = ++s->seq;
-    rc |= hpa_stream_write_value32(s->d_seq, seq);
+    rc |= s->d_seq ? hpa_stream_write_value32(s->d_seq, seq) : hpa_event_record(s->ev_ready[k]);
     for (int r = 0; r < s->nranks; r++) s->bytes[r] = (size_t)s->rows[r] * per;
     hpa_set_stream(s->stream);
-    rc |= hpa_stream_wait_value32(s->d_seq, seq);
+    rc |= s->d_seq ? hpa_stream_wait_value32(s->d_seq, seq) : hpa_stream_wait_event(s->ev_ready[k]);
     rc |= hpa_comm_gatherv(snd, (size_t)d->B * per, what ? (void*)s->recv_ids[k] : (void*)s->recv[k], s->bytes,
                            s->root, s->stream);
     rc |= hpa_event_record(s->ev_done[k]);

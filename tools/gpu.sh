@@ -67,8 +67,12 @@ for st in "$@"; do
       run "kstats_run_$a" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$o/prof_$a" -o run -- \
         python3 bench.py --cpu-baseline off $(cfg_args "$a")
       python3 tools/kstats.py "$o/prof_$a/run_kernel_trace.csv" 0 > "$o/kstats_$a.txt" ;;
-    pmc) run "pmc_$a" 900 bash tools/pmc_traffic.sh "$o/pmc_$a" --steps 6 --warmup 2 $(cfg_args "$a") ;;
-    mfma) run "mfma_$a" 600 bash tools/pmc_mfma.sh "$o/mfma_$a" --steps 6 --warmup 2 $(cfg_args "$a") ;;
+    pmc)  # per-dispatch csvs dropped after the summary (traffic.txt / traffic.json): gpurun_out stays small
+      run "pmc_$a" 900 bash tools/pmc_traffic.sh "$o/pmc_$a" --steps 6 --warmup 2 --spinup 0 $(cfg_args "$a")
+      rm -rf "$o/pmc_$a/FETCH_SIZE" "$o/pmc_$a/WRITE_SIZE" ;;
+    mfma)
+      run "mfma_$a" 600 bash tools/pmc_mfma.sh "$o/mfma_$a" --steps 6 --warmup 2 --spinup 0 $(cfg_args "$a")
+      rm -rf "$o/mfma_$a/pmc" ;;
     trace)  # trace:B[:MODE[:XL|b16]] on llm.c-paged_amd/libpl_trace.so (make BUILD=build_trace LIB=libpl_trace.so XFLAGS=-DHPA_LAYER_TRACE)
       HPA_LIB=llm.c-paged_amd/libpl_trace.so run "trace_${a}_${b:-5}${c:-}" 600 python -u tools/pl_trace.py "$a" 990 "${b:-5}" ${c:-} ;;
     ab)
