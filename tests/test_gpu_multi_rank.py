@@ -142,6 +142,9 @@ def test_rccl_gather_one_rank(hip):
         assert any("librccl" in x and x.startswith("/opt/rocm") for x in libs), libs
         assert not any("/torch/" in x for x in libs), libs
         assert L.hpa_comm_size() == 1 and L.hpa_comm_rank() == 0
+        # the gather's compute -> comm hand-off is a device word on MI355X
+        # (stream value ops; an event only where the device lacks them)
+        assert L.hpa_stream_value_ops() == 1
         B = 5
         m = _engine(hip, B)
         m.shard([B], root=0)
