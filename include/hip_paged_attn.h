@@ -359,7 +359,7 @@ typedef struct {
                                      tiles (T by batch, one unit per workgroup, the 12-wave
                                      summation order at every B <= 64), 16-byte epilogues,
                                      waits per row block (C = 768); 8: the chain for
-                                     MFMA-bound wide layers (C = 768 or 1600, GPT-2 XL): units of
+                                     MFMA-bound wide layers (C = 768, 1024, 1280 or 1600: GPT-2 124M to XL): units of
                                      12 waves x up to 7 tiles, weights streamed per tile */
     const HpaKVPool* pool;
     int layer;
@@ -395,8 +395,8 @@ typedef struct {
 } HpaLayerArgs;
 /* 1 if the persistent layer applies (shape, CU count, residency), else 0 */
 int hpa_decode_layer_eligible(int B, int C, int num_heads, int splits);
-/* 1 if chain form `form` (HpaLayerArgs.chain_only 6, 7: C = 768; 8: C = 768
- * or 1600) applies to B rows on this device's CU count, else 0 */
+/* 1 if chain form `form` (HpaLayerArgs.chain_only 6, 7: C = 768; 8: C = 768,
+ * 1024, 1280 or 1600) applies to B rows on this device's CU count, else 0 */
 int hpa_decode_chain_eligible(int B, int C, int num_heads, int form);
 /* splits the persistent layer uses by default for this batch */
 int hpa_decode_layer_pick_splits(int B, int num_heads, int max_ctx);

@@ -214,7 +214,7 @@ int  gpt2_decode_attn_waves(GPT2* model);
  * chain in round 3's wide units (C = 768); 5 chain form 6: every phase in
  * 12-wave units of T tiles, one per workgroup, 16-byte epilogues, waits per
  * row block (C = 768); 6 chain form 8: streamed-weight units for MFMA-bound
- * wide layers (C = 768 / 1600, GPT-2 XL); 1 (default, "auto") the form
+ * wide layers (C = 768 / 1024 / 1280 / 1600: GPT-2 124M to XL); 1 (default, "auto") the form
  * measured fastest (profiles/r4: 5 at C = 768, 6 at C >= 1024, else 3).
  * The persistent forms need fp32 weights and B <= 64 (else five launches).
  * HPA_LAYER_KERNEL=0..6 in the environment

@@ -2119,7 +2119,7 @@ int hpa_decode_layer_trace(unsigned long long* host, int layers) {
 #endif
 }
 
-// the chain forms 6 (C = 768) and 8 (C = 768 or 1600): B <= 64, fp32 or
+// the chain forms 6 (C = 768) and 8 (C = 768, 1024, 1280 or 1600): B <= 64, fp32 or
 // bf16 pool, a unit per workgroup in every phase
 int hpa_decode_chain_eligible(int B, int C, int num_heads, int form) {
     const int G = num_cus();
@@ -2129,8 +2129,8 @@ int hpa_decode_chain_eligible(int B, int C, int num_heads, int form) {
         const int R = (B + 15) / 16;
         return R * 48 <= G && 4 * R * 48 / (R == 1 ? 1 : R == 2 ? 2 : 3) <= G ? 1 : 0;
     }
-    if (form == 8) {
-        if (num_heads != 12 && num_heads != 25) return 0;
+    if (form == 8) {  // GPT-2 124M / medium / large / XL widths (C = 768, 1024, 1280, 1600)
+        if (num_heads != 12 && num_heads != 16 && num_heads != 20 && num_heads != 25) return 0;
         int xt[4], xng[4];
         return chainx_shape(B, num_heads, G, xt, xng) == 0 ? 1 : 0;
     }
@@ -2181,7 +2181,12 @@ int hpa_decode_layer(const HpaLayerArgs* h) {
     if (h->chain_only == 6 || h->chain_only == 8) {
         HPA_REQUIRE(hpa_decode_chain_eligible(h->B, h->C, h->num_heads, h->chain_only),
                     "decode layer: chain form not supported for this shape");
-        if (h->chain_only == 8) return h->num_heads == 25 ? dispatchx<25>(h, G) : dispatchx<12>(h, G);
+        if (h->chain_only == 8) switch (h->num_heads) {
+                case 16: return dispatchx<16>(h, G);
+                case 20: return dispatchx<20>(h, G);
+                case 25: return dispatchx<25>(h, G);
+                default: return dispatchx<12>(h, G);
+            }
         return dispatch<12>(h, G);
     }
     HPA_REQUIRE(hpa_decode_layer_eligible(h->B, h->C, h->num_heads, h->splits), "decode layer: shape not supported");

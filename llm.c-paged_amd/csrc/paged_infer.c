@@ -664,7 +664,7 @@ struct GPT2Decode {
     /* persistent layer (hpa_decode_layer): one launch per layer */
     int pl_want;      /* gpt2_decode_set_layer_kernel: 0 off, 1 auto, 2 full, 3 chain, 4 chain with wide units,
                          5 chain form 6 (12-wave multi-tile units), 6 chain form 8 (streamed-weight
-                         units, C = 768 / 1600) */
+                         units, C = 768 / 1024 / 1280 / 1600) */
     int pl_on;        /* in use: 0 five launches, 1 full persistent layer, 2 attention launch + chain,
                          3 attention launch + chain of wide units (hpa_layer.hip NWU = pl_nwu),
                          4 attention launch + the bf16-weight chain (hpa_chain_b16.hip) */

@@ -349,3 +349,40 @@ def test_chain8_xl_matches_launch_path(hip, B):
     print(f"XL B={B}: max |logit diff| form 8 vs launches {diff:.3e}; near-ties {int((~clear).sum())}")
     assert diff <= 5e-5, diff
     assert np.array_equal(i8[clear], i0[clear])
+
+
+@pytest.mark.parametrize("C,NH,B", [(1024, 16, 64), (1024, 16, 17), (1280, 20, 64), (1280, 20, 5)],
+                         ids=["medium-64", "medium-17", "large-64", "large-5"])
+def test_chain8_medium_large_matches_launch_path(hip, C, NH, B):
+    """chain form 8 at GPT-2 medium (C = 1024, 16 heads) and large (C = 1280,
+    20 heads) widths (round 6: the engine's auto form for C >= 1024, was five
+    launches), 2 layers, small vocabulary: logits within fp32 reassociation of
+    the five-launch layer, ids equal outside near-ties, status 0"""
+    cfgd = dict(maxT=256, V=2000, L=2, NH=NH, C=C)
+    assert hip.lib().hpa_decode_chain_eligible(B, C, NH, 8) == 1
+    params = hip.synthetic_params(cfgd, seed=97)
+    ctx, steps = 120, 3
+    toks = np.random.default_rng(97 + B).integers(0, cfgd["V"], (steps, B)).astype(np.int32)
+    out = []
+    for mode in (1, 0):  # 1 = auto: form 8 at these widths
+        m = hip.Model(cfgd, params=params)
+        m.decode_init(B, 16, ctx + 8)
+        assert m.set_layer_kernel(mode) == (mode != 0)
+        if mode:
+            assert m.layer_form() == 3
+        m.set_graph(True)
+        m.fill_random(ctx, seed=14)
+        lg, ids = [], []
+        for t in range(steps):
+            ids.append(m.step(toks[t]))
+            lg.append(m.logits())
+        m.status()
+        m.close()
+        out.append((np.stack(lg), np.stack(ids)))
+    (l8, i8), (l0, i0) = out
+    diff = float(np.abs(l8 - l0).max())
+    s = np.sort(l0, axis=-1)
+    clear = (s[..., -1] - s[..., -2]) > 4 * diff
+    print(f"C={C} B={B}: max |logit diff| form 8 vs launches {diff:.3e}")
+    assert diff <= 5e-5, diff
+    assert np.array_equal(i8[clear], i0[clear])
